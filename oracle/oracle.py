@@ -1,0 +1,224 @@
+"""ctypes wrapper over oracle/build/liboracle.so — the CPU restatement of the
+reference hot path (cover/cover.go, Go sort.Sort, prog/prio.go).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker / CPU baseline.  The product package
+(syzkaller_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+DIFFERENCE, SYMDIFF, UNION, INTERSECTION = 0, 1, 2, 3
+PDQSORT, LEGACY = 0, 1
+
+
+def build() -> str:
+    """Compile the oracle (gcc, seconds)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        p = C.c_void_p
+        sz = C.c_size_t
+        _lib.orc_canonicalize.argtypes = [p, sz]
+        _lib.orc_canonicalize.restype = sz
+        _lib.orc_setop.argtypes = [C.c_int, p, sz, p, sz, p]
+        _lib.orc_setop.restype = sz
+        _lib.orc_sort_min_inputs.argtypes = [p, p, sz, C.c_int]
+        _lib.orc_minimize.argtypes = [p, p, sz, C.c_int, p]
+        _lib.orc_minimize.restype = sz
+        _lib.orc_union_fold.argtypes = [p, p, sz, p]
+        _lib.orc_union_fold.restype = sz
+        _lib.orc_newcov_batch.argtypes = [p, p, C.c_int, p, sz, p, p, p, sz, p, p, p]
+        _lib.orc_dynamic_raw.argtypes = [p, sz, C.c_int, p]
+        _lib.orc_dynamic_raw.restype = C.c_int
+        _lib.orc_normalize_prio.argtypes = [p, C.c_int]
+        _lib.orc_calculate_priorities.argtypes = [p, sz, C.c_int, p, p]
+        _lib.orc_calculate_priorities.restype = C.c_int
+        _lib.orc_build_choice_table.argtypes = [p, p, C.c_int, p]
+        _lib.orc_synth_len.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
+        _lib.orc_synth_len.restype = C.c_uint32
+        _lib.orc_synth_input.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                         C.c_int, p]
+        _lib.orc_synth_universe.argtypes = [C.c_uint64, C.c_uint32]
+        _lib.orc_synth_universe.restype = C.c_uint32
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _u32(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint32))
+
+
+def canonicalize(cov) -> np.ndarray:
+    a = _u32(cov).copy()
+    n = lib().orc_canonicalize(_ptr(a), a.size)
+    return a[:n]
+
+
+def setop(op: int, a, b) -> np.ndarray:
+    a, b = _u32(a), _u32(b)
+    out = np.empty(a.size + b.size + 1, dtype=np.uint32)
+    n = lib().orc_setop(op, _ptr(a), a.size, _ptr(b), b.size, _ptr(out))
+    return out[:n]
+
+
+def difference(a, b):
+    return setop(DIFFERENCE, a, b)
+
+
+def symmetric_difference(a, b):
+    return setop(SYMDIFF, a, b)
+
+
+def union(a, b):
+    return setop(UNION, a, b)
+
+
+def intersection(a, b):
+    return setop(INTERSECTION, a, b)
+
+
+def to_csr(covers):
+    lens = np.array([len(c) for c in covers], dtype=np.uint64)
+    off = np.zeros(len(covers) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    pcs = (np.concatenate([_u32(c) for c in covers]) if covers and off[-1] > 0
+           else np.zeros(1, dtype=np.uint32))
+    return off, _u32(pcs)
+
+
+def sort_order(lens, variant: int = PDQSORT) -> np.ndarray:
+    """Go sort.Sort(minInputArray) over inputs with the given lengths:
+    returns the processing order (rank -> original index)."""
+    lens = np.ascontiguousarray(np.asarray(lens, dtype=np.int64))
+    idx = np.arange(lens.size, dtype=np.int32)
+    lib().orc_sort_min_inputs(_ptr(idx), _ptr(lens), lens.size, variant)
+    return idx
+
+
+def minimize_csr(off, pcs, variant: int = PDQSORT) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pcs = _u32(pcs)
+    n = off.size - 1
+    out = np.empty(max(n, 1), dtype=np.int32)
+    k = lib().orc_minimize(_ptr(off), _ptr(pcs), n, variant, _ptr(out))
+    return out[:k]
+
+
+def minimize(covers, variant: int = PDQSORT) -> np.ndarray:
+    off, pcs = to_csr(covers)
+    return minimize_csr(off, pcs, variant)
+
+
+def union_fold_csr(off, pcs) -> np.ndarray:
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pcs = _u32(pcs)
+    out = np.empty(int(off[-1]) + 1, dtype=np.uint32)
+    k = lib().orc_union_fold(_ptr(off), _ptr(pcs), off.size - 1, _ptr(out))
+    return out[:k]
+
+
+def newcov_batch(maxcover, flakes, callids, records):
+    """fuzzer.go:456-480 over a batch.  maxcover: list of per-call sorted lists.
+    Returns (is_new[nrec] uint8, new maxcover list)."""
+    ncalls = len(maxcover)
+    mc_off, mc_pcs = to_csr(maxcover)
+    r_off, r_pcs = to_csr(records)
+    fl = _u32(flakes) if len(flakes) else np.zeros(1, dtype=np.uint32)
+    cid = np.ascontiguousarray(np.asarray(callids, dtype=np.int32))
+    nrec = len(records)
+    is_new = np.zeros(max(nrec, 1), dtype=np.uint8)
+    new_off = np.zeros(ncalls + 1, dtype=np.uint64)
+    new_pcs = np.zeros(int(mc_off[-1]) + int(r_off[-1]) + 1, dtype=np.uint32)
+    lib().orc_newcov_batch(_ptr(mc_off), _ptr(mc_pcs), ncalls, _ptr(fl), len(flakes), _ptr(cid),
+                           _ptr(r_off), _ptr(r_pcs), nrec, _ptr(is_new), _ptr(new_off),
+                           _ptr(new_pcs))
+    mc = [new_pcs[new_off[c]:new_off[c + 1]].copy() for c in range(ncalls)]
+    return is_new[:nrec], mc
+
+
+def dynamic_raw(prog_lens, C_: int) -> np.ndarray:
+    pl = np.ascontiguousarray(np.asarray(prog_lens, dtype=np.int32))
+    out = np.zeros((C_, C_), dtype=np.float32)
+    if lib().orc_dynamic_raw(_ptr(pl), pl.size, C_, _ptr(out)) != 0:
+        raise IndexError("program longer than the call table (Go panics)")
+    return out
+
+
+def normalize_prio(prios: np.ndarray) -> np.ndarray:
+    p = np.ascontiguousarray(prios, dtype=np.float32).copy()
+    lib().orc_normalize_prio(_ptr(p), p.shape[0])
+    return p
+
+
+def calculate_priorities(prog_lens, static: np.ndarray) -> np.ndarray:
+    C_ = static.shape[0]
+    pl = np.ascontiguousarray(np.asarray(prog_lens, dtype=np.int32))
+    st = np.ascontiguousarray(static, dtype=np.float32)
+    out = np.zeros((C_, C_), dtype=np.float32)
+    if lib().orc_calculate_priorities(_ptr(pl), pl.size, C_, _ptr(st), _ptr(out)) != 0:
+        raise IndexError("program longer than the call table (Go panics)")
+    return out
+
+
+def build_choice_table(prios: np.ndarray, enabled) -> np.ndarray:
+    C_ = prios.shape[0]
+    pr = np.ascontiguousarray(prios, dtype=np.float32)
+    en = np.ascontiguousarray(np.asarray(enabled, dtype=np.uint8))
+    run = np.full((C_, C_), -1, dtype=np.int64)
+    lib().orc_build_choice_table(_ptr(pr), _ptr(en), C_, _ptr(run))
+    return run
+
+
+def synth_lens(seed: int, n: int, mean: int = 2048, sigma: int = 512, first: int = 0):
+    f = lib().orc_synth_len
+    return np.array([f(seed, first + i, mean, sigma) for i in range(n)], dtype=np.uint32)
+
+
+def synth_input(seed: int, i: int, length: int, log2_space: int = 22, uniform: bool = False):
+    out = np.empty(max(int(length), 1), dtype=np.uint32)
+    lib().orc_synth_input(seed, i, int(length), log2_space, int(uniform), _ptr(out))
+    return out[:length]
+
+
+def synth_corpus(seed: int, n: int, mean: int = 2048, sigma: int = 512, log2_space: int = 22,
+                 uniform: bool = False, first: int = 0):
+    """Raw (non-canonical) corpus in CSR form: (offsets u64[n+1], pcs u32)."""
+    lens = synth_lens(seed, n, mean, sigma, first)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens.astype(np.uint64), out=off[1:])
+    pcs = np.empty(max(int(off[-1]), 1), dtype=np.uint32)
+    f = lib().orc_synth_input
+    base = pcs.ctypes.data
+    for i in range(n):
+        f(seed, first + i, int(lens[i]), log2_space, int(uniform),
+          C.c_void_p(base + 4 * int(off[i])))
+    return off, pcs
+
+
+def canonicalize_csr(off, pcs):
+    """Canonicalize every input of a CSR corpus; returns a compacted CSR."""
+    n = off.size - 1
+    outs = []
+    for i in range(n):
+        outs.append(canonicalize(pcs[off[i]:off[i + 1]]))
+    return to_csr(outs)

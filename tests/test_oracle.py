@@ -1,0 +1,166 @@
+"""The CPU oracle against the reference's own known-answer tables
+(cover/cover_test.go:60-168) and against an independent pure-Python
+transcription.  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from oracle import pyref
+from tests.conftest import augment
+
+OPS = {
+    "difference": (orc.difference, pyref.difference),
+    "symmetric_difference": (orc.symmetric_difference, pyref.symmetric_difference),
+    "union": (orc.union, pyref.union),
+    "intersection": (orc.intersection, pyref.intersection),
+}
+
+
+def _is_sorted(a):
+    a = list(a)
+    return all(a[i] <= a[i + 1] for i in range(len(a) - 1))
+
+
+@pytest.mark.parametrize("name", list(OPS))
+def test_setop_kat(kat, name):
+    t = kat[name]
+    c_fn, py_fn = OPS[name]
+    for a, b, r in augment(t["cases"], t["symmetric"]):
+        assert _is_sorted(a) and _is_sorted(b) and _is_sorted(r)
+        assert list(c_fn(a, b)) == r, (name, a, b)
+        assert py_fn(a, b) == r
+
+
+def test_canonicalize_kat(kat):
+    for a, _, r in augment(kat["canonicalize"]["cases"], False):
+        assert list(orc.canonicalize(a)) == r
+        assert pyref.canonicalize(a) == r
+
+
+def test_minimize_kat(kat):
+    for case in kat["minimize"]["cases"]:
+        for variant in (orc.PDQSORT, orc.LEGACY):
+            assert list(orc.minimize(case["inp"], variant)) == case["out"], case["name"]
+        assert pyref.minimize(case["inp"]) == case["out"]
+
+
+def test_quirks(kat):
+    q = kat["quirks"]
+    for a, r in q["canonicalize"]:
+        assert list(orc.canonicalize(a)) == r
+        assert pyref.canonicalize(a) == r
+    for name, a, b, r in q["setops"]:
+        assert list(OPS[name][0](a, b)) == r
+        assert OPS[name][1](a, b) == r
+    for case in q["minimize"]:
+        assert list(orc.minimize(case["inp"])) == case["out"]
+        assert pyref.minimize(case["inp"]) == case["out"]
+
+
+def test_minimize_random_property():
+    """TestMinimizeRandom (cover_test.go:170-205) with fixed seeds instead of
+    time.Now(): Union of the kept inputs == Union of all inputs."""
+    rng = np.random.default_rng(0x5EED)
+    for _ in range(300):
+        n = int(rng.integers(0, 20))
+        covs = [list(orc.canonicalize(rng.integers(0, 100, size=int(rng.integers(0, 10)))))
+                for _ in range(n)]
+        total = []
+        for c in covs:
+            total = pyref.union(total, c)
+        mini = orc.minimize(covs)
+        m = []
+        for idx in mini:
+            m = pyref.union(m, covs[idx])
+        assert m == total
+
+
+def test_sort_c_vs_python():
+    """Two independent transcriptions of Go's pdqsort agree, including
+    tie-heavy inputs large enough to reach partition/partitionEqual,
+    breakPatterns and partialInsertionSort."""
+    rng = np.random.default_rng(1)
+    for trial in range(200):
+        n = int(rng.integers(0, 3000))
+        kind = trial % 5
+        if kind == 0:
+            lens = rng.integers(0, 10, size=n)
+        elif kind == 1:
+            lens = rng.integers(0, 1 << 16, size=n)
+        elif kind == 2:
+            lens = np.sort(rng.integers(0, 50, size=n))  # ascending = reverse of desired
+        elif kind == 3:
+            lens = np.sort(rng.integers(0, 50, size=n))[::-1].copy()
+            if n > 3:
+                lens[rng.integers(0, n)] = 1000  # nearly sorted
+        else:
+            lens = np.full(n, 7)
+        c = orc.sort_order(lens)
+        p = pyref.go_sort_order([int(x) for x in lens])
+        assert list(c) == p, (trial, n, kind)
+        # it must be a valid descending order
+        assert all(lens[c[i]] >= lens[c[i + 1]] for i in range(n - 1))
+
+
+def test_minimize_c_vs_python():
+    rng = np.random.default_rng(2)
+    for _ in range(100):
+        n = int(rng.integers(0, 200))
+        covs = [list(orc.canonicalize(rng.integers(0, 300, size=int(rng.integers(0, 12)))))
+                for _ in range(n)]
+        assert list(orc.minimize(covs)) == pyref.minimize(covs)
+
+
+def test_legacy_sort_is_a_sort():
+    rng = np.random.default_rng(3)
+    for _ in range(100):
+        n = int(rng.integers(0, 2000))
+        lens = rng.integers(0, 20, size=n)
+        c = orc.sort_order(lens, orc.LEGACY)
+        assert sorted(c) == list(range(n))
+        assert all(lens[c[i]] >= lens[c[i + 1]] for i in range(n - 1))
+    # n <= 6: both variants are the same stable insertion sort
+    for _ in range(100):
+        lens = rng.integers(0, 3, size=int(rng.integers(0, 7)))
+        assert list(orc.sort_order(lens, orc.LEGACY)) == list(orc.sort_order(lens))
+
+
+def test_newcov_batch_small():
+    """Sequential fuzzer.go:456-480 semantics on a hand-checked batch."""
+    mc = [[1, 2], [], [5]]
+    flakes = [9]
+    recs = [[1, 2], [2, 3], [3, 9], [9], [5, 6], [4]]
+    cids = [0, 0, 0, 1, 2, 0]
+    is_new, new_mc = orc.newcov_batch(mc, flakes, cids, recs)
+    assert list(is_new) == [0, 1, 0, 0, 1, 1]
+    assert [list(x) for x in new_mc] == [[1, 2, 3, 4], [], [5, 6]]
+
+
+def test_prio_small():
+    C = 5
+    lens = [3, 2, 0, 5, 1]
+    raw = orc.dynamic_raw(lens, C)
+    exp = np.zeros((C, C), np.float32)
+    for n in lens:
+        for i in range(n):
+            for j in range(n):
+                if i != j:
+                    exp[i, j] += 1
+    assert np.array_equal(raw, exp)
+    with pytest.raises(IndexError):
+        orc.dynamic_raw([6], C)
+    static = np.full((C, C), 0.5, np.float32)
+    pr = orc.calculate_priorities(lens, static)
+    assert pr.shape == (C, C) and np.all(pr > 0) and np.all(pr <= 0.5)
+    run = orc.build_choice_table(pr, [1, 0, 1, 1, 1])
+    assert np.all(run[1] == -1)  # disabled row stays nil
+    assert np.all(np.diff(run[0]) >= 0)
+
+
+def test_synth_deterministic():
+    off, pcs = orc.synth_corpus(0x5EED0001, 50)
+    off2, pcs2 = orc.synth_corpus(0x5EED0001, 50)
+    assert np.array_equal(pcs, pcs2)
+    lens = np.diff(off)
+    assert 1000 < lens.mean() < 3000
+    assert pcs.min() >= 0x81000000 and pcs.max() <= 0x84FFFFFF
