@@ -1,0 +1,243 @@
+/*
+ * syzcov.h — C-ABI of the MI355X coverage-analysis engine (libsyzcov.so).
+ *
+ * Plain pointers and sizes only; no torch or HIP types in any signature
+ * (streams and device pointers travel as void* / uint64_t).  Two tiers:
+ *
+ *  1. Drop-in host API.  Exactly what syzkaller's Go packages would bind over
+ *     cgo to replace the pure-Go hot path (INTEGRATION.md shows the shim).
+ *     Host buffers in, host buffers out; every call computes on the GPU
+ *     (no CPU fallback: with no usable HIP device a call returns
+ *     SYZCOV_ENODEV).  Reentrant: each host thread gets its own HIP stream
+ *     and scratch, so the fuzzer's <=32 goroutines may call concurrently
+ *     (syz-fuzzer/fuzzer.go:166, config/config.go:150).
+ *
+ *  2. Device-resident launch API (syzcov_dev_*).  Device pointers plus a HIP
+ *     stream; no host synchronisation, no allocation (caller-provided
+ *     workspace), so the calls can be captured into a hipGraph.  This is what
+ *     the corpus engine, bench.py and the multi-GPU path drive.
+ *
+ * Semantics follow the Go reference bit-for-bit (cover/cover.go, prog/prio.go)
+ * for the input domain the reference's callers produce.  Where the reference
+ * has undefined-looking behaviour the engine is explicit:
+ *   - set ops require each operand sorted non-decreasing (duplicates allowed:
+ *     they get foreach's multiset behaviour); unsorted operands -> SYZCOV_ENOTSORTED
+ *     (no reference caller passes one: SURVEY §7(d));
+ *   - 0xFFFFFFFF is dropped from set-op results (cover.go:17,97) and is an
+ *     ordinary PC for Minimize (cover.go:116-129);
+ *   - Canonicalize drops a 0xFFFFFFFF only when it is the sole distinct value
+ *     (cover.go:30 `last := sent`).
+ *
+ * Return codes: >= 0 success (a count where documented), < 0 error.
+ */
+#ifndef SYZCOV_H
+#define SYZCOV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYZCOV_OK 0
+#define SYZCOV_EINVAL -1      /* bad arguments */
+#define SYZCOV_ENOTSORTED -2  /* set-op operand not sorted */
+#define SYZCOV_ENODEV -3      /* no HIP device */
+#define SYZCOV_EHIP -4        /* HIP runtime error */
+#define SYZCOV_ERANGE -5      /* a PC outside the configured PC window */
+#define SYZCOV_ENOMEM -6      /* device allocation failed */
+#define SYZCOV_ETOOLONG -7    /* program longer than the call table (Go would panic) */
+
+/* Version / build identification: "syzcov <ver> gfx950". */
+const char *syzcov_version(void);
+/* Human-readable text for the last error on this thread. */
+const char *syzcov_last_error(void);
+
+/* ======================= 1. drop-in host API ========================= */
+
+/* cover.RestorePC (cover/cover.go:23-25). */
+uint64_t syzcov_restore_pc(uint32_t pc, uint32_t base);
+
+/* cover.Canonicalize (cover/cover.go:27-40): sorts and de-duplicates cov IN
+ * PLACE and returns the new length n' (the Go shim returns cov[:n'], keeping
+ * the reference's aliasing, html.go:236). */
+int64_t syzcov_canonicalize(uint32_t *cov, size_t n);
+
+/* cover.Difference / SymmetricDifference / Union / Intersection
+ * (cover/cover.go:42-79, merge core foreach :81-102).  `out` must hold
+ * na (Difference), na+nb (SymmetricDifference, Union), min(na,nb)
+ * (Intersection) entries.  Returns the result length (the shim returns nil
+ * for 0, matching foreach's nil result). */
+int64_t syzcov_difference(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                          uint32_t *out);
+int64_t syzcov_symmetric_difference(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                                    uint32_t *out);
+int64_t syzcov_union(const uint32_t *a, size_t na, const uint32_t *b, size_t nb, uint32_t *out);
+int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                            uint32_t *out);
+
+/* cover.Minimize (cover/cover.go:104-131).  The corpus is CSR:
+ * cover i = pcs[offsets[i] .. offsets[i+1]).  `order` (nullable) is the
+ * processing order — order[r] = index of the r-th input after Go's
+ * sort.Sort(minInputArray) (cover.go:113).  The Go shim passes the order its
+ * own sort.Sort produced (exact by construction); NULL makes the engine
+ * compute it with its restatement of Go >= 1.19 pdqsort (sort_variant 0) or
+ * the Go 1.8-1.18 quickSort (sort_variant 1).  Writes the kept input indices
+ * in processing order to out_idx (capacity n) and returns their count. */
+int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                        const int32_t *order, int sort_variant, int32_t *out_idx);
+
+/* Go sort.Sort(minInputArray) restatement: order[r] for inputs of the given
+ * lengths (len(cov) including duplicates).  Computed on the GPU. */
+int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order);
+
+/* Union of a whole corpus (the `total = Union(total, cov)` fold of
+ * manager.go:610 / html.go:72-79 / cover_test.go:182-185) in one pass.
+ * out must hold the total PC count; returns |union|. */
+int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n, uint32_t *out);
+
+/* prog.CalculatePriorities (prog/prio.go:29-38) given the static matrix
+ * (calcStaticPriorities, :40-135, stays with the caller: it depends only on
+ * sys.Calls).  key_mode 0 = positional, exactly the reference's
+ * calcDynamicPrio (:137-154, which indexes by call position); key_mode 1 =
+ * by syscall id.  prog_off/call_ids describe programs in CSR form (ids are
+ * only read in key_mode 1; in mode 0 only the lengths matter).  static_prios
+ * and out are row-major C*C float32.  raw_counts (nullable, C*C uint32)
+ * receives the exact co-occurrence counts before normalisation. */
+int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_ids,
+                                size_t nprog, int C, int key_mode, const float *static_prios,
+                                float *out, uint32_t *raw_counts);
+
+/* prog.normalizePrio (prog/prio.go:158-192), in place, C*C float32. */
+int syzcov_normalize_prio(float *prios, int C);
+
+/* prog.BuildChoiceTable (prog/prio.go:202-228): run[i][j] for enabled rows
+ * (int64, C*C); rows of disabled calls are left untouched (nil in Go).
+ * enabled == NULL enables every call (prio.go:203-208). */
+int syzcov_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run);
+
+/* Streaming new-coverage check of syz-fuzzer execute() (fuzzer.go:456-480)
+ * against resident state.  A handle holds per-CallID maxCover and the global
+ * flakes set as device bitmaps over a PC window [pc_lo, pc_lo + pc_span). */
+typedef uint64_t syzcov_cover_state;
+int syzcov_state_create(int ncalls, uint32_t pc_lo, uint64_t pc_span, syzcov_cover_state *out);
+int syzcov_state_destroy(syzcov_cover_state st);
+/* maxCover[call] = Union(maxCover[call], pcs) (sorted list). */
+int syzcov_state_add(syzcov_cover_state st, int call, const uint32_t *pcs, size_t n);
+int syzcov_state_set_flakes(syzcov_cover_state st, const uint32_t *pcs, size_t n);
+/* Reads maxCover[call] back as a sorted list (out capacity: pc_span or the
+ * count from a NULL-out call); returns its length. */
+int64_t syzcov_state_get(syzcov_cover_state st, int call, uint32_t *out, size_t cap);
+/* One batch of executed call records in batch order (record k: call id
+ * callid[k], sorted cover rec_pcs[rec_off[k] .. rec_off[k+1])).  Sets
+ * is_new[k] exactly as the sequential reference loop would, and updates
+ * maxCover as it would.  Returns the number of new records. */
+int64_t syzcov_newcov_batch(syzcov_cover_state st, const int32_t *callid, const uint64_t *rec_off,
+                            const uint32_t *rec_pcs, size_t nrec, uint8_t *is_new);
+
+/* =================== 2. device-resident launch API ==================== */
+/* All pointers below are device pointers; `stream` is a hipStream_t.
+ * `ws` is caller-provided device workspace of at least the returned size.  */
+
+/* Segmented Canonicalize of a CSR corpus, out of place (out may equal in).
+ * Segment i's canonical list goes to out[off[i] .. off[i] + new_len[i]).
+ * If pres != NULL, also marks pres[pc - pc_lo] = 1 (uint8 presence map over
+ * the PC window of pc_span bytes) and sets *err_flag (device u32) to nonzero
+ * when a PC falls outside the window. */
+size_t syzcov_dev_canon_ws_size(size_t nseg, size_t max_seg_len);
+int syzcov_dev_canonicalize(const uint64_t *off, const uint32_t *in, uint32_t *out,
+                            uint32_t *new_len, size_t nseg, size_t max_seg_len, uint8_t *pres,
+                            uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag, void *ws,
+                            size_t ws_size, void *stream);
+
+/* Presence marking of a CSR corpus with explicit lengths (len == NULL:
+ * lengths from offsets). */
+int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const uint32_t *pcs, size_t nseg,
+                    uint8_t *pres, uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag,
+                    void *stream);
+
+/* Dense PC-id dictionary from a presence map: tab[w] = {prefix:32 | bits:32}
+ * for 32-PC word w (prefix = set bits before w).  *n_ids receives the total
+ * (device u32).  ws: syzcov_dev_dict_ws_size(pc_span). */
+size_t syzcov_dev_dict_ws_size(uint64_t pc_span);
+int syzcov_dev_dict_build(const uint8_t *pres, uint64_t pc_span, uint64_t *tab, uint32_t *n_ids,
+                          void *ws, void *stream);
+
+/* Sorted list of the PCs present in the dictionary, minus 0xFFFFFFFF
+ * (Union drops the sentinel).  *n_out (device u32) receives the count. */
+int syzcov_dev_dict_to_list(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo,
+                            uint32_t *out, uint32_t *n_out, void *stream);
+
+/* Minimize pass 1 over n work items in rank order: item j is input
+ * order[j] with rank ranks[j] (ranks == NULL: rank j).  first[id] (pre-set to
+ * INT32_MAX) receives the minimum rank covering dense id `id`; cand[j] = 1
+ * iff item j lowered some first[] entry (a necessary condition for being
+ * kept).  Sharded runs pass each shard's items with their GLOBAL ranks and
+ * then MIN-all-reduce first[]. */
+int syzcov_dev_minimize_pass1(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                              const int32_t *order, const int32_t *ranks, size_t n,
+                              const uint64_t *tab, uint32_t pc_lo, int32_t *first, uint8_t *cand,
+                              void *stream);
+/* Minimize pass 2: kept[rank] = 1 for every candidate item j holding a PC
+ * with first[id(pc)] == rank (kept[] pre-zeroed, indexed by rank, so shards
+ * can MAX-all-reduce it). */
+int syzcov_dev_minimize_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                              const int32_t *order, const int32_t *ranks, size_t n,
+                              const uint64_t *tab, uint32_t pc_lo, const int32_t *first,
+                              const uint8_t *cand, uint8_t *kept, void *stream);
+/* Ordered compaction: out_idx = [order[r] for r if kept[r]]; *n_out (device u32). */
+size_t syzcov_dev_compact_ws_size(size_t n);
+int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n, int32_t *out_idx,
+                            uint32_t *n_out, void *ws, void *stream);
+
+/* Exact Go sort.Sort(minInputArray) order on the device from int64 lengths. */
+size_t syzcov_dev_sort_ws_size(size_t n);
+int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order,
+                          void *ws, size_t ws_size, void *stream);
+
+/* Bitmap/byte-map set algebra over a PC window (coalesced, ballot-packed):
+ * op 0: dst |= src  (Union)      op 1: dst &= src  (Intersection)
+ * op 2: dst &= ~src (Difference) op 3: dst ^= src  (SymmetricDifference)
+ * Maps are uint8 per PC; *popcount_out (device u64, nullable) receives the
+ * number of nonzero bytes of the result. */
+int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, uint64_t nbytes,
+                          uint64_t *popcount_out, void *stream);
+
+/* Synthetic corpus (integer-exact): lengths for inputs
+ * [first, first+n), then PCs into CSR. */
+int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean, uint32_t sigma,
+                          uint32_t *lens, void *stream);
+int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
+                         uint32_t log2_space, int uniform, uint32_t *pcs, void *stream);
+
+/* Dynamic priority counts as a dense contraction on i8 MFMA with i32
+ * accumulation: counts = AᵀA over the key-major matrix AT[key][program]
+ * (rows = syzcov_dev_prio_rows(C), program stride ldp =
+ * syzcov_dev_prio_ldp(nprog), zero padded).  Row C of AT is all ones, so
+ * counts[i][C] = colsum(A)[i] feeds the diagonal correction.
+ * key_mode 0 (positional, reference-exact: prio.go:142-150 indexes by call
+ * position): AT[k][p] = [k < lens[p]]; key_mode 1: AT[c][p] = number of calls
+ * of syscall id c in program p (CSR prog_off/call_ids, <= 127 per program).
+ * counts is rows x rows int32, zeroed by the caller; shards accumulate into
+ * it and may be summed with an RCCL int32 sum all-reduce. */
+size_t syzcov_dev_prio_rows(int C);
+size_t syzcov_dev_prio_ldp(size_t nprog);
+int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens, const uint64_t *prog_off,
+                             const uint16_t *call_ids, size_t nprog, int C, int8_t *at,
+                             size_t ldp, uint32_t *err_flag, void *stream);
+int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog, int C, int32_t *counts,
+                           void *stream);
+/* counts -> D = AᵀA - diag(colsum) -> float32 exactly as Go's repeated
+ * `+= 1.0` would hold it (min(n, 2^24)) -> normalizePrio -> * static
+ * (nullable).  raw_out (nullable, C*C uint32) receives D. */
+int syzcov_dev_prio_finish(const int32_t *counts, int C, const float *static_prios, float *out,
+                           uint32_t *raw_out, void *stream);
+int syzcov_dev_normalize_prio(float *prios, int C, void *stream);
+int syzcov_dev_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run,
+                            void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SYZCOV_H */

@@ -1,0 +1,118 @@
+"""ctypes binding of libsyzcov.so (include/syzcov.h).
+
+The product path has no CPU implementation: if the library is missing this
+module raises, and every compute entry point returns SYZCOV_ENODEV without a
+HIP device (raised as SyzcovError here)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsyzcov.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "syzcov.h")
+
+OK, EINVAL, ENOTSORTED, ENODEV, EHIP, ERANGE, ENOMEM, ETOOLONG = 0, -1, -2, -3, -4, -5, -6, -7
+_NAMES = {EINVAL: "EINVAL", ENOTSORTED: "ENOTSORTED", ENODEV: "ENODEV", EHIP: "EHIP",
+          ERANGE: "ERANGE", ENOMEM: "ENOMEM", ETOOLONG: "ETOOLONG"}
+
+
+class SyzcovError(RuntimeError):
+    def __init__(self, code: int, fn: str, msg: str):
+        self.code = code
+        super().__init__(f"{fn}: {_NAMES.get(code, code)} {msg}")
+
+
+def build(jobs: int = 8) -> str:
+    """Compile every HIP source for gfx950 into syzkaller_amd/libsyzcov.so."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+p_ = C.c_void_p
+sz = C.c_size_t
+u32, u64, i32, i64 = C.c_uint32, C.c_uint64, C.c_int32, C.c_int64
+
+# name: (restype, argtypes)
+_SIGS = {
+    "syzcov_version": (C.c_char_p, []),
+    "syzcov_last_error": (C.c_char_p, []),
+    "syzcov_restore_pc": (u64, [u32, u32]),
+    "syzcov_canonicalize": (i64, [p_, sz]),
+    "syzcov_difference": (i64, [p_, sz, p_, sz, p_]),
+    "syzcov_symmetric_difference": (i64, [p_, sz, p_, sz, p_]),
+    "syzcov_union": (i64, [p_, sz, p_, sz, p_]),
+    "syzcov_intersection": (i64, [p_, sz, p_, sz, p_]),
+    "syzcov_minimize": (i64, [p_, p_, sz, p_, C.c_int, p_]),
+    "syzcov_sort_order": (C.c_int, [p_, sz, C.c_int, p_]),
+    "syzcov_union_all": (i64, [p_, p_, sz, p_]),
+    "syzcov_calculate_priorities": (C.c_int, [p_, p_, sz, C.c_int, C.c_int, p_, p_, p_]),
+    "syzcov_normalize_prio": (C.c_int, [p_, C.c_int]),
+    "syzcov_build_choice_table": (C.c_int, [p_, p_, C.c_int, p_]),
+    "syzcov_state_create": (C.c_int, [C.c_int, u32, u64, p_]),
+    "syzcov_state_destroy": (C.c_int, [u64]),
+    "syzcov_state_add": (C.c_int, [u64, C.c_int, p_, sz]),
+    "syzcov_state_set_flakes": (C.c_int, [u64, p_, sz]),
+    "syzcov_state_get": (i64, [u64, C.c_int, p_, sz]),
+    "syzcov_newcov_batch": (i64, [u64, p_, p_, p_, sz, p_]),
+    # device tier
+    "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
+    "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
+    "syzcov_dev_mark": (C.c_int, [p_, p_, p_, sz, p_, u32, u64, p_, p_]),
+    "syzcov_dev_dict_ws_size": (sz, [u64]),
+    "syzcov_dev_dict_build": (C.c_int, [p_, u64, p_, p_, p_, p_]),
+    "syzcov_dev_dict_to_list": (C.c_int, [p_, u64, u32, p_, p_, p_]),
+    "syzcov_dev_minimize_pass1": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_]),
+    "syzcov_dev_minimize_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_, p_]),
+    "syzcov_dev_compact_ws_size": (sz, [sz]),
+    "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),
+    "syzcov_dev_sort_ws_size": (sz, [sz]),
+    "syzcov_dev_sort_order": (C.c_int, [p_, sz, C.c_int, p_, p_, sz, p_]),
+    "syzcov_dev_bytemap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),
+    "syzcov_dev_synth_lens": (C.c_int, [u64, u64, sz, u32, u32, p_, p_]),
+    "syzcov_dev_synth_pcs": (C.c_int, [u64, u64, sz, p_, u32, C.c_int, p_, p_]),
+    "syzcov_dev_prio_rows": (sz, [C.c_int]),
+    "syzcov_dev_prio_ldp": (sz, [sz]),
+    "syzcov_dev_prio_build_at": (C.c_int, [C.c_int, p_, p_, p_, sz, C.c_int, p_, sz, p_, p_]),
+    "syzcov_dev_prio_counts": (C.c_int, [p_, sz, sz, C.c_int, p_, p_]),
+    "syzcov_dev_prio_finish": (C.c_int, [p_, C.c_int, p_, p_, p_, p_]),
+    "syzcov_dev_normalize_prio": (C.c_int, [p_, C.c_int, p_]),
+    "syzcov_dev_choice_table": (C.c_int, [p_, p_, C.c_int, p_, p_]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libsyzcov.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built; run `make -C syzkaller_amd` "
+                              "(syzkaller_amd has no CPU fallback)")
+        # torch (if used) must own the HIP runtime first so both share one copy
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional for the C-ABI
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, fn: str) -> int:
+    if rc < 0:
+        raise SyzcovError(rc, fn, lib().syzcov_last_error().decode(errors="replace"))
+    return rc
+
+
+def header_symbols() -> list[str]:
+    import re
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(syzcov_[a-z0-9_]+)\(", txt)))

@@ -1,0 +1,519 @@
+// api.cc — drop-in host API of libsyzcov (include/syzcov.h tier 1).
+//
+// Each host thread owns a HIP stream and a grow-only device arena, so calls
+// are reentrant (the fuzzer's goroutines call cover ops concurrently under
+// coverMu.RLock: syz-fuzzer/fuzzer.go:383-386,458-478).  Every call stages its
+// host operands into the arena, runs the device kernels and copies the result
+// back; there is no host compute path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/syzcov.h"
+
+namespace syz {
+
+static thread_local char g_err[512];
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+size_t setop_ws_size(size_t ntot);
+int dev_setop(int op, const uint32_t *a, size_t na, const uint32_t *b, size_t nb, uint32_t *out,
+              uint32_t *n_out, uint32_t *err, void *ws, hipStream_t s);
+
+static inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+struct Ctx {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    void *arena = nullptr;
+    size_t cap = 0;
+    ~Ctx() {
+        if (arena) hipFree(arena);
+        if (s) hipStreamDestroy(s);
+    }
+};
+
+static thread_local Ctx *g_ctx[16];
+
+// Current device's per-thread context; nullptr + error if no device.
+static Ctx *ctx() {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device (libsyzcov has no CPU path)");
+        return nullptr;
+    }
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev < 0 || dev >= 16) return nullptr;
+    Ctx *c = g_ctx[dev];
+    if (!c) {
+        c = new Ctx();
+        c->dev = dev;
+        if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed");
+            delete c;
+            return nullptr;
+        }
+        g_ctx[dev] = c;
+    }
+    return c;
+}
+
+// Bump allocator over the arena: plan sizes first, then reserve once.
+struct Plan {
+    std::vector<size_t> sizes;
+    size_t add(size_t bytes) {
+        sizes.push_back(al(bytes ? bytes : 1));
+        return sizes.size() - 1;
+    }
+    size_t total() const {
+        size_t t = 0;
+        for (size_t s : sizes) t += s;
+        return t;
+    }
+};
+
+static int reserve(Ctx *c, const Plan &p, std::vector<uint8_t *> &ptrs) {
+    const size_t need = p.total();
+    if (need > c->cap) {
+        if (c->arena) {
+            hipStreamSynchronize(c->s);
+            hipFree(c->arena);
+        }
+        c->arena = nullptr;
+        c->cap = 0;
+        size_t cap = need + need / 4;
+        if (hipMalloc(&c->arena, cap) != hipSuccess) {
+            set_error("hipMalloc(%zu) failed", cap);
+            return SYZCOV_ENOMEM;
+        }
+        c->cap = cap;
+    }
+    ptrs.clear();
+    uint8_t *b = (uint8_t *)c->arena;
+    for (size_t s : p.sizes) {
+        ptrs.push_back(b);
+        b += s;
+    }
+    return 0;
+}
+
+#define CK(expr)                                                                         \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+            return SYZCOV_EHIP;                                                          \
+        }                                                                                \
+    } while (0)
+#define RC(expr)                  \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ < 0) return r_;    \
+    } while (0)
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+const char *syzcov_version(void) { return "syzcov 0.1 gfx950"; }
+const char *syzcov_last_error(void) { return g_err; }
+
+uint64_t syzcov_restore_pc(uint32_t pc, uint32_t base) {
+    return ((uint64_t)base << 32) + (uint64_t)pc;  // cover.go:23-25
+}
+
+int64_t syzcov_canonicalize(uint32_t *cov, size_t n) {
+    if (n == 0) return 0;
+    if (!cov) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_off = p.add(2 * 8), i_pcs = p.add(n * 4), i_len = p.add(4),
+           i_ws = p.add(syzcov_dev_canon_ws_size(1, n));
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    uint64_t hoff[2] = {0, n};
+    CK(hipMemcpyAsync(b[i_off], hoff, 16, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_pcs], cov, n * 4, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_canonicalize((uint64_t *)b[i_off], (uint32_t *)b[i_pcs], (uint32_t *)b[i_pcs],
+                               (uint32_t *)b[i_len], 1, n, nullptr, 0, 0, nullptr, b[i_ws],
+                               p.sizes[i_ws], c->s));
+    uint32_t nl = 0;
+    CK(hipMemcpyAsync(&nl, b[i_len], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (nl) {
+        CK(hipMemcpyAsync(cov, b[i_pcs], (size_t)nl * 4, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    return nl;
+}
+
+static int64_t setop(int op, const uint32_t *a, size_t na, const uint32_t *b_, size_t nb,
+                     uint32_t *out) {
+    if ((na && !a) || (nb && !b_) || !out) return SYZCOV_EINVAL;
+    if (na + nb == 0) return 0;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_a = p.add(na * 4), i_b = p.add(nb * 4), i_o = p.add((na + nb) * 4), i_n = p.add(8),
+           i_ws = p.add(setop_ws_size(na + nb));
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    uint32_t *dn = (uint32_t *)b[i_n], *derr = dn + 1;
+    CK(hipMemsetAsync(dn, 0, 8, c->s));
+    if (na) CK(hipMemcpyAsync(b[i_a], a, na * 4, hipMemcpyHostToDevice, c->s));
+    if (nb) CK(hipMemcpyAsync(b[i_b], b_, nb * 4, hipMemcpyHostToDevice, c->s));
+    RC(dev_setop(op, (uint32_t *)b[i_a], na, (uint32_t *)b[i_b], nb, (uint32_t *)b[i_o], dn, derr,
+                 b[i_ws], c->s));
+    uint32_t h[2];
+    CK(hipMemcpyAsync(h, dn, 8, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (h[1]) {
+        set_error("set-op operand is not sorted");
+        return SYZCOV_ENOTSORTED;
+    }
+    if (h[0]) {
+        CK(hipMemcpyAsync(out, b[i_o], (size_t)h[0] * 4, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    return h[0];
+}
+
+int64_t syzcov_difference(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                          uint32_t *out) {
+    return setop(0, a, na, b, nb, out);
+}
+int64_t syzcov_symmetric_difference(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                                    uint32_t *out) {
+    return setop(1, a, na, b, nb, out);
+}
+int64_t syzcov_union(const uint32_t *a, size_t na, const uint32_t *b, size_t nb, uint32_t *out) {
+    return setop(2, a, na, b, nb, out);
+}
+int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, size_t nb,
+                            uint32_t *out) {
+    return setop(3, a, na, b, nb, out);
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ corpus
+namespace syz {
+int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
+
+// Stage a CSR corpus and build its dense dictionary.  Fills device pointers.
+struct CorpusDev {
+    uint64_t *off;
+    uint32_t *pcs;
+    uint8_t *pres;
+    uint64_t *tab;
+    uint32_t pc_lo;
+    uint64_t span;
+    uint32_t n_ids;
+};
+
+static int stage_corpus(Ctx *c, const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                        CorpusDev &cd, std::vector<void *> &owned) {
+    const uint64_t base = offsets[0];
+    const uint64_t P = offsets[n] - base;
+    std::vector<uint64_t> hoff(n + 1);
+    for (size_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
+    void *d_off = nullptr, *d_pcs = nullptr;
+    if (hipMalloc(&d_off, (n + 1) * 8) != hipSuccess || hipMalloc(&d_pcs, P * 4 + 4) != hipSuccess)
+        return SYZCOV_ENOMEM;
+    owned.push_back(d_off);
+    owned.push_back(d_pcs);
+    CK(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->s));
+    if (P) CK(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, c->s));
+    cd.off = (uint64_t *)d_off;
+    cd.pcs = (uint32_t *)d_pcs;
+    // PC window from a device min/max reduction
+    void *d_mm = nullptr;
+    if (hipMalloc(&d_mm, 256) != hipSuccess) return SYZCOV_ENOMEM;
+    owned.push_back(d_mm);
+    uint32_t mm[2] = {0, 0};
+    if (P) {
+        RC(minmax_pcs(cd.pcs, P, (uint32_t *)d_mm, c->s));
+        CK(hipMemcpyAsync(mm, d_mm, 8, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    cd.pc_lo = mm[0];
+    cd.span = (uint64_t)mm[1] - mm[0] + 1;
+    void *d_pres = nullptr, *d_tab = nullptr, *d_ws = nullptr;
+    const uint64_t nwords = (cd.span + 31) / 32;
+    if (hipMalloc(&d_pres, al(cd.span)) != hipSuccess || hipMalloc(&d_tab, nwords * 8) != hipSuccess ||
+        hipMalloc(&d_ws, syzcov_dev_dict_ws_size(cd.span) + 256) != hipSuccess)
+        return SYZCOV_ENOMEM;
+    owned.push_back(d_pres);
+    owned.push_back(d_tab);
+    owned.push_back(d_ws);
+    cd.pres = (uint8_t *)d_pres;
+    cd.tab = (uint64_t *)d_tab;
+    uint32_t *d_err = (uint32_t *)d_mm + 4, *d_nids = (uint32_t *)d_mm + 8;
+    CK(hipMemsetAsync(d_pres, 0, al(cd.span), c->s));
+    CK(hipMemsetAsync(d_err, 0, 4, c->s));
+    RC(syzcov_dev_mark(cd.off, nullptr, cd.pcs, n, cd.pres, cd.pc_lo, cd.span, d_err, c->s));
+    RC(syzcov_dev_dict_build(cd.pres, cd.span, cd.tab, d_nids, d_ws, c->s));
+    uint32_t h[2];
+    CK(hipMemcpyAsync(h, d_err, 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipMemcpyAsync(h + 1, d_nids, 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (h[0]) {
+        set_error("internal: PC outside its own min/max window");
+        return SYZCOV_EHIP;
+    }
+    cd.n_ids = h[1];
+    return 0;
+}
+
+static void free_all(std::vector<void *> &v) {
+    for (void *p : v) hipFree(p);
+    v.clear();
+}
+}  // namespace syz
+
+extern "C" {
+
+int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order) {
+    if (n == 0) return 0;
+    if (!lens || !order) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_l = p.add(n * 8), i_o = p.add(n * 4), i_ws = p.add(syzcov_dev_sort_ws_size(n));
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_l], lens, n * 8, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_sort_order((int64_t *)b[i_l], n, sort_variant, (int32_t *)b[i_o], b[i_ws],
+                             p.sizes[i_ws], c->s));
+    CK(hipMemcpyAsync(order, b[i_o], n * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                        const int32_t *order, int sort_variant, int32_t *out_idx) {
+    if (n == 0) return 0;
+    if (!offsets || !out_idx || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
+    if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    std::vector<void *> owned;
+    CorpusDev cd;
+    int rc = stage_corpus(c, offsets, pcs, n, cd, owned);
+    if (rc) {
+        free_all(owned);
+        return rc;
+    }
+    Plan p;
+    size_t i_ord = p.add(n * 4), i_len = p.add(n * 8), i_first = p.add((size_t)cd.n_ids * 4 + 4),
+           i_cand = p.add(n), i_kept = p.add(n), i_out = p.add(n * 4), i_cnt = p.add(4),
+           i_ws = p.add(std::max(syzcov_dev_compact_ws_size(n), syzcov_dev_sort_ws_size(n)));
+    std::vector<uint8_t *> b;
+    rc = reserve(c, p, b);
+    if (rc) {
+        free_all(owned);
+        return rc;
+    }
+    int32_t *d_ord = (int32_t *)b[i_ord];
+    do {
+        if (order) {
+            for (size_t i = 0; i < n; i++)
+                if (order[i] < 0 || (size_t)order[i] >= n) {
+                    rc = SYZCOV_EINVAL;
+                    break;
+                }
+            if (rc) break;
+            if (hipMemcpyAsync(d_ord, order, n * 4, hipMemcpyHostToDevice, c->s) != hipSuccess) {
+                rc = SYZCOV_EHIP;
+                break;
+            }
+        } else {
+            std::vector<int64_t> lens(n);
+            for (size_t i = 0; i < n; i++) lens[i] = (int64_t)(offsets[i + 1] - offsets[i]);
+            if (hipMemcpyAsync(b[i_len], lens.data(), n * 8, hipMemcpyHostToDevice, c->s) !=
+                hipSuccess) {
+                rc = SYZCOV_EHIP;
+                break;
+            }
+            rc = syzcov_dev_sort_order((int64_t *)b[i_len], n, sort_variant, d_ord, b[i_ws],
+                                       p.sizes[i_ws], c->s);
+            if (rc) break;
+        }
+        hipMemsetD32Async((hipDeviceptr_t)b[i_first], 0x7FFFFFFF, cd.n_ids + 1, c->s);
+        hipMemsetAsync(b[i_kept], 0, n, c->s);
+        rc = syzcov_dev_minimize_pass1(cd.off, nullptr, cd.pcs, d_ord, nullptr, n, cd.tab, cd.pc_lo,
+                                       (int32_t *)b[i_first], b[i_cand], c->s);
+        if (rc) break;
+        rc = syzcov_dev_minimize_pass2(cd.off, nullptr, cd.pcs, d_ord, nullptr, n, cd.tab, cd.pc_lo,
+                                       (int32_t *)b[i_first], b[i_cand], b[i_kept], c->s);
+        if (rc) break;
+        rc = syzcov_dev_compact_kept(b[i_kept], d_ord, n, (int32_t *)b[i_out], (uint32_t *)b[i_cnt],
+                                     b[i_ws], c->s);
+        if (rc) break;
+        uint32_t k = 0;
+        if (hipMemcpyAsync(&k, b[i_cnt], 4, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+            hipStreamSynchronize(c->s) != hipSuccess) {
+            rc = SYZCOV_EHIP;
+            break;
+        }
+        if (k && (hipMemcpyAsync(out_idx, b[i_out], (size_t)k * 4, hipMemcpyDeviceToHost, c->s) !=
+                      hipSuccess ||
+                  hipStreamSynchronize(c->s) != hipSuccess)) {
+            rc = SYZCOV_EHIP;
+            break;
+        }
+        rc = (int)k;
+    } while (0);
+    hipStreamSynchronize(c->s);
+    free_all(owned);
+    return rc;
+}
+
+int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n, uint32_t *out) {
+    if (n == 0) return 0;
+    if (!offsets || !out) return SYZCOV_EINVAL;
+    if (offsets[n] == offsets[0]) return 0;
+    if (!pcs) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    std::vector<void *> owned;
+    CorpusDev cd;
+    int64_t rc = stage_corpus(c, offsets, pcs, n, cd, owned);
+    if (!rc) {
+        void *d_out = nullptr, *d_n = nullptr;
+        if (hipMalloc(&d_out, (size_t)cd.n_ids * 4 + 4) != hipSuccess ||
+            hipMalloc(&d_n, 256) != hipSuccess) {
+            rc = SYZCOV_ENOMEM;
+        } else {
+            owned.push_back(d_out);
+            owned.push_back(d_n);
+            rc = syzcov_dev_dict_to_list(cd.tab, cd.span, cd.pc_lo, (uint32_t *)d_out,
+                                         (uint32_t *)d_n, c->s);
+            uint32_t k = 0;
+            if (!rc && (hipMemcpyAsync(&k, d_n, 4, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+                        hipStreamSynchronize(c->s) != hipSuccess))
+                rc = SYZCOV_EHIP;
+            if (!rc && k &&
+                (hipMemcpyAsync(out, d_out, (size_t)k * 4, hipMemcpyDeviceToHost, c->s) !=
+                     hipSuccess ||
+                 hipStreamSynchronize(c->s) != hipSuccess))
+                rc = SYZCOV_EHIP;
+            if (!rc) rc = k;
+        }
+    }
+    hipStreamSynchronize(c->s);
+    free_all(owned);
+    return rc;
+}
+
+// ------------------------------------------------------------ priorities
+int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_ids, size_t nprog,
+                                int C, int key_mode, const float *static_prios, float *out,
+                                uint32_t *raw_counts) {
+    if (C <= 0 || !out || (nprog && !prog_off) || (key_mode != 0 && key_mode != 1))
+        return SYZCOV_EINVAL;
+    const uint64_t base = nprog ? prog_off[0] : 0;
+    const uint64_t ncalls = nprog ? prog_off[nprog] - base : 0;
+    if (key_mode == 1 && ncalls && !call_ids) return SYZCOV_EINVAL;
+    std::vector<int32_t> lens(nprog ? nprog : 1);
+    std::vector<uint64_t> hoff(nprog + 1);
+    for (size_t p = 0; p < nprog; p++) {
+        const uint64_t l = prog_off[p + 1] - prog_off[p];
+        if (key_mode == 0 && l > (uint64_t)C) {
+            set_error("program %zu has %llu calls > %d (prio.go:148 would panic)", p,
+                      (unsigned long long)l, C);
+            return SYZCOV_ETOOLONG;
+        }
+        if (l > 0x7FFFFFFF) return SYZCOV_EINVAL;
+        lens[p] = (int32_t)l;
+    }
+    for (size_t p = 0; p <= nprog; p++) hoff[p] = nprog ? prog_off[p] - base : 0;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    const size_t rows = syzcov_dev_prio_rows(C), ldp = syzcov_dev_prio_ldp(nprog ? nprog : 1);
+    Plan p;
+    size_t i_len = p.add(lens.size() * 4), i_off = p.add((nprog + 1) * 8),
+           i_ids = p.add(key_mode ? ncalls * 2 : 0), i_at = p.add(rows * ldp),
+           i_cnt = p.add(rows * rows * 4), i_st = p.add((size_t)C * C * 4),
+           i_out = p.add((size_t)C * C * 4), i_raw = p.add(raw_counts ? (size_t)C * C * 4 : 0),
+           i_err = p.add(4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemsetAsync(b[i_err], 0, 4, c->s));
+    CK(hipMemcpyAsync(b[i_len], lens.data(), lens.size() * 4, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_off], hoff.data(), (nprog + 1) * 8, hipMemcpyHostToDevice, c->s));
+    if (key_mode && ncalls)
+        CK(hipMemcpyAsync(b[i_ids], call_ids + base, ncalls * 2, hipMemcpyHostToDevice, c->s));
+    if (static_prios)
+        CK(hipMemcpyAsync(b[i_st], static_prios, (size_t)C * C * 4, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_prio_build_at(key_mode, (int32_t *)b[i_len], (uint64_t *)b[i_off],
+                                (uint16_t *)b[i_ids], nprog, C, (int8_t *)b[i_at], ldp,
+                                (uint32_t *)b[i_err], c->s));
+    CK(hipMemsetAsync(b[i_cnt], 0, rows * rows * 4, c->s));
+    RC(syzcov_dev_prio_counts((int8_t *)b[i_at], ldp, nprog, C, (int32_t *)b[i_cnt], c->s));
+    RC(syzcov_dev_prio_finish((int32_t *)b[i_cnt], C, static_prios ? (float *)b[i_st] : nullptr,
+                              (float *)b[i_out], raw_counts ? (uint32_t *)b[i_raw] : nullptr,
+                              c->s));
+    uint32_t herr = 0;
+    CK(hipMemcpyAsync(&herr, b[i_err], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipMemcpyAsync(out, b[i_out], (size_t)C * C * 4, hipMemcpyDeviceToHost, c->s));
+    if (raw_counts)
+        CK(hipMemcpyAsync(raw_counts, b[i_raw], (size_t)C * C * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (herr) {
+        set_error("call id >= C");
+        return SYZCOV_EINVAL;
+    }
+    return 0;
+}
+
+int syzcov_normalize_prio(float *prios, int C) {
+    if (C <= 0 || !prios) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_p = p.add((size_t)C * C * 4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_p], prios, (size_t)C * C * 4, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_normalize_prio((float *)b[i_p], C, c->s));
+    CK(hipMemcpyAsync(prios, b[i_p], (size_t)C * C * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+int syzcov_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run) {
+    if (C <= 0 || !prios || !run) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_p = p.add((size_t)C * C * 4), i_e = p.add(C), i_r = p.add((size_t)C * C * 8);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_p], prios, (size_t)C * C * 4, hipMemcpyHostToDevice, c->s));
+    if (enabled) CK(hipMemcpyAsync(b[i_e], enabled, C, hipMemcpyHostToDevice, c->s));
+    // disabled rows keep the caller's contents (nil rows in Go)
+    CK(hipMemcpyAsync(b[i_r], run, (size_t)C * C * 8, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_choice_table((float *)b[i_p], enabled ? b[i_e] : nullptr, C, (int64_t *)b[i_r],
+                               c->s));
+    CK(hipMemcpyAsync(run, b[i_r], (size_t)C * C * 8, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
+}  // extern "C"

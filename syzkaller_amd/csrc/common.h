@@ -1,0 +1,105 @@
+// common.h — shared device/host helpers for the syzcov HIP kernels (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/syzcov.h"
+
+#define SYZ_SENT 0xFFFFFFFFu
+#define SYZ_WAVE 64
+
+namespace syz {
+
+void set_error(const char *fmt, ...);
+
+#define SYZ_HIP(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::syz::set_error("%s:%d %s: %s", __FILE__, __LINE__, #expr,                \
+                             hipGetErrorString(e_));                                   \
+            return SYZCOV_EHIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+#define SYZ_LAUNCH_CHECK()                                                             \
+    do {                                                                               \
+        hipError_t e_ = hipGetLastError();                                             \
+        if (e_ != hipSuccess) {                                                        \
+            ::syz::set_error("%s:%d launch: %s", __FILE__, __LINE__,                   \
+                             hipGetErrorString(e_));                                   \
+            return SYZCOV_EHIP;                                                        \
+        }                                                                              \
+    } while (0)
+
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+static inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 16) {
+    size_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- device side
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-wide inclusive scan of a u32 (64 lanes) via DPP-lowered shuffles.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t l = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Block-wide exclusive scan; `tmp` is LDS with >= blockDim/64 + 1 entries.
+// Returns the exclusive prefix of v; *total receives the block total.
+template <int THREADS>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tmp, uint32_t *total) {
+    constexpr int NW = THREADS / 64;
+    const uint32_t w = threadIdx.x >> 6, l = __lane_id();
+    uint32_t inc = wave_incl_scan(v);
+    if (l == 63) tmp[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t s = (l < NW) ? tmp[l] : 0u;
+        uint32_t si = wave_incl_scan(s);
+        if (l < NW) tmp[l] = si - s;
+        if (l == NW - 1) tmp[NW] = si;
+    }
+    __syncthreads();
+    uint32_t res = tmp[w] + inc - v;
+    *total = tmp[NW];
+    __syncthreads();
+    return res;
+}
+
+// 64-bit splitmix (synthetic generator; identical to oracle/synth_oracle.c).
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Dense PC-id lookup: tab[w] = prefix(lo 32) | bits(hi 32).
+__device__ __forceinline__ uint32_t dense_id(const uint64_t *__restrict__ tab, uint32_t pc,
+                                             uint32_t pc_lo) {
+    uint32_t off = pc - pc_lo;
+    uint64_t e = tab[off >> 5];
+    uint32_t bits = (uint32_t)(e >> 32);
+    uint32_t mask = (1u << (off & 31)) - 1u;
+    return (uint32_t)e + __popc(bits & mask);
+}
+
+}  // namespace syz

@@ -1,0 +1,375 @@
+// prio.hip — prog.CalculatePriorities' dynamic part (prog/prio.go:137-154),
+// normalizePrio (:158-192), the static combine (:29-38) and BuildChoiceTable
+// (:202-228) on gfx950.
+//
+// Raw co-occurrence counts are the dense contraction D = AᵀA - diag(colsum A)
+// over a prog x key matrix A, on i8 MFMA (v_mfma_i32_32x32x32_i8) with i32
+// accumulation, so the counts are exact:
+//   key mode 0 (reference-exact): the reference indexes prios by call
+//     POSITION (prio.go:142-150 never reads Meta.ID), so A[p][k] = [k < len(p)];
+//   key mode 1: A[p][c] = number of calls with syscall id c in program p.
+// A is stored key-major (AT[key][program], program stride ldp, zero padded)
+// so an MFMA fragment — 16 consecutive programs of one key — is one 16-byte
+// LDS read.  An all-ones key row at index C makes the GEMM also produce
+// colsum(A) = D[i][C] for the diagonal correction.  Only tiles with I <= J are
+// computed (D is symmetric) and mirrored; K (programs) is split across
+// workgroups with exact int32 atomics in the epilogue.
+//
+// Counts convert to float32 as Go's repeated `+= 1.0` does: exact up to 2^24,
+// then stuck at 2^24 (round-to-even), i.e. min(n, 16777216).  All float
+// arithmetic uses explicit round-to-nearest intrinsics: no FMA contraction.
+#include "common.h"
+
+#include <algorithm>
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+namespace syz {
+
+constexpr int PT = 128;  // output tile (keys) per workgroup
+constexpr int PK = 64;   // programs per K-step
+
+__host__ __device__ inline size_t prio_rows(int C) { return ((size_t)C + 1 + PT - 1) / PT * PT; }
+__host__ __device__ inline size_t prio_ldp(size_t nprog) { return (nprog + PK - 1) / PK * PK; }
+
+// ---------------------------------------------------------------- A builders
+// positional: AT[c][p] = (c < len[p]) for c < C, AT[C][p] = (p < nprog)
+__global__ void prio_build_pos_kernel(const int32_t *__restrict__ lens, size_t nprog, int C,
+                                      size_t rows, size_t ldp, int8_t *__restrict__ at) {
+    const size_t nvec = rows * (ldp / 16);
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
+         v += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = v / (ldp / 16);
+        const size_t p0 = (v % (ldp / 16)) * 16;
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const size_t p = p0 + j;
+            uint32_t bit = 0;
+            if (p < nprog) {
+                if ((int)r < C)
+                    bit = (int32_t)r < lens[p];
+                else if ((int)r == C)
+                    bit = 1;
+            }
+            w[j >> 2] |= bit << (8 * (j & 3));
+        }
+        ((uint4 *)at)[v] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// by id: AT[cid][p] += 1 per call (byte counts in 32-bit atomics; <= 127
+// per program is checked by the host wrapper's caller contract)
+__global__ void prio_build_id_kernel(const uint64_t *__restrict__ prog_off,
+                                     const uint16_t *__restrict__ ids, size_t nprog, int C,
+                                     size_t ldp, int8_t *__restrict__ at,
+                                     uint32_t *__restrict__ err) {
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < nprog;
+         p += (size_t)gridDim.x * blockDim.x) {
+        for (uint64_t q = prog_off[p]; q < prog_off[p + 1]; q++) {
+            const uint32_t c = ids[q];
+            if ((int)c >= C) {
+                *err = 1u;
+                continue;
+            }
+            const size_t byte = c * ldp + p;
+            atomicAdd((unsigned int *)(at + (byte & ~(size_t)3)), 1u << (8 * (byte & 3)));
+        }
+        const size_t byte = (size_t)C * ldp + p;  // ones row
+        atomicAdd((unsigned int *)(at + (byte & ~(size_t)3)), 1u << (8 * (byte & 3)));
+    }
+}
+
+// ------------------------------------------------------------- MFMA AᵀA
+// LDS image: [128 keys][64 programs] bytes, 16-B chunk index XOR-swizzled by
+// (row >> 2) & 3 so a ds_read_b128 lane group hits distinct bank slots.
+__device__ __forceinline__ uint32_t lds_off(uint32_t row, uint32_t chunk) {
+    return row * PK + ((chunk ^ ((row >> 2) & 3u)) << 4);
+}
+
+__global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict__ at, size_t ldp,
+                                                        size_t kchunk, int ntile_dim,
+                                                        int ntiles, int32_t *__restrict__ counts,
+                                                        size_t rows) {
+    __shared__ __attribute__((aligned(16))) int8_t As[PT * PK];
+    __shared__ __attribute__((aligned(16))) int8_t Bs[PT * PK];
+    const int tile = blockIdx.x % ntiles;
+    const size_t split = blockIdx.x / ntiles;
+    // tile -> (I, J) with I <= J, row-major over the upper triangle
+    int I = 0, rem = tile;
+    while (rem >= ntile_dim - I) {
+        rem -= ntile_dim - I;
+        I++;
+    }
+    const int J = I + rem;
+    const bool diag = I == J;
+    const size_t i0 = (size_t)I * PT, j0 = (size_t)J * PT;
+    const size_t kb0 = split * kchunk, kb1 = std::min(kb0 + kchunk, ldp);
+    const uint32_t t = threadIdx.x, l = __lane_id(), w = t >> 6;
+    const uint32_t wr = w >> 1, wc = w & 1;
+    v16i acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0;
+
+    for (size_t kb = kb0; kb < kb1; kb += PK) {
+        // stage: 128 rows x 4 chunks = 512 chunks per operand, 2 per thread
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const uint32_t q = t + 256u * s;
+            const uint32_t row = q >> 2, ch = q & 3u;
+            const uint4 va = *(const uint4 *)(at + (i0 + row) * ldp + kb + ch * 16);
+            *(uint4 *)(As + lds_off(row, ch)) = va;
+            if (!diag) {
+                const uint4 vb = *(const uint4 *)(at + (j0 + row) * ldp + kb + ch * 16);
+                *(uint4 *)(Bs + lds_off(row, ch)) = vb;
+            }
+        }
+        __syncthreads();
+        const int8_t *Bsrc = diag ? As : Bs;
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+            const uint32_t ch = ks * 2 + (l >> 5);
+            v4i fa[2], fb[2];
+#pragma unroll
+            for (int mi = 0; mi < 2; mi++) {
+                const uint32_t row = wr * 64 + mi * 32 + (l & 31);
+                fa[mi] = *(const v4i *)(As + lds_off(row, ch));
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++) {
+                const uint32_t row = wc * 64 + ni * 32 + (l & 31);
+                fb[ni] = *(const v4i *)(Bsrc + lds_off(row, ch));
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+                for (int ni = 0; ni < 2; ni++)
+                    acc[mi][ni] =
+                        __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+        for (int ni = 0; ni < 2; ni++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int32_t v = acc[mi][ni][r];
+                if (!v) continue;
+                const size_t row = i0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+                const size_t col = j0 + wc * 64 + ni * 32 + (l & 31);
+                atomicAdd(&counts[row * rows + col], v);
+                if (!diag) atomicAdd(&counts[col * rows + row], v);
+            }
+}
+
+// ---------------------------------------------------- finish: float + normalize
+// counts -> float32 per Go's `+= 1.0` accumulation, diagonal corrected,
+// then normalizePrio per row, then * static.  One workgroup per row.
+__device__ __forceinline__ float go_f32_count(int64_t n) {
+    return n >= 16777216 ? 16777216.0f : (float)n;
+}
+
+template <int THREADS>
+__device__ __forceinline__ void row_stats(const float *__restrict__ row, int C, float *mx,
+                                          float *mn, int *nz, float *red) {
+    float lmax = 0.0f, lmin = 1e10f;
+    int lz = 0;
+    for (int i = threadIdx.x; i < C; i += THREADS) {
+        const float p = row[i];
+        lmax = fmaxf(lmax, p);
+        if (p != 0.0f) lmin = fminf(lmin, p);
+        lz += p == 0.0f;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        lmax = fmaxf(lmax, __shfl_xor(lmax, d, 64));
+        lmin = fminf(lmin, __shfl_xor(lmin, d, 64));
+        lz += __shfl_xor(lz, d, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if (__lane_id() == 0) {
+        red[w] = lmax;
+        red[THREADS / 64 + w] = lmin;
+        ((int *)red)[2 * THREADS / 64 + w] = lz;
+    }
+    __syncthreads();
+    float m0 = 0.0f, m1 = 1e10f;
+    int z = 0;
+    for (int q = 0; q < THREADS / 64; q++) {
+        m0 = fmaxf(m0, red[q]);
+        m1 = fminf(m1, red[THREADS / 64 + q]);
+        z += ((int *)red)[2 * THREADS / 64 + q];
+    }
+    __syncthreads();
+    *mx = m0;
+    *mn = m1;
+    *nz = z;
+}
+
+// prio.go:158-192 on one row (row in LDS or global), exact float32.
+template <int THREADS>
+__device__ __forceinline__ void normalize_row(float *__restrict__ row, int C, float *red) {
+    float mx, mn;
+    int nz;
+    row_stats<THREADS>(row, C, &mx, &mn, &nz, red);
+    if (nz != 0) mn = __fdiv_rn(mn, __fmul_rn(2.0f, (float)nz));
+    const float den = __fsub_rn(mx, mn);
+    for (int i = threadIdx.x; i < C; i += THREADS) {
+        float p = row[i];
+        if (mx == 0.0f) {
+            row[i] = 1.0f;
+            continue;
+        }
+        if (p == 0.0f) p = mn;
+        p = __fadd_rn(__fmul_rn(__fdiv_rn(__fsub_rn(p, mn), den), 0.9f), 0.1f);
+        if (p > 1.0f) p = 1.0f;
+        row[i] = p;
+    }
+    __syncthreads();
+}
+
+constexpr int FIN_THREADS = 256;
+
+__global__ __launch_bounds__(FIN_THREADS) void prio_finish_kernel(
+    const int32_t *__restrict__ counts, size_t rows, int C, const float *__restrict__ st,
+    float *__restrict__ out, uint32_t *__restrict__ raw) {
+    extern __shared__ float rowbuf[];
+    __shared__ float red[3 * FIN_THREADS / 64];
+    const int i = blockIdx.x;
+    const int32_t *crow = counts + (size_t)i * rows;
+    const int64_t colsum = crow[C];
+    for (int j = threadIdx.x; j < C; j += FIN_THREADS) {
+        int64_t n = crow[j];
+        if (j == i) n -= colsum;  // D = AᵀA - diag(colsum A)
+        if (raw) raw[(size_t)i * C + j] = (uint32_t)n;
+        rowbuf[j] = go_f32_count(n);
+    }
+    __syncthreads();
+    normalize_row<FIN_THREADS>(rowbuf, C, red);
+    for (int j = threadIdx.x; j < C; j += FIN_THREADS) {
+        float p = rowbuf[j];
+        if (st) p = __fmul_rn(p, st[(size_t)i * C + j]);  // prio.go:34 dynamic[i][j] *= p
+        out[(size_t)i * C + j] = p;
+    }
+}
+
+__global__ __launch_bounds__(FIN_THREADS) void prio_normalize_kernel(float *__restrict__ prios,
+                                                                     int C) {
+    __shared__ float red[3 * FIN_THREADS / 64];
+    normalize_row<FIN_THREADS>(prios + (size_t)blockIdx.x * C, C, red);
+}
+
+// prio.go:202-228: run[i][j] = sum_{j' <= j, enabled[j']} int(prios[i][j'] * 1000)
+__global__ __launch_bounds__(FIN_THREADS) void choice_table_kernel(
+    const float *__restrict__ prios, const uint8_t *__restrict__ enabled, int C,
+    int64_t *__restrict__ run) {
+    __shared__ int64_t wsum[FIN_THREADS / 64 + 1];
+    const int i = blockIdx.x;
+    if (enabled && !enabled[i]) return;  // nil row
+    int64_t carry = 0;
+    for (int c0 = 0; c0 < C; c0 += FIN_THREADS) {
+        const int j = c0 + threadIdx.x;
+        int64_t v = 0;
+        if (j < C && (!enabled || enabled[j]))
+            v = (int64_t)__fmul_rn(prios[(size_t)i * C + j], 1000.0f);  // truncation, as Go int()
+        // block inclusive scan (int64)
+        int64_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            int64_t y = __shfl_up(x, d, 64);
+            if ((int)__lane_id() >= d) x += y;
+        }
+        const int w = threadIdx.x >> 6;
+        if (__lane_id() == 63) wsum[w] = x;
+        __syncthreads();
+        int64_t pre = 0;
+        for (int q = 0; q < w; q++) pre += wsum[q];
+        int64_t tot = 0;
+        for (int q = 0; q < FIN_THREADS / 64; q++) tot += wsum[q];
+        if (j < C) run[(size_t)i * C + j] = carry + pre + x;
+        carry += tot;
+        __syncthreads();
+    }
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" size_t syzcov_dev_prio_rows(int C) { return prio_rows(C); }
+extern "C" size_t syzcov_dev_prio_ldp(size_t nprog) { return prio_ldp(nprog); }
+
+extern "C" int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens,
+                                        const uint64_t *prog_off, const uint16_t *call_ids,
+                                        size_t nprog, int C, int8_t *at, size_t ldp,
+                                        uint32_t *err_flag, void *stream) {
+    if (C <= 0 || !at || ldp % PK || ldp < nprog) return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t rows = prio_rows(C);
+    if (key_mode == 0) {
+        if (nprog && !lens) return SYZCOV_EINVAL;
+        const size_t nvec = rows * (ldp / 16);
+        hipLaunchKernelGGL(prio_build_pos_kernel, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
+                           s, lens, nprog, C, rows, ldp, at);
+        SYZ_LAUNCH_CHECK();
+        return 0;
+    }
+    if (key_mode != 1 || (nprog && (!prog_off || !call_ids || !err_flag))) return SYZCOV_EINVAL;
+    SYZ_HIP(hipMemsetAsync(at, 0, rows * ldp, s));
+    if (nprog) {
+        hipLaunchKernelGGL(prio_build_id_kernel, dim3(grid_for(nprog, 256, 8192)), dim3(256), 0, s,
+                           prog_off, call_ids, nprog, C, ldp, at, err_flag);
+        SYZ_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+extern "C" int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog, int C,
+                                      int32_t *counts, void *stream) {
+    if (C <= 0 || !at || !counts || ldp % PK || ldp < nprog) return SYZCOV_EINVAL;
+    if (nprog == 0) return 0;
+    const size_t rows = prio_rows(C);
+    const int nt = (int)(rows / PT);
+    const int ntiles = nt * (nt + 1) / 2;
+    // K split: enough workgroups to fill the chip ~3x over
+    size_t nk = ldp / PK;
+    size_t splits = std::max<size_t>(1, std::min<size_t>(nk, (768 + ntiles - 1) / ntiles));
+    size_t kchunk = (nk + splits - 1) / splits * PK;
+    splits = (ldp + kchunk - 1) / kchunk;
+    hipLaunchKernelGGL(prio_gemm_kernel, dim3((unsigned)(ntiles * splits)), dim3(256), 0,
+                       (hipStream_t)stream, at, ldp, kchunk, nt, ntiles, counts, rows);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_prio_finish(const int32_t *counts, int C, const float *static_prios,
+                                      float *out, uint32_t *raw_out, void *stream) {
+    if (C <= 0 || !counts || !out) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(prio_finish_kernel, dim3(C), dim3(FIN_THREADS), C * sizeof(float),
+                       (hipStream_t)stream, counts, prio_rows(C), C, static_prios, out, raw_out);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_normalize_prio(float *prios, int C, void *stream) {
+    if (C <= 0 || !prios) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(prio_normalize_kernel, dim3(C), dim3(FIN_THREADS), 0, (hipStream_t)stream,
+                       prios, C);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_choice_table(const float *prios, const uint8_t *enabled, int C,
+                                       int64_t *run, void *stream) {
+    if (C <= 0 || !prios || !run) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(choice_table_kernel, dim3(C), dim3(FIN_THREADS), 0, (hipStream_t)stream,
+                       prios, enabled, C, run);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}

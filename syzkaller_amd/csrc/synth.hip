@@ -1,0 +1,78 @@
+// synth.hip — counter-based synthetic corpus generator, written
+// directly into HBM.  Integer-exact, so the CPU twin (oracle/synth_oracle.c)
+// regenerates bit-identical inputs for parity checks and the CPU baseline
+// without shipping tens of GB.
+#include "common.h"
+
+namespace syz {
+
+__device__ __forceinline__ uint32_t synth_universe(uint64_t seed, uint32_t k) {
+    const uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)k);
+    return 0x81000000u + 16u * k + (uint32_t)(h & 15u);
+}
+
+__global__ void synth_lens_kernel(uint64_t seed, uint64_t first, uint64_t n, uint32_t mean,
+                                  uint32_t sigma, uint32_t *__restrict__ lens) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t base = splitmix64(seed ^ splitmix64((first + i) ^ 0x5851F42D4C957F2Dull));
+        int64_t sum = 0;
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+            const uint64_t h = splitmix64(base + (uint64_t)(t + 1) * 0x9E3779B97F4A7C15ull);
+            sum += (int64_t)(h & 0xFFFF) + (int64_t)((h >> 16) & 0xFFFF) +
+                   (int64_t)((h >> 32) & 0xFFFF) + (int64_t)(h >> 48);
+        }
+        const int64_t num = (int64_t)sigma * (sum - 6 * 65536) + 32768;
+        const int64_t off = num >= 0 ? num / 65536 : -((-num + 65535) / 65536);
+        int64_t L = (int64_t)mean + off;
+        L = L < 1 ? 1 : (L > 65535 ? 65535 : L);
+        lens[i] = (uint32_t)L;
+    }
+}
+
+__global__ void synth_pcs_kernel(uint64_t seed, uint64_t first, uint64_t n,
+                                 const uint64_t *__restrict__ off, uint32_t log2_space,
+                                 int uniform, uint32_t *__restrict__ pcs) {
+    for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint64_t base = splitmix64(seed ^ splitmix64((first + i) + 0x632BE59BD9B4E019ull));
+        const uint64_t b = off[i], len = off[i + 1] - b;
+        for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
+            const uint64_t h = splitmix64(base + (j + 1) * 0x9E3779B97F4A7C15ull);
+            uint32_t k;
+            if (uniform) {
+                k = (uint32_t)(h >> (64 - log2_space));
+            } else {
+                const uint64_t x = h >> 43;
+                k = (uint32_t)((x * x * x) >> (63 - log2_space));
+            }
+            pcs[b + j] = synth_universe(seed, k);
+        }
+    }
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean,
+                                     uint32_t sigma, uint32_t *lens, void *stream) {
+    if (n == 0) return 0;
+    if (!lens) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(synth_lens_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, seed, first, (uint64_t)n, mean, sigma, lens);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
+                                    uint32_t log2_space, int uniform, uint32_t *pcs,
+                                    void *stream) {
+    if (n == 0) return 0;
+    if (!off || !pcs || log2_space < 1 || log2_space > 26) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(synth_pcs_kernel, dim3(grid_for(n, 1, 16384)), dim3(256), 0,
+                       (hipStream_t)stream, seed, first, (uint64_t)n, off, log2_space, uniform,
+                       pcs);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}

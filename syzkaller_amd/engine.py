@@ -1,0 +1,194 @@
+"""Device-resident corpus engine: the manager-side hot path of syzkaller on
+one MI355X (or one shard of a multi-GPU node).
+
+One `step()` is the C2 workload of BASELINE.json on a raw corpus already in
+HBM (CSR: offsets u64[n+1], raw KCOV PCs u32):
+
+    Canonicalize    every input (cover.go:27-40), fused with presence marking
+    dictionary      dense PC ids over the PC window (the corpus union)
+    order           Go sort.Sort(minInputArray) over canonical lengths
+    Minimize        first-cover pass 1 / pass 2 / ordered compaction (cover.go:104-131)
+    Union           sorted union list of the corpus (the `Union(total, cov)` fold)
+    maxCover merge  resident maxCover |= union (manager.go:606-610 / fuzzer.go:470)
+
+torch supplies device memory, the stream and torch.distributed (RCCL);
+every computation is a libsyzcov HIP kernel launched on torch's current
+stream.  With a `shard` (engine.dist.Shard) the same step runs one rank of
+the sharded corpus and merges with RCCL: presence (uint8 MAX), first-cover
+(int32 MIN), kept flags (uint8 MAX).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from ._lib import check, lib
+
+INT32_MAX = 0x7FFFFFFF
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _u32(n, dev):
+    return torch.empty(n, dtype=torch.int32, device=dev)  # reinterpreted as uint32 by kernels
+
+
+@dataclass
+class StepResult:
+    kept_idx: torch.Tensor      # int32 [n_kept] original input indices, processing order
+    n_kept: int
+    union: torch.Tensor         # int32-viewed uint32 [n_union] sorted PCs
+    n_union: int
+    n_ids: int                  # distinct PCs in the corpus (incl. a 0xFFFFFFFF sentinel)
+    max_cover: int              # |maxCover| after the merge
+
+
+class CorpusEngine:
+    """Buffers sized for up to `n_max` inputs / `p_max` PCs over the PC window
+    [pc_lo, pc_lo + pc_span)."""
+
+    def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
+                 device="cuda", n_global: int | None = None, sort_variant: int = 0):
+        L = lib()
+        dev = torch.device(device)
+        self.dev, self.L = dev, L
+        self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
+        self.pc_lo, self.span = pc_lo, pc_span
+        self.sort_variant = sort_variant
+        self.n_global = n_global or n_max
+        nwords = (pc_span + 31) // 32
+        span16 = (pc_span + 15) // 16 * 16
+        self.canon = _u32(p_max + 1, dev)
+        self.new_len = _u32(n_max + 1, dev)
+        self.pres = torch.zeros(span16, dtype=torch.uint8, device=dev)
+        self.max_cover = torch.zeros(span16, dtype=torch.uint8, device=dev)
+        self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
+        ids_cap = min(pc_span, p_max) + 1
+        self.first = torch.empty(ids_cap, dtype=torch.int32, device=dev)
+        self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
+        self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
+        self.lens64 = torch.empty(self.n_global + 1, dtype=torch.int64, device=dev)
+        self.order = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
+        self.out_idx = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
+        self.union = _u32(ids_cap, dev)
+        self.scal = torch.zeros(16, dtype=torch.int64, device=dev)  # err, n_ids, n_kept, ...
+        ws = max(L.syzcov_dev_canon_ws_size(n_max, max_seg_len),
+                 L.syzcov_dev_dict_ws_size(pc_span),
+                 L.syzcov_dev_compact_ws_size(self.n_global),
+                 L.syzcov_dev_sort_ws_size(self.n_global))
+        self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+        self.ws_size = ws
+
+    # ---------------------------------------------------------------- phases
+    def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+        L, s = self.L, _stream()
+        self.pres.zero_()
+        self.scal.zero_()
+        check(L.syzcov_dev_canonicalize(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
+                                        self.max_seg, _p(self.pres), self.pc_lo, self.span,
+                                        _p(self.scal), _p(self.ws), self.ws_size, s),
+              "dev_canonicalize")
+
+    def build_dict(self):
+        L = self.L
+        nids = self.scal[1:2]
+        check(L.syzcov_dev_dict_build(_p(self.pres), self.span, _p(self.tab), _p(nids),
+                                      _p(self.ws), _stream()), "dev_dict_build")
+
+    def sort_order(self, lens32: torch.Tensor, n: int):
+        """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
+        self.lens64[:n].copy_(lens32[:n].to(torch.int64))
+        check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
+                                           _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
+
+    def minimize(self, off, n, order, ranks=None, n_items=None):
+        """Pass 1 + pass 2 over n_items work items (item j: input order[j],
+        rank ranks[j] or j); leaves kept[] indexed by rank."""
+        L, s = self.L, _stream()
+        n_items = n if n_items is None else n_items
+        self.first.fill_(INT32_MAX)
+        self.kept.zero_()
+        check(L.syzcov_dev_minimize_pass1(_p(off), _p(self.new_len), _p(self.canon), _p(order),
+                                          _p(ranks), n_items, _p(self.tab), self.pc_lo,
+                                          _p(self.first), _p(self.cand), s), "dev_minimize_pass1")
+        return n_items
+
+    def minimize_pass2(self, off, order, ranks, n_items):
+        check(self.L.syzcov_dev_minimize_pass2(
+            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items,
+            _p(self.tab), self.pc_lo, _p(self.first), _p(self.cand), _p(self.kept), _stream()),
+            "dev_minimize_pass2")
+
+    def compact(self, n_ranks: int):
+        n_kept = self.scal[2:3]
+        check(self.L.syzcov_dev_compact_kept(_p(self.kept), _p(self.order), n_ranks,
+                                             _p(self.out_idx), _p(n_kept), _p(self.ws),
+                                             _stream()), "dev_compact_kept")
+
+    def union_list(self):
+        check(self.L.syzcov_dev_dict_to_list(_p(self.tab), self.span, self.pc_lo, _p(self.union),
+                                             _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
+
+    def merge_max_cover(self):
+        check(self.L.syzcov_dev_bytemap_op(0, _p(self.max_cover), _p(self.pres),
+                                           self.pres.numel(), _p(self.scal[4:5]), _stream()),
+              "dev_bytemap_op")
+
+    # ------------------------------------------------------------------ step
+    def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True):
+        self.canonicalize(off, raw, n)
+        self.build_dict()
+        self.sort_order(self.new_len, n)
+        self.minimize(off, n, self.order)
+        self.minimize_pass2(off, self.order, None, n)
+        self.compact(n)
+        self.union_list()
+        self.merge_max_cover()
+        if sync:
+            return self.result()
+        return None
+
+    def result(self) -> StepResult:
+        sc = self.scal.cpu().tolist()
+        if sc[0] & 0xFFFFFFFF:
+            raise RuntimeError("a PC fell outside the engine's PC window")
+        n_ids, n_kept, n_union, mc = (int(x) & 0xFFFFFFFF for x in sc[1:5])
+        return StepResult(self.out_idx[:n_kept], n_kept, self.union[:n_union], n_union, n_ids,
+                          int(sc[4]))
+
+    def check_error(self):
+        if int(self.scal[0].item()) & 0xFFFFFFFF:
+            raise RuntimeError("a PC fell outside the engine's PC window")
+
+
+def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int = 512,
+                 log2_space: int = 22, uniform: bool = False, device="cuda"):
+    """Generate a raw synthetic corpus directly in HBM (counter-based, so the
+    CPU twin in oracle/ reproduces it bit-for-bit)."""
+    L = lib()
+    dev = torch.device(device)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    s = _stream()
+    check(L.syzcov_dev_synth_lens(seed, first, n, mean, sigma, _p(lens), s), "synth_lens")
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens.to(torch.int64), 0, out=off[1:])
+    total = int(off[-1].item())
+    pcs = torch.empty(total + 1, dtype=torch.int32, device=dev)
+    check(L.syzcov_dev_synth_pcs(seed, first, n, _p(off), log2_space, int(uniform), _p(pcs), s),
+          "synth_pcs")
+    return off, pcs, lens, total
+
+
+SYNTH_PC_LO = 0x81000000
+
+
+def synth_window(log2_space: int = 22):
+    return SYNTH_PC_LO, 16 << log2_space

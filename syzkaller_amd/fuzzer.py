@@ -1,0 +1,67 @@
+"""Resident fuzzer-side coverage state: per-CallID maxCover + flakes on the
+GPU, and the batched new-coverage check of syz-fuzzer execute()
+(syz-fuzzer/fuzzer.go:456-480)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class CoverState:
+    def __init__(self, ncalls: int, pc_lo: int = 0, pc_span: int = 1 << 32):
+        h = C.c_uint64(0)
+        check(lib().syzcov_state_create(ncalls, pc_lo, pc_span, C.byref(h)), "state_create")
+        self.h = h.value
+        self.ncalls = ncalls
+
+    def close(self):
+        if self.h:
+            lib().syzcov_state_destroy(self.h)
+            self.h = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, call: int, pcs):
+        a = np.ascontiguousarray(pcs, dtype=np.uint32)
+        check(lib().syzcov_state_add(self.h, call, _ptr(a), a.size), "state_add")
+
+    def set_flakes(self, pcs):
+        a = np.ascontiguousarray(pcs, dtype=np.uint32)
+        check(lib().syzcov_state_set_flakes(self.h, _ptr(a), a.size), "state_set_flakes")
+
+    def max_cover(self, call: int) -> np.ndarray:
+        n = check(lib().syzcov_state_get(self.h, call, None, 0), "state_get")
+        out = np.empty(max(n, 1), dtype=np.uint32)
+        n = check(lib().syzcov_state_get(self.h, call, _ptr(out), out.size), "state_get")
+        return out[:n]
+
+    def new_coverage(self, callids, records) -> np.ndarray:
+        """is_new[k] for a batch of executed call records, in batch order,
+        updating maxCover exactly like the sequential reference loop."""
+        lens = np.fromiter((len(r) for r in records), dtype=np.uint64, count=len(records))
+        off = np.zeros(len(records) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=off[1:])
+        pcs = (np.concatenate([np.asarray(r, dtype=np.uint32) for r in records])
+               if len(records) and off[-1] else np.zeros(1, dtype=np.uint32))
+        return self.new_coverage_csr(callids, off, pcs)
+
+    def new_coverage_csr(self, callids, off, pcs) -> np.ndarray:
+        cid = np.ascontiguousarray(callids, dtype=np.int32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        pcs = np.ascontiguousarray(pcs, dtype=np.uint32)
+        nrec = off.size - 1
+        is_new = np.zeros(max(nrec, 1), dtype=np.uint8)
+        check(lib().syzcov_newcov_batch(self.h, _ptr(cid), _ptr(off), _ptr(pcs), nrec,
+                                        _ptr(is_new)), "newcov_batch")
+        return is_new[:nrec]

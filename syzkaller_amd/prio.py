@@ -1,0 +1,93 @@
+"""Python mirror of prog/prio.go's public surface, backed by libsyzcov:
+
+    CalculatePriorities(corpus, static) -> C x C float32   (prio.go:29-38)
+    normalizePrio(prios)                                   (prio.go:158-192)
+    BuildChoiceTable(prios, enabled) -> ChoiceTable        (prio.go:202-228)
+    ChoiceTable.Choose(rnd, call)                          (prio.go:230-249)
+
+`corpus` is a list of programs, each the list of its calls' syscall ids
+(the reference's p.Calls[i].Meta.ID).  key_mode=0 reproduces the reference's
+calcDynamicPrio exactly — it counts call POSITIONS, not ids (prio.go:142-150)
+— key_mode=1 counts by syscall id.  The static matrix (calcStaticPriorities,
+prio.go:40-135) depends only on sys.Calls and is supplied by the caller.
+"""
+from __future__ import annotations
+
+import bisect
+import ctypes as C
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _csr(corpus):
+    lens = np.fromiter((len(p) for p in corpus), dtype=np.uint64, count=len(corpus))
+    off = np.zeros(len(corpus) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    ids = (np.concatenate([np.asarray(p, dtype=np.uint16) for p in corpus])
+           if len(corpus) and off[-1] else np.zeros(1, dtype=np.uint16))
+    return off, np.ascontiguousarray(ids, dtype=np.uint16)
+
+
+def CalculatePriorities(corpus, static=None, ncalls: int | None = None, key_mode: int = 0,
+                        return_raw: bool = False):
+    if static is not None:
+        static = np.ascontiguousarray(static, dtype=np.float32)
+        C_ = static.shape[0]
+    else:
+        if ncalls is None:
+            raise ValueError("need the static matrix or ncalls")
+        C_ = ncalls
+    off, ids = _csr(corpus)
+    out = np.empty((C_, C_), dtype=np.float32)
+    raw = np.empty((C_, C_), dtype=np.uint32) if return_raw else None
+    check(lib().syzcov_calculate_priorities(
+        _ptr(off), _ptr(ids), len(corpus), C_, key_mode,
+        _ptr(static) if static is not None else None, _ptr(out),
+        _ptr(raw) if raw is not None else None), "CalculatePriorities")
+    return (out, raw) if return_raw else out
+
+
+def normalizePrio(prios) -> np.ndarray:
+    p = np.ascontiguousarray(prios, dtype=np.float32).copy()
+    check(lib().syzcov_normalize_prio(_ptr(p), p.shape[0]), "normalizePrio")
+    return p
+
+
+class ChoiceTable:
+    """prio.go:196-200.  run[i] is None for disabled calls (nil in Go)."""
+
+    def __init__(self, run, enabled_calls, enabled):
+        self.run = run
+        self.enabledCalls = enabled_calls
+        self.enabled = enabled
+
+    def Choose(self, rnd, call: int) -> int:  # prio.go:230-249
+        if call < 0:
+            return self.enabledCalls[rnd.randrange(len(self.enabledCalls))]
+        run = self.run[call]
+        if run is None:
+            return self.enabledCalls[rnd.randrange(len(self.enabledCalls))]
+        while True:
+            x = rnd.randrange(int(run[-1]))
+            i = bisect.bisect_left(run, x)  # sort.SearchInts
+            if not self.enabled[i]:
+                continue
+            return i
+
+
+def BuildChoiceTable(prios, enabled=None) -> ChoiceTable:
+    prios = np.ascontiguousarray(prios, dtype=np.float32)
+    C_ = prios.shape[0]
+    en = (np.ones(C_, dtype=np.uint8) if enabled is None
+          else np.ascontiguousarray(np.asarray(enabled, dtype=np.uint8)))
+    run = np.zeros((C_, C_), dtype=np.int64)
+    check(lib().syzcov_build_choice_table(_ptr(prios), _ptr(en), C_, _ptr(run)),
+          "BuildChoiceTable")
+    rows = [run[i] if en[i] else None for i in range(C_)]
+    return ChoiceTable(rows, [i for i in range(C_) if en[i]], en.astype(bool))

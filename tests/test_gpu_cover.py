@@ -1,0 +1,190 @@
+"""GPU parity: libsyzcov's HIP kernels vs the CPU oracle (restatement of
+cover/cover.go + Go sort.Sort), on the reference's KATs, quirks, seeded random
+cases and synthetic corpora.  Bit-exact everywhere (integer/index work)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.conftest import augment
+
+pytestmark = pytest.mark.gpu
+
+SENT = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def cover():
+    from syzkaller_amd import cover as c
+    return c
+
+
+def _ops(cover):
+    return {
+        "difference": (cover.Difference, orc.difference),
+        "symmetric_difference": (cover.SymmetricDifference, orc.symmetric_difference),
+        "union": (cover.Union, orc.union),
+        "intersection": (cover.Intersection, orc.intersection),
+    }
+
+
+@pytest.mark.parametrize("name", ["difference", "symmetric_difference", "union", "intersection"])
+def test_setop_kat(cover, kat, name):
+    t = kat[name]
+    gpu, _ = _ops(cover)[name]
+    for a, b, r in augment(t["cases"], t["symmetric"]):
+        assert list(gpu(a, b)) == r, (name, a, b)
+
+
+def test_canonicalize_kat(cover, kat):
+    for a, _, r in augment(kat["canonicalize"]["cases"], False):
+        assert list(cover.Canonicalize(a)) == r
+    for a, r in kat["quirks"]["canonicalize"]:
+        assert list(cover.Canonicalize(a)) == r
+
+
+def test_quirk_setops(cover, kat):
+    ops = _ops(cover)
+    for name, a, b, r in kat["quirks"]["setops"]:
+        assert list(ops[name][0](a, b)) == r, (name, a, b)
+
+
+def test_minimize_kat(cover, kat):
+    for case in kat["minimize"]["cases"]:
+        assert cover.Minimize(case["inp"]) == case["out"], case["name"]
+    for case in kat["quirks"]["minimize"]:
+        assert cover.Minimize(case["inp"]) == case["out"]
+
+
+def test_canonicalize_in_place_aliasing(cover):
+    a = np.array([6, 1, 2, 6, 3, 3, 4, 5, 1], dtype=np.uint32)
+    r = cover.Canonicalize(a)
+    assert list(r) == [1, 2, 3, 4, 5, 6]
+    assert np.shares_memory(r, a) and list(a[:6]) == [1, 2, 3, 4, 5, 6]
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 64, 255, 256, 257, 1000, 2048, 4097, 8192, 16384, 16385,
+                               40000, 65535, 100000, 300001])
+def test_canonicalize_sizes(cover, n):
+    rng = np.random.default_rng(n)
+    for hi in (50, 1 << 20, 1 << 32):
+        a = rng.integers(0, hi, size=n, dtype=np.uint64).astype(np.uint32)
+        if n > 3:
+            a[rng.integers(0, n, size=3)] = SENT
+        assert np.array_equal(cover.Canonicalize(a.copy()), orc.canonicalize(a)), (n, hi)
+
+
+def test_canonicalize_all_sentinel(cover):
+    assert cover.Canonicalize(np.full(5000, SENT, np.uint32)).size == 0
+    assert cover.Canonicalize(np.full(20000, SENT, np.uint32)).size == 0
+
+
+def _rand_sorted(rng, n, hi, dups):
+    a = np.sort(rng.integers(0, hi, size=n, dtype=np.uint64)).astype(np.uint32)
+    return a if dups else np.unique(a)
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_setops_random(cover, dups):
+    rng = np.random.default_rng(7 + dups)
+    ops = _ops(cover)
+    for trial in range(60):
+        na, nb = (int(x) for x in rng.integers(0, 3000, size=2))
+        hi = int(rng.choice([10, 1000, 1 << 32]))
+        a, b = _rand_sorted(rng, na, hi, dups), _rand_sorted(rng, nb, hi, dups)
+        if trial % 5 == 0 and a.size:
+            a[-1] = SENT
+        for name, (g, o) in ops.items():
+            assert np.array_equal(g(a, b), o(a, b)), (name, trial)
+
+
+def test_setop_unsorted_rejected(cover):
+    from syzkaller_amd import SyzcovError
+    with pytest.raises(SyzcovError):
+        cover.Union([3, 1], [2])
+
+
+def test_sort_order_matches_go(cover):
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        n = int(rng.integers(0, 20000))
+        kind = trial % 4
+        lens = (rng.integers(0, 8, size=n) if kind == 0 else
+                rng.integers(0, 1 << 16, size=n) if kind == 1 else
+                np.sort(rng.integers(0, 100, size=n)) if kind == 2 else
+                rng.normal(2048, 512, size=n).astype(np.int64).clip(1, 65535))
+        for variant in (orc.PDQSORT, orc.LEGACY):
+            assert np.array_equal(cover.SortOrder(lens, variant), orc.sort_order(lens, variant)), \
+                (trial, variant)
+
+
+def test_minimize_random_vs_oracle(cover):
+    rng = np.random.default_rng(5)
+    for trial in range(60):
+        n = int(rng.integers(0, 400))
+        hi = int(rng.choice([30, 500, 1 << 32]))
+        covs = [orc.canonicalize(rng.integers(0, hi, size=int(rng.integers(0, 40)),
+                                              dtype=np.uint64).astype(np.uint32))
+                for _ in range(n)]
+        for variant in (orc.PDQSORT, orc.LEGACY):
+            assert cover.Minimize(covs, variant=variant) == list(orc.minimize(covs, variant)), \
+                (trial, variant)
+
+
+def test_minimize_non_canonical_covers(cover):
+    """Minimize accepts raw covers (duplicates count in len, cover.go:142)."""
+    rng = np.random.default_rng(9)
+    for _ in range(30):
+        covs = [rng.integers(0, 60, size=int(rng.integers(0, 25))).astype(np.uint32)
+                for _ in range(int(rng.integers(1, 150)))]
+        assert cover.Minimize(covs) == list(orc.minimize(covs))
+
+
+def test_minimize_explicit_order(cover):
+    covs = [[1, 2], [2, 3], [3, 4], [1, 4]]
+    order = [3, 2, 1, 0]
+    # processing order given by the caller's own sort.Sort
+    exp = []
+    seen = set()
+    for i in order:
+        if any(p not in seen for p in covs[i]):
+            exp.append(i)
+        seen.update(covs[i])
+    assert cover.Minimize(covs, order=order) == exp
+
+
+def test_minimize_synthetic_corpus(cover):
+    off, pcs = orc.synth_corpus(0x5EED0001, 3000, mean=512, sigma=128, log2_space=16)
+    coff, cpcs = orc.canonicalize_csr(off, pcs)
+    exp = orc.minimize_csr(coff, cpcs)
+    got = cover.MinimizeCSR(coff, cpcs)
+    assert got == list(exp)
+    assert np.array_equal(cover.UnionAllCSR(coff, cpcs), orc.union_fold_csr(coff, cpcs))
+
+
+def test_union_all_vs_fold(cover):
+    rng = np.random.default_rng(3)
+    covs = [orc.canonicalize(rng.integers(0, 5000, size=int(rng.integers(0, 300))))
+            for _ in range(200)]
+    covs.append(np.array([7, SENT], np.uint32))
+    off, p = orc.to_csr(covs)
+    assert np.array_equal(cover.UnionAll(covs), orc.union_fold_csr(off, p))
+
+
+def test_concurrent_callers(cover):
+    """The fuzzer calls cover ops from many goroutines: per-thread streams."""
+    import threading
+    rng = np.random.default_rng(1)
+    cases = [(_rand_sorted(rng, 500, 2000, False), _rand_sorted(rng, 700, 2000, False))
+             for _ in range(32)]
+    errors = []
+
+    def run(i):
+        a, b = cases[i]
+        for _ in range(5):
+            if not np.array_equal(cover.Union(a, b), orc.union(a, b)):
+                errors.append(i)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(cases))]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors

@@ -1,0 +1,169 @@
+"""GPU parity of the device-resident corpus pipeline (engine.CorpusEngine) and
+of the synthetic generator, the priorities path and the fuzzer new-coverage
+check, against the CPU oracle."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def _to_np_u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def test_synth_matches_cpu_twin(torch):
+    from syzkaller_amd.engine import synth_corpus
+    for uniform in (False, True):
+        off, pcs, lens, total = synth_corpus(300, 0x5EED0001, first=1000, uniform=uniform)
+        o_off, o_pcs = orc.synth_corpus(0x5EED0001, 300, first=1000, uniform=uniform)
+        assert np.array_equal(off.cpu().numpy().astype(np.uint64), o_off)
+        assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
+
+
+@pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
+                                               (500, 9000, 6000, 20)])
+def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    seed = 0x5EED0002
+    off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    res = eng.step(off, raw, n)
+    # oracle
+    o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    # canonical covers, per input, in their CSR slots
+    canon = _to_np_u32(eng.canon)
+    new_len = eng.new_len[:n].cpu().numpy()
+    offs = off.cpu().numpy()
+    assert np.array_equal(new_len, np.diff(c_off).astype(np.int32))
+    for i in range(0, n, max(1, n // 50)):
+        assert np.array_equal(canon[offs[i]:offs[i] + new_len[i]], c_pcs[c_off[i]:c_off[i + 1]])
+    exp_kept = orc.minimize_csr(c_off, c_pcs)
+    assert res.n_kept == len(exp_kept)
+    assert res.kept_idx.cpu().numpy().tolist() == list(exp_kept)
+    exp_union = orc.union_fold_csr(c_off, c_pcs)
+    assert res.n_union == exp_union.size
+    assert np.array_equal(_to_np_u32(res.union), exp_union)
+    assert res.max_cover == exp_union.size
+    # second step: maxCover is already saturated by the same corpus
+    res2 = eng.step(off, raw, n)
+    assert res2.kept_idx.cpu().numpy().tolist() == list(exp_kept)
+    assert res2.max_cover == exp_union.size
+
+
+def test_engine_properties_large(torch):
+    """Size-independent properties at 200k inputs: union(kept) == union(all),
+    kept order follows non-increasing canonical length, first kept = rank 0."""
+    from syzkaller_amd import cover
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    n = 200_000
+    off, raw, lens, total = synth_corpus(n, 0x5EED0003, mean=256, sigma=64, log2_space=20)
+    lo, span = synth_window(20)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    res = eng.step(off, raw, n)
+    kept = res.kept_idx.cpu().numpy()
+    new_len = eng.new_len[:n].cpu().numpy()
+    assert np.all(np.diff(new_len[kept].astype(np.int64)) <= 0)
+    order = eng.order[:n].cpu().numpy()
+    assert kept[0] == order[0]
+    canon = _to_np_u32(eng.canon)
+    offs = off.cpu().numpy()
+    kept_union = np.unique(np.concatenate([canon[offs[i]:offs[i] + new_len[i]] for i in kept]))
+    assert np.array_equal(kept_union, _to_np_u32(res.union))
+    # order equals Go's sort over the canonical lengths
+    assert np.array_equal(order, orc.sort_order(new_len.astype(np.int64)))
+    assert np.array_equal(cover.SortOrder(new_len), order)
+
+
+def test_prio_positional_vs_oracle(torch):
+    from syzkaller_amd import prio
+    rng = np.random.default_rng(4)
+    for C, nprog in ((40, 500), (300, 2000), (1170, 3000)):
+        lens = rng.integers(0, min(C, 60) + 1, size=nprog)
+        corpus = [rng.integers(0, C, size=int(l)).tolist() for l in lens]
+        static = rng.uniform(0.1, 1.0, size=(C, C)).astype(np.float32)
+        got, raw = prio.CalculatePriorities(corpus, static, return_raw=True)
+        exp_raw = orc.dynamic_raw(lens, C)
+        assert np.array_equal(raw.astype(np.float32), exp_raw)
+        exp = orc.calculate_priorities(lens, static)
+        np.testing.assert_allclose(got, exp, rtol=1e-6, atol=0)  # north-star tolerance
+        assert np.array_equal(got, exp)  # and in fact bit-exact
+
+
+def test_prio_by_id_vs_numpy(torch):
+    from syzkaller_amd import prio
+    rng = np.random.default_rng(8)
+    C, nprog = 200, 1500
+    corpus = [rng.integers(0, C, size=int(rng.integers(0, 40))).tolist() for _ in range(nprog)]
+    A = np.zeros((nprog, C), np.int64)
+    for p, calls in enumerate(corpus):
+        for c in calls:
+            A[p, c] += 1
+    D = A.T @ A - np.diag(A.sum(0))
+    _, raw = prio.CalculatePriorities(corpus, None, ncalls=C, key_mode=1, return_raw=True)
+    assert np.array_equal(raw.astype(np.int64), D)
+
+
+def test_prio_too_long_program(torch):
+    from syzkaller_amd import SyzcovError, prio
+    with pytest.raises(SyzcovError):
+        prio.CalculatePriorities([[0] * 11], None, ncalls=10)
+
+
+def test_normalize_and_choice_table(torch):
+    from syzkaller_amd import prio
+    rng = np.random.default_rng(6)
+    C = 257
+    p = rng.integers(0, 50, size=(C, C)).astype(np.float32)
+    p[3] = 0  # all-zero row -> 1
+    assert np.array_equal(prio.normalizePrio(p), orc.normalize_prio(p))
+    pr = orc.normalize_prio(p)
+    en = (rng.random(C) < 0.7).astype(np.uint8)
+    ct = prio.BuildChoiceTable(pr, en)
+    exp = orc.build_choice_table(pr, en)
+    for i in range(C):
+        if en[i]:
+            assert np.array_equal(ct.run[i], exp[i])
+        else:
+            assert ct.run[i] is None
+    import random
+    r = random.Random(0)
+    i = next(i for i in range(C) if en[i])
+    for _ in range(100):
+        assert ct.enabled[ct.Choose(r, i)]
+
+
+def test_newcov_batch_vs_sequential(torch):
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(12)
+    ncalls, lo, span = 30, 0x81000000, 1 << 16
+    st = CoverState(ncalls, lo, span)
+    mc = [[] for _ in range(ncalls)]
+    for c in range(0, ncalls, 3):
+        init = np.unique(rng.integers(lo, lo + span, size=200)).astype(np.uint32)
+        st.add(c, init)
+        mc[c] = init
+    flakes = np.unique(rng.integers(lo, lo + span, size=300)).astype(np.uint32)
+    st.set_flakes(flakes)
+    for batch in range(4):
+        nrec = 3000
+        cids = rng.integers(0, ncalls, size=nrec)
+        recs = [np.unique(rng.integers(lo, lo + int(rng.choice([512, span])),
+                                       size=int(rng.integers(0, 60)))).astype(np.uint32)
+                for _ in range(nrec)]
+        exp_new, mc = orc.newcov_batch(mc, flakes, cids, recs)
+        got = st.new_coverage(cids, recs)
+        assert np.array_equal(got, exp_new), batch
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
+    st.close()
