@@ -186,6 +186,38 @@ int syzcov_dev_minimize_pass2(const uint64_t *off, const uint32_t *len, const ui
                               const int32_t *order, const int32_t *ranks, size_t n,
                               const uint64_t *tab, uint32_t pc_lo, const int32_t *first,
                               const uint8_t *cand, uint8_t *kept, void *stream);
+/* ---- engine fast path: canonical covers in the dense PC-id space ----
+ * Canonicalize a CSR corpus whose PCs are all in the dictionary `tab`
+ * (built from a presence map of the same raw corpus): each segment's PCs are
+ * mapped to dense ids, radix-sorted in LDS and de-duplicated; canonical ids
+ * go to out_ids[off[i] ..), lengths to new_len.  n_ids: device u32 (from
+ * syzcov_dev_dict_build).  ws: syzcov_dev_canon_ws_size(nseg, max_seg_len). */
+int syzcov_dev_canon_ids(const uint64_t *off, const uint32_t *raw, uint32_t *out_ids,
+                         uint32_t *new_len, size_t nseg, size_t max_seg_len, const uint64_t *tab,
+                         uint32_t pc_lo, uint64_t pc_span, const uint32_t *n_ids,
+                         uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+/* Full id -> PC list (n_ids entries, a present 0xFFFFFFFF included). */
+int syzcov_dev_dict_pcs(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
+                        void *stream);
+/* out[off[s] + q] = table[in[off[s] + q]] for q < len[s] (ids -> PCs). */
+int syzcov_dev_gather_u32(const uint32_t *table, const uint64_t *off, const uint32_t *len,
+                          const uint32_t *in, size_t nseg, uint32_t *out, void *stream);
+/* Minimize over id-space covers: pass 1 in geometrically growing rank chunks
+ * with a covered-id bitmap filter rebuilt between chunks (first[] pre-set to
+ * INT32_MAX, n_ids_cap >= *n_ids), then (do_pass2) pass 2 into kept[] (by
+ * rank, pre-zeroed).  ws: syzcov_dev_minimize_ws_size(n_ids_cap).  Sharded
+ * runs call with do_pass2 = 0, MIN-all-reduce first[], then call
+ * syzcov_dev_minimize_ids_pass2. */
+size_t syzcov_dev_minimize_ws_size(size_t n_ids_cap);
+int syzcov_dev_minimize_ids(const uint64_t *off, const uint32_t *len, const uint32_t *ids,
+                            const int32_t *order, const int32_t *ranks, size_t n,
+                            const uint32_t *n_ids, size_t n_ids_cap, int32_t *first,
+                            uint8_t *cand, uint8_t *kept, int do_pass2, void *ws, void *stream);
+int syzcov_dev_minimize_ids_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *ids,
+                                  const int32_t *order, const int32_t *ranks, size_t n,
+                                  const int32_t *first, const uint8_t *cand, uint8_t *kept,
+                                  void *stream);
+
 /* Ordered compaction: out_idx = [order[r] for r if kept[r]]; *n_out (device u32). */
 size_t syzcov_dev_compact_ws_size(size_t n);
 int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n, int32_t *out_idx,

@@ -65,6 +65,13 @@ _SIGS = {
     "syzcov_dev_dict_to_list": (C.c_int, [p_, u64, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass1": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_, p_]),
+    "syzcov_dev_canon_ids": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, p_, sz, p_]),
+    "syzcov_dev_dict_pcs": (C.c_int, [p_, u64, u32, p_, p_]),
+    "syzcov_dev_gather_u32": (C.c_int, [p_, p_, p_, p_, sz, p_, p_]),
+    "syzcov_dev_minimize_ws_size": (sz, [sz]),
+    "syzcov_dev_minimize_ids": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, sz, p_, p_, p_, C.c_int, p_,
+                                          p_]),
+    "syzcov_dev_minimize_ids_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, p_, p_, p_]),
     "syzcov_dev_compact_ws_size": (sz, [sz]),
     "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),
     "syzcov_dev_sort_ws_size": (sz, [sz]),

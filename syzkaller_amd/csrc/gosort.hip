@@ -3,41 +3,541 @@
 //
 // sort.Sort is not stable, so equal-length inputs are ordered by the exact
 // swap sequence of Go's algorithm (pdqsort in Go >= 1.19, quickSort + gap-6
-// ShellSort in Go 1.8-1.18).  This file restates both over (idx, len) pairs.
+// ShellSort in Go 1.8-1.18).
 //
-// Stage 1 of the port: the restatement runs on the host over the D2H'd
-// lengths and the order is uploaded (one 12 B/input round trip).  The
-// level-synchronous device version (parallel Hoare partition by prefix sums,
-// see DESIGN.md) replaces it behind the same entry point.
+// Go >= 1.19 (pdqsort, the default) runs on the GPU, level-synchronously:
+// every round advances all live segments by one iteration of pdqsort's loop.
+// Per segment the O(1) control steps (breakPatterns, choosePivot, the
+// partitionEqual test) run in one lane; the O(n) steps are data-parallel:
+// Hoare's partition pairs the k-th left-misplaced element with the k-th
+// right-misplaced one, so both sides' ranks come from prefix sums and the m
+// swaps run independently — exactly the swaps Go performs.  Segments of up to
+// SMALL elements finish inside one workgroup in LDS; leaves of up to TINY
+// elements run gosort_core.h's sequential loop in one lane.  Segments never
+// touch anything outside [a, b) but the finished pivot at a-1, so their
+// processing order does not change the result.
+//
+// The legacy variant (Go 1.8-1.18 quickSort) is a host restatement at the end
+// of this file: its doPivot is a sequential 3-way scan and it is not the
+// default Go behaviour any more.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <vector>
 
 #include "common.h"
+#include "gosort_core.h"
 
 namespace syz {
-namespace gosort {
+namespace gsort {
 
-struct Arr {
-    int32_t *idx;
-    const int64_t *len;
-    bool less(long i, long j) const { return len[idx[i]] > len[idx[j]]; }
-    void swap(long i, long j) const {
-        int32_t t = idx[i];
-        idx[i] = idx[j];
-        idx[j] = t;
+constexpr int SMALL = 4096;  // segment finished in one workgroup's LDS
+constexpr int TINY = 64;     // leaf finished by one lane
+constexpr int CH = 4096;     // elements per block in the global rounds
+constexpr int WG = 256;
+
+struct Seg {
+    int a, b, limit, flags;  // flags: bit0 wasBalanced, bit1 wasPartitioned
+};
+enum { M_DONE = 0, M_HEAP = 1, M_ACTIVE = 2 };
+struct Plan {
+    int mode, pivot, rev, pis, eq, cnt, m;
+    uint32_t kp;
+};
+
+// accessor over the global key/index arrays
+struct GAcc {
+    uint32_t *K;
+    int32_t *I;
+    __device__ bool less(int i, int j) const { return K[i] > K[j]; }
+    __device__ void swap(int i, int j) const {
+        uint32_t k = K[i];
+        K[i] = K[j];
+        K[j] = k;
+        int32_t x = I[i];
+        I[i] = I[j];
+        I[j] = x;
     }
 };
 
-static int blen(unsigned long x) { return x ? 64 - __builtin_clzl(x) : 0; }
+// accessor over an LDS window holding global positions [base-1, base+len)
+struct LAcc {
+    uint32_t *K;  // K[g - base + 1]
+    int32_t *I;
+    int base;
+    __device__ bool less(int i, int j) const { return K[i - base + 1] > K[j - base + 1]; }
+    __device__ void swap(int i, int j) const {
+        const int p = i - base + 1, q = j - base + 1;
+        uint32_t k = K[p];
+        K[p] = K[q];
+        K[q] = k;
+        int32_t x = I[p];
+        I[p] = I[q];
+        I[q] = x;
+    }
+};
 
-static void insertion(const Arr &d, long a, long b) {
+struct Ctl {
+    Seg *next;
+    uint32_t *next_count, *next_maxlen;
+    Seg *small;
+    uint32_t *small_count;
+    uint32_t small_cap, next_cap;
+    uint32_t *err;
+};
+
+__device__ __forceinline__ void push_seg(const Ctl &c, Seg s) {
+    const int n = s.b - s.a;
+    if (n <= 1) return;
+    if (n <= SMALL) {
+        const uint32_t slot = atomicAdd(c.small_count, 1u);
+        if (slot < c.small_cap)
+            c.small[slot] = s;
+        else
+            *c.err = 2u;
+    } else {
+        const uint32_t slot = atomicAdd(c.next_count, 1u);
+        if (slot < c.next_cap)
+            c.next[slot] = s;
+        else
+            *c.err = 3u;
+        atomicMax(c.next_maxlen, (uint32_t)n);
+    }
+}
+
+__global__ void init_kernel(const int64_t *__restrict__ lens, uint32_t n, uint32_t *__restrict__ K,
+                            int32_t *__restrict__ I, uint32_t *__restrict__ err) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int64_t l = lens[i];
+        if (l < 0 || l > 0xFFFFFFFFll) *err = 1u;
+        K[i] = (uint32_t)l;
+        I[i] = (int32_t)i;
+    }
+}
+
+__global__ void seed_kernel(uint32_t n, Ctl c) {
+    push_seg(c, Seg{0, (int)n, gocore::bits_len(n), 3});
+}
+
+// one lane per segment: control steps of one pdqsort loop iteration
+__global__ void plan_kernel(Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+                            uint32_t *__restrict__ K, int32_t *__restrict__ I, Ctl c) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ncur) return;
+    Seg g = cur[s];
+    Plan p{};
+    const int n = g.b - g.a;
+    GAcc d{K, I};
+    if (n <= SMALL) {  // (only the seed can be small here)
+        push_seg(c, g);
+        p.mode = M_DONE;
+    } else if (g.limit == 0) {
+        p.mode = M_HEAP;
+    } else {
+        const bool wb = g.flags & 1, wp = g.flags & 2;
+        if (!wb) {
+            gocore::break_patterns(d, g.a, g.b);
+            g.limit--;
+            cur[s].limit = g.limit;
+        }
+        int hint;
+        int pivot = gocore::choose_pivot(d, g.a, g.b, &hint);
+        if (hint == gocore::kDecreasing) {
+            p.rev = 1;
+            pivot = (g.b - 1) - (pivot - g.a);
+            hint = gocore::kIncreasing;
+        }
+        p.pis = wb && wp && hint == gocore::kIncreasing;
+        p.pivot = pivot;
+        p.mode = M_ACTIVE;
+    }
+    plan[s] = p;
+}
+
+__global__ void heap_kernel(const Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+                            uint32_t *__restrict__ K, int32_t *__restrict__ I) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ncur || plan[s].mode != M_HEAP) return;
+    GAcc d{K, I};
+    gocore::heap_sort(d, cur[s].a, cur[s].b);
+    plan[s].mode = M_DONE;
+}
+
+__global__ void reverse_kernel(const Seg *__restrict__ cur, const Plan *__restrict__ plan,
+                               uint32_t *__restrict__ K, int32_t *__restrict__ I) {
+    const uint32_t s = blockIdx.y;
+    const Plan p = plan[s];
+    if (p.mode != M_ACTIVE || !p.rev) return;
+    const Seg g = cur[s];
+    const int half = (g.b - g.a) / 2;
+    GAcc d{K, I};
+    for (int i = blockIdx.x * CH + threadIdx.x; i < min(half, (int)(blockIdx.x + 1) * CH);
+         i += blockDim.x)
+        d.swap(g.a + i, g.b - 1 - i);
+}
+
+// WG-cooperative partialInsertionSort (cover: gosort_core.h's sequential form)
+__device__ int wg_find_first_descent(const uint32_t *K, int from, int b, int *sh) {
+    // first i in [from, b) with K[i] > K[i-1], or b
+    for (int c0 = from; c0 < b; c0 += WG) {
+        const int i = c0 + threadIdx.x;
+        const bool hit = i < b && K[i] > K[i - 1];
+        const uint64_t m = __ballot(hit);
+        if (__lane_id() == 0)
+            sh[threadIdx.x >> 6] = m ? (int)(c0 + (threadIdx.x & ~63u) + __builtin_ctzll(m)) : b;
+        __syncthreads();
+        int best = b;
+        for (int w = 0; w < WG / 64; w++) best = min(best, sh[w]);
+        __syncthreads();
+        if (best < b) return best;
+    }
+    return b;
+}
+
+__global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
+                                                  Plan *__restrict__ plan,
+                                                  uint32_t *__restrict__ K,
+                                                  int32_t *__restrict__ I) {
+    __shared__ int sh[WG / 64 + 2];
+    const uint32_t s = blockIdx.x;
+    if (plan[s].mode != M_ACTIVE || !plan[s].pis) return;
+    const Seg g = cur[s];
+    const int a = g.a, b = g.b;
+    int i = a + 1;
+    bool sorted = false;
+    for (int step = 0; step < 5; step++) {
+        i = wg_find_first_descent(K, i, b, sh);
+        if (i == b) {
+            sorted = true;
+            break;
+        }
+        if (b - a < 50) break;
+        // the three moves of one step run on lane 0 (bounded by the segment)
+        if (threadIdx.x == 0) {
+            GAcc d{K, I};
+            d.swap(i, i - 1);
+            if (i - a >= 2)
+                for (int j = i - 1; j >= 1 && d.less(j, j - 1); j--) d.swap(j, j - 1);
+            if (b - i >= 2)
+                for (int j = i + 1; j < b && d.less(j, j - 1); j++) d.swap(j, j - 1);
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && sorted) plan[s].mode = M_DONE;
+}
+
+__global__ void eq_kernel(const Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+                          uint32_t *__restrict__ K, int32_t *__restrict__ I) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ncur || plan[s].mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    const int pivot = plan[s].pivot;
+    GAcc d{K, I};
+    plan[s].eq = g.a > 0 && !d.less(g.a - 1, pivot);
+    d.swap(g.a, pivot);  // both partition forms start with Swap(a, pivot)
+    plan[s].kp = K[g.a];
+}
+
+// f(x): x belongs to the left group (partition: Less(x, a) = K[x] > kp;
+// partitionEqual: !Less(a, x) = K[x] >= kp)
+__device__ __forceinline__ bool left_group(uint32_t k, uint32_t kp, int eq) {
+    return eq ? k >= kp : k > kp;
+}
+
+__global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
+                                                    const Plan *__restrict__ plan,
+                                                    const uint32_t *__restrict__ K,
+                                                    uint32_t *__restrict__ cc, uint32_t stride) {
+    __shared__ uint32_t tmp[WG / 64 + 1];
+    const uint32_t s = blockIdx.y;
+    const Plan p = plan[s];
+    if (p.mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    const int x0 = g.a + 1 + (int)blockIdx.x * CH;
+    if (x0 >= g.b) return;
+    const int x1 = min(g.b, x0 + CH);
+    uint32_t c = 0;
+    for (int x = x0 + threadIdx.x; x < x1; x += WG) c += left_group(K[x], p.kp, p.eq);
+    uint32_t total;
+    block_excl_scan<WG>(c, tmp, &total);
+    if (threadIdx.x == 0) cc[(size_t)s * stride + blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(WG) void cscan_kernel(const Seg *__restrict__ cur,
+                                                    Plan *__restrict__ plan,
+                                                    uint32_t *__restrict__ cc, uint32_t stride) {
+    __shared__ uint32_t tmp[WG / 64 + 1];
+    const uint32_t s = blockIdx.x;
+    if (plan[s].mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += WG) {
+        const uint32_t c = c0 + threadIdx.x;
+        const uint32_t v = c < nch ? cc[(size_t)s * stride + c] : 0u;
+        uint32_t total;
+        const uint32_t pre = block_excl_scan<WG>(v, tmp, &total);
+        if (c < nch) cc[(size_t)s * stride + c] = carry + pre;
+        carry += total;
+    }
+    if (threadIdx.x == 0) {
+        plan[s].cnt = (int)carry;
+        plan[s].m = 0;
+    }
+}
+
+// ranks of the misplaced elements: PL[a + k] / PR[a + k] = position of the
+// k-th left-misplaced (from the left) / right-misplaced (from the right)
+__global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
+                                                   Plan *__restrict__ plan,
+                                                   const uint32_t *__restrict__ K,
+                                                   const uint32_t *__restrict__ cc,
+                                                   uint32_t stride, int32_t *__restrict__ PL,
+                                                   int32_t *__restrict__ PR) {
+    __shared__ uint32_t tmp[WG / 64 + 1];
+    const uint32_t s = blockIdx.y;
+    const Plan p = plan[s];
+    if (p.mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    const int x0 = g.a + 1 + (int)blockIdx.x * CH;
+    if (x0 >= g.b) return;
+    const int x1 = min(g.b, x0 + CH);
+    const int L = g.a + p.cnt;  // left region [a+1, L]
+    uint32_t base = cc[(size_t)s * stride + blockIdx.x];
+    uint32_t mloc = 0;
+    for (int c0 = x0; c0 < x1; c0 += WG) {
+        const int x = c0 + threadIdx.x;
+        const bool in = x < x1;
+        const bool f = in && left_group(K[x], p.kp, p.eq);
+        uint32_t total;
+        const uint32_t pf = base + block_excl_scan<WG>(f ? 1u : 0u, tmp, &total);
+        if (in) {
+            if (x > L && f) PR[g.a + (p.cnt - (int)pf - 1)] = x;
+            if (x <= L && !f) {
+                PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
+                mloc++;
+            }
+        }
+        base += total;
+    }
+    mloc = wave_sum(mloc);
+    if (__lane_id() == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
+}
+
+__global__ void swap_kernel(const Seg *__restrict__ cur, const Plan *__restrict__ plan,
+                            uint32_t *__restrict__ K, int32_t *__restrict__ I,
+                            const int32_t *__restrict__ PL, const int32_t *__restrict__ PR) {
+    const uint32_t s = blockIdx.y;
+    const Plan p = plan[s];
+    if (p.mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    GAcc d{K, I};
+    for (int k = blockIdx.x * CH + threadIdx.x; k < min(p.m, (int)(blockIdx.x + 1) * CH);
+         k += blockDim.x)
+        d.swap(PL[g.a + k], PR[g.a + k]);
+}
+
+__global__ void finish_kernel(const Seg *__restrict__ cur, uint32_t ncur,
+                              const Plan *__restrict__ plan, uint32_t *__restrict__ K,
+                              int32_t *__restrict__ I, Ctl c) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ncur) return;
+    const Plan p = plan[s];
+    if (p.mode != M_ACTIVE) return;
+    const Seg g = cur[s];
+    if (p.eq) {  // partitionEqual returns a + 1 + cnt; the loop continues
+        push_seg(c, Seg{g.a + 1 + p.cnt, g.b, g.limit, g.flags});
+        return;
+    }
+    const int mid = g.a + p.cnt;
+    GAcc d{K, I};
+    d.swap(mid, g.a);
+    const int already = p.m == 0;
+    const int n = g.b - g.a, ln = mid - g.a, rn = g.b - mid, thr = n / 8;
+    if (ln < rn) {
+        push_seg(c, Seg{g.a, mid, g.limit, 3});
+        push_seg(c, Seg{mid + 1, g.b, g.limit, (ln >= thr) | (already << 1)});
+    } else {
+        push_seg(c, Seg{mid + 1, g.b, g.limit, 3});
+        push_seg(c, Seg{g.a, mid, g.limit, (rn >= thr) | (already << 1)});
+    }
+}
+
+// ------------------------------------------------------- in-LDS finisher
+// One workgroup per segment of <= SMALL elements: tasks are popped by lane 0
+// (O(1) control steps), partitions run WG-parallel, leaves of <= TINY
+// elements are collected and finished one per lane at the end.
+struct LTask {
+    int16_t a, b;  // relative to the segment start
+    int16_t limit, flags;
+};
+
+__global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small,
+                                                    const uint32_t *__restrict__ nsmall_p,
+                                                    uint32_t *__restrict__ Kg,
+                                                    int32_t *__restrict__ Ig,
+                                                    uint32_t *__restrict__ err) {
+    constexpr int TCAP = SMALL / 2;
+    __shared__ uint32_t K[SMALL + 1];
+    __shared__ int32_t I[SMALL + 1];
+    __shared__ int32_t PL[SMALL];
+    __shared__ int32_t PR[SMALL];
+    __shared__ LTask tiny[TCAP];
+    __shared__ LTask stk[40];
+    __shared__ int sh[8];
+    __shared__ uint32_t tmp[WG / 64 + 1];
+    const uint32_t nsmall = *nsmall_p;
+    for (uint32_t si = blockIdx.x; si < nsmall; si += gridDim.x) {
+        const Seg g = small[si];
+        const int a = g.a, n = g.b - g.a;
+        for (int q = threadIdx.x; q < n; q += WG) {
+            K[q + 1] = Kg[a + q];
+            I[q + 1] = Ig[a + q];
+        }
+        if (threadIdx.x == 0) {
+            K[0] = a > 0 ? Kg[a - 1] : 0u;  // the finished pivot left of the segment
+            I[0] = -1;
+            stk[0] = LTask{0, (int16_t)n, (int16_t)g.limit, (int16_t)g.flags};
+            sh[0] = 1;  // stack size
+            sh[1] = 0;  // tiny count
+        }
+        __syncthreads();
+        LAcc d{K, I, a};
+        for (;;) {
+            // ---- lane 0: pop and run the O(1) control steps
+            if (threadIdx.x == 0) {
+                int mode = 3;  // 0 stop, 1 partition, 2 partitionEqual, 3 next task
+                if (sh[0] == 0) {
+                    mode = 0;
+                } else {
+                    const LTask lt = stk[--sh[0]];
+                    const int ta = a + lt.a, tb = a + lt.b, tn = lt.b - lt.a;
+                    int limit = lt.limit;
+                    if (tn <= TINY) {
+                        if (tn > 1) {
+                            if (sh[1] < TCAP)
+                                tiny[sh[1]++] = lt;
+                            else
+                                *err = 4u;
+                        }
+                    } else if (limit == 0) {
+                        gocore::heap_sort(d, ta, tb);
+                    } else {
+                        const bool wb = lt.flags & 1, wp = lt.flags & 2;
+                        if (!wb) {
+                            gocore::break_patterns(d, ta, tb);
+                            limit--;
+                        }
+                        int hint;
+                        int pivot = gocore::choose_pivot(d, ta, tb, &hint);
+                        if (hint == gocore::kDecreasing) {
+                            gocore::reverse_range(d, ta, tb);
+                            pivot = (tb - 1) - (pivot - ta);
+                            hint = gocore::kIncreasing;
+                        }
+                        if (!(wb && wp && hint == gocore::kIncreasing &&
+                              gocore::partial_insertion_sort(d, ta, tb))) {
+                            const int eq = ta > 0 && !d.less(ta - 1, pivot);
+                            d.swap(ta, pivot);
+                            mode = eq ? 2 : 1;
+                            sh[2] = ta;
+                            sh[3] = tb;
+                            sh[4] = limit;
+                            sh[5] = lt.flags;
+                        }
+                    }
+                }
+                sh[6] = mode;
+            }
+            __syncthreads();
+            const int mode = sh[6];
+            if (mode == 0) break;
+            if (mode == 3) continue;
+            // ---- WG-parallel Hoare partition of [ta+1, tb) around K[ta]
+            const int ta = sh[2], tb = sh[3], eq = mode == 2;
+            const uint32_t kp = K[ta - a + 1];
+            const int len = tb - ta - 1;
+            const int per = (len + WG - 1) / WG;
+            const int x0 = ta + 1 + (int)threadIdx.x * per, x1 = min(tb, x0 + per);
+            uint32_t c = 0;
+            for (int x = x0; x < x1; x++) c += left_group(K[x - a + 1], kp, eq);
+            uint32_t cnt;
+            uint32_t pf = block_excl_scan<WG>(c, tmp, &cnt);
+            const int L = ta + (int)cnt;
+            uint32_t mine = 0;
+            for (int x = x0; x < x1; x++) {
+                const bool f = left_group(K[x - a + 1], kp, eq);
+                if (x > L && f) PR[(int)cnt - (int)pf - 1] = x;
+                if (x <= L && !f) {
+                    PL[(x - (ta + 1)) - (int)pf] = x;
+                    mine++;
+                }
+                pf += f;
+            }
+            uint32_t m;
+            block_excl_scan<WG>(mine, tmp, &m);  // total misplaced pairs (barriers)
+            for (int k = threadIdx.x; k < (int)m; k += WG) d.swap(PL[k], PR[k]);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int limit = sh[4], flags = sh[5];
+                if (eq) {
+                    const int na = ta + 1 + (int)cnt;
+                    if (tb - na > 1)
+                        stk[sh[0]++] = LTask{(int16_t)(na - a), (int16_t)(tb - a), (int16_t)limit,
+                                             (int16_t)flags};
+                } else {
+                    const int mid = ta + (int)cnt;
+                    d.swap(mid, ta);
+                    const int already = m == 0;
+                    const int tn = tb - ta, ln = mid - ta, rn = tb - mid, thr = tn / 8;
+                    LTask cont, fresh;
+                    if (ln < rn) {
+                        cont = LTask{(int16_t)(mid + 1 - a), (int16_t)(tb - a), (int16_t)limit,
+                                     (int16_t)((ln >= thr) | (already << 1))};
+                        fresh = LTask{(int16_t)(ta - a), (int16_t)(mid - a), (int16_t)limit, 3};
+                    } else {
+                        cont = LTask{(int16_t)(ta - a), (int16_t)(mid - a), (int16_t)limit,
+                                     (int16_t)((rn >= thr) | (already << 1))};
+                        fresh = LTask{(int16_t)(mid + 1 - a), (int16_t)(tb - a), (int16_t)limit, 3};
+                    }
+                    // larger side parked, smaller side next (depth <= log2 n)
+                    if (cont.b - cont.a > 1) stk[sh[0]++] = cont;
+                    if (fresh.b - fresh.a > 1) stk[sh[0]++] = fresh;
+                }
+            }
+            __syncthreads();
+        }
+        // ---- leaves: one lane each, Go's sequential loop
+        const int nt = sh[1];
+        for (int q = threadIdx.x; q < nt; q += WG) {
+            const LTask lt = tiny[q];
+            gocore::pdq_loop<LAcc, 12>(d, gocore::Task{a + lt.a, a + lt.b, lt.limit,
+                                                       (bool)(lt.flags & 1),
+                                                       (bool)(lt.flags & 2)});
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < n; q += WG) Ig[a + q] = I[q + 1];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- legacy
+// Go 1.8-1.18 sort.Sort (quickSort + gap-6 ShellSort pass), host restatement.
+struct HArr {
+    int32_t *idx;
+    const int64_t *len;
+    bool less(long i, long j) const { return len[idx[i]] > len[idx[j]]; }
+    void swap(long i, long j) const { std::swap(idx[i], idx[j]); }
+};
+
+static void h_insertion(const HArr &d, long a, long b) {
     for (long i = a + 1; i < b; i++)
         for (long j = i; j > a && d.less(j, j - 1); j--) d.swap(j, j - 1);
 }
 
-static void sift(const Arr &d, long lo, long hi, long first) {
+static void h_sift(const HArr &d, long lo, long hi, long first) {
     for (long root = lo;;) {
         long child = 2 * root + 1;
         if (child >= hi) return;
@@ -48,165 +548,16 @@ static void sift(const Arr &d, long lo, long hi, long first) {
     }
 }
 
-static void heap(const Arr &d, long a, long b) {
+static void h_heap(const HArr &d, long a, long b) {
     long hi = b - a;
-    for (long i = (hi - 1) / 2; i >= 0; i--) sift(d, i, hi, a);
+    for (long i = (hi - 1) / 2; i >= 0; i--) h_sift(d, i, hi, a);
     for (long i = hi - 1; i >= 0; i--) {
         d.swap(a, a + i);
-        sift(d, 0, i, a);
+        h_sift(d, 0, i, a);
     }
 }
 
-// ---- Go >= 1.19 pdqsort
-struct Pivot {
-    long pos;
-    int hint;  // 0 unknown, 1 increasing, 2 decreasing
-};
-
-static Pivot choose_pivot(const Arr &d, long a, long b) {
-    long l = b - a;
-    int swaps = 0;
-    long i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
-    auto order2 = [&](long &x, long &y) {
-        if (d.less(y, x)) {
-            swaps++;
-            long t = x;
-            x = y;
-            y = t;
-        }
-    };
-    auto median = [&](long x, long y, long z) {
-        order2(x, y);
-        order2(y, z);
-        order2(x, y);
-        return y;
-    };
-    if (l >= 8) {
-        if (l >= 50) {
-            i = median(i - 1, i, i + 1);
-            j = median(j - 1, j, j + 1);
-            k = median(k - 1, k, k + 1);
-        }
-        j = median(i, j, k);
-    }
-    return {j, swaps == 0 ? 1 : (swaps == 12 ? 2 : 0)};
-}
-
-static bool partial_insertion(const Arr &d, long a, long b) {
-    long i = a + 1;
-    for (int step = 0; step < 5; step++) {
-        while (i < b && !d.less(i, i - 1)) i++;
-        if (i == b) return true;
-        if (b - a < 50) return false;
-        d.swap(i, i - 1);
-        if (i - a >= 2)
-            for (long j = i - 1; j >= 1 && d.less(j, j - 1); j--) d.swap(j, j - 1);
-        if (b - i >= 2)
-            for (long j = i + 1; j < b && d.less(j, j - 1); j++) d.swap(j, j - 1);
-    }
-    return false;
-}
-
-static void break_patterns(const Arr &d, long a, long b) {
-    long n = b - a;
-    if (n < 8) return;
-    uint64_t r = (uint64_t)n;
-    unsigned long mod = 1ul << blen((unsigned long)n);
-    long idx = a + (n / 4) * 2 - 1;
-    for (int i = 0; i < 3; i++) {
-        r ^= r << 13;
-        r ^= r >> 7;
-        r ^= r << 17;
-        long other = (long)((unsigned long)r & (mod - 1));
-        if (other >= n) other -= n;
-        d.swap(idx - 1 + i, a + other);
-    }
-}
-
-static long partition_equal(const Arr &d, long a, long b, long pivot) {
-    d.swap(a, pivot);
-    long i = a + 1, j = b - 1;
-    for (;;) {
-        while (i <= j && !d.less(a, i)) i++;
-        while (i <= j && d.less(a, j)) j--;
-        if (i > j) return i;
-        d.swap(i, j);
-        i++;
-        j--;
-    }
-}
-
-static long partition(const Arr &d, long a, long b, long pivot, bool &already) {
-    d.swap(a, pivot);
-    long i = a + 1, j = b - 1;
-    while (i <= j && d.less(i, a)) i++;
-    while (i <= j && !d.less(j, a)) j--;
-    if (i > j) {
-        d.swap(j, a);
-        already = true;
-        return j;
-    }
-    d.swap(i, j);
-    i++;
-    j--;
-    for (;;) {
-        while (i <= j && d.less(i, a)) i++;
-        while (i <= j && !d.less(j, a)) j--;
-        if (i > j) break;
-        d.swap(i, j);
-        i++;
-        j--;
-    }
-    d.swap(j, a);
-    already = false;
-    return j;
-}
-
-static void pdq(const Arr &d, long a, long b, int limit) {
-    bool balanced = true, partitioned = true;
-    for (;;) {
-        long n = b - a;
-        if (n <= 12) {
-            insertion(d, a, b);
-            return;
-        }
-        if (limit == 0) {
-            heap(d, a, b);
-            return;
-        }
-        if (!balanced) {
-            break_patterns(d, a, b);
-            limit--;
-        }
-        Pivot pv = choose_pivot(d, a, b);
-        if (pv.hint == 2) {
-            for (long i = a, j = b - 1; i < j; i++, j--) d.swap(i, j);
-            pv.pos = (b - 1) - (pv.pos - a);
-            pv.hint = 1;
-        }
-        if (balanced && partitioned && pv.hint == 1 && partial_insertion(d, a, b)) return;
-        if (a > 0 && !d.less(a - 1, pv.pos)) {
-            a = partition_equal(d, a, b, pv.pos);
-            continue;
-        }
-        bool already;
-        long mid = partition(d, a, b, pv.pos, already);
-        partitioned = already;
-        long ln = mid - a, rn = b - mid, thr = n / 8;
-        if (ln < rn) {
-            balanced = ln >= thr;
-            pdq(d, a, mid, limit);
-            a = mid + 1;
-        } else {
-            balanced = rn >= thr;
-            pdq(d, mid + 1, b, limit);
-            b = mid;
-        }
-    }
-}
-
-// ---- Go 1.8-1.18 quickSort
-static void median3(const Arr &d, long m1, long m0, long m2) {
+static void median3(const HArr &d, long m1, long m0, long m2) {
     if (d.less(m1, m0)) d.swap(m1, m0);
     if (d.less(m2, m1)) {
         d.swap(m2, m1);
@@ -214,7 +565,7 @@ static void median3(const Arr &d, long m1, long m0, long m2) {
     }
 }
 
-static void do_pivot(const Arr &d, long lo, long hi, long &midlo, long &midhi) {
+static void do_pivot(const HArr &d, long lo, long hi, long &midlo, long &midhi) {
     long m = (long)((unsigned long)(lo + hi) >> 1);
     if (hi - lo > 40) {
         long s = (hi - lo) / 8;
@@ -268,10 +619,10 @@ static void do_pivot(const Arr &d, long lo, long hi, long &midlo, long &midhi) {
     midhi = c;
 }
 
-static void quick(const Arr &d, long a, long b, int depth) {
+static void quick(const HArr &d, long a, long b, int depth) {
     while (b - a > 12) {
         if (depth == 0) {
-            heap(d, a, b);
+            h_heap(d, a, b);
             return;
         }
         depth--;
@@ -288,43 +639,141 @@ static void quick(const Arr &d, long a, long b, int depth) {
     if (b - a > 1) {
         for (long i = a + 6; i < b; i++)
             if (d.less(i, i - 6)) d.swap(i, i - 6);
-        insertion(d, a, b);
+        h_insertion(d, a, b);
     }
 }
 
-static void sort_host(int32_t *idx, const int64_t *len, size_t n, int variant) {
-    for (size_t i = 0; i < n; i++) idx[i] = (int32_t)i;
-    Arr d{idx, len};
-    if (variant == 1) {
-        int depth = 0;
-        for (long i = (long)n; i > 0; i >>= 1) depth++;
-        quick(d, 0, (long)n, 2 * depth);
-    } else if (n > 1) {
-        pdq(d, 0, (long)n, blen(n));
-    }
-}
-
-}  // namespace gosort
+}  // namespace gsort
 }  // namespace syz
 
 using namespace syz;
+using namespace syz::gsort;
 
-extern "C" size_t syzcov_dev_sort_ws_size(size_t n) { return 256 + n * 0; }
+// workspace layout (all 256-B aligned)
+struct SortWs {
+    uint32_t *K;
+    int32_t *I, *PL, *PR;
+    Seg *segA, *segB, *small;
+    Plan *plan;
+    uint32_t *cc;
+    uint32_t *ctl;  // [0] err [1] countA [2] countB [3] small count [4] maxA [5] maxB
+    uint32_t seg_cap, small_cap, cc_stride;
+};
 
-extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
-                                     int32_t *order, void *ws, size_t ws_size, void *stream) {
-    (void)ws;
-    (void)ws_size;
-    if (n == 0) return 0;
-    if (!lens || !order || (sort_variant != 0 && sort_variant != 1) || n > 0x7FFFFFFF)
-        return SYZCOV_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
+static size_t ws_layout(size_t n, SortWs *w, uint8_t *base) {
+    const uint32_t seg_cap = (uint32_t)(2 * (n / SMALL) + 16);
+    const uint32_t small_cap = (uint32_t)(2 * (n / SMALL + 1) * 64 + 64);
+    const uint32_t cc_stride = (uint32_t)(n / CH + 2);
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o += align_up(bytes, 256);
+        return r;
+    };
+    size_t oK = take(n * 4), oI = take(n * 4), oPL = take(n * 4), oPR = take(n * 4),
+           oA = take(seg_cap * sizeof(Seg)), oB = take(seg_cap * sizeof(Seg)),
+           oS = take(small_cap * sizeof(Seg)), oP = take(seg_cap * sizeof(Plan)),
+           oC = take((size_t)seg_cap * cc_stride * 4), oT = take(64);
+    if (w) {
+        w->K = (uint32_t *)(base + oK);
+        w->I = (int32_t *)(base + oI);
+        w->PL = (int32_t *)(base + oPL);
+        w->PR = (int32_t *)(base + oPR);
+        w->segA = (Seg *)(base + oA);
+        w->segB = (Seg *)(base + oB);
+        w->small = (Seg *)(base + oS);
+        w->plan = (Plan *)(base + oP);
+        w->cc = (uint32_t *)(base + oC);
+        w->ctl = (uint32_t *)(base + oT);
+        w->seg_cap = seg_cap;
+        w->small_cap = small_cap;
+        w->cc_stride = cc_stride;
+    }
+    return o;
+}
+
+extern "C" size_t syzcov_dev_sort_ws_size(size_t n) { return ws_layout(n ? n : 1, nullptr, nullptr); }
+
+static int legacy_host(const int64_t *lens, size_t n, int32_t *order, hipStream_t s) {
     std::vector<int64_t> hl(n);
     std::vector<int32_t> ho(n);
     SYZ_HIP(hipMemcpyAsync(hl.data(), lens, n * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
-    gosort::sort_host(ho.data(), hl.data(), n, sort_variant);
+    for (size_t i = 0; i < n; i++) ho[i] = (int32_t)i;
+    HArr d{ho.data(), hl.data()};
+    int depth = 0;
+    for (long i = (long)n; i > 0; i >>= 1) depth++;
+    quick(d, 0, (long)n, 2 * depth);
     SYZ_HIP(hipMemcpyAsync(order, ho.data(), n * 4, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
+                                     int32_t *order, void *ws, size_t ws_size, void *stream) {
+    if (n == 0) return 0;
+    if (!lens || !order || (sort_variant != 0 && sort_variant != 1) || n > 0x7FFFFFFF)
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (sort_variant == 1) return legacy_host(lens, n, order, s);
+    if (!ws || ws_size < syzcov_dev_sort_ws_size(n)) return SYZCOV_EINVAL;
+    SortWs w;
+    ws_layout(n, &w, (uint8_t *)ws);
+    SYZ_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
+    hipLaunchKernelGGL(init_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, lens, (uint32_t)n,
+                       w.K, w.I, w.ctl);
+    Seg *cur = w.segA, *nxt = w.segB;
+    uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
+    Ctl c{cur, ccount, cmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
+    if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
+    SYZ_LAUNCH_CHECK();
+    uint32_t h[6];
+    SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    uint32_t ncur = h[1], maxlen = h[4];
+    for (int round = 0; ncur > 0; round++) {
+        if (round > 4096) return SYZCOV_EHIP;
+        // the children of this round go to nxt
+        SYZ_HIP(hipMemsetAsync(ncount, 0, 4, s));
+        SYZ_HIP(hipMemsetAsync(nmax, 0, 4, s));
+        Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
+        const unsigned gs = (ncur + 63) / 64;
+        const unsigned nch = (unsigned)((maxlen + CH - 1) / CH);
+        hipLaunchKernelGGL(plan_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I, cn);
+        hipLaunchKernelGGL(heap_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(reverse_kernel, dim3((nch + 1) / 2 + 1, ncur), dim3(WG), 0, s, cur,
+                           w.plan, w.K, w.I);
+        hipLaunchKernelGGL(pis_kernel, dim3(ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(eq_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.cc,
+                           w.cc_stride);
+        hipLaunchKernelGGL(cscan_kernel, dim3(ncur), dim3(WG), 0, s, cur, w.plan, w.cc, w.cc_stride);
+        hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.cc,
+                           w.cc_stride, w.PL, w.PR);
+        hipLaunchKernelGGL(swap_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.I, w.PL,
+                           w.PR);
+        hipLaunchKernelGGL(finish_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I, cn);
+        SYZ_LAUNCH_CHECK();
+        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+        if (h[0]) break;
+        ncur = h[ncount - w.ctl];
+        maxlen = h[nmax - w.ctl];
+        std::swap(cur, nxt);
+        std::swap(ccount, ncount);
+        std::swap(cmax, nmax);
+    }
+    if (!h[0] && h[3]) {
+        hipLaunchKernelGGL(small_kernel, dim3(std::min<uint32_t>(h[3], 8192)), dim3(WG), 0, s, w.small,
+                           w.ctl + 3, w.K, w.I, w.ctl);
+        SYZ_LAUNCH_CHECK();
+        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+    }
+    if (h[0]) {
+        set_error("device sort: internal error %u", h[0]);
+        return h[0] == 1 ? SYZCOV_EINVAL : SYZCOV_EHIP;
+    }
+    SYZ_HIP(hipMemcpyAsync(order, w.I, n * 4, hipMemcpyDeviceToDevice, s));
     return 0;
 }

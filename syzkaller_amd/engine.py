@@ -72,6 +72,7 @@ class CorpusEngine:
         self.max_cover = torch.zeros(span16, dtype=torch.uint8, device=dev)
         self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
         ids_cap = min(pc_span, p_max) + 1
+        self.ids_cap = ids_cap
         self.first = torch.empty(ids_cap, dtype=torch.int32, device=dev)
         self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
         self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
@@ -83,25 +84,32 @@ class CorpusEngine:
         ws = max(L.syzcov_dev_canon_ws_size(n_max, max_seg_len),
                  L.syzcov_dev_dict_ws_size(pc_span),
                  L.syzcov_dev_compact_ws_size(self.n_global),
-                 L.syzcov_dev_sort_ws_size(self.n_global))
+                 L.syzcov_dev_sort_ws_size(self.n_global),
+                 L.syzcov_dev_minimize_ws_size(ids_cap))
         self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
         self.ws_size = ws
 
     # ---------------------------------------------------------------- phases
-    def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        L, s = self.L, _stream()
+    PHASES = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
+
+    def mark(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+        """Presence map of the raw corpus (test-then-store, no atomics)."""
         self.pres.zero_()
         self.scal.zero_()
-        check(L.syzcov_dev_canonicalize(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
-                                        self.max_seg, _p(self.pres), self.pc_lo, self.span,
-                                        _p(self.scal), _p(self.ws), self.ws_size, s),
-              "dev_canonicalize")
+        check(self.L.syzcov_dev_mark(_p(off), None, _p(raw), n, _p(self.pres), self.pc_lo,
+                                     self.span, _p(self.scal), _stream()), "dev_mark")
 
     def build_dict(self):
-        L = self.L
-        nids = self.scal[1:2]
-        check(L.syzcov_dev_dict_build(_p(self.pres), self.span, _p(self.tab), _p(nids),
-                                      _p(self.ws), _stream()), "dev_dict_build")
+        check(self.L.syzcov_dev_dict_build(_p(self.pres), self.span, _p(self.tab),
+                                           _p(self.scal[1:2]), _p(self.ws), _stream()),
+              "dev_dict_build")
+
+    def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+        """Canonical covers in the dense-id space (LDS radix sort + unique)."""
+        check(self.L.syzcov_dev_canon_ids(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
+                                          self.max_seg, _p(self.tab), self.pc_lo, self.span,
+                                          _p(self.scal[1:2]), _p(self.scal), _p(self.ws),
+                                          self.ws_size, _stream()), "dev_canon_ids")
 
     def sort_order(self, lens32: torch.Tensor, n: int):
         """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
@@ -109,28 +117,23 @@ class CorpusEngine:
         check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
                                            _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
 
-    def minimize(self, off, n, order, ranks=None, n_items=None):
-        """Pass 1 + pass 2 over n_items work items (item j: input order[j],
-        rank ranks[j] or j); leaves kept[] indexed by rank."""
-        L, s = self.L, _stream()
-        n_items = n if n_items is None else n_items
+    def minimize(self, off, order, ranks, n_items, do_pass2=True):
+        """Chunked pass 1 (+ pass 2) over n_items work items; kept[] by rank."""
         self.first.fill_(INT32_MAX)
         self.kept.zero_()
-        check(L.syzcov_dev_minimize_pass1(_p(off), _p(self.new_len), _p(self.canon), _p(order),
-                                          _p(ranks), n_items, _p(self.tab), self.pc_lo,
-                                          _p(self.first), _p(self.cand), s), "dev_minimize_pass1")
-        return n_items
+        check(self.L.syzcov_dev_minimize_ids(
+            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items,
+            _p(self.scal[1:2]), self.ids_cap, _p(self.first), _p(self.cand), _p(self.kept),
+            int(do_pass2), _p(self.ws), _stream()), "dev_minimize_ids")
 
     def minimize_pass2(self, off, order, ranks, n_items):
-        check(self.L.syzcov_dev_minimize_pass2(
+        check(self.L.syzcov_dev_minimize_ids_pass2(
             _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items,
-            _p(self.tab), self.pc_lo, _p(self.first), _p(self.cand), _p(self.kept), _stream()),
-            "dev_minimize_pass2")
+            _p(self.first), _p(self.cand), _p(self.kept), _stream()), "dev_minimize_ids_pass2")
 
     def compact(self, n_ranks: int):
-        n_kept = self.scal[2:3]
         check(self.L.syzcov_dev_compact_kept(_p(self.kept), _p(self.order), n_ranks,
-                                             _p(self.out_idx), _p(n_kept), _p(self.ws),
+                                             _p(self.out_idx), _p(self.scal[2:3]), _p(self.ws),
                                              _stream()), "dev_compact_kept")
 
     def union_list(self):
@@ -143,30 +146,46 @@ class CorpusEngine:
               "dev_bytemap_op")
 
     # ------------------------------------------------------------------ step
-    def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True):
-        self.canonicalize(off, raw, n)
+    def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True, ev=None):
+        def mark_ev(i):
+            if ev is not None:
+                ev[i].record()
+        mark_ev(0)
+        self.mark(off, raw, n)
+        mark_ev(1)
         self.build_dict()
+        mark_ev(2)
+        self.canonicalize(off, raw, n)
+        mark_ev(3)
         self.sort_order(self.new_len, n)
-        self.minimize(off, n, self.order)
-        self.minimize_pass2(off, self.order, None, n)
+        mark_ev(4)
+        self.minimize(off, self.order, None, n)
+        mark_ev(5)
         self.compact(n)
+        mark_ev(6)
         self.union_list()
+        mark_ev(7)
         self.merge_max_cover()
-        if sync:
-            return self.result()
-        return None
+        mark_ev(8)
+        return self.result() if sync else None
 
     def result(self) -> StepResult:
         sc = self.scal.cpu().tolist()
         if sc[0] & 0xFFFFFFFF:
             raise RuntimeError("a PC fell outside the engine's PC window")
-        n_ids, n_kept, n_union, mc = (int(x) & 0xFFFFFFFF for x in sc[1:5])
+        n_ids, n_kept, n_union = (int(x) & 0xFFFFFFFF for x in sc[1:4])
         return StepResult(self.out_idx[:n_kept], n_kept, self.union[:n_union], n_union, n_ids,
                           int(sc[4]))
 
-    def check_error(self):
-        if int(self.scal[0].item()) & 0xFFFFFFFF:
-            raise RuntimeError("a PC fell outside the engine's PC window")
+    def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
+        """Materialise the canonical covers as PCs (CSR slots of `off`)."""
+        table = _u32(self.ids_cap, self.dev)
+        check(self.L.syzcov_dev_dict_pcs(_p(self.tab), self.span, self.pc_lo, _p(table),
+                                         _stream()), "dev_dict_pcs")
+        out = torch.zeros_like(self.canon)
+        check(self.L.syzcov_dev_gather_u32(_p(table), _p(off), _p(self.new_len), _p(self.canon),
+                                           n, _p(out), _stream()), "dev_gather_u32")
+        return out
 
 
 def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int = 512,

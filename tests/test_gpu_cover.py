@@ -115,6 +115,12 @@ def test_sort_order_matches_go(cover):
         for variant in (orc.PDQSORT, orc.LEGACY):
             assert np.array_equal(cover.SortOrder(lens, variant), orc.sort_order(lens, variant)), \
                 (trial, variant)
+    # C2-sized: 1M canonical lengths ~ N(2048, 512) (deep global rounds + LDS finisher)
+    lens = rng.normal(2048, 512, size=1_000_000).astype(np.int64).clip(1, 65535)
+    assert np.array_equal(cover.SortOrder(lens), orc.sort_order(lens))
+    # nearly sorted / reversed / all-equal at scale (partialInsertionSort, reverse, partitionEqual)
+    for lens in (np.sort(lens)[::-1].copy(), np.sort(lens), np.full(300_000, 7)):
+        assert np.array_equal(cover.SortOrder(lens), orc.sort_order(lens))
 
 
 def test_minimize_random_vs_oracle(cover):

@@ -42,7 +42,7 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
     c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
     # canonical covers, per input, in their CSR slots
-    canon = _to_np_u32(eng.canon)
+    canon = _to_np_u32(eng.canonical_pcs(off, n))
     new_len = eng.new_len[:n].cpu().numpy()
     offs = off.cpu().numpy()
     assert np.array_equal(new_len, np.diff(c_off).astype(np.int32))
@@ -76,7 +76,7 @@ def test_engine_properties_large(torch):
     assert np.all(np.diff(new_len[kept].astype(np.int64)) <= 0)
     order = eng.order[:n].cpu().numpy()
     assert kept[0] == order[0]
-    canon = _to_np_u32(eng.canon)
+    canon = _to_np_u32(eng.canonical_pcs(off, n))
     offs = off.cpu().numpy()
     kept_union = np.unique(np.concatenate([canon[offs[i]:offs[i] + new_len[i]] for i in kept]))
     assert np.array_equal(kept_union, _to_np_u32(res.union))
