@@ -109,6 +109,19 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
                                 size_t nprog, int C, int key_mode, const float *static_prios,
                                 float *out, uint32_t *raw_counts);
 
+/* prog.calcStaticPriorities (prog/prio.go:40-135) from the syscall usage
+ * table (usage id -> (call, weight) pairs, as noteUsage builds it, :42-104),
+ * in two CSR views: by id (id_off[nids+1], id_calls, id_w) and by call
+ * (call_off[C+1], call_ids = usage-id indices ascending, call_w = the call's
+ * weight in that id).  out: C*C float32, normalised (:133).  The reference
+ * sums in Go map order; the engine uses ascending id order. */
+int syzcov_static_priorities(const uint32_t *id_off, const uint16_t *id_calls, const float *id_w,
+                             size_t nids, const uint32_t *call_off, const uint32_t *call_ids,
+                             const float *call_w, int C, float *out);
+int syzcov_dev_static_prio(const uint32_t *id_off, const uint16_t *id_calls, const float *id_w,
+                           const uint32_t *call_off, const uint32_t *call_ids,
+                           const float *call_w, int C, float *out, void *stream);
+
 /* prog.normalizePrio (prog/prio.go:158-192), in place, C*C float32. */
 int syzcov_normalize_prio(float *prios, int C);
 

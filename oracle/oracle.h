@@ -70,6 +70,11 @@ void orc_normalize_prio(float *prios, int C);
 int orc_calculate_priorities(const int32_t *prog_len, size_t nprog, int C,
                              const float *static_prios, float *out);
 
+/* prog/prio.go:106-133 (calcStaticPriorities' accumulation, diagonal and
+ * normalisation) over a usage table in CSR form, ids in ascending order. */
+void orc_static_prio(const uint32_t *id_off, const uint16_t *id_calls, const float *id_w,
+                     size_t nids, int C, float *prios);
+
 /* prog/prio.go:202-228.  enabled[C] (0/1); run must hold C*C int64; rows of
  * disabled calls are left untouched (nil in Go) — the caller pre-fills them. */
 void orc_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run);

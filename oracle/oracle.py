@@ -51,6 +51,7 @@ def lib():
         _lib.orc_calculate_priorities.argtypes = [p, sz, C.c_int, p, p]
         _lib.orc_calculate_priorities.restype = C.c_int
         _lib.orc_build_choice_table.argtypes = [p, p, C.c_int, p]
+        _lib.orc_static_prio.argtypes = [p, p, p, sz, C.c_int, p]
         _lib.orc_synth_len.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]
         _lib.orc_synth_len.restype = C.c_uint32
         _lib.orc_synth_input.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
@@ -222,3 +223,21 @@ def canonicalize_csr(off, pcs):
     for i in range(n):
         outs.append(canonicalize(pcs[off[i]:off[i + 1]]))
     return to_csr(outs)
+
+
+def static_prio(table: dict) -> np.ndarray:
+    """calcStaticPriorities over the usage table JSON (ids ascending)."""
+    ids = sorted(table["uses"])
+    off = np.zeros(len(ids) + 1, np.uint32)
+    calls, ws = [], []
+    for k, ident in enumerate(ids):
+        for c, w in sorted(table["uses"][ident]):
+            calls.append(c)
+            ws.append(w)
+        off[k + 1] = len(calls)
+    calls = np.asarray(calls, np.uint16)
+    ws = np.asarray(ws, np.float32)
+    C_ = table["ncalls"]
+    out = np.zeros((C_, C_), np.float32)
+    lib().orc_static_prio(_ptr(off), _ptr(calls), _ptr(ws), len(ids), C_, _ptr(out))
+    return out

@@ -66,6 +66,29 @@ int orc_calculate_priorities(const int32_t *prog_len, size_t nprog, int C,
     return 0;
 }
 
+/* prog/prio.go:106-133 over a usage table (id -> (call, weight) pairs, ids in
+ * the order given; Go walks its `uses` map in random order, this restatement
+ * fixes ascending id order). */
+void orc_static_prio(const uint32_t *id_off, const uint16_t *id_calls, const float *id_w,
+                     size_t nids, int C, float *prios) {
+    memset(prios, 0, (size_t)C * (size_t)C * sizeof(float));
+    for (size_t k = 0; k < nids; k++) /* for _, calls := range uses */
+        for (uint32_t a = id_off[k]; a < id_off[k + 1]; a++)     /* c0, w0 */
+            for (uint32_t b = id_off[k]; b < id_off[k + 1]; b++) { /* c1, w1 */
+                int c0 = id_calls[a], c1 = id_calls[b];
+                if (c0 == c1) continue;
+                float prod = id_w[a] * id_w[b];
+                prios[(size_t)c0 * C + c1] += prod;
+            }
+    for (int c0 = 0; c0 < C; c0++) { /* :124-132 */
+        float max = 0;
+        for (int j = 0; j < C; j++)
+            if (max < prios[(size_t)c0 * C + j]) max = prios[(size_t)c0 * C + j];
+        prios[(size_t)c0 * C + c0] = max;
+    }
+    orc_normalize_prio(prios, C); /* :133 */
+}
+
 /* prog/prio.go:202-228 */
 void orc_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run) {
     for (int i = 0; i < C; i++) {

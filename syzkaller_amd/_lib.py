@@ -48,6 +48,8 @@ _SIGS = {
     "syzcov_sort_order": (C.c_int, [p_, sz, C.c_int, p_]),
     "syzcov_union_all": (i64, [p_, p_, sz, p_]),
     "syzcov_calculate_priorities": (C.c_int, [p_, p_, sz, C.c_int, C.c_int, p_, p_, p_]),
+    "syzcov_static_priorities": (C.c_int, [p_, p_, p_, sz, p_, p_, p_, C.c_int, p_]),
+    "syzcov_dev_static_prio": (C.c_int, [p_, p_, p_, p_, p_, p_, C.c_int, p_, p_]),
     "syzcov_normalize_prio": (C.c_int, [p_, C.c_int]),
     "syzcov_build_choice_table": (C.c_int, [p_, p_, C.c_int, p_]),
     "syzcov_state_create": (C.c_int, [C.c_int, u32, u64, p_]),

@@ -482,6 +482,34 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
     return 0;
 }
 
+int syzcov_static_priorities(const uint32_t *id_off, const uint16_t *id_calls, const float *id_w,
+                             size_t nids, const uint32_t *call_off, const uint32_t *call_ids,
+                             const float *call_w, int C, float *out) {
+    if (C <= 0 || !id_off || !call_off || !out) return SYZCOV_EINVAL;
+    const size_t nm = id_off[nids], nc = call_off[C];
+    if ((nm && (!id_calls || !id_w)) || (nc && (!call_ids || !call_w))) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_io = p.add((nids + 1) * 4), i_ic = p.add(nm * 2), i_iw = p.add(nm * 4),
+           i_co = p.add(((size_t)C + 1) * 4), i_ci = p.add(nc * 4), i_cw = p.add(nc * 4),
+           i_o = p.add((size_t)C * C * 4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_io], id_off, (nids + 1) * 4, hipMemcpyHostToDevice, c->s));
+    if (nm) CK(hipMemcpyAsync(b[i_ic], id_calls, nm * 2, hipMemcpyHostToDevice, c->s));
+    if (nm) CK(hipMemcpyAsync(b[i_iw], id_w, nm * 4, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_co], call_off, ((size_t)C + 1) * 4, hipMemcpyHostToDevice, c->s));
+    if (nc) CK(hipMemcpyAsync(b[i_ci], call_ids, nc * 4, hipMemcpyHostToDevice, c->s));
+    if (nc) CK(hipMemcpyAsync(b[i_cw], call_w, nc * 4, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_static_prio((uint32_t *)b[i_io], (uint16_t *)b[i_ic], (float *)b[i_iw],
+                              (uint32_t *)b[i_co], (uint32_t *)b[i_ci], (float *)b[i_cw], C,
+                              (float *)b[i_o], c->s));
+    CK(hipMemcpyAsync(out, b[i_o], (size_t)C * C * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    return 0;
+}
+
 int syzcov_normalize_prio(float *prios, int C) {
     if (C <= 0 || !prios) return SYZCOV_EINVAL;
     Ctx *c = ctx();

@@ -34,6 +34,41 @@ __global__ void mark_kernel(const uint64_t *__restrict__ off, const uint32_t *__
     }
 }
 
+// Contiguous corpus (lengths from offsets): mark is a flat stream over
+// pcs[off[0] .. off[n]) with 16-byte vector loads (head/tail scalar).
+__device__ __forceinline__ void mark_one(uint8_t *__restrict__ pres, uint32_t pc, uint32_t pc_lo,
+                                         uint64_t pc_span, uint32_t *__restrict__ err) {
+    const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
+    if (pc < pc_lo || o >= pc_span) {
+        *err = 1u;
+        return;
+    }
+    if (pres[o] == 0) pres[o] = 1;
+}
+
+__global__ void mark_flat_kernel(const uint64_t *__restrict__ off, size_t nseg,
+                                 const uint32_t *__restrict__ pcs, uint8_t *__restrict__ pres,
+                                 uint32_t pc_lo, uint64_t pc_span, uint32_t *__restrict__ err) {
+    const uint64_t start = off[0], end = off[nseg];
+    // first 16-B aligned element at or after start
+    const uint64_t a0 = (start + 3) & ~3ull;
+    const uint64_t head_end = a0 < end ? a0 : end;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    if (tid < head_end - start) mark_one(pres, pcs[start + tid], pc_lo, pc_span, err);
+    const uint64_t nvec = end > a0 ? (end - a0) / 4 : 0;
+    const uint4 *v = (const uint4 *)(pcs + a0);
+    for (uint64_t i = tid; i < nvec; i += nthr) {
+        const uint4 x = v[i];
+        mark_one(pres, x.x, pc_lo, pc_span, err);
+        mark_one(pres, x.y, pc_lo, pc_span, err);
+        mark_one(pres, x.z, pc_lo, pc_span, err);
+        mark_one(pres, x.w, pc_lo, pc_span, err);
+    }
+    const uint64_t tail = a0 + nvec * 4;
+    if (end > tail && tid < end - tail) mark_one(pres, pcs[tail + tid], pc_lo, pc_span, err);
+}
+
 // Pass A: each thread packs WPT consecutive 32-byte groups into words,
 // writes {in-block exclusive prefix | bits << 32}, block total -> bsum[blk].
 constexpr int DICT_THREADS = 256, DICT_WPT = 4, DICT_WPB = DICT_THREADS * DICT_WPT;
@@ -229,8 +264,13 @@ extern "C" int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const u
                                uint32_t *err_flag, void *stream) {
     if (nseg == 0) return 0;
     if (!off || !pcs || !pres || !err_flag) return SYZCOV_EINVAL;
-    hipLaunchKernelGGL(mark_kernel, dim3(grid_for(nseg, 1, 8192)), dim3(256), 0,
-                       (hipStream_t)stream, off, len, pcs, nseg, pres, pc_lo, pc_span, err_flag);
+    if (!len)  // contiguous CSR: one flat vectorised stream
+        hipLaunchKernelGGL(mark_flat_kernel, dim3(256 * 16), dim3(256), 0, (hipStream_t)stream,
+                           off, nseg, pcs, pres, pc_lo, pc_span, err_flag);
+    else
+        hipLaunchKernelGGL(mark_kernel, dim3(grid_for(nseg, 1, 8192)), dim3(256), 0,
+                           (hipStream_t)stream, off, len, pcs, nseg, pres, pc_lo, pc_span,
+                           err_flag);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -298,9 +298,56 @@ __global__ __launch_bounds__(FIN_THREADS) void choice_table_kernel(
     }
 }
 
+// calcStaticPriorities (prio.go:40-135) from the usage table: one workgroup
+// per row c0 accumulates prios[c0][c1] += w0 * w1 over the usage ids holding
+// c0 in ascending id order (one fixed order of Go's map walk; the members of
+// one id are distinct calls, so a row update per id is race-free), sets the
+// diagonal to the row max (:124-132) and normalises the row (:133).
+__global__ __launch_bounds__(FIN_THREADS) void static_prio_kernel(
+    const uint32_t *__restrict__ id_off, const uint16_t *__restrict__ id_calls,
+    const float *__restrict__ id_w, const uint32_t *__restrict__ call_off,
+    const uint32_t *__restrict__ call_ids, const float *__restrict__ call_w, int C,
+    float *__restrict__ out) {
+    extern __shared__ float row[];
+    __shared__ float red[3 * FIN_THREADS / 64];
+    const int c0 = blockIdx.x;
+    for (int j = threadIdx.x; j < C; j += FIN_THREADS) row[j] = 0.0f;
+    __syncthreads();
+    for (uint32_t q = call_off[c0]; q < call_off[c0 + 1]; q++) {
+        const uint32_t id = call_ids[q];
+        const float w0 = call_w[q];
+        for (uint32_t m = id_off[id] + threadIdx.x; m < id_off[id + 1]; m += FIN_THREADS) {
+            const int c1 = id_calls[m];
+            if (c1 != c0) row[c1] = __fadd_rn(row[c1], __fmul_rn(w0, id_w[m]));
+        }
+        __syncthreads();
+    }
+    // diagonal = row max (the diagonal itself is still 0 here)
+    float mx = 0.0f, mn;
+    int nz;
+    row_stats<FIN_THREADS>(row, C, &mx, &mn, &nz, red);
+    if (threadIdx.x == 0) row[c0] = mx;
+    __syncthreads();
+    normalize_row<FIN_THREADS>(row, C, red);
+    for (int j = threadIdx.x; j < C; j += FIN_THREADS) out[(size_t)c0 * C + j] = row[j];
+}
+
 }  // namespace syz
 
 using namespace syz;
+
+extern "C" int syzcov_dev_static_prio(const uint32_t *id_off, const uint16_t *id_calls,
+                                      const float *id_w, const uint32_t *call_off,
+                                      const uint32_t *call_ids, const float *call_w, int C,
+                                      float *out, void *stream) {
+    if (C <= 0 || !id_off || !id_calls || !id_w || !call_off || !call_ids || !call_w || !out)
+        return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(static_prio_kernel, dim3(C), dim3(FIN_THREADS), C * sizeof(float),
+                       (hipStream_t)stream, id_off, id_calls, id_w, call_off, call_ids, call_w, C,
+                       out);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" size_t syzcov_dev_prio_rows(int C) { return prio_rows(C); }
 extern "C" size_t syzcov_dev_prio_ldp(size_t nprog) { return prio_ldp(nprog); }

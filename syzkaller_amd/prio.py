@@ -34,8 +34,64 @@ def _csr(corpus):
     return off, np.ascontiguousarray(ids, dtype=np.uint16)
 
 
+_TABLE = None
+
+
+def sys_table():
+    """The syscall usage table (sys/*.txt restated by tools/gen_sys_table.py):
+    1170 calls in Call.ID order, CallID per call, usage id -> [(call, weight)]."""
+    global _TABLE
+    if _TABLE is None:
+        import json
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "sys_table.json")
+        with open(path) as f:
+            _TABLE = json.load(f)
+    return _TABLE
+
+
+def usage_csr(table=None):
+    """Both CSR views of the usage table (see syzcov_static_priorities)."""
+    t = table or sys_table()
+    C_ = t["ncalls"]
+    ids = sorted(t["uses"])
+    id_off = np.zeros(len(ids) + 1, np.uint32)
+    calls, ws = [], []
+    by_call = [[] for _ in range(C_)]
+    for k, ident in enumerate(ids):
+        members = sorted(t["uses"][ident])
+        for c, w in members:
+            calls.append(c)
+            ws.append(w)
+            by_call[c].append((k, w))
+        id_off[k + 1] = len(calls)
+    call_off = np.zeros(C_ + 1, np.uint32)
+    cids, cws = [], []
+    for c in range(C_):
+        for k, w in by_call[c]:
+            cids.append(k)
+            cws.append(w)
+        call_off[c + 1] = len(cids)
+    return (id_off, np.asarray(calls, np.uint16), np.asarray(ws, np.float32), call_off,
+            np.asarray(cids, np.uint32), np.asarray(cws, np.float32), C_)
+
+
+def StaticPriorities(table=None) -> np.ndarray:
+    """calcStaticPriorities (prio.go:40-135) on the GPU."""
+    id_off, calls, ws, call_off, cids, cws, C_ = usage_csr(table)
+    out = np.empty((C_, C_), dtype=np.float32)
+    check(lib().syzcov_static_priorities(
+        _ptr(id_off), _ptr(calls), _ptr(ws), id_off.size - 1, _ptr(call_off), _ptr(cids),
+        _ptr(cws), C_, _ptr(out)), "StaticPriorities")
+    return out
+
+
 def CalculatePriorities(corpus, static=None, ncalls: int | None = None, key_mode: int = 0,
                         return_raw: bool = False):
+    """prio.go:29-38.  static=None with ncalls=None uses the sys/*.txt table
+    (calcStaticPriorities on the GPU) like the reference does."""
+    if static is None and ncalls is None:
+        static = StaticPriorities()
     if static is not None:
         static = np.ascontiguousarray(static, dtype=np.float32)
         C_ = static.shape[0]

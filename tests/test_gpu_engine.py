@@ -100,6 +100,23 @@ def test_prio_positional_vs_oracle(torch):
         assert np.array_equal(got, exp)  # and in fact bit-exact
 
 
+def test_static_prio_vs_oracle(torch):
+    """calcStaticPriorities over all sys/*.txt calls (1170) on the GPU vs the
+    float32 restatement (same ascending-id summation order): bit-exact."""
+    from syzkaller_amd import prio
+    st = prio.StaticPriorities()
+    exp = orc.static_prio(prio.sys_table())
+    assert st.shape == (1170, 1170)
+    np.testing.assert_allclose(st, exp, rtol=1e-6, atol=0)
+    assert np.array_equal(st, exp)
+    # and the default CalculatePriorities path multiplies it in (prio.go:32-36)
+    rng = np.random.default_rng(2)
+    lens = rng.integers(1, 40, size=500)
+    corpus = [[0] * int(l) for l in lens]
+    got = prio.CalculatePriorities(corpus)
+    assert np.array_equal(got, orc.calculate_priorities(lens, exp))
+
+
 def test_prio_by_id_vs_numpy(torch):
     from syzkaller_amd import prio
     rng = np.random.default_rng(8)
