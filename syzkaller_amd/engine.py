@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from ._lib import check, lib
@@ -186,6 +187,66 @@ class CorpusEngine:
         check(self.L.syzcov_dev_gather_u32(_p(table), _p(off), _p(self.new_len), _p(self.canon),
                                            n, _p(out), _stream()), "dev_gather_u32")
         return out
+
+
+class PrioEngine:
+    """Device-resident prog.CalculatePriorities (prio.go:29-38) for a corpus of
+    `nprog` programs given by their lengths (positional key mode, exactly the
+    reference's calcDynamicPrio) over the C = 1170 calls of sys/*.txt."""
+
+    PHASES = ("static", "build", "gemm", "finish")
+
+    def __init__(self, nprog: int, device="cuda", table=None):
+        from . import prio as P
+        L = lib()
+        self.L, self.dev = L, torch.device(device)
+        id_off, calls, ws, call_off, cids, cws, C_ = P.usage_csr(table)
+        def dev_copy(a):  # unsigned arrays travel as same-width signed views
+            return torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
+        self.id_off = dev_copy(id_off.view(np.int32))
+        self.calls = dev_copy(calls.view(np.int16))
+        self.ws = dev_copy(ws)
+        self.call_off = dev_copy(call_off.view(np.int32))
+        self.cids = dev_copy(cids.view(np.int32))
+        self.cws = dev_copy(cws)
+        self.C = C_
+        self.nprog = nprog
+        self.rows = L.syzcov_dev_prio_rows(C_)
+        self.ldp = L.syzcov_dev_prio_ldp(nprog)
+        self.at = torch.empty(self.rows * self.ldp, dtype=torch.int8, device=self.dev)
+        self.counts = torch.empty(self.rows * self.rows, dtype=torch.int32, device=self.dev)
+        self.static = torch.empty(C_ * C_, dtype=torch.float32, device=self.dev)
+        self.out = torch.empty(C_ * C_, dtype=torch.float32, device=self.dev)
+        self.err = torch.zeros(4, dtype=torch.int32, device=self.dev)
+
+    def gemm_ops(self) -> int:
+        """MFMA ops one counts launch executes (upper-triangle 128x128 tiles)."""
+        nt = self.rows // 128
+        return nt * (nt + 1) // 2 * 128 * 128 * 2 * self.ldp
+
+    def step(self, lens: torch.Tensor, ev=None):
+        L, s = self.L, _stream()
+
+        def mark_ev(i):
+            if ev is not None:
+                ev[i].record()
+        mark_ev(0)
+        check(L.syzcov_dev_static_prio(_p(self.id_off), _p(self.calls), _p(self.ws),
+                                       _p(self.call_off), _p(self.cids), _p(self.cws), self.C,
+                                       _p(self.static), s), "dev_static_prio")
+        mark_ev(1)
+        check(L.syzcov_dev_prio_build_at(0, _p(lens), None, None, self.nprog, self.C,
+                                         _p(self.at), self.ldp, _p(self.err), s),
+              "dev_prio_build_at")
+        self.counts.zero_()
+        mark_ev(2)
+        check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
+                                       _p(self.counts), s), "dev_prio_counts")
+        mark_ev(3)
+        check(L.syzcov_dev_prio_finish(_p(self.counts), self.C, _p(self.static), _p(self.out),
+                                       None, s), "dev_prio_finish")
+        mark_ev(4)
+        return self.out
 
 
 def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int = 512,
