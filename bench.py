@@ -1,16 +1,21 @@
 #!/usr/bin/env python3
-"""Headline benchmark: input-PCs processed/sec for Canonicalize + Minimize +
-maxCover Union on MI355X (BASELINE.json metric, config C2 at N=1; the same
-per-GPU shard with RCCL merges at N>1, weak scaling).
+"""Benchmarks of the syzkaller coverage hot path on MI355X.
+
+Default (the driver's headline line): input-PCs processed/sec for
+Canonicalize + Minimize + maxCover Union (BASELINE.json metric; config C2 at
+N=1, the same per-GPU shard with RCCL merges at N>1 — weak scaling).
 
 One step = one pass of the hot path over one synthetic corpus already
 resident in HBM (raw KCOV lists, CSR):
-  Canonicalize every input -> dense-id dictionary (= corpus union) ->
-  Go sort.Sort order -> Minimize (first-cover pass 1/2 + ordered compaction) ->
-  sorted Union list -> maxCover merge.
+  mark (presence) -> dense-id dictionary (= corpus union) -> Canonicalize
+  (id space) -> Go sort.Sort order -> Minimize (chunked first-cover pass 1 +
+  pass 2) -> ordered compaction -> sorted Union list -> maxCover merge.
 Prints ONE JSON line (rank 0).  Per-phase device times come from HIP events
 on the stream the kernels run on; the dominant kernel's roofline uses its
-ALGORITHMIC bytes (DESIGN.md §Measurement).
+ALGORITHMIC bytes (DESIGN.md §4, §6).
+
+--workload prio: config C4 (CalculatePriorities, 1M programs x 1170 calls,
+i8 MFMA AᵀA) — a separate line with an MFMA roofline.
 """
 from __future__ import annotations
 
@@ -24,8 +29,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED = 0x5EED0002
+SEED_PRIO = 0x5EED0004
 
 
 def parse():
@@ -33,7 +40,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inputs", type=int, default=1_000_000, help="inputs per GPU")
+    ap.add_argument("--workload", choices=["corpus", "prio"], default="corpus")
+    ap.add_argument("--inputs", type=int, default=1_000_000, help="inputs (programs) per GPU")
     ap.add_argument("--mean", type=int, default=2048)
     ap.add_argument("--sigma", type=int, default=512)
     ap.add_argument("--log2-space", type=int, default=22)
@@ -58,24 +66,35 @@ def cpu_baseline(args):
     t2 = time.perf_counter()
     orc.union_fold_csr(c_off, c_pcs)
     t3 = time.perf_counter()
-    total = t3 - t0
     return {
-        "value": raw_pcs / total, "unit": "input-PCs/s", "cores": 1, "kind": "port",
+        "value": raw_pcs / (t3 - t0), "unit": "input-PCs/s", "cores": 1, "kind": "port",
         "sample": (f"first {n} inputs of the same synthetic corpus ({raw_pcs} raw PCs): "
                    f"Canonicalize {t1 - t0:.2f}s + Minimize {t2 - t1:.2f}s + Union fold "
                    f"{t3 - t2:.2f}s, 1 thread, oracle/ C restatement of cover/cover.go "
-                   f"(Go toolchain absent); the reference's Union fold is O(N*|U|) so the "
+                   f"(Go toolchain absent); the reference's Union fold is O(N*|U|), so the "
                    f"CPU rate falls further as N grows"),
         "host": platform.processor() or platform.machine(),
         "nproc": os.cpu_count(),
     }
 
 
-def main():
-    args = parse()
+def cpu_baseline_prio(nprog: int, C: int):
+    from oracle import oracle as orc
+    import numpy as np
+    orc.lib()
+    lens = orc.synth_lens(SEED_PRIO, nprog, 30, 8)
+    static = np.ones((C, C), np.float32)
+    t0 = time.perf_counter()
+    orc.calculate_priorities(lens.astype(np.int32), static)
+    dt = time.perf_counter() - t0
+    return {"value": nprog / dt, "unit": "programs/s", "cores": 1, "kind": "port",
+            "sample": f"{nprog} programs, calcDynamicPrio + normalizePrio + combine, "
+                      f"oracle/ C restatement of prog/prio.go, 1 thread"}
+
+
+def init_dist():
     import torch
     import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -84,58 +103,64 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
+    return world, rank, dev
 
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
 
-    n = args.inputs
-    lo, span = synth_window(args.log2_space)
-    off, raw, lens, total = synth_corpus(n, SEED, first=rank * n, mean=args.mean,
-                                         sigma=args.sigma, log2_space=args.log2_space, device=dev)
-    max_len = int(lens.max().item())
-    if world > 1:
-        from syzkaller_amd import dist as sdist
-        eng = sdist.ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev)
-    else:
-        eng = CorpusEngine(n, total, max_len, lo, span, device=dev)
-    torch.cuda.synchronize()
-
-    phases = list(eng.PHASES)
-
-    def run_step(ev=None):
-        eng.step(off, raw, n, sync=False, ev=ev)
-
+def timed(run_step, nphase, args, world, dev):
+    """W warmup steps, then K timed steps bracketed by barrier + sync; per-phase
+    HIP-event times; returns (seconds (max over ranks), per-phase ms)."""
+    import torch
+    import torch.distributed as dist
     for _ in range(args.warmup):
-        run_step()
+        run_step(None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     evs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(nphase + 1)]
         run_step(ev)
         evs.append(ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    res = eng.result()
-    dt = t1 - t0
+    dt = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    # per-phase device times (ms, averaged over steps)
-    ph = {p: 0.0 for p in phases}
+    ph = [0.0] * nphase
     for ev in evs:
-        for i, p in enumerate(phases):
-            ph[p] += ev[i].elapsed_time(ev[i + 1]) / len(evs)
+        for i in range(nphase):
+            ph[i] += ev[i].elapsed_time(ev[i + 1]) / len(evs)
+    return dt, ph
+
+
+def bench_corpus(args):
+    import torch
+    world, rank, dev = init_dist()
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    n = args.inputs
+    lo, span = synth_window(args.log2_space)
+    off, raw, lens, total = synth_corpus(n, SEED, first=rank * n, mean=args.mean,
+                                         sigma=args.sigma, log2_space=args.log2_space, device=dev)
+    max_len = int(lens.max().item())
+    if world > 1:
+        from syzkaller_amd.dist import ShardedEngine
+        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev)
+    else:
+        eng = CorpusEngine(n, total, max_len, lo, span, device=dev)
+    torch.cuda.synchronize()
+    phases = list(eng.PHASES)
+    dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), args,
+                    world, dev)
+    ph = dict(zip(phases, phl))
+    res = eng.result()
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
-    total_all = total * world
-    value = total_all * args.steps / dt
-    # dominant kernel roofline: algorithmic bytes per launch / launch time
-    # mark: read raw (4 B/PC); canon: read raw + write canonical ids;
-    # minimize: read canonical ids once (pass 2 only re-reads candidates)
+    value = total * world * args.steps / dt
+    # algorithmic bytes per launch (DESIGN.md §4): mark reads raw (4 B/PC);
+    # canon reads raw + writes canonical ids; minimize reads canonical ids once
     alg = {"mark": 4 * total, "canon": 4 * total + 4 * canon_pcs, "minimize": 4 * canon_pcs}
     dom = max(alg, key=lambda p: ph[p])
     achieved = alg[dom] / (ph[dom] * 1e-3) / 1e9
@@ -145,23 +170,75 @@ def main():
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (counter-based generator, SURVEY §8d)",
-        "config": {"workload": "C2: Canonicalize + Minimize + maxCover union",
+        "config": {"workload": "C2: Canonicalize + Minimize + maxCover union"
+                               + (" (C3 sharding)" if world > 1 else ""),
                    "inputs_per_gpu": n, "global_inputs": n * world, "raw_pcs_per_gpu": total,
                    "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
                    "len_mean": args.mean, "len_sigma": args.sigma,
                    "parallelism": f"shard-by-input x{world}"},
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},
-        "results": {"kept": res.n_kept, "union": res.n_union, "max_cover": res.max_cover},
+        "results": {"kept": res.n_kept, "union": res.n_union, "max_cover": res.max_cover,
+                    "n_ids": res.n_ids},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "alg_bytes_per_launch": alg[dom]},
+        "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph["compact"]
+                                                          + ph["union"] + ph["merge"]) * 1e-3),
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = value / out["cpu_baseline"]["value"]
+    return rank, world, out
+
+
+def bench_prio(args):
+    import ctypes as C
+    import torch
+    world, rank, dev = init_dist()
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import PrioEngine
+    L = _lib.lib()
+    nprog = args.inputs
+    eng = PrioEngine(nprog, device=dev)
+    lens = torch.empty(nprog, dtype=torch.int32, device=dev)
+    _lib.check(L.syzcov_dev_synth_lens(SEED_PRIO, rank * nprog, nprog, 30, 8,
+                                       C.c_void_p(lens.data_ptr()),
+                                       C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+               "synth_lens")
+    torch.cuda.synchronize()
+    phases = list(eng.PHASES)
+    dt, phl = timed(lambda ev: eng.step(lens, ev), len(phases), args, world, dev)
+    ph = dict(zip(phases, phl))
+    ops = eng.gemm_ops()
+    achieved = ops / (ph["gemm"] * 1e-3) / 1e12
+    out = {
+        "metric": "programs/sec for CalculatePriorities (static + i8-MFMA AᵀA dynamic + normalize)",
+        "value": nprog * world * args.steps / dt, "unit": "programs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "i8",
+        "data": "synthetic program lengths ~ N(30, 8) (SURVEY §8d C4)",
+        "config": {"workload": "C4: CalculatePriorities, positional (reference-exact) keys",
+                   "programs_per_gpu": nprog, "calls": eng.C, "at_rows": eng.rows,
+                   "at_cols": eng.ldp},
+        "phases_ms": {k: round(v, 4) for k, v in ph.items()},
+        "roofline": {"bound": "mfma", "kernel": "prio_gemm", "achieved": achieved,
+                     "peak": I8_PEAK_TOPS, "unit": "TOPS", "frac": achieved / I8_PEAK_TOPS,
+                     "traffic": None, "mfma_ops_per_launch": ops,
+                     "algorithmic_ops_2NC2": 2 * nprog * eng.C * eng.C},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_prio(min(nprog, 200_000), eng.C)
+    return rank, world, out
+
+
+def main():
+    args = parse()
+    fn = bench_prio if args.workload == "prio" else bench_corpus
+    rank, world, out = fn(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
