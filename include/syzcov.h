@@ -170,6 +170,23 @@ int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const uint32_t *pc
                     uint8_t *pres, uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag,
                     void *stream);
 
+/* Bit-packed presence (engine default): bit (pc - pc_lo) of bits[] (u32
+ * words, zeroed by the caller) is set for every PC of the contiguous CSR
+ * corpus; test-before-atomicOr.  The bitmap is 1/8 of the byte map, so the
+ * hot part of the window stays in L2.  The byte form is only used to merge
+ * shards (RCCL uint8 MAX); the conversions below are exact. */
+int syzcov_dev_mark_bits(const uint64_t *off, const uint32_t *pcs, size_t nseg, uint32_t *bits,
+                         uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag, void *stream);
+/* bytes must hold ceil(nbits/32)*32 bytes. */
+int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nbits, uint8_t *bytes, void *stream);
+int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nbits, uint32_t *bits, void *stream);
+/* Bitmap set algebra on u32 words (ops as syzcov_dev_bytemap_op) + popcount. */
+int syzcov_dev_bitmap_op(int op, uint32_t *dst, const uint32_t *src, uint64_t nwords,
+                         uint64_t *popcount_out, void *stream);
+/* Dictionary from a presence bitmap (see syzcov_dev_dict_build). */
+int syzcov_dev_dict_build_bits(const uint32_t *bits, uint64_t pc_span, uint64_t *tab,
+                               uint32_t *n_ids, void *ws, void *stream);
+
 /* Dense PC-id dictionary from a presence map: tab[w] = {prefix:32 | bits:32}
  * for 32-PC word w (prefix = set bits before w).  *n_ids receives the total
  * (device u32).  ws: syzcov_dev_dict_ws_size(pc_span). */

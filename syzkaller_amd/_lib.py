@@ -62,6 +62,11 @@ _SIGS = {
     "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
     "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
     "syzcov_dev_mark": (C.c_int, [p_, p_, p_, sz, p_, u32, u64, p_, p_]),
+    "syzcov_dev_mark_bits": (C.c_int, [p_, p_, sz, p_, u32, u64, p_, p_]),
+    "syzcov_dev_bits_to_bytes": (C.c_int, [p_, u64, p_, p_]),
+    "syzcov_dev_bytes_to_bits": (C.c_int, [p_, u64, p_, p_]),
+    "syzcov_dev_bitmap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),
+    "syzcov_dev_dict_build_bits": (C.c_int, [p_, u64, p_, p_, p_, p_]),
     "syzcov_dev_dict_ws_size": (sz, [u64]),
     "syzcov_dev_dict_build": (C.c_int, [p_, u64, p_, p_, p_, p_]),
     "syzcov_dev_dict_to_list": (C.c_int, [p_, u64, u32, p_, p_, p_]),

@@ -69,6 +69,117 @@ __global__ void mark_flat_kernel(const uint64_t *__restrict__ off, size_t nseg,
     if (end > tail && tid < end - tail) mark_one(pres, pcs[tail + tid], pc_lo, pc_span, err);
 }
 
+// Bit-packed presence (8x smaller than the byte map, so the hot part of the
+// window stays L2-resident): 16-B vector stream of PCs, the four word tests
+// issued together, atomicOr only for bits not yet set.
+__device__ __forceinline__ bool in_window(uint32_t pc, uint32_t pc_lo, uint64_t pc_span,
+                                          uint64_t *o) {
+    *o = (uint64_t)(uint32_t)(pc - pc_lo);
+    return pc >= pc_lo && *o < pc_span;
+}
+
+__device__ __forceinline__ void mark_bit(uint32_t *__restrict__ bits, uint32_t pc, uint32_t pc_lo,
+                                         uint64_t pc_span, uint32_t *__restrict__ err) {
+    uint64_t o;
+    if (!in_window(pc, pc_lo, pc_span, &o)) {
+        *err = 1u;
+        return;
+    }
+    const uint32_t m = 1u << (o & 31);
+    if (!(bits[o >> 5] & m)) atomicOr(&bits[o >> 5], m);
+}
+
+__global__ void mark_bits_kernel(const uint64_t *__restrict__ off, size_t nseg,
+                                 const uint32_t *__restrict__ pcs, uint32_t *__restrict__ bits,
+                                 uint32_t pc_lo, uint64_t pc_span, uint32_t *__restrict__ err) {
+    const uint64_t start = off[0], end = off[nseg];
+    const uint64_t a0 = (start + 3) & ~3ull;
+    const uint64_t head_end = a0 < end ? a0 : end;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    if (tid < head_end - start) mark_bit(bits, pcs[start + tid], pc_lo, pc_span, err);
+    const uint64_t nvec = end > a0 ? (end - a0) / 4 : 0;
+    const uint4 *v = (const uint4 *)(pcs + a0);
+    for (uint64_t i = tid; i < nvec; i += nthr) {
+        const uint4 x = v[i];
+        const uint32_t p[4] = {x.x, x.y, x.z, x.w};
+        uint64_t o[4];
+        bool ok[4];
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            ok[q] = in_window(p[q], pc_lo, pc_span, &o[q]);
+            w[q] = ok[q] ? bits[o[q] >> 5] : 0xFFFFFFFFu;  // all loads in flight together
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!ok[q]) {
+                *err = 1u;
+                continue;
+            }
+            const uint32_t m = 1u << (o[q] & 31);
+            if (!(w[q] & m)) atomicOr(&bits[o[q] >> 5], m);
+        }
+    }
+    const uint64_t tail = a0 + nvec * 4;
+    if (end > tail && tid < end - tail) mark_bit(bits, pcs[tail + tid], pc_lo, pc_span, err);
+}
+
+// bits <-> bytes for the cross-GPU union (RCCL has no OR: uint8 MAX on bytes)
+__global__ void bits_to_bytes_kernel(const uint32_t *__restrict__ bits, uint64_t nwords,
+                                     uint8_t *__restrict__ bytes) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = bits[w];
+        uint4 lo, hi;
+        uint32_t o[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int by = 0; by < 4; by++) v |= ((b >> (q * 4 + by)) & 1u) << (8 * by);
+            o[q] = v;
+        }
+        lo = make_uint4(o[0], o[1], o[2], o[3]);
+        hi = make_uint4(o[4], o[5], o[6], o[7]);
+        ((uint4 *)bytes)[2 * w] = lo;
+        ((uint4 *)bytes)[2 * w + 1] = hi;
+    }
+}
+
+__global__ void bytes_to_bits_kernel(const uint8_t *__restrict__ bytes, uint64_t nwords,
+                                     uint32_t *__restrict__ bits) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 a = ((const uint4 *)bytes)[2 * w], c = ((const uint4 *)bytes)[2 * w + 1];
+        const uint32_t x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+        uint32_t b = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+#pragma unroll
+            for (int by = 0; by < 4; by++) b |= (((x[q] >> (8 * by)) & 0xFFu) != 0) << (q * 4 + by);
+        bits[w] = b;
+    }
+}
+
+// Bitmap set algebra on u32 words + popcount of the result.
+__global__ void bitmap_op_kernel(int op, uint32_t *__restrict__ dst,
+                                 const uint32_t *__restrict__ src, uint64_t nwords,
+                                 unsigned long long *__restrict__ pop) {
+    uint32_t cnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t a = dst[i], b = src[i];
+        const uint32_t r = op == 0 ? (a | b) : op == 1 ? (a & b) : op == 2 ? (a & ~b) : (a ^ b);
+        dst[i] = r;
+        cnt += __popc(r);
+    }
+    if (pop) {
+        cnt = wave_sum(cnt);
+        if (__lane_id() == 0 && cnt) atomicAdd(pop, (unsigned long long)cnt);
+    }
+}
+
 // Pass A: each thread packs WPT consecutive 32-byte groups into words,
 // writes {in-block exclusive prefix | bits << 32}, block total -> bsum[blk].
 constexpr int DICT_THREADS = 256, DICT_WPT = 4, DICT_WPB = DICT_THREADS * DICT_WPT;
@@ -271,6 +382,68 @@ extern "C" int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const u
         hipLaunchKernelGGL(mark_kernel, dim3(grid_for(nseg, 1, 8192)), dim3(256), 0,
                            (hipStream_t)stream, off, len, pcs, nseg, pres, pc_lo, pc_span,
                            err_flag);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_mark_bits(const uint64_t *off, const uint32_t *pcs, size_t nseg,
+                                    uint32_t *bits, uint32_t pc_lo, uint64_t pc_span,
+                                    uint32_t *err_flag, void *stream) {
+    if (nseg == 0) return 0;
+    if (!off || !pcs || !bits || !err_flag) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(mark_bits_kernel, dim3(256 * 16), dim3(256), 0, (hipStream_t)stream, off,
+                       nseg, pcs, bits, pc_lo, pc_span, err_flag);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nbits, uint8_t *bytes,
+                                        void *stream) {
+    if (!bits || !bytes) return SYZCOV_EINVAL;
+    const uint64_t nwords = (nbits + 31) / 32;
+    hipLaunchKernelGGL(bits_to_bytes_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
+                       (hipStream_t)stream, bits, nwords, bytes);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nbits, uint32_t *bits,
+                                        void *stream) {
+    if (!bits || !bytes) return SYZCOV_EINVAL;
+    const uint64_t nwords = (nbits + 31) / 32;
+    hipLaunchKernelGGL(bytes_to_bits_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
+                       (hipStream_t)stream, bytes, nwords, bits);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_bitmap_op(int op, uint32_t *dst, const uint32_t *src, uint64_t nwords,
+                                    uint64_t *popcount_out, void *stream) {
+    if (op < 0 || op > 3 || !dst || !src) return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *pop = (unsigned long long *)popcount_out;
+    if (pop) SYZ_HIP(hipMemsetAsync(pop, 0, sizeof(uint64_t), s));
+    if (nwords) {
+        hipLaunchKernelGGL(bitmap_op_kernel, dim3(grid_for(nwords, 256, 8192)), dim3(256), 0, s, op,
+                           dst, src, nwords, pop);
+        SYZ_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+extern "C" int syzcov_dev_dict_build_bits(const uint32_t *bits, uint64_t pc_span, uint64_t *tab,
+                                          uint32_t *n_ids, void *ws, void *stream) {
+    if (!bits || !tab || !n_ids || !ws || pc_span == 0 || pc_span > (1ull << 32))
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t nwords = (pc_span + 31) / 32;
+    const uint64_t nblk = (nwords + DICT_WPB - 1) / DICT_WPB;
+    uint32_t *bsum = (uint32_t *)ws;
+    hipLaunchKernelGGL(dict_pass_a_bits, dim3((unsigned)nblk), dim3(DICT_THREADS), 0, s, bits,
+                       nwords, tab, bsum);
+    hipLaunchKernelGGL(dict_pass_b, dim3(1), dim3(1024), 0, s, bsum, nblk, n_ids);
+    hipLaunchKernelGGL(dict_pass_c, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0, s, tab,
+                       nwords, bsum);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

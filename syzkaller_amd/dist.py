@@ -68,6 +68,16 @@ class ShardedEngine(CorpusEngine):
                          n_global=n * world, sort_variant=sort_variant)
         self.rank, self.world, self.n_local = rank, world, n
         self.glens = torch.empty(n * world, dtype=torch.int32, device=self.dev)
+        self.pres_bytes = torch.empty(self.nwords * 32, dtype=torch.uint8, device=self.dev)
+
+    def merge_presence_bits(self):
+        """bits -> uint8 per PC -> RCCL MAX -> bits (exact OR of the shards)."""
+        L, s = self.L, _stream()
+        check(L.syzcov_dev_bits_to_bytes(_p(self.pres), self.span, _p(self.pres_bytes), s),
+              "dev_bits_to_bytes")
+        merge_presence(self.pres_bytes)
+        check(L.syzcov_dev_bytes_to_bits(_p(self.pres_bytes), self.span, _p(self.pres), s),
+              "dev_bytes_to_bits")
 
     def step(self, off, raw, n, sync: bool = True, ev=None):
         def mark_ev(i):
@@ -77,7 +87,7 @@ class ShardedEngine(CorpusEngine):
         N = n * self.world
         mark_ev(0)
         self.mark(off, raw, n)
-        merge_presence(self.pres)                       # RCCL uint8 MAX
+        self.merge_presence_bits()                      # RCCL uint8 MAX
         mark_ev(1)
         self.build_dict()
         mark_ev(2)

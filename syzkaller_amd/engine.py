@@ -66,11 +66,12 @@ class CorpusEngine:
         self.sort_variant = sort_variant
         self.n_global = n_global or n_max
         nwords = (pc_span + 31) // 32
-        span16 = (pc_span + 15) // 16 * 16
+        self.nwords = nwords
         self.canon = _u32(p_max + 1, dev)
         self.new_len = _u32(n_max + 1, dev)
-        self.pres = torch.zeros(span16, dtype=torch.uint8, device=dev)
-        self.max_cover = torch.zeros(span16, dtype=torch.uint8, device=dev)
+        # presence and resident maxCover: one bit per PC of the window
+        self.pres = torch.zeros(nwords, dtype=torch.int32, device=dev)
+        self.max_cover = torch.zeros(nwords, dtype=torch.int32, device=dev)
         self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
         ids_cap = min(pc_span, p_max) + 1
         self.ids_cap = ids_cap
@@ -94,16 +95,16 @@ class CorpusEngine:
     PHASES = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
 
     def mark(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        """Presence map of the raw corpus (test-then-store, no atomics)."""
+        """Presence bitmap of the raw corpus (test-before-atomicOr)."""
         self.pres.zero_()
         self.scal.zero_()
-        check(self.L.syzcov_dev_mark(_p(off), None, _p(raw), n, _p(self.pres), self.pc_lo,
-                                     self.span, _p(self.scal), _stream()), "dev_mark")
+        check(self.L.syzcov_dev_mark_bits(_p(off), _p(raw), n, _p(self.pres), self.pc_lo,
+                                          self.span, _p(self.scal), _stream()), "dev_mark_bits")
 
     def build_dict(self):
-        check(self.L.syzcov_dev_dict_build(_p(self.pres), self.span, _p(self.tab),
-                                           _p(self.scal[1:2]), _p(self.ws), _stream()),
-              "dev_dict_build")
+        check(self.L.syzcov_dev_dict_build_bits(_p(self.pres), self.span, _p(self.tab),
+                                                _p(self.scal[1:2]), _p(self.ws), _stream()),
+              "dev_dict_build_bits")
 
     def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
         """Canonical covers in the dense-id space (LDS radix sort + unique)."""
@@ -142,9 +143,8 @@ class CorpusEngine:
                                              _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
 
     def merge_max_cover(self):
-        check(self.L.syzcov_dev_bytemap_op(0, _p(self.max_cover), _p(self.pres),
-                                           self.pres.numel(), _p(self.scal[4:5]), _stream()),
-              "dev_bytemap_op")
+        check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.pres), self.nwords,
+                                          _p(self.scal[4:5]), _stream()), "dev_bitmap_op")
 
     # ------------------------------------------------------------------ step
     def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True, ev=None):

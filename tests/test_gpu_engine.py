@@ -61,6 +61,18 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
     assert res2.max_cover == exp_union.size
 
 
+def test_sharded_engine_world1(torch):
+    """The RCCL path (bits->bytes MAX all-reduce, all-gather of lengths, MIN
+    all-reduce of first[], MAX of kept) at world size 1, in a subprocess."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_dist_check.py")],
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
 def test_engine_properties_large(torch):
     """Size-independent properties at 200k inputs: union(kept) == union(all),
     kept order follows non-increasing canonical length, first kept = rank 0."""
