@@ -7,9 +7,10 @@ N=1, the same per-GPU shard with RCCL merges at N>1 — weak scaling).
 
 One step = one pass of the hot path over one synthetic corpus already
 resident in HBM (raw KCOV lists, CSR):
-  mark (presence) -> dense-id dictionary (= corpus union) -> Canonicalize
-  (id space) -> Go sort.Sort order -> Minimize (chunked first-cover pass 1 +
-  pass 2) -> ordered compaction -> sorted Union list -> maxCover merge.
+  Canonicalize (LDS radix sort over window offsets, presence bitmap marked
+  in-kernel) -> PC dictionary (= corpus union) -> Go sort.Sort order ->
+  Minimize (chunked first-cover pass 1 + pass 2) -> ordered compaction ->
+  sorted Union list -> maxCover merge.  (--engine ids: the dense-id variant.)
 Prints ONE JSON line (rank 0).  Per-phase device times come from HIP events
 on the stream the kernels run on; the dominant kernel's roofline uses its
 ALGORITHMIC bytes.
@@ -48,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2000,
                     help="inputs timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--engine", choices=["pc", "ids"], default="pc",
+                    help="canonical form: window PCs (default) or dense ids")
     return ap.parse_args()
 
 
@@ -148,9 +151,10 @@ def bench_corpus(args):
     max_len = int(lens.max().item())
     if world > 1:
         from syzkaller_amd.dist import ShardedEngine
-        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev)
+        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev,
+                            mode=args.engine)
     else:
-        eng = CorpusEngine(n, total, max_len, lo, span, device=dev)
+        eng = CorpusEngine(n, total, max_len, lo, span, device=dev, mode=args.engine)
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
     dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), args,
@@ -159,9 +163,9 @@ def bench_corpus(args):
     res = eng.result()
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
     value = total * world * args.steps / dt
-    # algorithmic bytes per launch: mark reads raw (4 B/PC);
-    # canon reads raw + writes canonical ids; minimize reads canonical ids once
-    alg = {"mark": 4 * total, "canon": 4 * total + 4 * canon_pcs, "minimize": 4 * canon_pcs}
+    # algorithmic bytes per launch: canon reads raw + writes the
+    # canonical list; minimize reads the canonical list once (ids mode: + mark)
+    alg = eng.alg_bytes(total, canon_pcs)
     dom = max(alg, key=lambda p: ph[p])
     achieved = alg[dom] / (ph[dom] * 1e-3) / 1e9
     out = {
@@ -174,6 +178,7 @@ def bench_corpus(args):
                                + (" (C3 sharding)" if world > 1 else ""),
                    "inputs_per_gpu": n, "global_inputs": n * world, "raw_pcs_per_gpu": total,
                    "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
+                   "engine": args.engine,
                    "len_mean": args.mean, "len_sigma": args.sigma,
                    "parallelism": f"shard-by-input x{world}"},
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},

@@ -248,6 +248,36 @@ int syzcov_dev_minimize_ids_pass2(const uint64_t *off, const uint32_t *len, cons
                                   const int32_t *first, const uint8_t *cand, uint8_t *kept,
                                   void *stream);
 
+/* ---- engine PC-space path (default): no dictionary before the sort ----
+ * Canonicalize a CSR corpus inside the window [pc_lo, pc_lo + pc_span): keys
+ * are window offsets, radix-sorted in LDS, de-duplicated (cover.go:36-52
+ * semantics), written back as PCs to out_pcs[off[i] ..), and every canonical
+ * PC is OR-ed into the presence bitmap pres_bits (pre-zeroed or carrying the
+ * previous step) — the mark pass fused into the sort.  PCs outside the window
+ * set *err_flag.  ws: syzcov_dev_canon_ws_size(nseg, max_seg_len). */
+int syzcov_dev_canon_pcs(const uint64_t *off, const uint32_t *raw, uint32_t *out_pcs,
+                         uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
+                         uint64_t pc_span, uint32_t *pres_bits, uint32_t *err_flag, void *ws,
+                         size_t ws_size, void *stream);
+/* Minimize over canonical PC covers with first_w[] indexed by pc - pc_lo
+ * (pc_span int32, pre-set to INT32_MAX): pass 1 in doubling rank chunks with
+ * covered/touched window bitmaps, then (do_pass2) pass 2 into kept[] (by
+ * rank, pre-zeroed).  ws: syzcov_dev_minimize_win_ws_size(pc_span). */
+size_t syzcov_dev_minimize_win_ws_size(uint64_t pc_span);
+int syzcov_dev_minimize_win(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                            const int32_t *order, const int32_t *ranks, size_t n, uint32_t pc_lo,
+                            uint64_t pc_span, int32_t *first_w, uint8_t *cand, uint8_t *kept,
+                            int do_pass2, void *ws, void *stream);
+int syzcov_dev_minimize_win_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                                  const int32_t *order, const int32_t *ranks, size_t n,
+                                  uint32_t pc_lo, const int32_t *first_w, const uint8_t *cand,
+                                  uint8_t *kept, void *stream);
+/* Sharded runs: window-indexed first_w <-> dense-id first (one int32 per
+ * present PC of the dictionary `tab`) so the RCCL MIN moves n_ids, not
+ * pc_span, entries.  to_dense = 1 gathers, 0 scatters back. */
+int syzcov_dev_first_dense(const uint64_t *tab, uint64_t pc_span, int32_t *first_w,
+                           int32_t *dense, int to_dense, void *stream);
+
 /* Ordered compaction: out_idx = [order[r] for r if kept[r]]; *n_out (device u32). */
 size_t syzcov_dev_compact_ws_size(size_t n);
 int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n, int32_t *out_idx,

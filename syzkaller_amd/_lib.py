@@ -79,6 +79,12 @@ _SIGS = {
     "syzcov_dev_minimize_ids": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, sz, p_, p_, p_, C.c_int, p_,
                                           p_]),
     "syzcov_dev_minimize_ids_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, p_, p_, p_]),
+    "syzcov_dev_canon_pcs": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, p_, p_, p_, sz, p_]),
+    "syzcov_dev_minimize_win_ws_size": (sz, [u64]),
+    "syzcov_dev_minimize_win": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, u64, p_, p_, p_, C.c_int,
+                                          p_, p_]),
+    "syzcov_dev_minimize_win_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, p_, p_, p_, p_]),
+    "syzcov_dev_first_dense": (C.c_int, [p_, u64, p_, p_, C.c_int, p_]),
     "syzcov_dev_compact_ws_size": (sz, [sz]),
     "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),
     "syzcov_dev_sort_ws_size": (sz, [sz]),

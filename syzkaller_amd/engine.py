@@ -54,13 +54,25 @@ class StepResult:
 
 class CorpusEngine:
     """Buffers sized for up to `n_max` inputs / `p_max` PCs over the PC window
-    [pc_lo, pc_lo + pc_span)."""
+    [pc_lo, pc_lo + pc_span).
+
+    mode "pc" (default): canonical covers stay PCs; the presence bitmap is
+    marked by the canonicalize kernel itself and Minimize's first-cover table
+    is indexed by window offset (4 B x pc_span of HBM) — no dictionary lookup
+    anywhere on the per-PC path.
+    mode "ids": presence mark -> dense-id dictionary -> canonical covers as
+    dense ids -> Minimize over a first table of n_ids entries (smaller table,
+    one extra gather per raw PC)."""
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 device="cuda", n_global: int | None = None, sort_variant: int = 0):
+                 device="cuda", n_global: int | None = None, sort_variant: int = 0,
+                 mode: str = "pc"):
+        if mode not in ("pc", "ids"):
+            raise ValueError(mode)
         L = lib()
         dev = torch.device(device)
-        self.dev, self.L = dev, L
+        self.dev, self.L, self.mode = dev, L, mode
+        self.PHASES = self.PHASES_PC if mode == "pc" else self.PHASES_IDS
         self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
         self.pc_lo, self.span = pc_lo, pc_span
         self.sort_variant = sort_variant
@@ -75,7 +87,8 @@ class CorpusEngine:
         self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
         ids_cap = min(pc_span, p_max) + 1
         self.ids_cap = ids_cap
-        self.first = torch.empty(ids_cap, dtype=torch.int32, device=dev)
+        self.first = torch.empty(pc_span if mode == "pc" else ids_cap, dtype=torch.int32,
+                                 device=dev)
         self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
         self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
         self.lens64 = torch.empty(self.n_global + 1, dtype=torch.int64, device=dev)
@@ -87,12 +100,46 @@ class CorpusEngine:
                  L.syzcov_dev_dict_ws_size(pc_span),
                  L.syzcov_dev_compact_ws_size(self.n_global),
                  L.syzcov_dev_sort_ws_size(self.n_global),
-                 L.syzcov_dev_minimize_ws_size(ids_cap))
+                 L.syzcov_dev_minimize_ws_size(ids_cap),
+                 L.syzcov_dev_minimize_win_ws_size(pc_span))
         self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
         self.ws_size = ws
 
     # ---------------------------------------------------------------- phases
-    PHASES = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
+    PHASES_IDS = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
+    PHASES_PC = ("canon", "dict", "order", "minimize", "compact", "union", "merge")
+    PHASES = PHASES_PC
+
+    def alg_bytes(self, raw_pcs: int, canon_pcs: int) -> dict:
+        """Algorithmic HBM bytes per launch of the streaming phases (DESIGN.md
+        §4): every raw PC read once (4 B), every canonical PC written once and
+        read once by Minimize pass 1."""
+        if self.mode == "pc":
+            return {"canon": 4 * raw_pcs + 4 * canon_pcs, "minimize": 4 * canon_pcs}
+        return {"mark": 4 * raw_pcs, "canon": 4 * raw_pcs + 4 * canon_pcs,
+                "minimize": 4 * canon_pcs}
+
+    def canonicalize_pcs(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+        """Canonical covers as PCs with the presence bitmap marked in-kernel."""
+        self.pres.zero_()
+        self.scal.zero_()
+        check(self.L.syzcov_dev_canon_pcs(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
+                                          self.max_seg, self.pc_lo, self.span, _p(self.pres),
+                                          _p(self.scal), _p(self.ws), self.ws_size, _stream()),
+              "dev_canon_pcs")
+
+    def minimize_win(self, off, order, ranks, n_items, do_pass2=True):
+        self.first.fill_(INT32_MAX)
+        self.kept.zero_()
+        check(self.L.syzcov_dev_minimize_win(
+            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items, self.pc_lo,
+            self.span, _p(self.first), _p(self.cand), _p(self.kept), int(do_pass2), _p(self.ws),
+            _stream()), "dev_minimize_win")
+
+    def minimize_win_pass2(self, off, order, ranks, n_items):
+        check(self.L.syzcov_dev_minimize_win_pass2(
+            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items, self.pc_lo,
+            _p(self.first), _p(self.cand), _p(self.kept), _stream()), "dev_minimize_win_pass2")
 
     def mark(self, off: torch.Tensor, raw: torch.Tensor, n: int):
         """Presence bitmap of the raw corpus (test-before-atomicOr)."""
@@ -148,26 +195,38 @@ class CorpusEngine:
 
     # ------------------------------------------------------------------ step
     def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True, ev=None):
-        def mark_ev(i):
+        k = [0]
+
+        def mark_ev():
             if ev is not None:
-                ev[i].record()
-        mark_ev(0)
-        self.mark(off, raw, n)
-        mark_ev(1)
-        self.build_dict()
-        mark_ev(2)
-        self.canonicalize(off, raw, n)
-        mark_ev(3)
+                ev[k[0]].record()
+            k[0] += 1
+        mark_ev()
+        if self.mode == "pc":
+            self.canonicalize_pcs(off, raw, n)
+            mark_ev()
+            self.build_dict()
+            mark_ev()
+        else:
+            self.mark(off, raw, n)
+            mark_ev()
+            self.build_dict()
+            mark_ev()
+            self.canonicalize(off, raw, n)
+            mark_ev()
         self.sort_order(self.new_len, n)
-        mark_ev(4)
-        self.minimize(off, self.order, None, n)
-        mark_ev(5)
+        mark_ev()
+        if self.mode == "pc":
+            self.minimize_win(off, self.order, None, n)
+        else:
+            self.minimize(off, self.order, None, n)
+        mark_ev()
         self.compact(n)
-        mark_ev(6)
+        mark_ev()
         self.union_list()
-        mark_ev(7)
+        mark_ev()
         self.merge_max_cover()
-        mark_ev(8)
+        mark_ev()
         return self.result() if sync else None
 
     def result(self) -> StepResult:
@@ -180,6 +239,8 @@ class CorpusEngine:
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """Materialise the canonical covers as PCs (CSR slots of `off`)."""
+        if self.mode == "pc":
+            return self.canon
         table = _u32(self.ids_cap, self.dev)
         check(self.L.syzcov_dev_dict_pcs(_p(self.tab), self.span, self.pc_lo, _p(table),
                                          _stream()), "dev_dict_pcs")

@@ -26,11 +26,12 @@ def main():
     off, raw, lens, total = synth_corpus(n, 0x5EED0009, mean=700, sigma=300, log2_space=18)
     lo, span = synth_window(18)
     a = CorpusEngine(n, total, int(lens.max().item()), lo, span).step(off, raw, n)
-    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, 0, 1)
-    b = eng.step(off, raw, n)
-    assert a.n_kept == b.n_kept and a.n_union == b.n_union and a.max_cover == b.max_cover
-    assert torch.equal(a.kept_idx.cpu(), b.kept_idx.cpu())
-    assert np.array_equal(a.union.cpu().numpy(), b.union.cpu().numpy())
+    for mode in ("pc", "ids"):
+        eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, 0, 1, mode=mode)
+        b = eng.step(off, raw, n)
+        assert a.n_kept == b.n_kept and a.n_union == b.n_union and a.max_cover == b.max_cover
+        assert torch.equal(a.kept_idx.cpu(), b.kept_idx.cpu())
+        assert np.array_equal(a.union.cpu().numpy(), b.union.cpu().numpy())
     dist.destroy_process_group()
     print("OK", a.n_kept, a.n_union)
 

@@ -29,14 +29,15 @@ def test_synth_matches_cpu_twin(torch):
         assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
 
 
+@pytest.mark.parametrize("mode", ["pc", "ids"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
                                                (500, 9000, 6000, 20)])
-def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
+def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, mode):
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
     seed = 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
     lo, span = synth_window(log2)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, mode=mode)
     res = eng.step(off, raw, n)
     # oracle
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
@@ -61,6 +62,37 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
     assert res2.max_cover == exp_union.size
 
 
+@pytest.mark.parametrize("mode", ["pc", "ids"])
+def test_engine_sentinel_window(torch, mode):
+    """Window touching 0xFFFFFFFF: inputs made only of the sentinel canonicalize
+    to empty, otherwise it is an ordinary PC (cover.go:36-52, 104-131)."""
+    from syzkaller_amd.engine import CorpusEngine
+    rng = np.random.default_rng(21)
+    lo, span = 0xFFFF0000, 1 << 16
+    covers = []
+    for i in range(700):
+        l = int(rng.integers(0, 400))
+        c = rng.integers(0, 1 << 16, size=l, dtype=np.uint64) | np.uint64(0xFFFF0000)
+        if i % 7 == 0:
+            c = np.full(int(rng.integers(1, 5)), 0xFFFFFFFF, np.uint64)
+        elif i % 5 == 0:
+            c = np.concatenate([c, [0xFFFFFFFF] * 3])
+        covers.append(c.astype(np.uint32))
+    lens = np.array([len(c) for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers + [np.zeros(1, np.uint32)])
+    n = len(covers)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
+    eng = CorpusEngine(n, int(lens.sum()), int(lens.max()), lo, span, mode=mode)
+    res = eng.step(off, raw, n)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs[:int(lens.sum())])
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(_to_np_u32(res.union), orc.union_fold_csr(c_off, c_pcs))
+
+
 def test_sharded_engine_world1(torch):
     """The RCCL path (bits->bytes MAX all-reduce, all-gather of lengths, MIN
     all-reduce of first[], MAX of kept) at world size 1, in a subprocess."""
@@ -73,7 +105,8 @@ def test_sharded_engine_world1(torch):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 
-def test_engine_properties_large(torch):
+@pytest.mark.parametrize("mode", ["pc", "ids"])
+def test_engine_properties_large(torch, mode):
     """Size-independent properties at 200k inputs: union(kept) == union(all),
     kept order follows non-increasing canonical length, first kept = rank 0."""
     from syzkaller_amd import cover
@@ -81,7 +114,7 @@ def test_engine_properties_large(torch):
     n = 200_000
     off, raw, lens, total = synth_corpus(n, 0x5EED0003, mean=256, sigma=64, log2_space=20)
     lo, span = synth_window(20)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, mode=mode)
     res = eng.step(off, raw, n)
     kept = res.kept_idx.cpu().numpy()
     new_len = eng.new_len[:n].cpu().numpy()
