@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Kernel micro-bench on the C2 corpus: times one engine phase at a time.
+    python tools/kbench.py canon|minimize|step [--inputs N] [--reps R]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="?", default="canon")
+    ap.add_argument("--inputs", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--mean", type=int, default=2048)
+    ap.add_argument("--sigma", type=int, default=512)
+    ap.add_argument("--log2-space", type=int, default=22)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    n = a.inputs
+    lo, span = synth_window(a.log2_space)
+    off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
+                                         log2_space=a.log2_space)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    eng.step(off, raw, n)
+    torch.cuda.synchronize()
+    fns = {
+        "canon": lambda: eng.canonicalize_pcs(off, raw, n),
+        "minimize": lambda: eng.minimize_win(off, eng.order, None, n),
+        "step": lambda: eng.step(off, raw, n, sync=False),
+    }
+    f = fns[a.what]
+    for _ in range(a.reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        f()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e)
+        print(f"{a.what}: {ms:.3f} ms  raw {total} PCs  {8 * total / ms / 1e6:.1f} GB/s (8 B/PC)",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
