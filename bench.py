@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2000,
                     help="inputs timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--engine", choices=["pc", "ids"], default="pc",
+    ap.add_argument("--engine", choices=["range", "pc", "ids"], default="range",
                     help="canonical form: window PCs (default) or dense ids")
     return ap.parse_args()
 

@@ -278,6 +278,41 @@ int syzcov_dev_minimize_win_pass2(const uint64_t *off, const uint32_t *len, cons
 int syzcov_dev_first_dense(const uint64_t *tab, uint64_t pc_span, int32_t *first_w,
                            int32_t *dense, int to_dense, void *stream);
 
+/* ---- engine default path: wavefront canonicalize + range-partitioned Minimize ----
+ * Canonicalize (cover.go:27-40) with ONE wavefront per segment (LDS radix
+ * sort over window offsets, unique, PCs written to out[off[i] ..), in place
+ * allowed when max_seg_len <= 16384).  PCs outside [pc_lo, pc_lo + pc_span)
+ * set *err_flag.  If split != NULL (nrange = ceil(pc_span / 2^range_shift)
+ * <= 256 columns per segment), split[i * nrange + j] = number of canonical
+ * PCs of segment i below pc_lo + ((j + 1) << range_shift) and range_tot[j]
+ * (u64, pre-zeroed) accumulates the canonical PCs of range j.
+ * ws: syzcov_dev_canon_split_ws_size(nseg). */
+size_t syzcov_dev_canon_split_ws_size(size_t nseg);
+int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                           uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
+                           uint64_t pc_span, uint32_t range_shift, uint32_t *split,
+                           uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
+                           void *stream);
+/* Minimize (cover.go:104-131) over canonical covers with split[] from
+ * syzcov_dev_canon_split.  Item j (processing order) is input order[j] with
+ * rank ranks[j] (NULL: j).  covered: window bitmap of nrange << range_shift
+ * bits (pre-zeroed, or a shard's covered set); on return it holds the union
+ * of the items' covers.  first_w: int32 per window PC, all INT32_MAX on entry
+ * and on return.  rec: capacity rec_cap of (rank << 32 | offset) records;
+ * *rec_cnt (device u64) receives the record count (> rec_cap: overflow,
+ * handled exactly by fallback kernels).  cand: u8 per item (pre-zeroed).
+ * kept: u8 per rank (pre-zeroed) receives kept[rank] = 1.  first_chunk /
+ * growth / pcs_per_wg_hint tune the chunk schedule (0 = defaults: 64, 4,
+ * 2^18); any values give the same result.  ws: syzcov_dev_minimize_range_ws_size(). */
+size_t syzcov_dev_minimize_range_ws_size(void);
+int syzcov_dev_minimize_range(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                              const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                              size_t n_items, uint32_t pc_lo, uint64_t pc_span,
+                              uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered,
+                              int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
+                              uint8_t *cand, uint8_t *kept, size_t first_chunk, uint32_t growth,
+                              uint64_t pcs_per_wg_hint, void *ws, void *stream);
+
 /* Ordered compaction: out_idx = [order[r] for r if kept[r]]; *n_out (device u32). */
 size_t syzcov_dev_compact_ws_size(size_t n);
 int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n, int32_t *out_idx,

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(THREADS) void canon_class_kernel(
     for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
         const uint32_t seg = list[li];
         const uint64_t base = off[seg];
+        if (off[seg + 1] - base > (uint64_t)CAP) continue;  // belongs to the large path
         const uint32_t n = (uint32_t)(off[seg + 1] - base);
         // coalesced striped load -> LDS -> blocked registers
         for (uint32_t k = t; k < (uint32_t)CAP; k += THREADS) sm[k] = k < n ? in[base + k] : SYZ_SENT;
@@ -369,6 +370,18 @@ extern "C" int syzcov_dev_canonicalize(const uint64_t *off, const uint32_t *in, 
 }
 
 namespace syz {
+// Listed segments of up to 16384 keys (a device-side list and count), one
+// workgroup each: the fallback of the wavefront canonicalizer (canon_wave.hip)
+// for segments too long for a wave and for any segment whose wave sort failed
+// its order check.  Longer listed segments are skipped (large path).
+int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
+                    const uint32_t *list, const uint32_t *count, hipStream_t s) {
+    hipLaunchKernelGGL((canon_class_kernel<1024, 16>), dim3(256), dim3(1024), 0, s, off, in, out,
+                       new_len, list, count, nullptr, 0u, (uint64_t)0, nullptr);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
                      uint64_t pc_span, uint32_t *err, hipStream_t s) {

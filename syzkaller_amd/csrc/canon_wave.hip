@@ -1,0 +1,393 @@
+// canon_wave.hip — corpus-scale cover.Canonicalize (cover/cover.go:27-40):
+// one WAVEFRONT per segment, no workgroup barriers.
+//
+// A segment of n <= 8189 raw PCs is sorted by an LSD radix sort over its
+// window offsets (key = pc - pc_lo, nbits = bit_length(span-1), <= 9-bit
+// digits) entirely in the wave's private LDS slice:
+//   load     16-byte vector loads of the raw list (head/tail masked);
+//   pass 0   lowest digit, unstable: count (ds_add), exclusive scan of the
+//            512-entry histogram, scatter with ds_add_rtn positions;
+//   pass k   stable: the keys are re-read row-major from LDS (row r = slots
+//            64r..64r+63) and ranked with ds_add_rtn one row after another.
+//            Stability needs same-address LDS atomics of ONE wave instruction
+//            to be applied in lane order.  gfx950 does that
+//            (tools/probe/lds_order.hip: 0 violations in 3M rows), but the
+//            ISA does not promise it, so the result is CHECKED: a segment
+//            whose final keys are not non-decreasing is not written and goes
+//            to the workgroup bitonic fallback (canon.hip) instead.
+//   unique   the reference loop (`last := sent`: the key of PC 0xFFFFFFFF is
+//            dropped only in first position), ballot-compacted, written back
+//            as PCs to the segment's own CSR slots (in place is safe: the
+//            wave holds its keys before it writes).
+// Optional outputs for the range-partitioned Minimize (minimize_range.hip):
+//   split[seg * R + j] = number of canonical PCs with offset < (j+1) << rshift
+//   range_tot[j]      += canonical PCs of range j over the corpus.
+// Segments longer than 8189 keys are listed for the workgroup paths.
+#include "common.h"
+
+#include <algorithm>
+
+namespace syz {
+
+int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
+                    const uint32_t *list, const uint32_t *count, hipStream_t s);
+int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
+                     const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
+                     uint64_t pc_span, uint32_t *err, hipStream_t s);
+
+namespace cw {
+
+constexpr int WPB = 2;        // waves per workgroup (independent segments)
+constexpr int HIST = 512;     // 9-bit digits
+constexpr int MAX_RPL = 4;    // ranges per lane (R <= 256)
+constexpr uint32_t WAVE_MAX = 8192 - 3;  // a CAP-slot wave holds head (<= 3) + n keys
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Exclusive scan of the 512-entry histogram in place (8 entries per lane).
+__device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
+    uint4 *h4 = reinterpret_cast<uint4 *>(hist);
+    uint4 a = h4[2 * l], b = h4[2 * l + 1];
+    const uint32_t s = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
+    uint32_t p = wave_incl_scan(s) - s;
+    uint4 oa, ob;
+    oa.x = p; p += a.x; oa.y = p; p += a.y; oa.z = p; p += a.z; oa.w = p; p += a.w;
+    ob.x = p; p += b.x; ob.y = p; p += b.y; ob.z = p; p += b.z; ob.w = p;
+    h4[2 * l] = oa;
+    h4[2 * l + 1] = ob;
+}
+
+__device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
+    uint4 *h4 = reinterpret_cast<uint4 *>(hist);
+    h4[2 * l] = make_uint4(0, 0, 0, 0);
+    h4[2 * l + 1] = make_uint4(0, 0, 0, 0);
+}
+
+struct Params {
+    const uint64_t *off;
+    const uint32_t *raw;
+    uint32_t *out;
+    uint32_t *new_len;
+    uint64_t nseg;
+    uint32_t lo_len, hi_len;  // this launch: lo_len <= n <= hi_len
+    uint32_t pc_lo;
+    uint64_t span;
+    uint32_t nbits;
+    uint32_t sent_key;        // window offset of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
+    uint32_t *split;          // nullable: [nseg][nrange]
+    uint32_t nrange, rshift;
+    unsigned long long *range_tot;  // nullable: [nrange]
+    uint32_t *redo_list, *redo_cnt;  // wave sort failed its order check
+    uint32_t *big_list, *big_cnt;    // n > WAVE_MAX (listed by the launch with list_big)
+    int list_big;
+    uint32_t *err;
+};
+
+// NK = keys per lane (CAP = 64 * NK, NK a multiple of 4).
+template <int NK>
+__global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P) {
+    constexpr int CAP = 64 * NK;
+    constexpr int NQ = NK / 4;  // 16-byte loads per lane
+    __shared__ uint32_t s_buf[WPB][CAP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t l = __lane_id();
+    uint32_t *buf = s_buf[w];
+    uint32_t *hist = s_hist[w];
+    const uint32_t nbits = P.nbits < 1 ? 1 : P.nbits;
+    const uint32_t npass = (nbits + 8) / 9;
+    const uint32_t dbits = (nbits + npass - 1) / npass;  // <= 9
+    const uint32_t dmask = (1u << dbits) - 1u;
+    uint32_t racc[MAX_RPL];
+#pragma unroll
+    for (int q = 0; q < MAX_RPL; q++) racc[q] = 0;
+    const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    for (uint64_t seg = (uint64_t)blockIdx.x * WPB + w; seg < P.nseg; seg += nw) {
+        const uint64_t base = P.off[seg];
+        const uint64_t n64 = P.off[seg + 1] - base;
+        if (P.list_big && n64 > WAVE_MAX) {
+            if (l == 0) P.big_list[atomicAdd(P.big_cnt, 1u)] = (uint32_t)seg;
+            continue;
+        }
+        if (n64 < P.lo_len || n64 > P.hi_len) continue;
+        const uint32_t n = (uint32_t)n64;
+        // ---------------------------------------------------------- load
+        const uint64_t a0 = base & ~3ull;
+        const uint32_t head = (uint32_t)(base - a0);
+        const uint32_t end = head + n;  // aligned-window index of the end
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.raw + a0);
+        uint32_t k[NK];
+        bool oob = false;
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (e4 < end) v = src[q * 64 + l];
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t idx = e4 + c;
+                const uint32_t key = vv[c] - P.pc_lo;
+                const bool valid = idx >= head && idx < end;
+                oob |= valid && (uint64_t)key >= P.span;
+                k[q * 4 + c] = key;
+            }
+        }
+        if (__ballot(oob) && l == 0) *P.err = 1u;
+        // ------------------------------------------- pass 0 (unstable)
+        hist_zero(hist, l);
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            if ((uint32_t)(q * 256) < end) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t idx = e4 + c;
+                    if (idx >= head && idx < end) atomicAdd(&hist[k[q * 4 + c] & dmask], 1u);
+                }
+            }
+        }
+        wave_sync();
+        hist_scan(hist, l);
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            if ((uint32_t)(q * 256) < end) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t idx = e4 + c;
+                    if (idx >= head && idx < end) {
+                        const uint32_t key = k[q * 4 + c];
+                        buf[atomicAdd(&hist[key & dmask], 1u)] = key;
+                    }
+                }
+            }
+        }
+        wave_sync();
+        // --------------------------------------------- stable passes
+        for (uint32_t p = 1; p < npass; p++) {
+            const uint32_t sh = p * dbits;
+#pragma unroll
+            for (int r = 0; r < NK; r++)
+                if ((uint32_t)(r * 64) < n) k[r] = buf[r * 64 + l];
+            hist_zero(hist, l);
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < NK; r++)
+                if ((uint32_t)(r * 64) < n && (uint32_t)(r * 64) + l < n)
+                    atomicAdd(&hist[(k[r] >> sh) & dmask], 1u);
+            wave_sync();
+            hist_scan(hist, l);
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < NK; r++)
+                if ((uint32_t)(r * 64) < n && (uint32_t)(r * 64) + l < n)
+                    buf[atomicAdd(&hist[(k[r] >> sh) & dmask], 1u)] = k[r];
+            wave_sync();
+        }
+        // ------------------------------------------- order check
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < NK; r++) {
+            const uint32_t e = (uint32_t)(r * 64) + l;
+            if ((uint32_t)(r * 64) < n && e < n && e > 0) bad |= buf[e] < buf[e - 1];
+        }
+        if (__ballot(bad)) {
+            if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = (uint32_t)seg;
+            continue;
+        }
+        // ------------------------------------------- unique + write
+        uint32_t cnt = 0;
+        const uint64_t lt = (1ull << l) - 1ull;
+#pragma unroll
+        for (int r = 0; r < NK; r++) {
+            if ((uint32_t)(r * 64) < n) {
+                const uint32_t e = (uint32_t)(r * 64) + l;
+                const uint32_t v = buf[e];
+                const uint32_t prev = e == 0 ? P.sent_key : buf[e - 1];
+                const bool keep = e < n && v != prev;
+                const uint64_t m = __ballot(keep);
+                const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                if (keep) {
+                    P.out[base + pos] = v + P.pc_lo;
+                    buf[pos] = v;
+                }
+                cnt += (uint32_t)__popcll(m);
+            }
+        }
+        if (l == 0) P.new_len[seg] = cnt;
+        // ------------------------------------------- range splits
+        if (!P.split) {
+            if (l == 0) racc[0] += cnt;  // one range: its total is the PC count
+        } else {
+            wave_sync();
+            uint32_t carry = 0;
+            uint32_t *sp = P.split + seg * P.nrange;
+#pragma unroll
+            for (int q = 0; q < MAX_RPL; q++) {
+                const uint32_t j = q * 64 + l;
+                if (q * 64 < (int)P.nrange) {
+                    uint32_t s = cnt;
+                    if (j + 1 < P.nrange) {
+                        const uint32_t b = (j + 1) << P.rshift;
+                        uint32_t lo = 0, hi = cnt;  // lower_bound(b) in buf[0, cnt)
+                        while (lo < hi) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (buf[mid] < b) lo = mid + 1; else hi = mid;
+                        }
+                        s = lo;
+                    }
+                    const uint32_t prev_s = __shfl_up(s, 1, 64);
+                    const uint32_t c = s - (l == 0 ? carry : prev_s);
+                    carry = __shfl(s, 63, 64);
+                    if (j < P.nrange) {
+                        sp[j] = s;
+                        racc[q] += c;
+                    }
+                }
+            }
+        }
+    }
+    if (P.range_tot) {
+#pragma unroll
+        for (int q = 0; q < MAX_RPL; q++) {
+            const uint32_t j = q * 64 + l;
+            if (j < P.nrange && racc[q]) atomicAdd(&P.range_tot[j], (unsigned long long)racc[q]);
+        }
+    }
+}
+
+// Splits + range totals of listed segments (fallback / long paths), from the
+// canonical lists already in `out`.  One wave per listed segment.
+__global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t *list,
+                                                        const uint32_t *count, int big_only) {
+    const uint32_t l = __lane_id();
+    const uint32_t nl = *count;
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint32_t seg = list[li];
+        if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
+        const uint32_t *c = P.out + P.off[seg];
+        const uint32_t cnt = P.new_len[seg];
+        uint32_t carry = 0;
+        for (uint32_t jb = 0; jb < P.nrange; jb += 64) {
+            const uint32_t j = jb + l;
+            uint32_t s = cnt;
+            if (j + 1 < P.nrange) {
+                const uint32_t b = (j + 1) << P.rshift;
+                uint32_t lo = 0, hi = cnt;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (c[mid] - P.pc_lo < b) lo = mid + 1; else hi = mid;
+                }
+                s = lo;
+            }
+            const uint32_t prev_s = __shfl_up(s, 1, 64);
+            const uint32_t cc = s - (l == 0 ? carry : prev_s);
+            carry = __shfl(s, 63, 64);
+            if (j < P.nrange) {
+                P.split[(uint64_t)seg * P.nrange + j] = s;
+                if (P.range_tot && cc) atomicAdd(&P.range_tot[j], (unsigned long long)cc);
+            }
+        }
+    }
+}
+
+}  // namespace cw
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
+    return 256 + 2 * align_up(nseg * sizeof(uint32_t), 256);
+}
+
+extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                                      uint32_t *new_len, size_t nseg, size_t max_seg_len,
+                                      uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+                                      uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
+                                      void *ws, size_t ws_size, void *stream) {
+    if (nseg == 0) return 0;
+    if (!off || !raw || !out || !new_len || !err_flag || !ws) return SYZCOV_EINVAL;
+    if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
+        return SYZCOV_ERANGE;
+    if (ws_size < syzcov_dev_canon_split_ws_size(nseg) || nseg > 0xFFFFFFFFull)
+        return SYZCOV_EINVAL;
+    if (out == raw && max_seg_len > 16384) return SYZCOV_EINVAL;  // large path is out of place
+    if (range_shift > 20) return SYZCOV_EINVAL;
+    const uint64_t nrange = (pc_span + (1ull << range_shift) - 1) >> range_shift;
+    if (split && nrange > (uint64_t)cw::MAX_RPL * 64) return SYZCOV_ERANGE;
+    hipStream_t s = (hipStream_t)stream;
+    uint8_t *w = (uint8_t *)ws;
+    uint32_t *cnts = (uint32_t *)w;  // [0] redo, [1] big
+    uint32_t *redo = (uint32_t *)(w + 256);
+    uint32_t *big = (uint32_t *)(w + 256 + align_up(nseg * sizeof(uint32_t), 256));
+    SYZ_HIP(hipMemsetAsync(cnts, 0, 2 * sizeof(uint32_t), s));
+    cw::Params P{};
+    P.off = off;
+    P.raw = raw;
+    P.out = out;
+    P.new_len = new_len;
+    P.nseg = nseg;
+    P.pc_lo = pc_lo;
+    P.span = pc_span;
+    P.nbits = pc_span <= 1 ? 1 : 64 - __builtin_clzll(pc_span - 1);
+    const uint64_t so = (uint64_t)(uint32_t)(0xFFFFFFFFu - pc_lo);
+    P.sent_key = so < pc_span ? (uint32_t)so : 0xFFFFFFFFu;
+    P.split = split;
+    P.nrange = (uint32_t)nrange;
+    P.rshift = range_shift;
+    P.range_tot = (unsigned long long *)range_tot;
+    P.redo_list = redo;
+    P.redo_cnt = cnts;
+    P.big_list = big;
+    P.big_cnt = cnts + 1;
+    P.err = err_flag;
+    // one launch per capacity class; each grid-strides over all segments
+    struct Cls { uint32_t lo, hi; };
+    const Cls cls[4] = {{0, 1021}, {1022, 2045}, {2046, 4093}, {4094, cw::WAVE_MAX}};
+    const unsigned grid = (unsigned)std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, 4096);
+    for (int c = 0; c < 4; c++) {
+        if (c > 0 && max_seg_len < cls[c].lo) break;
+        P.lo_len = cls[c].lo;
+        P.hi_len = cls[c].hi;
+        P.list_big = c == 0;
+        switch (c) {
+        case 0: hipLaunchKernelGGL(cw::canon_wave_kernel<16>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
+        case 1: hipLaunchKernelGGL(cw::canon_wave_kernel<32>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
+        case 2: hipLaunchKernelGGL(cw::canon_wave_kernel<64>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
+        case 3: hipLaunchKernelGGL(cw::canon_wave_kernel<128>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
+        }
+        SYZ_LAUNCH_CHECK();
+    }
+    // segments whose wave sort failed the order check (not expected on gfx950)
+    int rc = canon_list_path(off, raw, out, new_len, redo, cnts, s);
+    if (rc) return rc;
+    if (split)
+        hipLaunchKernelGGL(cw::split_list_kernel, dim3(64), dim3(64), 0, s, P, (const uint32_t *)redo,
+                           (const uint32_t *)cnts, 0);
+    if (max_seg_len > cw::WAVE_MAX) {
+        if (max_seg_len <= 16384) {
+            rc = canon_list_path(off, raw, out, new_len, big, cnts + 1, s);
+            if (rc) return rc;
+        } else {
+            uint32_t nbig = 0;
+            SYZ_HIP(hipMemcpyAsync(&nbig, cnts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            SYZ_HIP(hipStreamSynchronize(s));
+            if (nbig) {
+                rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr, pc_lo, pc_span,
+                                      err_flag, s);
+                if (rc) return rc;
+            }
+        }
+        if (split)
+            hipLaunchKernelGGL(cw::split_list_kernel, dim3(256), dim3(64), 0, s, P,
+                               (const uint32_t *)big, (const uint32_t *)(cnts + 1), 1);
+    }
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}

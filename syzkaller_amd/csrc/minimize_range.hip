@@ -1,0 +1,375 @@
+// minimize_range.hip — cover.Minimize (cover/cover.go:104-131) as a
+// first-cover problem whose per-PC test never leaves LDS.
+//
+// kept(r) <=> some pc of cov_r has first(pc) == r, first(pc) = min rank
+// covering pc.  Items (inputs in rank order) are processed in
+// geometrically growing chunks.  Before chunk c, `covered` holds every PC
+// whose first cover lies in an earlier chunk; inside the chunk a PC that is
+// covered cannot be first for any rank of the chunk, so it costs one LDS bit
+// test.  Every uncovered occurrence (rank, pc) is RECORDED and atomicMin-ed
+// into first_w[pc - pc_lo]; the first cover of every PC is always recorded
+// (nothing before it covers the PC).  Hence, after the last chunk:
+//   first_w[pc]  = first(pc) for every recorded pc,
+//   covered      = the union of the corpus (the maxCover merge operand),
+//   kept(r)      <=> some record (r, pc) has first_w[pc] == r   (pass 2),
+// and pass 2 touches only the records (a few per distinct PC), not the corpus.
+//
+// LDS residency: the PC window is cut into ranges of 2^rshift PCs (128 KB of
+// bitmap at rshift 20).  A workgroup owns one range for a slice of the
+// chunk's items, loads that range's covered bitmap into LDS, and streams the
+// items' sub-runs inside the range (canonical lists are sorted, so a sub-run
+// is contiguous: split[] from canon_wave.hip).  Ranges get workgroups in
+// proportion to their PC counts (range_tot), so a hot range is cut into many
+// short item slices.  Each wave flattens the sub-runs of 64 items into full
+// 64-lane rows (a scalar walk over the items starting inside each row) and
+// keeps ROWS row loads in flight before it tests them.
+//
+// Record overflow (more uncovered occurrences than rec_cap, only for
+// adversarial corpora) is detected on the device; the fallback kernels then
+// rescan candidate items and derive the union from first_w, so the result
+// stays exact for every input.
+#include "common.h"
+
+#include <algorithm>
+
+namespace syz {
+namespace mr {
+
+constexpr int THREADS = 1024;
+constexpr int NWAVE = THREADS / 64;
+constexpr int ROWS = 8;          // row loads in flight per wave
+constexpr int MAX_R = 256;
+
+struct Args {
+    const uint64_t *off;
+    const uint32_t *len;       // canonical lengths (used when split == NULL)
+    const uint32_t *pcs;
+    const uint32_t *split;     // [nseg][nrange] or NULL (nrange == 1)
+    const int32_t *order;      // item -> local input index
+    const int32_t *ranks;      // item -> rank (NULL: item index)
+    uint32_t pc_lo;
+    uint32_t rshift, nrange;
+    const unsigned long long *range_tot;
+    const uint32_t *covered;   // window bitmap (nrange << rshift bits)
+    int32_t *first_w;          // [span], INT32_MAX outside records
+    unsigned long long *rec;   // (rank << 32) | window offset
+    uint64_t rec_cap;
+    unsigned long long *rec_cnt;  // may exceed rec_cap (overflow)
+    uint8_t *cand;             // [items] item had an uncovered PC
+};
+
+// Workgroup -> (range, item slice [i0, i1)) with pieces proportional to the
+// range's weight: p_j = 1 + floor(w_j * (G - R) / W).
+__device__ bool piece_of(const Args &A, uint32_t G, uint32_t a, uint32_t b, uint32_t *rho,
+                         uint32_t *i0, uint32_t *i1, uint32_t *sh) {
+    // sh: LDS scratch of MAX_R + 1 entries; computed by wave 0
+    const uint32_t l = __lane_id();
+    if (threadIdx.x < 64) {
+        unsigned long long wsum = 0;
+        for (uint32_t j = l; j < A.nrange; j += 64) wsum += A.range_tot[j];
+        for (int d = 32; d >= 1; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
+        const uint64_t spare = G > A.nrange ? G - A.nrange : 0;
+        uint32_t carry = 0;
+        for (uint32_t jb = 0; jb < A.nrange; jb += 64) {
+            const uint32_t j = jb + l;
+            uint32_t p = 0;
+            if (j < A.nrange)  // integer: the pieces never exceed G
+                p = 1u + (wsum ? (uint32_t)(A.range_tot[j] * spare / wsum) : 0u);
+            const uint32_t inc = wave_incl_scan(p);
+            if (j < A.nrange) sh[j + 1] = carry + inc;
+            carry += __shfl(inc, 63, 64);
+        }
+        if (l == 0) sh[0] = 0;
+    }
+    __syncthreads();
+    const uint32_t g = blockIdx.x;
+    if (g >= sh[A.nrange]) return false;
+    uint32_t lo = 0, hi = A.nrange;  // largest j with sh[j] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sh[mid] <= g) lo = mid; else hi = mid;
+    }
+    const uint32_t p = sh[lo + 1] - sh[lo], q = g - sh[lo];
+    const uint64_t n = b - a;
+    *rho = lo;
+    *i0 = a + (uint32_t)(n * q / p);
+    *i1 = a + (uint32_t)(n * (q + 1) / p);
+    return true;
+}
+
+// Pass 1 over items [a, b) (one chunk).
+__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b) {
+    extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
+    __shared__ uint32_t s_plan[MAX_R + 1];
+    uint32_t rho, i0, i1;
+    if (!piece_of(A, gridDim.x, a, b, &rho, &i0, &i1, s_plan)) return;
+    const uint32_t nwords = (1u << A.rshift) >> 5;
+    {
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
+        uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
+        for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
+        for (uint32_t q = (nwords / 4) * 4 + threadIdx.x; q < nwords; q += THREADS)
+            s_cov[q] = A.covered[(uint64_t)rho * nwords + q];
+    }
+    __syncthreads();
+    const uint32_t l = __lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t lt = (1ull << l) - 1ull;
+    const uint32_t rbase = rho << A.rshift;  // window offset of the range
+    for (uint32_t ib = i0 + w * 64; ib < i1; ib += NWAVE * 64) {
+        // ---- per-lane item descriptor: sub-run of range rho
+        const uint32_t item = ib + l;
+        uint64_t st = 0;
+        uint32_t m = 0;
+        int32_t rk = 0;
+        if (item < i1) {
+            const uint32_t seg = (uint32_t)A.order[item];
+            rk = A.ranks ? A.ranks[item] : (int32_t)item;
+            const uint64_t o = A.off[seg];
+            uint32_t s0 = 0, s1;
+            if (A.split) {
+                const uint32_t *sp = A.split + (uint64_t)seg * A.nrange;
+                s1 = sp[rho];
+                if (rho) s0 = sp[rho - 1];
+            } else {
+                s1 = A.len[seg];
+            }
+            st = o + s0;
+            m = s1 - s0;
+        }
+        const uint32_t incl = wave_incl_scan(m);
+        const uint32_t pre = incl - m;                      // exclusive prefix
+        const uint32_t T = __shfl(incl, 63, 64);            // flattened length
+        if (T == 0) continue;
+        // per-lane state: item containing flattened element R0 + l
+        uint64_t my_st = 0;
+        uint32_t my_pre = 0, my_item = 0;
+        int32_t my_rk = 0;
+        for (uint32_t R0 = 0; R0 < T; R0 += ROWS * 64) {
+            uint32_t v[ROWS], ix[ROWS], rkv[ROWS];
+            bool act[ROWS];
+#pragma unroll
+            for (int u = 0; u < ROWS; u++) {
+                const uint32_t r0 = R0 + u * 64;
+                act[u] = false;
+                if (r0 < T) {
+                    // carry the item of the previous row's last element
+                    my_st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)my_st, 63) |
+                            ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_st >> 32), 63) << 32);
+                    my_pre = __builtin_amdgcn_readlane(my_pre, 63);
+                    my_item = __builtin_amdgcn_readlane(my_item, 63);
+                    my_rk = __builtin_amdgcn_readlane(my_rk, 63);
+                    uint64_t starts = __ballot(m > 0 && pre >= r0 && pre < r0 + 64);
+                    while (starts) {
+                        const uint32_t i = __builtin_ctzll(starts);
+                        starts &= starts - 1;
+                        const uint32_t pi = __builtin_amdgcn_readlane(pre, i);
+                        if (l >= pi - r0) {
+                            my_st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)st, i) |
+                                    ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), i) << 32);
+                            my_pre = pi;
+                            my_item = ib + i;
+                            my_rk = __builtin_amdgcn_readlane(rk, i);
+                        }
+                    }
+                    const uint32_t f = r0 + l;
+                    act[u] = f < T;
+                    ix[u] = my_item;
+                    rkv[u] = (uint32_t)my_rk;
+                    v[u] = act[u] ? A.pcs[my_st + (f - my_pre)] : 0u;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < ROWS; u++) {
+                if (R0 + u * 64 < T) {
+                    const uint32_t wo = v[u] - A.pc_lo;           // window offset
+                    const uint32_t bit = act[u] ? wo - rbase : 0u;  // < 2^rshift
+                    const bool unc = act[u] && !((s_cov[bit >> 5] >> (bit & 31)) & 1u);
+                    const uint64_t um = __ballot(unc);
+                    if (um) {
+                        unsigned long long basei = 0;
+                        if (l == __builtin_ctzll(um))
+                            basei = atomicAdd(A.rec_cnt, (unsigned long long)__popcll(um));
+                        basei = __shfl(basei, __builtin_ctzll(um), 64);
+                        if (unc) {
+                            atomicMin(&A.first_w[wo], (int32_t)rkv[u]);
+                            const uint64_t slot = basei + (uint64_t)__popcll(um & lt);
+                            if (slot < A.rec_cap)
+                                A.rec[slot] = ((unsigned long long)rkv[u] << 32) | wo;
+                            A.cand[ix[u]] = 1;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// covered |= records [*done, min(*cnt, cap)); then *done advances (next kernel).
+__global__ void cover_records_kernel(const unsigned long long *rec, uint64_t cap,
+                                     const unsigned long long *cnt, const unsigned long long *done,
+                                     uint32_t *covered) {
+    const uint64_t lo = *done, hi = std::min<uint64_t>(*cnt, cap);
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t wo = (uint32_t)rec[i];
+        const uint32_t mbit = 1u << (wo & 31);
+        if (!(covered[wo >> 5] & mbit)) atomicOr(&covered[wo >> 5], mbit);
+    }
+}
+
+__global__ void advance_kernel(const unsigned long long *cnt, unsigned long long *done,
+                               uint64_t cap) {
+    if (threadIdx.x == 0) *done = std::min<uint64_t>(*cnt, cap);
+}
+
+// Pass 2 over the records: kept[rank] = 1 iff first_w[pc] == rank.
+__global__ void pass2_kernel(const unsigned long long *rec, uint64_t cap,
+                             const unsigned long long *cnt, const int32_t *first_w,
+                             uint8_t *kept) {
+    const uint64_t hi = std::min<uint64_t>(*cnt, cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long r = rec[i];
+        const int32_t rank = (int32_t)(r >> 32);
+        if (first_w[(uint32_t)r] == rank) kept[rank] = 1;
+    }
+}
+
+// first_w back to INT32_MAX at every recorded offset (after pass 2).
+__global__ void reset_kernel(const unsigned long long *rec, uint64_t cap,
+                             const unsigned long long *cnt, int32_t *first_w) {
+    const uint64_t hi = std::min<uint64_t>(*cnt, cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        first_w[(uint32_t)rec[i]] = INT32_MAX;
+}
+
+// ---- overflow fallbacks (early exit unless *cnt > cap)
+__global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_w, uint8_t *kept) {
+    if (*A.rec_cnt <= A.rec_cap) return;
+    for (uint32_t j = blockIdx.x; j < n_items; j += gridDim.x) {
+        if (!A.cand[j]) continue;
+        const uint32_t seg = (uint32_t)A.order[j];
+        const int32_t rank = A.ranks ? A.ranks[j] : (int32_t)j;
+        const uint64_t o = A.off[seg];
+        const uint32_t n = A.split ? A.split[(uint64_t)seg * A.nrange + A.nrange - 1] : A.len[seg];
+        bool hit = false;
+        for (uint32_t q = threadIdx.x; q < n; q += blockDim.x)
+            hit |= first_w[A.pcs[o + q] - A.pc_lo] == rank;
+        if (__syncthreads_or(hit) && threadIdx.x == 0) kept[rank] = 1;
+    }
+}
+
+__global__ void ovf_union_kernel(const unsigned long long *cnt, uint64_t cap, const int32_t *first_w,
+                                 uint64_t span, uint32_t *covered) {
+    if (*cnt <= cap) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < span;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const bool set = first_w[i] != INT32_MAX;
+        const uint64_t m = __ballot(set);
+        if ((threadIdx.x & 31) == 0) {
+            const uint32_t word = (uint32_t)(m >> (threadIdx.x & 32));
+            if (word) atomicOr(&covered[i >> 5], word);
+        }
+    }
+}
+
+__global__ void ovf_reset_kernel(const unsigned long long *cnt, uint64_t cap, int32_t *first_w,
+                                 uint64_t span) {
+    if (*cnt <= cap) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < span;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        first_w[i] = INT32_MAX;
+}
+
+}  // namespace mr
+}  // namespace syz
+
+using namespace syz;
+
+/* ws: rec_done (u64) */
+extern "C" size_t syzcov_dev_minimize_range_ws_size(void) { return 256; }
+
+extern "C" int syzcov_dev_minimize_range(
+    const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
+    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
+    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream) {
+    if (n_items == 0) return 0;
+    if (!off || !pcs || !order || !range_tot || !covered || !first_w || !rec || !rec_cnt || !cand ||
+        !kept || !ws || n_items > 0x7FFFFFFF)
+        return SYZCOV_EINVAL;
+    if (range_shift < 10 || range_shift > 20 || pc_span == 0 || pc_span > (1ull << 32))
+        return SYZCOV_EINVAL;
+    const uint64_t nrange = (pc_span + (1ull << range_shift) - 1) >> range_shift;
+    if (nrange > (uint64_t)mr::MAX_R) return SYZCOV_ERANGE;
+    if (!split && nrange != 1) return SYZCOV_EINVAL;
+    if (!split && !len) return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long *done = (unsigned long long *)ws;
+    SYZ_HIP(hipMemsetAsync(done, 0, sizeof(uint64_t), s));
+    SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
+    mr::Args A;
+    A.off = off;
+    A.len = len;
+    A.pcs = pcs;
+    A.split = split;
+    A.order = order;
+    A.ranks = ranks;
+    A.pc_lo = pc_lo;
+    A.rshift = range_shift;
+    A.nrange = (uint32_t)nrange;
+    A.range_tot = (const unsigned long long *)range_tot;
+    A.covered = covered;
+    A.first_w = first_w;
+    A.rec = (unsigned long long *)rec;
+    A.rec_cap = rec_cap;
+    A.rec_cnt = (unsigned long long *)rec_cnt;
+    A.cand = cand;
+    const size_t lds = ((size_t)1 << range_shift) / 8;
+    static bool attr_set = false;  // idempotent; races only repeat the call
+    if (!attr_set) {
+        SYZ_HIP(hipFuncSetAttribute((const void *)mr::pass1_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+        attr_set = true;
+    }
+    if (first_chunk == 0) first_chunk = 64;
+    if (growth < 2) growth = 4;
+    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 18;
+    const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
+    uint64_t a = 0, step = first_chunk;
+    while (a < n_items) {
+        const uint64_t b = std::min<uint64_t>(n_items, a + step);
+        uint64_t G = (b - a) * avg_len / pcs_per_wg_hint;
+        G = std::max<uint64_t>(G, nrange);
+        G = std::min<uint64_t>(G, 8192);
+        hipLaunchKernelGGL(mr::pass1_kernel, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A,
+                           (uint32_t)a, (uint32_t)b);
+        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s,
+                           (const unsigned long long *)rec, rec_cap,
+                           (const unsigned long long *)rec_cnt, (const unsigned long long *)done,
+                           covered);
+        hipLaunchKernelGGL(mr::advance_kernel, dim3(1), dim3(64), 0, s,
+                           (const unsigned long long *)rec_cnt, done, rec_cap);
+        a = b;
+        step *= growth;
+    }
+    SYZ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s,
+                       (const unsigned long long *)rec, rec_cap, (const unsigned long long *)rec_cnt,
+                       (const int32_t *)first_w, kept);
+    hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, (uint32_t)n_items,
+                       (const int32_t *)first_w, kept);
+    hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
+                       (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
+                       pc_span, covered);
+    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s,
+                       (const unsigned long long *)rec, rec_cap, (const unsigned long long *)rec_cnt,
+                       first_w);
+    hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s,
+                       (const unsigned long long *)rec_cnt, rec_cap, first_w, pc_span);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}

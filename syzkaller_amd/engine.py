@@ -28,6 +28,7 @@ import torch
 from ._lib import check, lib
 
 INT32_MAX = 0x7FFFFFFF
+RANGE_SHIFT = 20  # 2^20 PCs per LDS-resident range (128 KB covered bitmap)
 
 
 def _p(t: torch.Tensor | None):
@@ -66,13 +67,14 @@ class CorpusEngine:
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  device="cuda", n_global: int | None = None, sort_variant: int = 0,
-                 mode: str = "pc"):
-        if mode not in ("pc", "ids"):
+                 mode: str = "range", rec_cap: int = 0):
+        if mode not in ("range", "pc", "ids"):
             raise ValueError(mode)
         L = lib()
         dev = torch.device(device)
         self.dev, self.L, self.mode = dev, L, mode
-        self.PHASES = self.PHASES_PC if mode == "pc" else self.PHASES_IDS
+        self.PHASES = {"range": self.PHASES_RANGE, "pc": self.PHASES_PC,
+                       "ids": self.PHASES_IDS}[mode]
         self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
         self.pc_lo, self.span = pc_lo, pc_span
         self.sort_variant = sort_variant
@@ -87,8 +89,24 @@ class CorpusEngine:
         self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
         ids_cap = min(pc_span, p_max) + 1
         self.ids_cap = ids_cap
-        self.first = torch.empty(pc_span if mode == "pc" else ids_cap, dtype=torch.int32,
-                                 device=dev)
+        self.first = torch.empty(pc_span if mode in ("pc", "range") else ids_cap,
+                                 dtype=torch.int32, device=dev)
+        if mode == "range":
+            # LDS-resident ranges of 2^rshift PCs; split[] columns per segment
+            self.rshift = RANGE_SHIFT
+            self.nrange = (pc_span + (1 << RANGE_SHIFT) - 1) >> RANGE_SHIFT
+            if self.nrange > 256:
+                raise ValueError("PC window too wide for the range engine (> 256 ranges)")
+            self.split = (torch.empty(n_max * self.nrange, dtype=torch.int32, device=dev)
+                          if self.nrange > 1 else None)
+            self.range_tot = torch.zeros(self.nrange, dtype=torch.int64, device=dev)
+            self.covered = torch.zeros((self.nrange << RANGE_SHIFT) // 32, dtype=torch.int32,
+                                       device=dev)
+            self.first.fill_(INT32_MAX)  # minimize_range leaves it INT32_MAX on return
+            self.rec_cap = rec_cap or max(1 << 22, min(p_max, 1 << 26))
+            self.rec = torch.empty(self.rec_cap, dtype=torch.int64, device=dev)
+            self.rec_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.cover_words = self.covered.numel()
         self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
         self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
         self.lens64 = torch.empty(self.n_global + 1, dtype=torch.int64, device=dev)
@@ -101,20 +119,23 @@ class CorpusEngine:
                  L.syzcov_dev_compact_ws_size(self.n_global),
                  L.syzcov_dev_sort_ws_size(self.n_global),
                  L.syzcov_dev_minimize_ws_size(ids_cap),
-                 L.syzcov_dev_minimize_win_ws_size(pc_span))
+                 L.syzcov_dev_minimize_win_ws_size(pc_span),
+                 L.syzcov_dev_canon_split_ws_size(n_max),
+                 L.syzcov_dev_minimize_range_ws_size())
         self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
         self.ws_size = ws
 
     # ---------------------------------------------------------------- phases
     PHASES_IDS = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
     PHASES_PC = ("canon", "dict", "order", "minimize", "compact", "union", "merge")
+    PHASES_RANGE = ("canon", "order", "minimize", "compact", "union", "merge")
     PHASES = PHASES_PC
 
     def alg_bytes(self, raw_pcs: int, canon_pcs: int) -> dict:
         """Algorithmic HBM bytes per launch of the streaming phases (DESIGN.md
         §4): every raw PC read once (4 B), every canonical PC written once and
         read once by Minimize pass 1."""
-        if self.mode == "pc":
+        if self.mode in ("pc", "range"):
             return {"canon": 4 * raw_pcs + 4 * canon_pcs, "minimize": 4 * canon_pcs}
         return {"mark": 4 * raw_pcs, "canon": 4 * raw_pcs + 4 * canon_pcs,
                 "minimize": 4 * canon_pcs}
@@ -127,6 +148,33 @@ class CorpusEngine:
                                           self.max_seg, self.pc_lo, self.span, _p(self.pres),
                                           _p(self.scal), _p(self.ws), self.ws_size, _stream()),
               "dev_canon_pcs")
+
+    def canonicalize_split(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+        """Wavefront canonicalize + per-range split points and range totals."""
+        self.scal.zero_()
+        self.range_tot.zero_()
+        check(self.L.syzcov_dev_canon_split(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
+                                            self.max_seg, self.pc_lo, self.span, self.rshift,
+                                            _p(self.split), _p(self.range_tot), _p(self.scal),
+                                            _p(self.ws), self.ws_size, _stream()),
+              "dev_canon_split")
+
+    def minimize_range(self, off, order, ranks, n_items):
+        """Range-partitioned first-cover Minimize; leaves the union in covered."""
+        self.covered.zero_()
+        self.cand[:n_items].zero_()
+        self.kept.zero_()
+        check(self.L.syzcov_dev_minimize_range(
+            _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
+            n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
+            _p(self.first), _p(self.rec), self.rec_cap, _p(self.rec_cnt), _p(self.cand),
+            _p(self.kept), 0, 0, 0, _p(self.ws), _stream()), "dev_minimize_range")
+
+    def union_from_covered(self):
+        check(self.L.syzcov_dev_dict_build_bits(_p(self.covered), self.span, _p(self.tab),
+                                                _p(self.scal[1:2]), _p(self.ws), _stream()),
+              "dev_dict_build_bits")
+        self.union_list()
 
     def minimize_win(self, off, order, ranks, n_items, do_pass2=True):
         self.first.fill_(INT32_MAX)
@@ -202,6 +250,22 @@ class CorpusEngine:
                 ev[k[0]].record()
             k[0] += 1
         mark_ev()
+        if self.mode == "range":
+            self.canonicalize_split(off, raw, n)
+            mark_ev()
+            self.sort_order(self.new_len, n)
+            mark_ev()
+            self.minimize_range(off, self.order, None, n)
+            mark_ev()
+            self.compact(n)
+            mark_ev()
+            self.union_from_covered()
+            mark_ev()
+            check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered),
+                                              self.nwords, _p(self.scal[4:5]), _stream()),
+                  "dev_bitmap_op")
+            mark_ev()
+            return self.result() if sync else None
         if self.mode == "pc":
             self.canonicalize_pcs(off, raw, n)
             mark_ev()
@@ -239,7 +303,7 @@ class CorpusEngine:
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """Materialise the canonical covers as PCs (CSR slots of `off`)."""
-        if self.mode == "pc":
+        if self.mode in ("pc", "range"):
             return self.canon
         table = _u32(self.ids_cap, self.dev)
         check(self.L.syzcov_dev_dict_pcs(_p(self.tab), self.span, self.pc_lo, _p(table),

@@ -29,7 +29,7 @@ def test_synth_matches_cpu_twin(torch):
         assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
 
 
-@pytest.mark.parametrize("mode", ["pc", "ids"])
+@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
                                                (500, 9000, 6000, 20)])
 def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, mode):
@@ -62,7 +62,7 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, mode):
     assert res2.max_cover == exp_union.size
 
 
-@pytest.mark.parametrize("mode", ["pc", "ids"])
+@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
 def test_engine_sentinel_window(torch, mode):
     """Window touching 0xFFFFFFFF: inputs made only of the sentinel canonicalize
     to empty, otherwise it is an ordinary PC (cover.go:36-52, 104-131)."""
@@ -105,7 +105,7 @@ def test_sharded_engine_world1(torch):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("mode", ["pc", "ids"])
+@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
 def test_engine_properties_large(torch, mode):
     """Size-independent properties at 200k inputs: union(kept) == union(all),
     kept order follows non-increasing canonical length, first kept = rank 0."""
