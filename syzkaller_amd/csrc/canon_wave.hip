@@ -72,7 +72,6 @@ struct Params {
     uint32_t *out;
     uint32_t *new_len;
     uint64_t nseg;
-    uint32_t lo_len, hi_len;  // this launch: lo_len <= n <= hi_len
     uint32_t pc_lo;
     uint64_t span;
     uint32_t nbits;
@@ -81,14 +80,59 @@ struct Params {
     uint32_t nrange, rshift;
     unsigned long long *range_tot;  // nullable: [nrange]
     uint32_t *redo_list, *redo_cnt;  // wave sort failed its order check
-    uint32_t *big_list, *big_cnt;    // n > WAVE_MAX (listed by the launch with list_big)
-    int list_big;
+    uint32_t *big_list, *big_cnt;    // n > WAVE_MAX (listed by bin_kernel)
     uint32_t *err;
 };
 
-// NK = keys per lane (CAP = 64 * NK, NK a multiple of 4).
+// Wave-aggregated binning of segments into capacity classes (one atomic per
+// wave and class): lists[c][..] = segments with cls_lo[c] <= n <= cls_hi[c].
+constexpr int NCLS = 5;
+struct Classes { uint32_t lo[NCLS], hi[NCLS]; };
+
+__global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ off, uint64_t nseg,
+                                                  Classes C, uint32_t *__restrict__ counts,
+                                                  uint32_t *__restrict__ lists, uint64_t stride,
+                                                  uint32_t *__restrict__ big_list,
+                                                  uint32_t *__restrict__ big_cnt) {
+    const uint32_t l = __lane_id();
+    const uint64_t lt = (1ull << l) - 1ull;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < nseg;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = b + l;
+        int c = -1;
+        bool big = false;
+        if (i < nseg) {
+            const uint64_t n = off[i + 1] - off[i];
+            big = n > WAVE_MAX;
+#pragma unroll
+            for (int k = 0; k < NCLS; k++)
+                if (n >= C.lo[k] && n <= C.hi[k]) c = k;
+        }
+#pragma unroll
+        for (int k = 0; k <= NCLS; k++) {
+            const bool mine = k < NCLS ? c == k : big;
+            const uint64_t m = __ballot(mine);
+            if (!m) continue;
+            const uint32_t leader = __builtin_ctzll(m);
+            uint32_t base = 0;
+            if (l == leader) base = atomicAdd(k < NCLS ? &counts[k] : big_cnt, (uint32_t)__popcll(m));
+            base = __shfl(base, leader, 64);
+            if (mine) {
+                const uint32_t slot = base + (uint32_t)__popcll(m & lt);
+                if (k < NCLS) lists[k * stride + slot] = (uint32_t)i; else big_list[slot] = (uint32_t)i;
+            }
+        }
+    }
+}
+
+// NK = keys per lane (CAP = 64 * NK, NK a multiple of 4).  Segments come from
+// a class list; the next segment's raw keys are loaded while the current one
+// is sorted (software pipelining hides the HBM latency of the 16-byte loads).
+// Slots outside the segment hold PAD (all digits maximal), so every row is
+// full and the sorted real keys are exactly buf[0, n).
 template <int NK>
-__global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P) {
+__global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P, const uint32_t *list,
+                                                              const uint32_t *count) {
     constexpr int CAP = 64 * NK;
     constexpr int NQ = NK / 4;  // 16-byte loads per lane
     __shared__ uint32_t s_buf[WPB][CAP];
@@ -101,93 +145,96 @@ __global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P) {
     const uint32_t npass = (nbits + 8) / 9;
     const uint32_t dbits = (nbits + npass - 1) / npass;  // <= 9
     const uint32_t dmask = (1u << dbits) - 1u;
+    const uint32_t PAD = npass * dbits >= 32 ? 0xFFFFFFFFu : (1u << (npass * dbits)) - 1u;
+    const uint64_t lt = (1ull << l) - 1ull;
     uint32_t racc[MAX_RPL];
 #pragma unroll
     for (int q = 0; q < MAX_RPL; q++) racc[q] = 0;
-    const uint64_t nw = (uint64_t)gridDim.x * WPB;
-    for (uint64_t seg = (uint64_t)blockIdx.x * WPB + w; seg < P.nseg; seg += nw) {
-        const uint64_t base = P.off[seg];
-        const uint64_t n64 = P.off[seg + 1] - base;
-        if (P.list_big && n64 > WAVE_MAX) {
-            if (l == 0) P.big_list[atomicAdd(P.big_cnt, 1u)] = (uint32_t)seg;
-            continue;
-        }
-        if (n64 < P.lo_len || n64 > P.hi_len) continue;
-        const uint32_t n = (uint32_t)n64;
-        // ---------------------------------------------------------- load
-        const uint64_t a0 = base & ~3ull;
-        const uint32_t head = (uint32_t)(base - a0);
-        const uint32_t end = head + n;  // aligned-window index of the end
+    const uint32_t nl = *count;
+    const uint32_t nw = gridDim.x * WPB;
+    uint32_t li = blockIdx.x * WPB + w;
+    // prefetch state
+    uint32_t kn[NK];
+    uint64_t nbase = 0;
+    uint32_t nseg = 0, nhead = 0, nend = 0;
+    auto fetch = [&](uint32_t idx) {
+        nseg = list[idx];
+        nbase = P.off[nseg];
+        const uint32_t n = (uint32_t)(P.off[nseg + 1] - nbase);
+        const uint64_t a0 = nbase & ~3ull;
+        nhead = (uint32_t)(nbase - a0);
+        nend = nhead + n;
         const uint4 *src = reinterpret_cast<const uint4 *>(P.raw + a0);
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if ((uint32_t)(q * 256) < nend && e4 < nend) v = src[q * 64 + l];
+            kn[q * 4 + 0] = v.x; kn[q * 4 + 1] = v.y; kn[q * 4 + 2] = v.z; kn[q * 4 + 3] = v.w;
+        }
+    };
+    if (li < nl) fetch(li);
+    for (; li < nl; li += nw) {
+        const uint32_t seg = nseg;
+        const uint64_t base = nbase;
+        const uint32_t head = nhead, end = nend, n = end - head;
+        const uint32_t nq = (end + 255) >> 8;  // active 256-key quads
         uint32_t k[NK];
         bool oob = false;
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
             const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (e4 < end) v = src[q * 64 + l];
-            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 const uint32_t idx = e4 + c;
-                const uint32_t key = vv[c] - P.pc_lo;
+                const uint32_t key = kn[q * 4 + c] - P.pc_lo;
                 const bool valid = idx >= head && idx < end;
                 oob |= valid && (uint64_t)key >= P.span;
-                k[q * 4 + c] = key;
+                k[q * 4 + c] = valid ? key : PAD;
             }
         }
+        if (li + nw < nl) fetch(li + nw);
         if (__ballot(oob) && l == 0) *P.err = 1u;
         // ------------------------------------------- pass 0 (unstable)
         hist_zero(hist, l);
         wave_sync();
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-            if ((uint32_t)(q * 256) < end) {
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
 #pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const uint32_t idx = e4 + c;
-                    if (idx >= head && idx < end) atomicAdd(&hist[k[q * 4 + c] & dmask], 1u);
-                }
+                for (int c = 0; c < 4; c++) atomicAdd(&hist[k[q * 4 + c] & dmask], 1u);
             }
-        }
         wave_sync();
         hist_scan(hist, l);
         wave_sync();
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-            if ((uint32_t)(q * 256) < end) {
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-                    const uint32_t idx = e4 + c;
-                    if (idx >= head && idx < end) {
-                        const uint32_t key = k[q * 4 + c];
-                        buf[atomicAdd(&hist[key & dmask], 1u)] = key;
-                    }
+                    const uint32_t key = k[q * 4 + c];
+                    buf[atomicAdd(&hist[key & dmask], 1u)] = key;
                 }
             }
-        }
         wave_sync();
         // --------------------------------------------- stable passes
+        const uint32_t nrow = nq * 4;
         for (uint32_t p = 1; p < npass; p++) {
             const uint32_t sh = p * dbits;
 #pragma unroll
             for (int r = 0; r < NK; r++)
-                if ((uint32_t)(r * 64) < n) k[r] = buf[r * 64 + l];
+                if ((uint32_t)r < nrow) k[r] = buf[r * 64 + l];
             hist_zero(hist, l);
             wave_sync();
 #pragma unroll
             for (int r = 0; r < NK; r++)
-                if ((uint32_t)(r * 64) < n && (uint32_t)(r * 64) + l < n)
-                    atomicAdd(&hist[(k[r] >> sh) & dmask], 1u);
+                if ((uint32_t)r < nrow) atomicAdd(&hist[(k[r] >> sh) & dmask], 1u);
             wave_sync();
             hist_scan(hist, l);
             wave_sync();
 #pragma unroll
             for (int r = 0; r < NK; r++)
-                if ((uint32_t)(r * 64) < n && (uint32_t)(r * 64) + l < n)
-                    buf[atomicAdd(&hist[(k[r] >> sh) & dmask], 1u)] = k[r];
+                if ((uint32_t)r < nrow) buf[atomicAdd(&hist[(k[r] >> sh) & dmask], 1u)] = k[r];
             wave_sync();
         }
         // ------------------------------------------- order check
@@ -195,15 +242,14 @@ __global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P) {
 #pragma unroll
         for (int r = 0; r < NK; r++) {
             const uint32_t e = (uint32_t)(r * 64) + l;
-            if ((uint32_t)(r * 64) < n && e < n && e > 0) bad |= buf[e] < buf[e - 1];
+            if ((uint32_t)r < nrow && e > 0 && e < n) bad |= buf[e] < buf[e - 1];
         }
         if (__ballot(bad)) {
-            if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = (uint32_t)seg;
+            if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = seg;
             continue;
         }
         // ------------------------------------------- unique + write
         uint32_t cnt = 0;
-        const uint64_t lt = (1ull << l) - 1ull;
 #pragma unroll
         for (int r = 0; r < NK; r++) {
             if ((uint32_t)(r * 64) < n) {
@@ -227,7 +273,7 @@ __global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P) {
         } else {
             wave_sync();
             uint32_t carry = 0;
-            uint32_t *sp = P.split + seg * P.nrange;
+            uint32_t *sp = P.split + (uint64_t)seg * P.nrange;
 #pragma unroll
             for (int q = 0; q < MAX_RPL; q++) {
                 const uint32_t j = q * 64 + l;
@@ -303,7 +349,8 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
 using namespace syz;
 
 extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
-    return 256 + 2 * align_up(nseg * sizeof(uint32_t), 256);
+    // counters | redo list | big list | class lists
+    return 256 + (2 + cw::NCLS) * align_up(nseg * sizeof(uint32_t), 256);
 }
 
 extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *out,
@@ -323,7 +370,7 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     if (split && nrange > (uint64_t)cw::MAX_RPL * 64) return SYZCOV_ERANGE;
     hipStream_t s = (hipStream_t)stream;
     uint8_t *w = (uint8_t *)ws;
-    uint32_t *cnts = (uint32_t *)w;  // [0] redo, [1] big
+    uint32_t *cnts = (uint32_t *)w;  // [0] redo, [1] big, [2..] classes
     uint32_t *redo = (uint32_t *)(w + 256);
     uint32_t *big = (uint32_t *)(w + 256 + align_up(nseg * sizeof(uint32_t), 256));
     SYZ_HIP(hipMemsetAsync(cnts, 0, 2 * sizeof(uint32_t), s));
@@ -347,20 +394,28 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     P.big_list = big;
     P.big_cnt = cnts + 1;
     P.err = err_flag;
-    // one launch per capacity class; each grid-strides over all segments
-    struct Cls { uint32_t lo, hi; };
-    const Cls cls[4] = {{0, 1021}, {1022, 2045}, {2046, 4093}, {4094, cw::WAVE_MAX}};
+    // bin by capacity class (wave-aggregated atomics), one launch per class
+    cw::Classes C;
+    const uint32_t nk[cw::NCLS] = {16, 32, 48, 64, 128};
+    for (int c = 0; c < cw::NCLS; c++) {
+        C.lo[c] = c ? nk[c - 1] * 64 - 2 : 0;  // CAP - 3 + 1 of the previous class
+        C.hi[c] = nk[c] * 64 - 3;
+    }
+    uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
+    uint32_t *ccnt = cnts + 2;
+    SYZ_HIP(hipMemsetAsync(ccnt, 0, cw::NCLS * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 4096)), dim3(256), 0, s, off,
+                       (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1);
     const unsigned grid = (unsigned)std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, 4096);
-    for (int c = 0; c < 4; c++) {
-        if (c > 0 && max_seg_len < cls[c].lo) break;
-        P.lo_len = cls[c].lo;
-        P.hi_len = cls[c].hi;
-        P.list_big = c == 0;
+    for (int c = 0; c < cw::NCLS; c++) {
+        if (max_seg_len < C.lo[c]) break;
+        const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
-        case 0: hipLaunchKernelGGL(cw::canon_wave_kernel<16>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
-        case 1: hipLaunchKernelGGL(cw::canon_wave_kernel<32>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
-        case 2: hipLaunchKernelGGL(cw::canon_wave_kernel<64>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
-        case 3: hipLaunchKernelGGL(cw::canon_wave_kernel<128>, dim3(grid), dim3(64 * cw::WPB), 0, s, P); break;
+        case 0: hipLaunchKernelGGL(cw::canon_wave_kernel<16>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 1: hipLaunchKernelGGL(cw::canon_wave_kernel<32>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL(cw::canon_wave_kernel<48>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 3: hipLaunchKernelGGL(cw::canon_wave_kernel<64>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 4: hipLaunchKernelGGL(cw::canon_wave_kernel<128>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         }
         SYZ_LAUNCH_CHECK();
     }

@@ -56,7 +56,26 @@ struct Args {
     uint64_t rec_cap;
     unsigned long long *rec_cnt;  // may exceed rec_cap (overflow)
     uint8_t *cand;             // [items] item had an uncovered PC
+    // rank-ordered descriptors (prep_kernel): coalesced per (range, item slice)
+    const uint64_t *base_r;    // [items] off[order[j]]
+    const uint32_t *split_t;   // [nrange][items] split[order[j]][rho]
+    uint32_t n_items;
 };
+
+// Gather the items' CSR bases and split columns into rank order, transposed
+// so that a workgroup owning range rho reads split_t[rho][i0..i1) contiguously.
+__global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uint32_t *split_t) {
+    const uint32_t n = A.n_items;
+    for (uint32_t t0 = blockIdx.x * 64; t0 < n; t0 += gridDim.x * 64) {
+        const uint32_t j = t0 + (threadIdx.x & 63);
+        if (j >= n) continue;
+        const uint32_t seg = (uint32_t)A.order[j];
+        if (threadIdx.x < 64) base_r[j] = A.off[seg];
+        for (uint32_t rho = threadIdx.x >> 6; rho < A.nrange; rho += 4)
+            split_t[(uint64_t)rho * n + j] =
+                A.split ? A.split[(uint64_t)seg * A.nrange + rho] : A.len[seg];
+    }
+}
 
 // Workgroup -> (range, item slice [i0, i1)) with pieces proportional to the
 // range's weight: p_j = 1 + floor(w_j * (G - R) / W).
@@ -123,18 +142,10 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
         uint32_t m = 0;
         int32_t rk = 0;
         if (item < i1) {
-            const uint32_t seg = (uint32_t)A.order[item];
             rk = A.ranks ? A.ranks[item] : (int32_t)item;
-            const uint64_t o = A.off[seg];
-            uint32_t s0 = 0, s1;
-            if (A.split) {
-                const uint32_t *sp = A.split + (uint64_t)seg * A.nrange;
-                s1 = sp[rho];
-                if (rho) s0 = sp[rho - 1];
-            } else {
-                s1 = A.len[seg];
-            }
-            st = o + s0;
+            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            st = A.base_r[item] + s0;
             m = s1 - s0;
         }
         const uint32_t incl = wave_incl_scan(m);
@@ -250,10 +261,9 @@ __global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_
     if (*A.rec_cnt <= A.rec_cap) return;
     for (uint32_t j = blockIdx.x; j < n_items; j += gridDim.x) {
         if (!A.cand[j]) continue;
-        const uint32_t seg = (uint32_t)A.order[j];
         const int32_t rank = A.ranks ? A.ranks[j] : (int32_t)j;
-        const uint64_t o = A.off[seg];
-        const uint32_t n = A.split ? A.split[(uint64_t)seg * A.nrange + A.nrange - 1] : A.len[seg];
+        const uint64_t o = A.base_r[j];
+        const uint32_t n = A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + j];
         bool hit = false;
         for (uint32_t q = threadIdx.x; q < n; q += blockDim.x)
             hit |= first_w[A.pcs[o + q] - A.pc_lo] == rank;
@@ -288,8 +298,17 @@ __global__ void ovf_reset_kernel(const unsigned long long *cnt, uint64_t cap, in
 
 using namespace syz;
 
-/* ws: rec_done (u64) */
-extern "C" size_t syzcov_dev_minimize_range_ws_size(void) { return 256; }
+/* ws: rec_done (u64) | base_r [n_items] u64 | split_t [nrange][n_items] u32 */
+static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
+    return (span + (1ull << rshift) - 1) >> rshift;
+}
+
+extern "C" size_t syzcov_dev_minimize_range_ws_size(size_t n_items, uint64_t pc_span,
+                                                    uint32_t range_shift) {
+    if (range_shift > 20) range_shift = 20;
+    return 256 + align_up(n_items * 8, 256) +
+           align_up(mr_nrange(pc_span, range_shift) * n_items * 4, 256);
+}
 
 extern "C" int syzcov_dev_minimize_range(
     const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
@@ -303,7 +322,7 @@ extern "C" int syzcov_dev_minimize_range(
         return SYZCOV_EINVAL;
     if (range_shift < 10 || range_shift > 20 || pc_span == 0 || pc_span > (1ull << 32))
         return SYZCOV_EINVAL;
-    const uint64_t nrange = (pc_span + (1ull << range_shift) - 1) >> range_shift;
+    const uint64_t nrange = mr_nrange(pc_span, range_shift);
     if (nrange > (uint64_t)mr::MAX_R) return SYZCOV_ERANGE;
     if (!split && nrange != 1) return SYZCOV_EINVAL;
     if (!split && !len) return SYZCOV_EINVAL;
@@ -328,6 +347,13 @@ extern "C" int syzcov_dev_minimize_range(
     A.rec_cap = rec_cap;
     A.rec_cnt = (unsigned long long *)rec_cnt;
     A.cand = cand;
+    A.n_items = (uint32_t)n_items;
+    uint64_t *base_r = (uint64_t *)((uint8_t *)ws + 256);
+    uint32_t *split_t = (uint32_t *)((uint8_t *)base_r + align_up(n_items * 8, 256));
+    A.base_r = base_r;
+    A.split_t = split_t;
+    hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
+                       base_r, split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
     static bool attr_set = false;  // idempotent; races only repeat the call
     if (!attr_set) {

@@ -121,7 +121,7 @@ class CorpusEngine:
                  L.syzcov_dev_minimize_ws_size(ids_cap),
                  L.syzcov_dev_minimize_win_ws_size(pc_span),
                  L.syzcov_dev_canon_split_ws_size(n_max),
-                 L.syzcov_dev_minimize_range_ws_size())
+                 L.syzcov_dev_minimize_range_ws_size(self.n_global, pc_span, RANGE_SHIFT))
         self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
         self.ws_size = ws
 
