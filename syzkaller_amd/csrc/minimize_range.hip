@@ -37,7 +37,7 @@ namespace mr {
 
 constexpr int THREADS = 1024;
 constexpr int NWAVE = THREADS / 64;
-constexpr int ROWS = 8;          // row loads in flight per wave
+constexpr int ROWS = 16;         // row loads in flight per wave
 constexpr int MAX_R = 256;
 
 struct Args {
@@ -117,7 +117,8 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t a, uint32_t b, uint
 }
 
 // Pass 1 over items [a, b) (one chunk).
-__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b) {
+__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b,
+                                                        int load_cov) {
     extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
     __shared__ uint32_t s_plan[MAX_R + 1];
     uint32_t rho, i0, i1;
@@ -126,22 +127,28 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
     {
         const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
-        for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
-        for (uint32_t q = (nwords / 4) * 4 + threadIdx.x; q < nwords; q += THREADS)
-            s_cov[q] = A.covered[(uint64_t)rho * nwords + q];
+        if (load_cov) {
+            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
+        } else {  // first chunk: nothing is covered yet
+            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
+                s4[q] = make_uint4(0, 0, 0, 0);
+        }
     }
     __syncthreads();
     const uint32_t l = __lane_id();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t rbase = rho << A.rshift;  // window offset of the range
-    for (uint32_t ib = i0 + w * 64; ib < i1; ib += NWAVE * 64) {
+    // the slice is split evenly over the waves, 64 items per batch
+    const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+    const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+    for (uint32_t ib = w0; ib < w1; ib += 64) {
         // ---- per-lane item descriptor: sub-run of range rho
         const uint32_t item = ib + l;
         uint64_t st = 0;
         uint32_t m = 0;
         int32_t rk = 0;
-        if (item < i1) {
+        if (item < w1) {
             rk = A.ranks ? A.ranks[item] : (int32_t)item;
             const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
             const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
@@ -190,26 +197,34 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                     v[u] = act[u] ? A.pcs[my_st + (f - my_pre)] : 0u;
                 }
             }
+            // LDS bit tests; one record reservation per batch of ROWS rows
+            uint64_t um[ROWS];
+            uint32_t nunc = 0;
 #pragma unroll
             for (int u = 0; u < ROWS; u++) {
+                um[u] = 0;
                 if (R0 + u * 64 < T) {
-                    const uint32_t wo = v[u] - A.pc_lo;           // window offset
-                    const uint32_t bit = act[u] ? wo - rbase : 0u;  // < 2^rshift
+                    const uint32_t bit = act[u] ? v[u] - A.pc_lo - rbase : 0u;  // < 2^rshift
                     const bool unc = act[u] && !((s_cov[bit >> 5] >> (bit & 31)) & 1u);
-                    const uint64_t um = __ballot(unc);
-                    if (um) {
-                        unsigned long long basei = 0;
-                        if (l == __builtin_ctzll(um))
-                            basei = atomicAdd(A.rec_cnt, (unsigned long long)__popcll(um));
-                        basei = __shfl(basei, __builtin_ctzll(um), 64);
-                        if (unc) {
-                            atomicMin(&A.first_w[wo], (int32_t)rkv[u]);
-                            const uint64_t slot = basei + (uint64_t)__popcll(um & lt);
-                            if (slot < A.rec_cap)
-                                A.rec[slot] = ((unsigned long long)rkv[u] << 32) | wo;
-                            A.cand[ix[u]] = 1;
-                        }
+                    um[u] = __ballot(unc);
+                    nunc += (uint32_t)__popcll(um[u]);
+                }
+            }
+            if (nunc) {
+                unsigned long long basei = 0;
+                if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)nunc);
+                basei = __shfl(basei, 0, 64);
+#pragma unroll
+                for (int u = 0; u < ROWS; u++) {
+                    if ((um[u] >> l) & 1u) {
+                        const uint32_t wo = v[u] - A.pc_lo;
+                        atomicMin(&A.first_w[wo], (int32_t)rkv[u]);
+                        const uint64_t slot = basei + (uint64_t)__popcll(um[u] & lt);
+                        if (slot < A.rec_cap)
+                            A.rec[slot] = ((unsigned long long)rkv[u] << 32) | wo;
+                        A.cand[ix[u]] = 1;
                     }
+                    basei += (uint64_t)__popcll(um[u]);
                 }
             }
         }
@@ -369,10 +384,10 @@ extern "C" int syzcov_dev_minimize_range(
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
         uint64_t G = (b - a) * avg_len / pcs_per_wg_hint;
-        G = std::max<uint64_t>(G, nrange);
+        G = std::max<uint64_t>(G, std::max<uint64_t>(4 * nrange, 1024));
         G = std::min<uint64_t>(G, 8192);
         hipLaunchKernelGGL(mr::pass1_kernel, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A,
-                           (uint32_t)a, (uint32_t)b);
+                           (uint32_t)a, (uint32_t)b, (int)(a != 0));
         hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s,
                            (const unsigned long long *)rec, rec_cap,
                            (const unsigned long long *)rec_cnt, (const unsigned long long *)done,
