@@ -60,6 +60,11 @@ __device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
     h4[2 * l + 1] = ob;
 }
 
+// Lane l receives v of lane l-1; lane 0 receives `first` (DPP wave_shr:1).
+__device__ __forceinline__ uint32_t shift_up(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
     h4[2 * l] = make_uint4(0, 0, 0, 0);
@@ -125,146 +130,163 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
     }
 }
 
-// NK = keys per lane (CAP = 64 * NK, NK a multiple of 4).  Segments come from
-// a class list; the next segment's raw keys are loaded while the current one
-// is sorted (software pipelining hides the HBM latency of the 16-byte loads).
-// Slots outside the segment hold PAD (all digits maximal), so every row is
-// full and the sorted real keys are exactly buf[0, n).
-template <int NK>
-__global__ __launch_bounds__(64 * WPB) void canon_wave_kernel(Params P, const uint32_t *list,
-                                                              const uint32_t *count) {
+// NK = keys per lane (CAP = 64 * NK, NK a multiple of 4); MINW = waves per
+// SIMD the register budget must allow (LDS caps residency anyway).  Segments
+// come from a class list.  Slots outside the segment hold PAD (all digits
+// maximal), so every row is full and the sorted real keys are buf[0, n).  Each
+// pass counts the NEXT pass's digits while it scatters (two histograms), so a
+// pass is one read-back and one scatter loop; the keys of the pass being
+// scattered live in registers only between those two loops.
+template <int NK, int MINW>
+__global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, const uint32_t *list,
+                                                                    const uint32_t *count) {
     constexpr int CAP = 64 * NK;
-    constexpr int NQ = NK / 4;  // 16-byte loads per lane
+    constexpr int NQ = NK / 4;  // 16-byte loads per lane = row quads
     __shared__ uint32_t s_buf[WPB][CAP];
-    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][2][HIST];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
-    uint32_t *hist = s_hist[w];
     const uint32_t nbits = P.nbits < 1 ? 1 : P.nbits;
     const uint32_t npass = (nbits + 8) / 9;
     const uint32_t dbits = (nbits + npass - 1) / npass;  // <= 9
     const uint32_t dmask = (1u << dbits) - 1u;
     const uint32_t PAD = npass * dbits >= 32 ? 0xFFFFFFFFu : (1u << (npass * dbits)) - 1u;
     const uint64_t lt = (1ull << l) - 1ull;
+    const uint32_t span_m1 = (uint32_t)(P.span - 1);
+    const bool inplace = P.out == P.raw;
     uint32_t racc[MAX_RPL];
 #pragma unroll
     for (int q = 0; q < MAX_RPL; q++) racc[q] = 0;
     const uint32_t nl = *count;
     const uint32_t nw = gridDim.x * WPB;
-    uint32_t li = blockIdx.x * WPB + w;
-    // prefetch state
-    uint32_t kn[NK];
-    uint64_t nbase = 0;
-    uint32_t nseg = 0, nhead = 0, nend = 0;
-    auto fetch = [&](uint32_t idx) {
-        nseg = list[idx];
-        nbase = P.off[nseg];
-        const uint32_t n = (uint32_t)(P.off[nseg + 1] - nbase);
-        const uint64_t a0 = nbase & ~3ull;
-        nhead = (uint32_t)(nbase - a0);
-        nend = nhead + n;
+    for (uint32_t li = blockIdx.x * WPB + w; li < nl; li += nw) {
+        const uint32_t seg = list[li];
+        const uint64_t base = P.off[seg];
+        const uint32_t n = (uint32_t)(P.off[seg + 1] - base);
+        const uint64_t a0 = base & ~3ull;
+        const uint32_t head = (uint32_t)(base - a0), end = head + n;
+        const uint32_t nq = (end + 255) >> 8;  // active row quads (256 keys each)
         const uint4 *src = reinterpret_cast<const uint4 *>(P.raw + a0);
-#pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if ((uint32_t)(q * 256) < nend && e4 < nend) v = src[q * 64 + l];
-            kn[q * 4 + 0] = v.x; kn[q * 4 + 1] = v.y; kn[q * 4 + 2] = v.z; kn[q * 4 + 3] = v.w;
-        }
-    };
-    if (li < nl) fetch(li);
-    for (; li < nl; li += nw) {
-        const uint32_t seg = nseg;
-        const uint64_t base = nbase;
-        const uint32_t head = nhead, end = nend, n = end - head;
-        const uint32_t nq = (end + 255) >> 8;  // active 256-key quads
         uint32_t k[NK];
         bool oob = false;
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
-            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            if ((uint32_t)q < nq) {
+                const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+                // chunks past the end re-read chunk 0 (always inside the buffer)
+                const uint4 v = src[e4 < end ? q * 64 + l : 0];
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const uint32_t idx = e4 + c;
-                const uint32_t key = kn[q * 4 + c] - P.pc_lo;
-                const bool valid = idx >= head && idx < end;
-                oob |= valid && (uint64_t)key >= P.span;
-                k[q * 4 + c] = valid ? key : PAD;
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t idx = e4 + c;
+                    const uint32_t key = vv[c] - P.pc_lo;
+                    const bool valid = idx >= head && idx < end;
+                    oob |= valid && key > span_m1;
+                    k[q * 4 + c] = valid ? key : PAD;
+                }
             }
         }
-        if (li + nw < nl) fetch(li + nw);
         if (__ballot(oob) && l == 0) *P.err = 1u;
         // ------------------------------------------- pass 0 (unstable)
-        hist_zero(hist, l);
+        hist_zero(s_hist[w][0], l);
+        hist_zero(s_hist[w][1], l);
         wave_sync();
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
 #pragma unroll
-                for (int c = 0; c < 4; c++) atomicAdd(&hist[k[q * 4 + c] & dmask], 1u);
+                for (int c = 0; c < 4; c++) atomicAdd(&s_hist[w][0][k[q * 4 + c] & dmask], 1u);
             }
         wave_sync();
-        hist_scan(hist, l);
+        hist_scan(s_hist[w][0], l);
         wave_sync();
+        const bool two = npass > 1;
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t key = k[q * 4 + c];
-                    buf[atomicAdd(&hist[key & dmask], 1u)] = key;
+                    buf[atomicAdd(&s_hist[w][0][key & dmask], 1u)] = key;
+                    if (two) atomicAdd(&s_hist[w][1][(key >> dbits) & dmask], 1u);
                 }
             }
         wave_sync();
         // --------------------------------------------- stable passes
-        const uint32_t nrow = nq * 4;
         for (uint32_t p = 1; p < npass; p++) {
             const uint32_t sh = p * dbits;
+            const uint32_t pc = p & 1, pn = pc ^ 1;
+            const bool more = p + 1 < npass;
 #pragma unroll
-            for (int r = 0; r < NK; r++)
-                if ((uint32_t)r < nrow) k[r] = buf[r * 64 + l];
-            hist_zero(hist, l);
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
+#pragma unroll
+                    for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
+                }
+            hist_scan(s_hist[w][pc], l);
+            if (more) hist_zero(s_hist[w][pn], l);
             wave_sync();
 #pragma unroll
-            for (int r = 0; r < NK; r++)
-                if ((uint32_t)r < nrow) atomicAdd(&hist[(k[r] >> sh) & dmask], 1u);
-            wave_sync();
-            hist_scan(hist, l);
-            wave_sync();
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
 #pragma unroll
-            for (int r = 0; r < NK; r++)
-                if ((uint32_t)r < nrow) buf[atomicAdd(&hist[(k[r] >> sh) & dmask], 1u)] = k[r];
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t key = k[q * 4 + c];
+                        buf[atomicAdd(&s_hist[w][pc][(key >> sh) & dmask], 1u)] = key;
+                        if (more) atomicAdd(&s_hist[w][pn][(key >> (sh + dbits)) & dmask], 1u);
+                    }
+                }
             wave_sync();
         }
-        // ------------------------------------------- order check
-        bool bad = false;
+        // --------------------------------- order check + unique + write
+        // prev of slot e is slot e-1 (lane l-1 of the row, or lane 63 of the
+        // previous row); the reference's `last := sent` for e == 0.
+        uint32_t bad = 0;
+        if (inplace) {  // nothing may be written before the order is known
+            uint32_t carry = P.sent_key;
 #pragma unroll
-        for (int r = 0; r < NK; r++) {
-            const uint32_t e = (uint32_t)(r * 64) + l;
-            if ((uint32_t)r < nrow && e > 0 && e < n) bad |= buf[e] < buf[e - 1];
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                        const uint32_t v = buf[e];
+                        const uint32_t prev = shift_up(v, carry);
+                        carry = __builtin_amdgcn_readlane(v, 63);
+                        bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                    }
+                }
+            if (__ballot(bad)) {
+                if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = seg;
+                continue;
+            }
         }
-        if (__ballot(bad)) {
+        uint32_t cnt = 0, carry = P.sent_key;
+        uint32_t *outp = P.out + base;
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                    const uint32_t v = buf[e];
+                    const uint32_t prev = shift_up(v, carry);
+                    carry = __builtin_amdgcn_readlane(v, 63);
+                    bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                    const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
+                    const uint64_t m = __ballot(keep);
+                    const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                    if (keep) {
+                        outp[pos] = v + P.pc_lo;
+                        buf[pos] = v;
+                    }
+                    cnt += (uint32_t)__popcll(m);
+                }
+            }
+        if (__ballot(bad)) {  // out-of-place: the fallback rewrites this segment
             if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = seg;
             continue;
-        }
-        // ------------------------------------------- unique + write
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int r = 0; r < NK; r++) {
-            if ((uint32_t)(r * 64) < n) {
-                const uint32_t e = (uint32_t)(r * 64) + l;
-                const uint32_t v = buf[e];
-                const uint32_t prev = e == 0 ? P.sent_key : buf[e - 1];
-                const bool keep = e < n && v != prev;
-                const uint64_t m = __ballot(keep);
-                const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
-                if (keep) {
-                    P.out[base + pos] = v + P.pc_lo;
-                    buf[pos] = v;
-                }
-                cnt += (uint32_t)__popcll(m);
-            }
         }
         if (l == 0) P.new_len[seg] = cnt;
         // ------------------------------------------- range splits
@@ -411,11 +433,11 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
-        case 0: hipLaunchKernelGGL(cw::canon_wave_kernel<16>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 1: hipLaunchKernelGGL(cw::canon_wave_kernel<32>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL(cw::canon_wave_kernel<48>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 3: hipLaunchKernelGGL(cw::canon_wave_kernel<64>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 4: hipLaunchKernelGGL(cw::canon_wave_kernel<128>, dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, 3>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<48, 3>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         }
         SYZ_LAUNCH_CHECK();
     }
