@@ -31,6 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
+# this same bench command (tools/profile.sh -> tools/traffic.py), committed per round
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED = 0x5EED0002
 SEED_PRIO = 0x5EED0004
@@ -50,7 +53,8 @@ def parse():
                     help="inputs timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--engine", choices=["range", "pc", "ids"], default="range",
-                    help="canonical form: window PCs (default) or dense ids")
+                    help="range: wavefront canonicalize + range-partitioned Minimize "
+                         "(default); pc / ids: earlier engines kept for comparison")
     return ap.parse_args()
 
 
@@ -168,6 +172,10 @@ def bench_corpus(args):
     alg = eng.alg_bytes(total, canon_pcs)
     dom = max(alg, key=lambda p: ph[p])
     achieved = alg[dom] / (ph[dom] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(TRAFFIC_JSON) and args.engine == "range" and world == 1:
+        with open(TRAFFIC_JSON) as f:
+            traffic = json.load(f).get(dom, {}).get("bytes")
     out = {
         "metric": "input-PCs processed/sec for Canonicalize+Minimize+Union (maxCover merge)",
         "value": value, "unit": "input-PCs/s", "n_gpus": world, "steps": args.steps,
@@ -185,7 +193,8 @@ def bench_corpus(args):
         "results": {"kept": res.n_kept, "union": res.n_union, "max_cover": res.max_cover,
                     "n_ids": res.n_ids},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None,
                      "alg_bytes_per_launch": alg[dom]},
         "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph["compact"]
                                                           + ph["union"] + ph["merge"]) * 1e-3),

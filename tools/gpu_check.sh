@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, bench, rocprofv3 kernel stats.
+# One GPU-box pass: parity tests, bench, rocprofv3 evidence.
 #   tools/gpu_check.sh <tag> [pytest -k expr]
 set -o pipefail
 tag=${1:-r01}
@@ -11,5 +11,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -3 $out/pytest.log
 timeout -k 10 300 python3 bench.py > $out/bench.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu > $out/prof.log 2>&1 || { tail -20 $out/prof.log; exit 1; }
-find $out/prof -name '*kernel_stats.csv' -exec cat {} \; | cut -c1-200 | head -40
+bash tools/profile.sh $tag || exit 1

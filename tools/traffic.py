@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""HBM traffic per engine phase from rocprofv3 PMC passes (FETCH_SIZE and
+WRITE_SIZE in separate runs, MI355X_MICROARCH.md 'HBM'):
+  bytes_read  = 2 * FETCH_SIZE[KB] * 1024   (gfx950 tallies 128-B requests at 64 B)
+  bytes_write = WRITE_SIZE[KB] * 1024
+per launch of each phase = sum over the phase's kernels of the per-dispatch
+average.  Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+PHASES = {
+    "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
+              "large_"),
+    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel", "advance_kernel",
+                 "pass2_kernel", "ovf_", "reset_kernel"),
+    "order": ("gsort::",),
+    "compact": ("compact_", "scan_blocks"),
+    "union": ("dict_",),
+    "merge": ("bitmap_op_kernel",),
+}
+
+
+def per_dispatch(d, counter):
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"]
+            tot[k] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: tot[k] / len(disp[k]) for k in tot}
+
+
+def phase_of(name):
+    for ph, keys in PHASES.items():
+        if any(k in name for k in keys):
+            return ph
+    return None
+
+
+def main(fd, wd, out=None):
+    fetch = per_dispatch(fd, "FETCH_SIZE")
+    write = per_dispatch(wd, "WRITE_SIZE")
+    res = {}
+    for name in set(fetch) | set(write):
+        ph = phase_of(name)
+        if ph is None:
+            continue
+        r = res.setdefault(ph, {"read_bytes": 0.0, "write_bytes": 0.0})
+        r["read_bytes"] += 2 * fetch.get(name, 0.0) * 1024
+        r["write_bytes"] += write.get(name, 0.0) * 1024
+    for ph, r in res.items():
+        r["bytes"] = r["read_bytes"] + r["write_bytes"]
+    js = json.dumps(res, indent=1, sort_keys=True)
+    print(js)
+    if out:
+        with open(out, "w") as f:
+            f.write(js + "\n")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
