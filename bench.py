@@ -7,10 +7,10 @@ N=1, the same per-GPU shard with RCCL merges at N>1 — weak scaling).
 
 One step = one pass of the hot path over one synthetic corpus already
 resident in HBM (raw KCOV lists, CSR):
-  Canonicalize (LDS radix sort over window offsets, presence bitmap marked
-  in-kernel) -> PC dictionary (= corpus union) -> Go sort.Sort order ->
-  Minimize (chunked first-cover pass 1 + pass 2) -> ordered compaction ->
-  sorted Union list -> maxCover merge.  (--engine ids: the dense-id variant.)
+  Canonicalize (one wavefront per input: LDS radix sort + unique, range
+  split points) -> Go sort.Sort order -> Minimize (first-cover pass 1 with
+  LDS-resident covered ranges, pass 2 over the records) -> ordered
+  compaction -> sorted Union list -> maxCover merge.
 Prints ONE JSON line (rank 0).  Per-phase device times come from HIP events
 on the stream the kernels run on; the dominant kernel's roofline uses its
 ALGORITHMIC bytes.
@@ -52,9 +52,6 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2000,
                     help="inputs timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--engine", choices=["range", "pc", "ids"], default="range",
-                    help="range: wavefront canonicalize + range-partitioned Minimize "
-                         "(default); pc / ids: earlier engines kept for comparison")
     return ap.parse_args()
 
 
@@ -155,10 +152,9 @@ def bench_corpus(args):
     max_len = int(lens.max().item())
     if world > 1:
         from syzkaller_amd.dist import ShardedEngine
-        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev,
-                            mode=args.engine)
+        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev)
     else:
-        eng = CorpusEngine(n, total, max_len, lo, span, device=dev, mode=args.engine)
+        eng = CorpusEngine(n, total, max_len, lo, span, device=dev)
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
     dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), args,
@@ -168,12 +164,12 @@ def bench_corpus(args):
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
     value = total * world * args.steps / dt
     # algorithmic bytes per launch: canon reads raw + writes the
-    # canonical list; minimize reads the canonical list once (ids mode: + mark)
+    # canonical list; minimize reads the canonical list once
     alg = eng.alg_bytes(total, canon_pcs)
     dom = max(alg, key=lambda p: ph[p])
     achieved = alg[dom] / (ph[dom] * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(TRAFFIC_JSON) and args.engine == "range" and world == 1:
+    if os.path.exists(TRAFFIC_JSON) and world == 1:
         with open(TRAFFIC_JSON) as f:
             traffic = json.load(f).get(dom, {}).get("bytes")
     out = {
@@ -186,7 +182,6 @@ def bench_corpus(args):
                                + (" (C3 sharding)" if world > 1 else ""),
                    "inputs_per_gpu": n, "global_inputs": n * world, "raw_pcs_per_gpu": total,
                    "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
-                   "engine": args.engine,
                    "len_mean": args.mean, "len_sigma": args.sigma,
                    "parallelism": f"shard-by-input x{world}"},
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},

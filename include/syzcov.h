@@ -170,16 +170,6 @@ int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const uint32_t *pc
                     uint8_t *pres, uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag,
                     void *stream);
 
-/* Bit-packed presence (engine default): bit (pc - pc_lo) of bits[] (u32
- * words, zeroed by the caller) is set for every PC of the contiguous CSR
- * corpus; test-before-atomicOr.  The bitmap is 1/8 of the byte map, so the
- * hot part of the window stays in L2.  The byte form is only used to merge
- * shards (RCCL uint8 MAX); the conversions below are exact. */
-int syzcov_dev_mark_bits(const uint64_t *off, const uint32_t *pcs, size_t nseg, uint32_t *bits,
-                         uint32_t pc_lo, uint64_t pc_span, uint32_t *err_flag, void *stream);
-/* bytes must hold ceil(nbits/32)*32 bytes. */
-int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nbits, uint8_t *bytes, void *stream);
-int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nbits, uint32_t *bits, void *stream);
 /* Bitmap set algebra on u32 words (ops as syzcov_dev_bytemap_op) + popcount. */
 int syzcov_dev_bitmap_op(int op, uint32_t *dst, const uint32_t *src, uint64_t nwords,
                          uint64_t *popcount_out, void *stream);
@@ -216,62 +206,6 @@ int syzcov_dev_minimize_pass2(const uint64_t *off, const uint32_t *len, const ui
                               const int32_t *order, const int32_t *ranks, size_t n,
                               const uint64_t *tab, uint32_t pc_lo, const int32_t *first,
                               const uint8_t *cand, uint8_t *kept, void *stream);
-/* ---- engine fast path: canonical covers in the dense PC-id space ----
- * Canonicalize a CSR corpus whose PCs are all in the dictionary `tab`
- * (built from a presence map of the same raw corpus): each segment's PCs are
- * mapped to dense ids, radix-sorted in LDS and de-duplicated; canonical ids
- * go to out_ids[off[i] ..), lengths to new_len.  n_ids: device u32 (from
- * syzcov_dev_dict_build).  ws: syzcov_dev_canon_ws_size(nseg, max_seg_len). */
-int syzcov_dev_canon_ids(const uint64_t *off, const uint32_t *raw, uint32_t *out_ids,
-                         uint32_t *new_len, size_t nseg, size_t max_seg_len, const uint64_t *tab,
-                         uint32_t pc_lo, uint64_t pc_span, const uint32_t *n_ids,
-                         uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
-/* Full id -> PC list (n_ids entries, a present 0xFFFFFFFF included). */
-int syzcov_dev_dict_pcs(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
-                        void *stream);
-/* out[off[s] + q] = table[in[off[s] + q]] for q < len[s] (ids -> PCs). */
-int syzcov_dev_gather_u32(const uint32_t *table, const uint64_t *off, const uint32_t *len,
-                          const uint32_t *in, size_t nseg, uint32_t *out, void *stream);
-/* Minimize over id-space covers: pass 1 in geometrically growing rank chunks
- * with a covered-id bitmap filter rebuilt between chunks (first[] pre-set to
- * INT32_MAX, n_ids_cap >= *n_ids), then (do_pass2) pass 2 into kept[] (by
- * rank, pre-zeroed).  ws: syzcov_dev_minimize_ws_size(n_ids_cap).  Sharded
- * runs call with do_pass2 = 0, MIN-all-reduce first[], then call
- * syzcov_dev_minimize_ids_pass2. */
-size_t syzcov_dev_minimize_ws_size(size_t n_ids_cap);
-int syzcov_dev_minimize_ids(const uint64_t *off, const uint32_t *len, const uint32_t *ids,
-                            const int32_t *order, const int32_t *ranks, size_t n,
-                            const uint32_t *n_ids, size_t n_ids_cap, int32_t *first,
-                            uint8_t *cand, uint8_t *kept, int do_pass2, void *ws, void *stream);
-int syzcov_dev_minimize_ids_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *ids,
-                                  const int32_t *order, const int32_t *ranks, size_t n,
-                                  const int32_t *first, const uint8_t *cand, uint8_t *kept,
-                                  void *stream);
-
-/* ---- engine PC-space path (default): no dictionary before the sort ----
- * Canonicalize a CSR corpus inside the window [pc_lo, pc_lo + pc_span): keys
- * are window offsets, radix-sorted in LDS, de-duplicated (cover.go:36-52
- * semantics), written back as PCs to out_pcs[off[i] ..), and every canonical
- * PC is OR-ed into the presence bitmap pres_bits (pre-zeroed or carrying the
- * previous step) — the mark pass fused into the sort.  PCs outside the window
- * set *err_flag.  ws: syzcov_dev_canon_ws_size(nseg, max_seg_len). */
-int syzcov_dev_canon_pcs(const uint64_t *off, const uint32_t *raw, uint32_t *out_pcs,
-                         uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
-                         uint64_t pc_span, uint32_t *pres_bits, uint32_t *err_flag, void *ws,
-                         size_t ws_size, void *stream);
-/* Minimize over canonical PC covers with first_w[] indexed by pc - pc_lo
- * (pc_span int32, pre-set to INT32_MAX): pass 1 in doubling rank chunks with
- * covered/touched window bitmaps, then (do_pass2) pass 2 into kept[] (by
- * rank, pre-zeroed).  ws: syzcov_dev_minimize_win_ws_size(pc_span). */
-size_t syzcov_dev_minimize_win_ws_size(uint64_t pc_span);
-int syzcov_dev_minimize_win(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
-                            const int32_t *order, const int32_t *ranks, size_t n, uint32_t pc_lo,
-                            uint64_t pc_span, int32_t *first_w, uint8_t *cand, uint8_t *kept,
-                            int do_pass2, void *ws, void *stream);
-int syzcov_dev_minimize_win_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
-                                  const int32_t *order, const int32_t *ranks, size_t n,
-                                  uint32_t pc_lo, const int32_t *first_w, const uint8_t *cand,
-                                  uint8_t *kept, void *stream);
 /* Sharded runs: window-indexed first_w <-> dense-id first (one int32 per
  * present PC of the dictionary `tab`) so the RCCL MIN moves n_ids, not
  * pc_span, entries.  to_dense = 1 gathers, 0 scatters back. */
@@ -301,7 +235,7 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
  * and on return.  rec: capacity rec_cap of (rank << 32 | offset) records;
  * *rec_cnt (device u64) receives the record count (> rec_cap: overflow,
  * handled exactly by fallback kernels).  cand: u8 per item (pre-zeroed).
- * kept: u8 per rank (pre-zeroed) receives kept[rank] = 1.  first_chunk /
+ * kept: u8 per rank (pre-zeroed) receives kept[rank] = 1 (do_pass2).  first_chunk /
  * growth / pcs_per_wg_hint tune the chunk schedule (0 = defaults: 64, 4,
  * 2^18); any values give the same result.
  * ws: syzcov_dev_minimize_range_ws_size(n_items, pc_span, range_shift). */
@@ -311,8 +245,23 @@ int syzcov_dev_minimize_range(const uint64_t *off, const uint32_t *len, const ui
                               size_t n_items, uint32_t pc_lo, uint64_t pc_span,
                               uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered,
                               int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
-                              uint8_t *cand, uint8_t *kept, size_t first_chunk, uint32_t growth,
-                              uint64_t pcs_per_wg_hint, void *ws, void *stream);
+                              uint8_t *cand, uint8_t *kept, int do_pass2, size_t first_chunk,
+                              uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream);
+/* Sharded runs: call syzcov_dev_minimize_range with do_pass2 = 0 (first_w then
+ * holds this shard's first ranks and covered its union), merge the shards'
+ * covered bitmaps (OR) into the dictionary `tab` (syzcov_dev_dict_build_bits),
+ * MIN-merge first_dense (syzcov_dev_first_dense to_dense = 1 over tab), then
+ * call this with the same arguments and ws: kept[rank] = 1 iff the merged
+ * first rank of one of the item's PCs equals its rank; first_w is reset.
+ * tab == NULL: single-GPU pass 2 from first_w. */
+int syzcov_dev_minimize_range_pass2(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                                    const uint32_t *split, const int32_t *order,
+                                    const int32_t *ranks, size_t n_items, uint32_t pc_lo,
+                                    uint64_t pc_span, uint32_t range_shift,
+                                    const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+                                    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
+                                    uint8_t *cand, const uint64_t *tab, const int32_t *first_dense,
+                                    uint8_t *kept, void *ws, void *stream);
 
 /* Ordered compaction: out_idx = [order[r] for r if kept[r]]; *n_out (device u32). */
 size_t syzcov_dev_compact_ws_size(size_t n);

@@ -62,9 +62,6 @@ _SIGS = {
     "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
     "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
     "syzcov_dev_mark": (C.c_int, [p_, p_, p_, sz, p_, u32, u64, p_, p_]),
-    "syzcov_dev_mark_bits": (C.c_int, [p_, p_, sz, p_, u32, u64, p_, p_]),
-    "syzcov_dev_bits_to_bytes": (C.c_int, [p_, u64, p_, p_]),
-    "syzcov_dev_bytes_to_bits": (C.c_int, [p_, u64, p_, p_]),
     "syzcov_dev_bitmap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),
     "syzcov_dev_dict_build_bits": (C.c_int, [p_, u64, p_, p_, p_, p_]),
     "syzcov_dev_dict_ws_size": (sz, [u64]),
@@ -72,24 +69,14 @@ _SIGS = {
     "syzcov_dev_dict_to_list": (C.c_int, [p_, u64, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass1": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_, p_]),
-    "syzcov_dev_canon_ids": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, p_, sz, p_]),
-    "syzcov_dev_dict_pcs": (C.c_int, [p_, u64, u32, p_, p_]),
-    "syzcov_dev_gather_u32": (C.c_int, [p_, p_, p_, p_, sz, p_, p_]),
-    "syzcov_dev_minimize_ws_size": (sz, [sz]),
-    "syzcov_dev_minimize_ids": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, sz, p_, p_, p_, C.c_int, p_,
-                                          p_]),
-    "syzcov_dev_minimize_ids_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, p_, p_, p_]),
-    "syzcov_dev_canon_pcs": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, p_, p_, p_, sz, p_]),
-    "syzcov_dev_minimize_win_ws_size": (sz, [u64]),
-    "syzcov_dev_minimize_win": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, u64, p_, p_, p_, C.c_int,
-                                          p_, p_]),
-    "syzcov_dev_minimize_win_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, p_, p_, p_, p_]),
     "syzcov_dev_canon_split_ws_size": (sz, [sz]),
     "syzcov_dev_canon_split": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, p_, p_, p_, p_, sz,
                                          p_]),
     "syzcov_dev_minimize_range_ws_size": (sz, [sz, u64, u32]),
     "syzcov_dev_minimize_range": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u32, u64, u32, p_, p_, p_,
-                                            p_, u64, p_, p_, p_, sz, u32, u64, p_, p_]),
+                                            p_, u64, p_, p_, p_, C.c_int, sz, u32, u64, p_, p_]),
+    "syzcov_dev_minimize_range_pass2": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u32, u64, u32, p_,
+                                                  p_, p_, p_, u64, p_, p_, p_, p_, p_, p_, p_]),
     "syzcov_dev_first_dense": (C.c_int, [p_, u64, p_, p_, C.c_int, p_]),
     "syzcov_dev_compact_ws_size": (sz, [sz]),
     "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),

@@ -99,34 +99,46 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
                                                   uint32_t *__restrict__ lists, uint64_t stride,
                                                   uint32_t *__restrict__ big_list,
                                                   uint32_t *__restrict__ big_cnt) {
+    // block-aggregated: LDS counts per class, ONE global atomic per block and class
+    __shared__ uint32_t s_cnt[NCLS + 1], s_base[NCLS + 1];
     const uint32_t l = __lane_id();
     const uint64_t lt = (1ull << l) - 1ull;
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < nseg;
-         b += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = b + l;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nseg;
+         b0 += (uint64_t)gridDim.x * blockDim.x) {
+        if (threadIdx.x <= NCLS) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t i = b0 + threadIdx.x;
         int c = -1;
-        bool big = false;
         if (i < nseg) {
             const uint64_t n = off[i + 1] - off[i];
-            big = n > WAVE_MAX;
+            c = n > WAVE_MAX ? NCLS : -1;  // NCLS = big list
 #pragma unroll
             for (int k = 0; k < NCLS; k++)
                 if (n >= C.lo[k] && n <= C.hi[k]) c = k;
         }
+        uint32_t wofs[NCLS + 1];
+        uint64_t msk[NCLS + 1];
 #pragma unroll
         for (int k = 0; k <= NCLS; k++) {
-            const bool mine = k < NCLS ? c == k : big;
-            const uint64_t m = __ballot(mine);
-            if (!m) continue;
-            const uint32_t leader = __builtin_ctzll(m);
-            uint32_t base = 0;
-            if (l == leader) base = atomicAdd(k < NCLS ? &counts[k] : big_cnt, (uint32_t)__popcll(m));
-            base = __shfl(base, leader, 64);
-            if (mine) {
-                const uint32_t slot = base + (uint32_t)__popcll(m & lt);
+            msk[k] = __ballot(c == k);
+            wofs[k] = 0;
+            if (msk[k] && l == 0) wofs[k] = atomicAdd(&s_cnt[k], (uint32_t)__popcll(msk[k]));
+        }
+        __syncthreads();
+        if (threadIdx.x <= NCLS) {
+            const uint32_t k = threadIdx.x;
+            s_base[k] = s_cnt[k] ? atomicAdd(k < NCLS ? &counts[k] : big_cnt, s_cnt[k]) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k <= NCLS; k++) {
+            const uint32_t wo = __builtin_amdgcn_readfirstlane(wofs[k]);  // lane 0's slot
+            if (c == k) {
+                const uint32_t slot = s_base[k] + wo + (uint32_t)__popcll(msk[k] & lt);
                 if (k < NCLS) lists[k * stride + slot] = (uint32_t)i; else big_list[slot] = (uint32_t)i;
             }
         }
+        __syncthreads();
     }
 }
 
@@ -426,7 +438,7 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
     uint32_t *ccnt = cnts + 2;
     SYZ_HIP(hipMemsetAsync(ccnt, 0, cw::NCLS * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 4096)), dim3(256), 0, s, off,
+    hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 2048)), dim3(256), 0, s, off,
                        (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1);
     const unsigned grid = (unsigned)std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, 4096);
     for (int c = 0; c < cw::NCLS; c++) {

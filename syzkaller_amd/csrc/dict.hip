@@ -89,94 +89,42 @@ __device__ __forceinline__ void mark_bit(uint32_t *__restrict__ bits, uint32_t p
     if (!(bits[o >> 5] & m)) atomicOr(&bits[o >> 5], m);
 }
 
-__global__ void mark_bits_kernel(const uint64_t *__restrict__ off, size_t nseg,
-                                 const uint32_t *__restrict__ pcs, uint32_t *__restrict__ bits,
-                                 uint32_t pc_lo, uint64_t pc_span, uint32_t *__restrict__ err) {
-    const uint64_t start = off[0], end = off[nseg];
-    const uint64_t a0 = (start + 3) & ~3ull;
-    const uint64_t head_end = a0 < end ? a0 : end;
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
-    if (tid < head_end - start) mark_bit(bits, pcs[start + tid], pc_lo, pc_span, err);
-    const uint64_t nvec = end > a0 ? (end - a0) / 4 : 0;
-    const uint4 *v = (const uint4 *)(pcs + a0);
-    for (uint64_t i = tid; i < nvec; i += nthr) {
-        const uint4 x = v[i];
-        const uint32_t p[4] = {x.x, x.y, x.z, x.w};
-        uint64_t o[4];
-        bool ok[4];
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            ok[q] = in_window(p[q], pc_lo, pc_span, &o[q]);
-            w[q] = ok[q] ? bits[o[q] >> 5] : 0xFFFFFFFFu;  // all loads in flight together
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (!ok[q]) {
-                *err = 1u;
-                continue;
-            }
-            const uint32_t m = 1u << (o[q] & 31);
-            if (!(w[q] & m)) atomicOr(&bits[o[q] >> 5], m);
-        }
-    }
-    const uint64_t tail = a0 + nvec * 4;
-    if (end > tail && tid < end - tail) mark_bit(bits, pcs[tail + tid], pc_lo, pc_span, err);
-}
-
-// bits <-> bytes for the cross-GPU union (RCCL has no OR: uint8 MAX on bytes)
-__global__ void bits_to_bytes_kernel(const uint32_t *__restrict__ bits, uint64_t nwords,
-                                     uint8_t *__restrict__ bytes) {
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
-         w += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t b = bits[w];
-        uint4 lo, hi;
-        uint32_t o[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int by = 0; by < 4; by++) v |= ((b >> (q * 4 + by)) & 1u) << (8 * by);
-            o[q] = v;
-        }
-        lo = make_uint4(o[0], o[1], o[2], o[3]);
-        hi = make_uint4(o[4], o[5], o[6], o[7]);
-        ((uint4 *)bytes)[2 * w] = lo;
-        ((uint4 *)bytes)[2 * w + 1] = hi;
-    }
-}
-
-__global__ void bytes_to_bits_kernel(const uint8_t *__restrict__ bytes, uint64_t nwords,
-                                     uint32_t *__restrict__ bits) {
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
-         w += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 a = ((const uint4 *)bytes)[2 * w], c = ((const uint4 *)bytes)[2 * w + 1];
-        const uint32_t x[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-        uint32_t b = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++)
-#pragma unroll
-            for (int by = 0; by < 4; by++) b |= (((x[q] >> (8 * by)) & 0xFFu) != 0) << (q * 4 + by);
-        bits[w] = b;
-    }
-}
-
 // Bitmap set algebra on u32 words + popcount of the result.
-__global__ void bitmap_op_kernel(int op, uint32_t *__restrict__ dst,
-                                 const uint32_t *__restrict__ src, uint64_t nwords,
-                                 unsigned long long *__restrict__ pop) {
+__global__ __launch_bounds__(256) void bitmap_op_kernel(int op, uint32_t *__restrict__ dst,
+                                                        const uint32_t *__restrict__ src,
+                                                        uint64_t nwords,
+                                                        unsigned long long *__restrict__ pop) {
+    // 16-byte words per lane; popcount reduced per block, one atomic per block
+    __shared__ uint32_t s_part[256 / 64];
     uint32_t cnt = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t a = dst[i], b = src[i];
-        const uint32_t r = op == 0 ? (a | b) : op == 1 ? (a & b) : op == 2 ? (a & ~b) : (a ^ b);
+    auto f = [op](uint32_t a, uint32_t b) {
+        return op == 0 ? (a | b) : op == 1 ? (a & b) : op == 2 ? (a & ~b) : (a ^ b);
+    };
+    const bool al = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+    const uint64_t n4 = al ? nwords / 4 : 0;
+    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const uint4 a = d4[i], b = s4[i];
+        const uint4 r = make_uint4(f(a.x, b.x), f(a.y, b.y), f(a.z, b.z), f(a.w, b.w));
+        d4[i] = r;
+        cnt += __popc(r.x) + __popc(r.y) + __popc(r.z) + __popc(r.w);
+    }
+    for (uint64_t i = n4 * 4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+         i += stride) {
+        const uint32_t r = f(dst[i], src[i]);
         dst[i] = r;
         cnt += __popc(r);
     }
     if (pop) {
         cnt = wave_sum(cnt);
-        if (__lane_id() == 0 && cnt) atomicAdd(pop, (unsigned long long)cnt);
+        if (__lane_id() == 0) s_part[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t t = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+            if (t) atomicAdd(pop, (unsigned long long)t);
+        }
     }
 }
 
@@ -386,36 +334,8 @@ extern "C" int syzcov_dev_mark(const uint64_t *off, const uint32_t *len, const u
     return 0;
 }
 
-extern "C" int syzcov_dev_mark_bits(const uint64_t *off, const uint32_t *pcs, size_t nseg,
-                                    uint32_t *bits, uint32_t pc_lo, uint64_t pc_span,
-                                    uint32_t *err_flag, void *stream) {
-    if (nseg == 0) return 0;
-    if (!off || !pcs || !bits || !err_flag) return SYZCOV_EINVAL;
-    hipLaunchKernelGGL(mark_bits_kernel, dim3(256 * 16), dim3(256), 0, (hipStream_t)stream, off,
-                       nseg, pcs, bits, pc_lo, pc_span, err_flag);
-    SYZ_LAUNCH_CHECK();
-    return 0;
-}
 
-extern "C" int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nbits, uint8_t *bytes,
-                                        void *stream) {
-    if (!bits || !bytes) return SYZCOV_EINVAL;
-    const uint64_t nwords = (nbits + 31) / 32;
-    hipLaunchKernelGGL(bits_to_bytes_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
-                       (hipStream_t)stream, bits, nwords, bytes);
-    SYZ_LAUNCH_CHECK();
-    return 0;
-}
 
-extern "C" int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nbits, uint32_t *bits,
-                                        void *stream) {
-    if (!bits || !bytes) return SYZCOV_EINVAL;
-    const uint64_t nwords = (nbits + 31) / 32;
-    hipLaunchKernelGGL(bytes_to_bits_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
-                       (hipStream_t)stream, bytes, nwords, bits);
-    SYZ_LAUNCH_CHECK();
-    return 0;
-}
 
 extern "C" int syzcov_dev_bitmap_op(int op, uint32_t *dst, const uint32_t *src, uint64_t nwords,
                                     uint64_t *popcount_out, void *stream) {
@@ -424,7 +344,8 @@ extern "C" int syzcov_dev_bitmap_op(int op, uint32_t *dst, const uint32_t *src, 
     unsigned long long *pop = (unsigned long long *)popcount_out;
     if (pop) SYZ_HIP(hipMemsetAsync(pop, 0, sizeof(uint64_t), s));
     if (nwords) {
-        hipLaunchKernelGGL(bitmap_op_kernel, dim3(grid_for(nwords, 256, 8192)), dim3(256), 0, s, op,
+        hipLaunchKernelGGL(bitmap_op_kernel, dim3(grid_for((nwords + 3) / 4, 256, 1024)), dim3(256),
+                           0, s, op,
                            dst, src, nwords, pop);
         SYZ_LAUNCH_CHECK();
     }

@@ -249,16 +249,28 @@ __global__ void advance_kernel(const unsigned long long *cnt, unsigned long long
     if (threadIdx.x == 0) *done = std::min<uint64_t>(*cnt, cap);
 }
 
-// Pass 2 over the records: kept[rank] = 1 iff first_w[pc] == rank.
+// The first-cover rank of window offset wo: first_w[wo] on one GPU; across
+// shards the MIN-merged dense table first_d[id(wo)] (tab: dictionary of the
+// merged union, syzcov_dev_dict_build_bits layout).
+__device__ __forceinline__ int32_t first_of(const int32_t *first_w, const uint64_t *tab,
+                                            const int32_t *first_d, uint32_t wo) {
+    if (!tab) return first_w[wo];
+    const uint64_t e = tab[wo >> 5];
+    const uint32_t bits = (uint32_t)(e >> 32), b = wo & 31;
+    if (!((bits >> b) & 1u)) return INT32_MAX;
+    return first_d[(uint32_t)e + __popc(bits & ((1u << b) - 1u))];
+}
+
+// Pass 2 over the records: kept[rank] = 1 iff first(pc) == rank.
 __global__ void pass2_kernel(const unsigned long long *rec, uint64_t cap,
                              const unsigned long long *cnt, const int32_t *first_w,
-                             uint8_t *kept) {
+                             const uint64_t *tab, const int32_t *first_d, uint8_t *kept) {
     const uint64_t hi = std::min<uint64_t>(*cnt, cap);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long r = rec[i];
         const int32_t rank = (int32_t)(r >> 32);
-        if (first_w[(uint32_t)r] == rank) kept[rank] = 1;
+        if (first_of(first_w, tab, first_d, (uint32_t)r) == rank) kept[rank] = 1;
     }
 }
 
@@ -272,7 +284,8 @@ __global__ void reset_kernel(const unsigned long long *rec, uint64_t cap,
 }
 
 // ---- overflow fallbacks (early exit unless *cnt > cap)
-__global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_w, uint8_t *kept) {
+__global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_w,
+                                 const uint64_t *tab, const int32_t *first_d, uint8_t *kept) {
     if (*A.rec_cnt <= A.rec_cap) return;
     for (uint32_t j = blockIdx.x; j < n_items; j += gridDim.x) {
         if (!A.cand[j]) continue;
@@ -281,7 +294,7 @@ __global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_
         const uint32_t n = A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + j];
         bool hit = false;
         for (uint32_t q = threadIdx.x; q < n; q += blockDim.x)
-            hit |= first_w[A.pcs[o + q] - A.pc_lo] == rank;
+            hit |= first_of(first_w, tab, first_d, A.pcs[o + q] - A.pc_lo) == rank;
         if (__syncthreads_or(hit) && threadIdx.x == 0) kept[rank] = 1;
     }
 }
@@ -308,6 +321,25 @@ __global__ void ovf_reset_kernel(const unsigned long long *cnt, uint64_t cap, in
         first_w[i] = INT32_MAX;
 }
 
+// window-indexed first_w <-> dense table over a dictionary (shard exchange)
+__global__ void first_dense_kernel(const uint64_t *__restrict__ tab, uint64_t nwords,
+                                   int32_t *__restrict__ first_w, int32_t *__restrict__ dense,
+                                   int to_dense) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = tab[w];
+        uint32_t bits = (uint32_t)(e >> 32), pos = (uint32_t)e;
+        while (bits) {
+            const int b = __ffs(bits) - 1;
+            bits &= bits - 1;
+            if (to_dense)
+                dense[pos++] = first_w[w * 32 + b];
+            else
+                first_w[w * 32 + b] = dense[pos++];
+        }
+    }
+}
+
 }  // namespace mr
 }  // namespace syz
 
@@ -325,15 +357,13 @@ extern "C" size_t syzcov_dev_minimize_range_ws_size(size_t n_items, uint64_t pc_
            align_up(mr_nrange(pc_span, range_shift) * n_items * 4, 256);
 }
 
-extern "C" int syzcov_dev_minimize_range(
-    const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
-    const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
-    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
-    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
-    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream) {
-    if (n_items == 0) return 0;
+static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                   const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                   size_t n_items, uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+                   const uint64_t *range_tot, uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                   uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, void *ws) {
     if (!off || !pcs || !order || !range_tot || !covered || !first_w || !rec || !rec_cnt || !cand ||
-        !kept || !ws || n_items > 0x7FFFFFFF)
+        !ws || n_items > 0x7FFFFFFF)
         return SYZCOV_EINVAL;
     if (range_shift < 10 || range_shift > 20 || pc_span == 0 || pc_span > (1ull << 32))
         return SYZCOV_EINVAL;
@@ -341,11 +371,6 @@ extern "C" int syzcov_dev_minimize_range(
     if (nrange > (uint64_t)mr::MAX_R) return SYZCOV_ERANGE;
     if (!split && nrange != 1) return SYZCOV_EINVAL;
     if (!split && !len) return SYZCOV_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
-    unsigned long long *done = (unsigned long long *)ws;
-    SYZ_HIP(hipMemsetAsync(done, 0, sizeof(uint64_t), s));
-    SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
-    mr::Args A;
     A.off = off;
     A.len = len;
     A.pcs = pcs;
@@ -363,12 +388,49 @@ extern "C" int syzcov_dev_minimize_range(
     A.rec_cnt = (unsigned long long *)rec_cnt;
     A.cand = cand;
     A.n_items = (uint32_t)n_items;
-    uint64_t *base_r = (uint64_t *)((uint8_t *)ws + 256);
-    uint32_t *split_t = (uint32_t *)((uint8_t *)base_r + align_up(n_items * 8, 256));
-    A.base_r = base_r;
-    A.split_t = split_t;
+    A.base_r = (uint64_t *)((uint8_t *)ws + 256);
+    A.split_t = (uint32_t *)((uint8_t *)A.base_r + align_up(n_items * 8, 256));
+    return 0;
+}
+
+// pass 2 + resets (first_w back to INT32_MAX)
+static int mr_pass2(const mr::Args &A, uint64_t pc_span, const uint64_t *tab,
+                    const int32_t *first_d, uint8_t *kept, hipStream_t s) {
+    const unsigned long long *rec = A.rec, *cnt = A.rec_cnt;
+    hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, rec, A.rec_cap, cnt,
+                       (const int32_t *)A.first_w, tab, first_d, kept);
+    hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, A.n_items,
+                       (const int32_t *)A.first_w, tab, first_d, kept);
+    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, rec, A.rec_cap, cnt,
+                       A.first_w);
+    hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s, cnt, A.rec_cap, A.first_w,
+                       pc_span);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_minimize_range(
+    const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
+    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
+    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (n_items == 0) {
+        if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
+        return 0;
+    }
+    if (do_pass2 && !kept) return SYZCOV_EINVAL;
+    mr::Args A;
+    int rc = mr_args(A, off, len, pcs, split, order, ranks, n_items, pc_lo, pc_span, range_shift,
+                     range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
+    if (rc) return rc;
+    const uint64_t nrange = A.nrange;
+    unsigned long long *done = (unsigned long long *)ws;
+    SYZ_HIP(hipMemsetAsync(done, 0, sizeof(uint64_t), s));
+    SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
-                       base_r, split_t);
+                       (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
     static bool attr_set = false;  // idempotent; races only repeat the call
     if (!attr_set) {
@@ -397,20 +459,36 @@ extern "C" int syzcov_dev_minimize_range(
         a = b;
         step *= growth;
     }
-    SYZ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s,
-                       (const unsigned long long *)rec, rec_cap, (const unsigned long long *)rec_cnt,
-                       (const int32_t *)first_w, kept);
-    hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, (uint32_t)n_items,
-                       (const int32_t *)first_w, kept);
+    // record overflow: the union comes from first_w instead
     hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
                        (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
                        pc_span, covered);
-    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s,
-                       (const unsigned long long *)rec, rec_cap, (const unsigned long long *)rec_cnt,
-                       first_w);
-    hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s,
-                       (const unsigned long long *)rec_cnt, rec_cap, first_w, pc_span);
+    SYZ_LAUNCH_CHECK();
+    if (!do_pass2) return 0;
+    return mr_pass2(A, pc_span, nullptr, nullptr, kept, s);
+}
+
+extern "C" int syzcov_dev_minimize_range_pass2(
+    const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
+    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, const uint64_t *tab,
+    const int32_t *first_dense, uint8_t *kept, void *ws, void *stream) {
+    if (n_items == 0) return 0;
+    if (!kept || (tab && !first_dense)) return SYZCOV_EINVAL;
+    mr::Args A;
+    int rc = mr_args(A, off, len, pcs, split, order, ranks, n_items, pc_lo, pc_span, range_shift,
+                     range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
+    if (rc) return rc;
+    return mr_pass2(A, pc_span, tab, first_dense, kept, (hipStream_t)stream);
+}
+
+extern "C" int syzcov_dev_first_dense(const uint64_t *tab, uint64_t pc_span, int32_t *first_w,
+                                      int32_t *dense, int to_dense, void *stream) {
+    if (!tab || !first_w || !dense || pc_span == 0) return SYZCOV_EINVAL;
+    const uint64_t nwords = (pc_span + 31) / 32;
+    hipLaunchKernelGGL(mr::first_dense_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
+                       (hipStream_t)stream, tab, nwords, first_w, dense, to_dense);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -5,10 +5,10 @@ One process per GPU, torch.distributed over RCCL ("nccl" backend on ROCm).
 The only exchanges are the reductions the first-cover formulation needs
 (SURVEY §8e):
 
-    presence map   uint8 MAX all-reduce   -> identical dense-id dictionary
-    canonical lens all-gather             -> identical Go sort.Sort order
-    first[]        int32 MIN all-reduce   -> global first-cover rank per PC id
-    kept flags     uint8 MAX all-reduce   -> identical kept list on every rank
+    canonical lens all-gather              -> identical Go sort.Sort order
+    covered bitmap all-gather + OR          -> the corpus union = identical dictionary
+    first[]        int32 MIN all-reduce    -> global first-cover rank per dense PC id
+    kept flags     uint8 MAX all-reduce    -> identical kept list on every rank
 
 The collective glue below is device-agnostic (it runs under gloo on CPU
 tensors in tests/test_dist_gloo.py); the per-shard compute is libsyzcov's
@@ -19,31 +19,65 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .engine import CorpusEngine, StepResult, _p, _stream
+from .engine import CorpusEngine, _p, _stream
 from ._lib import check
 
 
 # ------------------------------------------------------------------ glue
-def merge_presence(pres: torch.Tensor) -> None:
-    """Union of the shards' presence maps (RCCL has no OR: uint8 MAX)."""
-    dist.all_reduce(pres, op=dist.ReduceOp.MAX)
+def _staged(t: torch.Tensor):
+    """gloo moves host tensors only: device tensors go through a host copy
+    (multi-rank tests on one GPU); with RCCL the tensor is used in place."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _all_reduce(t: torch.Tensor, op) -> None:
+    if _staged(t):
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+
+
+def _all_gather(out: torch.Tensor, t: torch.Tensor) -> None:
+    if _staged(t):
+        h = out.cpu()
+        dist.all_gather_into_tensor(h, t.cpu())
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, t)
 
 
 def merge_first(first: torch.Tensor) -> None:
     """Global first-cover rank per dense PC id."""
-    dist.all_reduce(first, op=dist.ReduceOp.MIN)
+    _all_reduce(first, dist.ReduceOp.MIN)
 
 
 def merge_kept(kept: torch.Tensor) -> None:
     """kept[] is indexed by global rank; each rank set only its own items."""
-    dist.all_reduce(kept, op=dist.ReduceOp.MAX)
+    _all_reduce(kept, dist.ReduceOp.MAX)
+
+
+def merge_covered(covered: torch.Tensor, world: int, or_into) -> None:
+    """Union of the shards' covered bitmaps (u32 words).  RCCL has no bitwise
+    OR, so the bitmaps are all-gathered (world x |bitmap|, 8 MB each at C3)
+    and OR-ed locally with `or_into(dst, src)` (the HIP bitmap kernel on GPU,
+    torch.bitwise_or under gloo)."""
+    if world == 1:
+        return
+    out = torch.empty(world * covered.numel(), dtype=covered.dtype, device=covered.device)
+    _all_gather(out, covered.contiguous())
+    parts = out.view(world, -1)
+    covered.copy_(parts[0])
+    for r in range(1, world):
+        or_into(covered, parts[r])
 
 
 def gather_lens(local_lens: torch.Tensor, world: int) -> torch.Tensor:
     """Canonical lengths of every shard, in global input order."""
     out = torch.empty(local_lens.numel() * world, dtype=local_lens.dtype,
                       device=local_lens.device)
-    dist.all_gather_into_tensor(out, local_lens.contiguous())
+    _all_gather(out, local_lens.contiguous())
     return out
 
 
@@ -58,48 +92,34 @@ def local_items(order: torch.Tensor, rank: int, n_local: int):
 
 # ---------------------------------------------------------------- engine
 class ShardedEngine(CorpusEngine):
-    """Rank `rank` of `world`: n local inputs of a global corpus of n*world."""
+    """Rank `rank` of `world`: n local inputs of a global corpus of n*world
+    (global input i lives on rank i // n)."""
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 rank: int, world: int, device="cuda", sort_variant: int = 0, mode: str = "pc"):
+                 rank: int, world: int, device="cuda", sort_variant: int = 0):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
-                         n_global=n * world, sort_variant=sort_variant, mode=mode)
+                         n_global=n * world, sort_variant=sort_variant)
         self.rank, self.world, self.n_local = rank, world, n
         self.glens = torch.empty(n * world, dtype=torch.int32, device=self.dev)
-        self.pres_bytes = torch.empty(self.nwords * 32, dtype=torch.uint8, device=self.dev)
-        # the global dictionary can be larger than this shard's PC count
+        # the merged union can be larger than this shard's PC count
         gcap = min(pc_span, p_max * world) + 1
         self.union = torch.empty(gcap, dtype=torch.int32, device=self.dev)
-        if mode == "pc":
-            # compact first-cover exchange: one int32 per present PC, not per window slot
-            self.first_dense = torch.empty(gcap, dtype=torch.int32, device=self.dev)
-        else:
-            self.ids_cap = gcap
-            self.first = torch.empty(gcap, dtype=torch.int32, device=self.dev)
-            self.ws = torch.empty(max(self.ws_size, self.L.syzcov_dev_minimize_ws_size(gcap)),
-                                  dtype=torch.uint8, device=self.dev)
-            self.ws_size = self.ws.numel()
+        # compact first-cover exchange: one int32 per PC of the merged union
+        self.first_dense = torch.empty(gcap, dtype=torch.int32, device=self.dev)
+        # dictionary/compaction scratch apart from ws, which carries minimize's
+        # rank-ordered descriptors from pass 1 to pass 2
+        self.ws2 = torch.empty(max(self.L.syzcov_dev_dict_ws_size(pc_span),
+                                   self.L.syzcov_dev_compact_ws_size(n * world)),
+                               dtype=torch.uint8, device=self.dev)
 
-    def merge_first_window(self):
-        """first_w (window-indexed) -> dense ids -> RCCL MIN -> back."""
-        L, s = self.L, _stream()
-        n_ids = int(self.scal[1].item()) & 0xFFFFFFFF
-        check(L.syzcov_dev_first_dense(_p(self.tab), self.span, _p(self.first),
-                                       _p(self.first_dense), 1, s), "dev_first_dense")
-        merge_first(self.first_dense[:n_ids])
-        check(L.syzcov_dev_first_dense(_p(self.tab), self.span, _p(self.first),
-                                       _p(self.first_dense), 0, s), "dev_first_dense")
-
-    def merge_presence_bits(self):
-        """bits -> uint8 per PC -> RCCL MAX -> bits (exact OR of the shards)."""
-        L, s = self.L, _stream()
-        check(L.syzcov_dev_bits_to_bytes(_p(self.pres), self.span, _p(self.pres_bytes), s),
-              "dev_bits_to_bytes")
-        merge_presence(self.pres_bytes)
-        check(L.syzcov_dev_bytes_to_bits(_p(self.pres_bytes), self.span, _p(self.pres), s),
-              "dev_bytes_to_bits")
+    def _or_into(self, dst, src):
+        check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
+              "dev_bitmap_op")
 
     def step(self, off, raw, n, sync: bool = True, ev=None):
+        """One rank's step.  Exchanges: canonical lengths (all-gather), covered
+        bitmaps (all-gather + OR), first ranks over the merged dictionary (int32
+        MIN), kept flags by global rank (uint8 MAX)."""
         k = [0]
 
         def mark_ev():
@@ -108,37 +128,26 @@ class ShardedEngine(CorpusEngine):
             k[0] += 1
         assert n == self.n_local
         N = n * self.world
-        pc = self.mode == "pc"
+        L, s = self.L, _stream()
         mark_ev()
-        if pc:
-            self.canonicalize_pcs(off, raw, n)          # local presence marked in-kernel
-            mark_ev()
-            self.merge_presence_bits()                  # RCCL uint8 MAX
-            self.build_dict()
-            mark_ev()
-        else:
-            self.mark(off, raw, n)
-            self.merge_presence_bits()                  # RCCL uint8 MAX
-            mark_ev()
-            self.build_dict()
-            mark_ev()
-            self.canonicalize(off, raw, n)
-            mark_ev()
-        self.glens = gather_lens(self.new_len[:n], self.world)  # RCCL all-gather
-        self.sort_order(self.glens, N)                  # identical on every rank
+        self.canonicalize(off, raw, n)
+        mark_ev()
+        self.glens = gather_lens(self.new_len[:n], self.world)   # RCCL all-gather
+        self.sort_order(self.glens, N)                          # identical on every rank
         mark_ev()
         items, ranks = local_items(self.order[:N], self.rank, n)
-        if pc:
-            self.minimize_win(off, items, ranks, items.numel(), do_pass2=False)
-            self.merge_first_window()                   # RCCL int32 MIN over dense ids
-            self.minimize_win_pass2(off, items, ranks, items.numel())
-        else:
-            self.minimize(off, items, ranks, items.numel(), do_pass2=False)
-            merge_first(self.first)                     # RCCL int32 MIN
-            self.minimize_pass2(off, items, ranks, items.numel())
-        merge_kept(self.kept[:N])                       # RCCL uint8 MAX
+        m = items.numel()
+        self.minimize(off, items, ranks, m, do_pass2=False)
+        merge_covered(self.covered[:self.nwords], self.world, self._or_into)
+        self.build_dict(self.ws2)
+        n_ids = int(self.scal[1].item()) & 0xFFFFFFFF
+        check(L.syzcov_dev_first_dense(_p(self.tab), self.span, _p(self.first),
+                                       _p(self.first_dense), 1, s), "dev_first_dense")
+        merge_first(self.first_dense[:n_ids])                    # RCCL int32 MIN
+        self.minimize_pass2(off, items, ranks, m, tab=self.tab, first_dense=self.first_dense)
+        merge_kept(self.kept[:N])                                 # RCCL uint8 MAX
         mark_ev()
-        self.compact(N)
+        self.compact(N, self.ws2)
         mark_ev()
         self.union_list()
         mark_ev()

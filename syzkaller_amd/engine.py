@@ -4,18 +4,19 @@ one MI355X (or one shard of a multi-GPU node).
 One `step()` is the C2 workload of BASELINE.json on a raw corpus already in
 HBM (CSR: offsets u64[n+1], raw KCOV PCs u32):
 
-    Canonicalize    every input (cover.go:27-40), fused with presence marking
-    dictionary      dense PC ids over the PC window (the corpus union)
-    order           Go sort.Sort(minInputArray) over canonical lengths
-    Minimize        first-cover pass 1 / pass 2 / ordered compaction (cover.go:104-131)
-    Union           sorted union list of the corpus (the `Union(total, cov)` fold)
-    maxCover merge  resident maxCover |= union (manager.go:606-610 / fuzzer.go:470)
+    canon     Canonicalize every input (cover.go:27-40): one wavefront per
+              segment, LDS radix sort + unique, plus per-range split points
+    order     Go sort.Sort(minInputArray) over canonical lengths (pdqsort restated)
+    minimize  first-cover Minimize (cover.go:104-131): geometric rank chunks,
+              LDS-resident covered bitmaps per 2^20-PC range, records of first
+              covers, pass 2 over the records; leaves the corpus union in `covered`
+    compact   kept inputs in processing order (the []int Minimize returns)
+    union     sorted union list (the `Union(total, cov)` fold, manager.go:606-610)
+    merge     resident maxCover |= union (manager.go:606-610 / fuzzer.go:470)
 
 torch supplies device memory, the stream and torch.distributed (RCCL);
 every computation is a libsyzcov HIP kernel launched on torch's current
-stream.  With a `shard` (engine.dist.Shard) the same step runs one rank of
-the sharded corpus and merges with RCCL: presence (uint8 MAX), first-cover
-(int32 MIN), kept flags (uint8 MAX).
+stream (syzkaller_amd.dist.ShardedEngine adds the RCCL merges).
 """
 from __future__ import annotations
 
@@ -54,102 +55,69 @@ class StepResult:
 
 
 class CorpusEngine:
-    """Buffers sized for up to `n_max` inputs / `p_max` PCs over the PC window
-    [pc_lo, pc_lo + pc_span).
+    """Buffers sized for up to `n_max` inputs / `p_max` raw PCs (longest input
+    `max_seg_len`) over the PC window [pc_lo, pc_lo + pc_span), at most 256
+    ranges of 2^20 PCs.  `n_global` > n_max: a shard of a larger corpus
+    (ranks, kept flags and the order span the whole corpus)."""
 
-    mode "pc" (default): canonical covers stay PCs; the presence bitmap is
-    marked by the canonicalize kernel itself and Minimize's first-cover table
-    is indexed by window offset (4 B x pc_span of HBM) — no dictionary lookup
-    anywhere on the per-PC path.
-    mode "ids": presence mark -> dense-id dictionary -> canonical covers as
-    dense ids -> Minimize over a first table of n_ids entries (smaller table,
-    one extra gather per raw PC)."""
+    PHASES = ("canon", "order", "minimize", "compact", "union", "merge")
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  device="cuda", n_global: int | None = None, sort_variant: int = 0,
-                 mode: str = "range", rec_cap: int = 0):
-        if mode not in ("range", "pc", "ids"):
-            raise ValueError(mode)
+                 rec_cap: int = 0):
         L = lib()
         dev = torch.device(device)
-        self.dev, self.L, self.mode = dev, L, mode
-        self.PHASES = {"range": self.PHASES_RANGE, "pc": self.PHASES_PC,
-                       "ids": self.PHASES_IDS}[mode]
+        self.dev, self.L = dev, L
         self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
         self.pc_lo, self.span = pc_lo, pc_span
         self.sort_variant = sort_variant
         self.n_global = n_global or n_max
+        self.rshift = RANGE_SHIFT
+        self.nrange = (pc_span + (1 << RANGE_SHIFT) - 1) >> RANGE_SHIFT
+        if self.nrange > 256:
+            raise ValueError("PC window too wide for the range engine (> 256 ranges of 2^20)")
         nwords = (pc_span + 31) // 32
         self.nwords = nwords
         self.canon = _u32(p_max + 1, dev)
         self.new_len = _u32(n_max + 1, dev)
-        # presence and resident maxCover: one bit per PC of the window
-        self.pres = torch.zeros(nwords, dtype=torch.int32, device=dev)
+        # split points (columns per segment) and PCs per range, from canon
+        self.split = (torch.empty(n_max * self.nrange, dtype=torch.int32, device=dev)
+                      if self.nrange > 1 else None)
+        self.range_tot = torch.zeros(self.nrange, dtype=torch.int64, device=dev)
+        # covered set (one bit per window PC; ends up as the corpus union) and
+        # the resident maxCover
+        self.covered = torch.zeros((self.nrange << RANGE_SHIFT) // 32, dtype=torch.int32,
+                                   device=dev)
         self.max_cover = torch.zeros(nwords, dtype=torch.int32, device=dev)
         self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
-        ids_cap = min(pc_span, p_max) + 1
-        self.ids_cap = ids_cap
-        self.first = torch.empty(pc_span if mode in ("pc", "range") else ids_cap,
-                                 dtype=torch.int32, device=dev)
-        if mode == "range":
-            # LDS-resident ranges of 2^rshift PCs; split[] columns per segment
-            self.rshift = RANGE_SHIFT
-            self.nrange = (pc_span + (1 << RANGE_SHIFT) - 1) >> RANGE_SHIFT
-            if self.nrange > 256:
-                raise ValueError("PC window too wide for the range engine (> 256 ranges)")
-            self.split = (torch.empty(n_max * self.nrange, dtype=torch.int32, device=dev)
-                          if self.nrange > 1 else None)
-            self.range_tot = torch.zeros(self.nrange, dtype=torch.int64, device=dev)
-            self.covered = torch.zeros((self.nrange << RANGE_SHIFT) // 32, dtype=torch.int32,
-                                       device=dev)
-            self.first.fill_(INT32_MAX)  # minimize_range leaves it INT32_MAX on return
-            self.rec_cap = rec_cap or max(1 << 22, min(p_max, 1 << 26))
-            self.rec = torch.empty(self.rec_cap, dtype=torch.int64, device=dev)
-            self.rec_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-            self.cover_words = self.covered.numel()
+        # first-cover rank per window PC: INT32_MAX outside a step's records
+        self.first = torch.full((pc_span,), INT32_MAX, dtype=torch.int32, device=dev)
+        self.rec_cap = rec_cap or max(1 << 22, min(p_max, 1 << 26))
+        self.rec = torch.empty(self.rec_cap, dtype=torch.int64, device=dev)
+        self.rec_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
         self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
         self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
         self.lens64 = torch.empty(self.n_global + 1, dtype=torch.int64, device=dev)
         self.order = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
         self.out_idx = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
-        self.union = _u32(ids_cap, dev)
+        self.union = _u32(min(pc_span, p_max) + 1, dev)
         self.scal = torch.zeros(16, dtype=torch.int64, device=dev)  # err, n_ids, n_kept, ...
-        ws = max(L.syzcov_dev_canon_ws_size(n_max, max_seg_len),
+        ws = max(L.syzcov_dev_canon_split_ws_size(n_max),
                  L.syzcov_dev_dict_ws_size(pc_span),
                  L.syzcov_dev_compact_ws_size(self.n_global),
                  L.syzcov_dev_sort_ws_size(self.n_global),
-                 L.syzcov_dev_minimize_ws_size(ids_cap),
-                 L.syzcov_dev_minimize_win_ws_size(pc_span),
-                 L.syzcov_dev_canon_split_ws_size(n_max),
                  L.syzcov_dev_minimize_range_ws_size(self.n_global, pc_span, RANGE_SHIFT))
         self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
         self.ws_size = ws
 
-    # ---------------------------------------------------------------- phases
-    PHASES_IDS = ("mark", "dict", "canon", "order", "minimize", "compact", "union", "merge")
-    PHASES_PC = ("canon", "dict", "order", "minimize", "compact", "union", "merge")
-    PHASES_RANGE = ("canon", "order", "minimize", "compact", "union", "merge")
-    PHASES = PHASES_PC
-
     def alg_bytes(self, raw_pcs: int, canon_pcs: int) -> dict:
         """Algorithmic HBM bytes per launch of the streaming phases (DESIGN.md
-        §4): every raw PC read once (4 B), every canonical PC written once and
-        read once by Minimize pass 1."""
-        if self.mode in ("pc", "range"):
-            return {"canon": 4 * raw_pcs + 4 * canon_pcs, "minimize": 4 * canon_pcs}
-        return {"mark": 4 * raw_pcs, "canon": 4 * raw_pcs + 4 * canon_pcs,
-                "minimize": 4 * canon_pcs}
+        §4): canon reads every raw PC and writes every canonical PC once;
+        Minimize pass 1 reads every canonical PC once."""
+        return {"canon": 4 * raw_pcs + 4 * canon_pcs, "minimize": 4 * canon_pcs}
 
-    def canonicalize_pcs(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        """Canonical covers as PCs with the presence bitmap marked in-kernel."""
-        self.pres.zero_()
-        self.scal.zero_()
-        check(self.L.syzcov_dev_canon_pcs(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
-                                          self.max_seg, self.pc_lo, self.span, _p(self.pres),
-                                          _p(self.scal), _p(self.ws), self.ws_size, _stream()),
-              "dev_canon_pcs")
-
-    def canonicalize_split(self, off: torch.Tensor, raw: torch.Tensor, n: int):
+    # ---------------------------------------------------------------- phases
+    def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
         """Wavefront canonicalize + per-range split points and range totals."""
         self.scal.zero_()
         self.range_tot.zero_()
@@ -159,7 +127,13 @@ class CorpusEngine:
                                             _p(self.ws), self.ws_size, _stream()),
               "dev_canon_split")
 
-    def minimize_range(self, off, order, ranks, n_items):
+    def sort_order(self, lens32: torch.Tensor, n: int):
+        """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
+        self.lens64[:n].copy_(lens32[:n].to(torch.int64))
+        check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
+                                           _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
+
+    def minimize(self, off, order, ranks, n_items, do_pass2=True):
         """Range-partitioned first-cover Minimize; leaves the union in covered."""
         self.covered.zero_()
         self.cand[:n_items].zero_()
@@ -168,77 +142,35 @@ class CorpusEngine:
             _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
             n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
             _p(self.first), _p(self.rec), self.rec_cap, _p(self.rec_cnt), _p(self.cand),
-            _p(self.kept), 0, 0, 0, _p(self.ws), _stream()), "dev_minimize_range")
+            _p(self.kept), int(do_pass2), 0, 0, 0, _p(self.ws), _stream()), "dev_minimize_range")
 
-    def union_from_covered(self):
-        check(self.L.syzcov_dev_dict_build_bits(_p(self.covered), self.span, _p(self.tab),
-                                                _p(self.scal[1:2]), _p(self.ws), _stream()),
-              "dev_dict_build_bits")
-        self.union_list()
+    def minimize_pass2(self, off, order, ranks, n_items, tab=None, first_dense=None):
+        """Pass 2 over the records (sharded: against the MIN-merged dense table)."""
+        check(self.L.syzcov_dev_minimize_range_pass2(
+            _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
+            n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
+            _p(self.first), _p(self.rec), self.rec_cap, _p(self.rec_cnt), _p(self.cand), _p(tab),
+            _p(first_dense), _p(self.kept), _p(self.ws), _stream()), "dev_minimize_range_pass2")
 
-    def minimize_win(self, off, order, ranks, n_items, do_pass2=True):
-        self.first.fill_(INT32_MAX)
-        self.kept.zero_()
-        check(self.L.syzcov_dev_minimize_win(
-            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items, self.pc_lo,
-            self.span, _p(self.first), _p(self.cand), _p(self.kept), int(do_pass2), _p(self.ws),
-            _stream()), "dev_minimize_win")
-
-    def minimize_win_pass2(self, off, order, ranks, n_items):
-        check(self.L.syzcov_dev_minimize_win_pass2(
-            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items, self.pc_lo,
-            _p(self.first), _p(self.cand), _p(self.kept), _stream()), "dev_minimize_win_pass2")
-
-    def mark(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        """Presence bitmap of the raw corpus (test-before-atomicOr)."""
-        self.pres.zero_()
-        self.scal.zero_()
-        check(self.L.syzcov_dev_mark_bits(_p(off), _p(raw), n, _p(self.pres), self.pc_lo,
-                                          self.span, _p(self.scal), _stream()), "dev_mark_bits")
-
-    def build_dict(self):
-        check(self.L.syzcov_dev_dict_build_bits(_p(self.pres), self.span, _p(self.tab),
-                                                _p(self.scal[1:2]), _p(self.ws), _stream()),
-              "dev_dict_build_bits")
-
-    def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        """Canonical covers in the dense-id space (LDS radix sort + unique)."""
-        check(self.L.syzcov_dev_canon_ids(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
-                                          self.max_seg, _p(self.tab), self.pc_lo, self.span,
-                                          _p(self.scal[1:2]), _p(self.scal), _p(self.ws),
-                                          self.ws_size, _stream()), "dev_canon_ids")
-
-    def sort_order(self, lens32: torch.Tensor, n: int):
-        """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
-        self.lens64[:n].copy_(lens32[:n].to(torch.int64))
-        check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
-                                           _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
-
-    def minimize(self, off, order, ranks, n_items, do_pass2=True):
-        """Chunked pass 1 (+ pass 2) over n_items work items; kept[] by rank."""
-        self.first.fill_(INT32_MAX)
-        self.kept.zero_()
-        check(self.L.syzcov_dev_minimize_ids(
-            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items,
-            _p(self.scal[1:2]), self.ids_cap, _p(self.first), _p(self.cand), _p(self.kept),
-            int(do_pass2), _p(self.ws), _stream()), "dev_minimize_ids")
-
-    def minimize_pass2(self, off, order, ranks, n_items):
-        check(self.L.syzcov_dev_minimize_ids_pass2(
-            _p(off), _p(self.new_len), _p(self.canon), _p(order), _p(ranks), n_items,
-            _p(self.first), _p(self.cand), _p(self.kept), _stream()), "dev_minimize_ids_pass2")
-
-    def compact(self, n_ranks: int):
+    def compact(self, n_ranks: int, ws=None):
         check(self.L.syzcov_dev_compact_kept(_p(self.kept), _p(self.order), n_ranks,
-                                             _p(self.out_idx), _p(self.scal[2:3]), _p(self.ws),
-                                             _stream()), "dev_compact_kept")
+                                             _p(self.out_idx), _p(self.scal[2:3]),
+                                             _p(self.ws if ws is None else ws), _stream()),
+              "dev_compact_kept")
+
+    def build_dict(self, ws=None):
+        """Dense-id dictionary of the covered set; *n_ids -> scal[1]."""
+        check(self.L.syzcov_dev_dict_build_bits(_p(self.covered), self.span, _p(self.tab),
+                                                _p(self.scal[1:2]),
+                                                _p(self.ws if ws is None else ws), _stream()),
+              "dev_dict_build_bits")
 
     def union_list(self):
         check(self.L.syzcov_dev_dict_to_list(_p(self.tab), self.span, self.pc_lo, _p(self.union),
                                              _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
 
     def merge_max_cover(self):
-        check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.pres), self.nwords,
+        check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered), self.nwords,
                                           _p(self.scal[4:5]), _stream()), "dev_bitmap_op")
 
     # ------------------------------------------------------------------ step
@@ -250,43 +182,15 @@ class CorpusEngine:
                 ev[k[0]].record()
             k[0] += 1
         mark_ev()
-        if self.mode == "range":
-            self.canonicalize_split(off, raw, n)
-            mark_ev()
-            self.sort_order(self.new_len, n)
-            mark_ev()
-            self.minimize_range(off, self.order, None, n)
-            mark_ev()
-            self.compact(n)
-            mark_ev()
-            self.union_from_covered()
-            mark_ev()
-            check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered),
-                                              self.nwords, _p(self.scal[4:5]), _stream()),
-                  "dev_bitmap_op")
-            mark_ev()
-            return self.result() if sync else None
-        if self.mode == "pc":
-            self.canonicalize_pcs(off, raw, n)
-            mark_ev()
-            self.build_dict()
-            mark_ev()
-        else:
-            self.mark(off, raw, n)
-            mark_ev()
-            self.build_dict()
-            mark_ev()
-            self.canonicalize(off, raw, n)
-            mark_ev()
+        self.canonicalize(off, raw, n)
+        mark_ev()
         self.sort_order(self.new_len, n)
         mark_ev()
-        if self.mode == "pc":
-            self.minimize_win(off, self.order, None, n)
-        else:
-            self.minimize(off, self.order, None, n)
+        self.minimize(off, self.order, None, n)
         mark_ev()
         self.compact(n)
         mark_ev()
+        self.build_dict()
         self.union_list()
         mark_ev()
         self.merge_max_cover()
@@ -302,16 +206,8 @@ class CorpusEngine:
                           int(sc[4]))
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
-        """Materialise the canonical covers as PCs (CSR slots of `off`)."""
-        if self.mode in ("pc", "range"):
-            return self.canon
-        table = _u32(self.ids_cap, self.dev)
-        check(self.L.syzcov_dev_dict_pcs(_p(self.tab), self.span, self.pc_lo, _p(table),
-                                         _stream()), "dev_dict_pcs")
-        out = torch.zeros_like(self.canon)
-        check(self.L.syzcov_dev_gather_u32(_p(table), _p(off), _p(self.new_len), _p(self.canon),
-                                           n, _p(out), _stream()), "dev_gather_u32")
-        return out
+        """The canonical covers as PCs, in the CSR slots of `off`."""
+        return self.canon
 
 
 class PrioEngine:

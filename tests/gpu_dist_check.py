@@ -26,8 +26,8 @@ def main():
     off, raw, lens, total = synth_corpus(n, 0x5EED0009, mean=700, sigma=300, log2_space=18)
     lo, span = synth_window(18)
     a = CorpusEngine(n, total, int(lens.max().item()), lo, span).step(off, raw, n)
-    for mode in ("pc", "ids"):
-        eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, 0, 1, mode=mode)
+    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, 0, 1)
+    for _ in range(2):
         b = eng.step(off, raw, n)
         assert a.n_kept == b.n_kept and a.n_union == b.n_union and a.max_cover == b.max_cover
         assert torch.equal(a.kept_idx.cpu(), b.kept_idx.cpu())

@@ -29,15 +29,14 @@ def test_synth_matches_cpu_twin(torch):
         assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
 
 
-@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
                                                (500, 9000, 6000, 20)])
-def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, mode):
+def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
     seed = 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
     lo, span = synth_window(log2)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, mode=mode)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
     res = eng.step(off, raw, n)
     # oracle
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
@@ -62,8 +61,7 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, mode):
     assert res2.max_cover == exp_union.size
 
 
-@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
-def test_engine_sentinel_window(torch, mode):
+def test_engine_sentinel_window(torch):
     """Window touching 0xFFFFFFFF: inputs made only of the sentinel canonicalize
     to empty, otherwise it is an ordinary PC (cover.go:36-52, 104-131)."""
     from syzkaller_amd.engine import CorpusEngine
@@ -85,7 +83,7 @@ def test_engine_sentinel_window(torch, mode):
     n = len(covers)
     off = torch.from_numpy(o_off.astype(np.int64)).cuda()
     raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
-    eng = CorpusEngine(n, int(lens.sum()), int(lens.max()), lo, span, mode=mode)
+    eng = CorpusEngine(n, int(lens.sum()), int(lens.max()), lo, span)
     res = eng.step(off, raw, n)
     c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs[:int(lens.sum())])
     assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
@@ -105,8 +103,20 @@ def test_sharded_engine_world1(torch):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("mode", ["range", "pc", "ids"])
-def test_engine_properties_large(torch, mode):
+def test_sharded_engine_two_ranks(torch):
+    """Two ranks of the sharded range engine on one GPU (gloo collectives
+    staged through the host): covered OR merge, first MIN merge over the
+    merged dictionary, kept MAX merge, against the single-GPU engine."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_dist_multi.py"), "2"],
+                       capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout + r.stderr
+
+
+def test_engine_properties_large(torch):
     """Size-independent properties at 200k inputs: union(kept) == union(all),
     kept order follows non-increasing canonical length, first kept = rank 0."""
     from syzkaller_amd import cover
@@ -114,7 +124,7 @@ def test_engine_properties_large(torch, mode):
     n = 200_000
     off, raw, lens, total = synth_corpus(n, 0x5EED0003, mean=256, sigma=64, log2_space=20)
     lo, span = synth_window(20)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, mode=mode)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
     res = eng.step(off, raw, n)
     kept = res.kept_idx.cpu().numpy()
     new_len = eng.new_len[:n].cpu().numpy()

@@ -32,8 +32,8 @@ def main():
     eng.step(off, raw, n)
     torch.cuda.synchronize()
     fns = {
-        "canon": lambda: eng.canonicalize_split(off, raw, n),
-        "minimize": lambda: eng.minimize_range(off, eng.order, None, n),
+        "canon": lambda: eng.canonicalize(off, raw, n),
+        "minimize": lambda: eng.minimize(off, eng.order, None, n),
         "step": lambda: eng.step(off, raw, n, sync=False),
     }
     f = fns[a.what]
