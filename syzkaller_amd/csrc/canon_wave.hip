@@ -24,8 +24,11 @@
 //   range_tot[j]      += canonical PCs of range j over the corpus.
 // Segments longer than 8189 keys are listed for the workgroup paths.
 #include "common.h"
+#include "xperm.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 namespace syz {
 
@@ -34,6 +37,11 @@ int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
                      uint64_t pc_span, uint32_t *err, hipStream_t s);
+int canon_bitonic_launch(int W, const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                         uint32_t *new_len, uint32_t pc_lo, uint64_t pc_span, uint32_t sent_key,
+                         uint32_t *split, uint32_t nrange, uint32_t rshift, uint64_t *range_tot,
+                         uint32_t *err, const uint32_t *list, const uint32_t *cnt, uint64_t nseg,
+                         hipStream_t s);
 
 namespace cw {
 
@@ -60,10 +68,6 @@ __device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
     h4[2 * l + 1] = ob;
 }
 
-// Lane l receives v of lane l-1; lane 0 receives `first` (DPP wave_shr:1).
-__device__ __forceinline__ uint32_t shift_up(uint32_t v, uint32_t first) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
-}
 
 __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
@@ -429,11 +433,20 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     P.big_cnt = cnts + 1;
     P.err = err_flag;
     // bin by capacity class (wave-aggregated atomics), one launch per class
+    // algorithm: the LDS radix sort (default; 11.9 ms at C2) or the register
+    // bitonic network (SYZCOV_CANON=bitonic; 20.3 ms at C2: 147 VALU ops per
+    // key at 2 waves/SIMD lose to ~13 LDS ops per 64 keys).  Both are exact.
+    bool bitonic = false;
+    if (const char *e = getenv("SYZCOV_CANON")) bitonic = strcmp(e, "bitonic") == 0;
     cw::Classes C;
     const uint32_t nk[cw::NCLS] = {16, 32, 48, 64, 128};
     for (int c = 0; c < cw::NCLS; c++) {
         C.lo[c] = c ? nk[c - 1] * 64 - 2 : 0;  // CAP - 3 + 1 of the previous class
         C.hi[c] = nk[c] * 64 - 3;
+    }
+    if (bitonic) {  // 1, 2, 4 waves of 2048 keys
+        const uint32_t bl[cw::NCLS] = {0, 2046, 4094, 1, 1}, bh[cw::NCLS] = {2045, 4093, 8189, 0, 0};
+        for (int c = 0; c < cw::NCLS; c++) C.lo[c] = bl[c], C.hi[c] = bh[c];
     }
     uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
     uint32_t *ccnt = cnts + 2;
@@ -441,7 +454,14 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 2048)), dim3(256), 0, s, off,
                        (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1);
     const unsigned grid = (unsigned)std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, 4096);
-    for (int c = 0; c < cw::NCLS; c++) {
+    for (int c = 0; bitonic && c < 3; c++) {
+        if (max_seg_len < C.lo[c]) break;
+        int rc = canon_bitonic_launch(1 << c, off, raw, out, new_len, pc_lo, pc_span, P.sent_key,
+                                      split, (uint32_t)nrange, range_shift, range_tot, err_flag,
+                                      clists + (size_t)c * nseg, ccnt + c, nseg, s);
+        if (rc) return rc;
+    }
+    for (int c = 0; !bitonic && c < cw::NCLS; c++) {
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {

@@ -20,9 +20,11 @@
 // items' sub-runs inside the range (canonical lists are sorted, so a sub-run
 // is contiguous: split[] from canon_wave.hip).  Ranges get workgroups in
 // proportion to their PC counts (range_tot), so a hot range is cut into many
-// short item slices.  Each wave flattens the sub-runs of 64 items into full
-// 64-lane rows (a scalar walk over the items starting inside each row) and
-// keeps ROWS row loads in flight before it tests them.
+// short item slices.  A wave takes 64 items at a time: short sub-runs (the
+// cold ranges) are read one lane per item in 16-byte chunks, U chunks in
+// flight per lane; long sub-runs (the hot ranges) by the whole wave, 256 PCs
+// per row and UB rows in flight.  Either way one VMEM instruction carries up
+// to 1 KB and the per-PC work is a subtract, a shift and one LDS bit test.
 //
 // Record overflow (more uncovered occurrences than rec_cap, only for
 // adversarial corpora) is detected on the device; the fallback kernels then
@@ -31,13 +33,22 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 namespace syz {
 namespace mr {
 
 constexpr int THREADS = 1024;
 constexpr int NWAVE = THREADS / 64;
-constexpr int ROWS = 16;         // row loads in flight per wave
+constexpr int U = 8;             // 16-byte chunks in flight per lane (short sub-runs)
+constexpr int UB = 4;            // 256-PC rows in flight per wave (long sub-runs)
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
 constexpr int MAX_R = 256;
 
 struct Args {
@@ -77,22 +88,27 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
     }
 }
 
-// Workgroup -> (range, item slice [i0, i1)) with pieces proportional to the
-// range's weight: p_j = 1 + floor(w_j * (G - R) / W).
-__device__ bool piece_of(const Args &A, uint32_t G, uint32_t a, uint32_t b, uint32_t *rho,
-                         uint32_t *i0, uint32_t *i1, uint32_t *sh) {
+// Workgroup -> (range, item slice [i0, i1)).  The chunk's items are cut into
+// S slices; each slice is covered by P = G / S consecutive workgroups, range j
+// getting p_j = 1 + floor(w_j * (P - R) / W) of them (w_j: its PC count), so
+// a hot range's part of a slice is split further.  Consecutive workgroups
+// thus read different ranges of the SAME segments at the same time: the
+// sub-runs of one segment are neighbours in HBM (DRAM row locality) and a
+// line shared by two ranges is still in L2 when the second one asks for it.
+__device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint32_t b,
+                         uint32_t *rho, uint32_t *i0, uint32_t *i1, uint32_t *sh) {
     // sh: LDS scratch of MAX_R + 1 entries; computed by wave 0
     const uint32_t l = __lane_id();
     if (threadIdx.x < 64) {
         unsigned long long wsum = 0;
         for (uint32_t j = l; j < A.nrange; j += 64) wsum += A.range_tot[j];
         for (int d = 32; d >= 1; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
-        const uint64_t spare = G > A.nrange ? G - A.nrange : 0;
+        const uint64_t spare = P > A.nrange ? P - A.nrange : 0;
         uint32_t carry = 0;
         for (uint32_t jb = 0; jb < A.nrange; jb += 64) {
             const uint32_t j = jb + l;
             uint32_t p = 0;
-            if (j < A.nrange)  // integer: the pieces never exceed G
+            if (j < A.nrange)  // integer: the pieces never exceed P
                 p = 1u + (wsum ? (uint32_t)(A.range_tot[j] * spare / wsum) : 0u);
             const uint32_t inc = wave_incl_scan(p);
             if (j < A.nrange) sh[j + 1] = carry + inc;
@@ -101,28 +117,34 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t a, uint32_t b, uint
         if (l == 0) sh[0] = 0;
     }
     __syncthreads();
-    const uint32_t g = blockIdx.x;
-    if (g >= sh[A.nrange]) return false;
-    uint32_t lo = 0, hi = A.nrange;  // largest j with sh[j] <= g
+    const uint32_t S = G / P;  // slices
+    const uint32_t g = blockIdx.x, sl = g / P, r = g % P;
+    if (sl >= S || r >= sh[A.nrange]) return false;
+    uint32_t lo = 0, hi = A.nrange;  // largest j with sh[j] <= r
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (sh[mid] <= g) lo = mid; else hi = mid;
+        if (sh[mid] <= r) lo = mid; else hi = mid;
     }
-    const uint32_t p = sh[lo + 1] - sh[lo], q = g - sh[lo];
+    const uint32_t p = sh[lo + 1] - sh[lo], q = r - sh[lo];
     const uint64_t n = b - a;
+    const uint64_t s0 = n * sl / S, s1 = n * (sl + 1) / S;  // the slice
     *rho = lo;
-    *i0 = a + (uint32_t)(n * q / p);
-    *i1 = a + (uint32_t)(n * (q + 1) / p);
+    *i0 = a + (uint32_t)(s0 + (s1 - s0) * q / p);
+    *i1 = a + (uint32_t)(s0 + (s1 - s0) * (q + 1) / p);
     return true;
 }
 
 // Pass 1 over items [a, b) (one chunk).
-__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b,
+// SMALL_M: sub-runs up to this length take the lane-per-item path.
+// TEST = false is a tuning variant that streams the data without the
+// covered tests (not exact; selected only through SYZCOV_MR_CFG).
+template <uint32_t SMALL_M, bool TEST, bool WHOLE = false>
+__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b, uint32_t P,
                                                         int load_cov) {
     extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
     __shared__ uint32_t s_plan[MAX_R + 1];
     uint32_t rho, i0, i1;
-    if (!piece_of(A, gridDim.x, a, b, &rho, &i0, &i1, s_plan)) return;
+    if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
     const uint32_t nwords = (1u << A.rshift) >> 5;
     {
         const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
@@ -137,7 +159,6 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
     __syncthreads();
     const uint32_t l = __lane_id();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t rbase = rho << A.rshift;  // window offset of the range
     // the slice is split evenly over the waves, 64 items per batch
     const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
@@ -150,81 +171,139 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
         int32_t rk = 0;
         if (item < w1) {
             rk = A.ranks ? A.ranks[item] : (int32_t)item;
-            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
-            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            if (WHOLE) {  // tuning probe: the whole canonical list, one range
+                s0 = 0;
+                s1 = rho == 0 ? A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + item] : 0u;
+            }
             st = A.base_r[item] + s0;
             m = s1 - s0;
         }
-        const uint32_t incl = wave_incl_scan(m);
-        const uint32_t pre = incl - m;                      // exclusive prefix
-        const uint32_t T = __shfl(incl, 63, 64);            // flattened length
-        if (T == 0) continue;
-        // per-lane state: item containing flattened element R0 + l
-        uint64_t my_st = 0;
-        uint32_t my_pre = 0, my_item = 0;
-        int32_t my_rk = 0;
-        for (uint32_t R0 = 0; R0 < T; R0 += ROWS * 64) {
-            uint32_t v[ROWS], ix[ROWS], rkv[ROWS];
-            bool act[ROWS];
+        // ---- (1) short sub-runs: one lane per item, 16-byte chunks, U in flight
+        {
+            const bool mine = m > 0 && m <= SMALL_M;
+            const uint64_t a0 = st & ~3ull;
+            const uint32_t head = (uint32_t)(st - a0), end = head + m;
+            const uint32_t nch = mine ? (end + 3) >> 2 : 0u;
+            const uint32_t maxch = wave_max(nch);
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
+            for (uint32_t c0 = 0; c0 < maxch; c0 += U) {
+                uint4 v[U];
 #pragma unroll
-            for (int u = 0; u < ROWS; u++) {
-                const uint32_t r0 = R0 + u * 64;
-                act[u] = false;
-                if (r0 < T) {
-                    // carry the item of the previous row's last element
-                    my_st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)my_st, 63) |
-                            ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_st >> 32), 63) << 32);
-                    my_pre = __builtin_amdgcn_readlane(my_pre, 63);
-                    my_item = __builtin_amdgcn_readlane(my_item, 63);
-                    my_rk = __builtin_amdgcn_readlane(my_rk, 63);
-                    uint64_t starts = __ballot(m > 0 && pre >= r0 && pre < r0 + 64);
-                    while (starts) {
-                        const uint32_t i = __builtin_ctzll(starts);
-                        starts &= starts - 1;
-                        const uint32_t pi = __builtin_amdgcn_readlane(pre, i);
-                        if (l >= pi - r0) {
-                            my_st = (uint64_t)__builtin_amdgcn_readlane((uint32_t)st, i) |
-                                    ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), i) << 32);
-                            my_pre = pi;
-                            my_item = ib + i;
-                            my_rk = __builtin_amdgcn_readlane(rk, i);
+                for (int u = 0; u < U; u++)
+                    v[u] = c0 + u < nch ? src[c0 + u] : make_uint4(0, 0, 0, 0);
+                uint32_t um = 0;
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t idx = (c0 + u) * 4 + k;
+                        const bool valid = c0 + u < nch && idx >= head && idx < end;
+                        const uint32_t bit = valid ? vv[k] - A.pc_lo - rbase : 0u;
+                        if (TEST && WHOLE) {  // probe: window-wide test in global memory
+                            const uint32_t wo = valid ? vv[k] - A.pc_lo : 0u;
+                            um |= (uint32_t)(valid && !((A.covered[wo >> 5] >> (wo & 31)) & 1u))
+                                  << (u * 4 + k);
+                        } else if (TEST)
+                            um |= (uint32_t)(valid && !((s_cov[bit >> 5] >> (bit & 31)) & 1u))
+                                  << (u * 4 + k);
+                        else
+                            um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
+                    }
+                }
+                if (__ballot(um != 0)) {
+                    // reserve this lane's records, then write them
+                    const uint32_t cnt = (uint32_t)__popc(um);
+                    const uint32_t incl = wave_incl_scan(cnt);
+                    const uint32_t tot = __shfl(incl, 63, 64);
+                    unsigned long long basei = 0;
+                    if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)tot);
+                    uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
+                    if (um) {
+                        A.cand[item] = 1;
+#pragma unroll
+                        for (int u = 0; u < U; u++) {
+                            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int k = 0; k < 4; k++)
+                                if ((um >> (u * 4 + k)) & 1u) {
+                                    const uint32_t wo = vv[k] - A.pc_lo;
+                                    atomicMin(&A.first_w[wo], rk);
+                                    if (slot < A.rec_cap)
+                                        A.rec[slot] = ((unsigned long long)(uint32_t)rk << 32) | wo;
+                                    slot++;
+                                }
                         }
                     }
-                    const uint32_t f = r0 + l;
-                    act[u] = f < T;
-                    ix[u] = my_item;
-                    rkv[u] = (uint32_t)my_rk;
-                    v[u] = act[u] ? A.pcs[my_st + (f - my_pre)] : 0u;
                 }
             }
-            // LDS bit tests; one record reservation per batch of ROWS rows
-            uint64_t um[ROWS];
-            uint32_t nunc = 0;
+        }
+        // ---- (2) long sub-runs: the whole wave per item, 256 PCs per row
+        uint64_t big = __ballot(m > SMALL_M);
+        while (big) {
+            const uint32_t i = __builtin_ctzll(big);
+            big &= big - 1;
+            const uint64_t sti = (uint64_t)__builtin_amdgcn_readlane((uint32_t)st, i) |
+                                 ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), i) << 32);
+            const uint32_t mi = __builtin_amdgcn_readlane(m, i);
+            const int32_t rki = __builtin_amdgcn_readlane(rk, i);
+            const uint64_t a0 = sti & ~3ull;
+            const uint32_t head = (uint32_t)(sti - a0), end = head + mi;
+            const uint32_t nch = (end + 3) >> 2;
+            const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
+            for (uint32_t c0 = 0; c0 < nch; c0 += 64 * UB) {
+                uint4 v[UB];
 #pragma unroll
-            for (int u = 0; u < ROWS; u++) {
-                um[u] = 0;
-                if (R0 + u * 64 < T) {
-                    const uint32_t bit = act[u] ? v[u] - A.pc_lo - rbase : 0u;  // < 2^rshift
-                    const bool unc = act[u] && !((s_cov[bit >> 5] >> (bit & 31)) & 1u);
-                    um[u] = __ballot(unc);
-                    nunc += (uint32_t)__popcll(um[u]);
+                for (int u = 0; u < UB; u++) {
+                    const uint32_t ch = c0 + u * 64 + l;
+                    v[u] = ch < nch ? src[ch] : make_uint4(0, 0, 0, 0);
                 }
-            }
-            if (nunc) {
-                unsigned long long basei = 0;
-                if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)nunc);
-                basei = __shfl(basei, 0, 64);
+                uint32_t um = 0;
 #pragma unroll
-                for (int u = 0; u < ROWS; u++) {
-                    if ((um[u] >> l) & 1u) {
-                        const uint32_t wo = v[u] - A.pc_lo;
-                        atomicMin(&A.first_w[wo], (int32_t)rkv[u]);
-                        const uint64_t slot = basei + (uint64_t)__popcll(um[u] & lt);
-                        if (slot < A.rec_cap)
-                            A.rec[slot] = ((unsigned long long)rkv[u] << 32) | wo;
-                        A.cand[ix[u]] = 1;
+                for (int u = 0; u < UB; u++) {
+                    const uint32_t ch = c0 + u * 64 + l;
+                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t idx = ch * 4 + k;
+                        const bool valid = ch < nch && idx >= head && idx < end;
+                        const uint32_t bit = valid ? vv[k] - A.pc_lo - rbase : 0u;
+                        if (TEST && WHOLE) {  // probe: window-wide test in global memory
+                            const uint32_t wo = valid ? vv[k] - A.pc_lo : 0u;
+                            um |= (uint32_t)(valid && !((A.covered[wo >> 5] >> (wo & 31)) & 1u))
+                                  << (u * 4 + k);
+                        } else if (TEST)
+                            um |= (uint32_t)(valid && !((s_cov[bit >> 5] >> (bit & 31)) & 1u))
+                                  << (u * 4 + k);
+                        else
+                            um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
                     }
-                    basei += (uint64_t)__popcll(um[u]);
+                }
+                if (__ballot(um != 0)) {
+                    const uint32_t cnt = (uint32_t)__popc(um);
+                    const uint32_t incl = wave_incl_scan(cnt);
+                    const uint32_t tot = __shfl(incl, 63, 64);
+                    unsigned long long basei = 0;
+                    if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)tot);
+                    uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
+                    if (l == 0) A.cand[ib + i] = 1;
+                    if (um) {
+#pragma unroll
+                        for (int u = 0; u < UB; u++) {
+                            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int k = 0; k < 4; k++)
+                                if ((um >> (u * 4 + k)) & 1u) {
+                                    const uint32_t wo = vv[k] - A.pc_lo;
+                                    atomicMin(&A.first_w[wo], rki);
+                                    if (slot < A.rec_cap)
+                                        A.rec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    slot++;
+                                }
+                        }
+                    }
                 }
             }
         }
@@ -432,24 +511,48 @@ extern "C" int syzcov_dev_minimize_range(
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
-    static bool attr_set = false;  // idempotent; races only repeat the call
-    if (!attr_set) {
-        SYZ_HIP(hipFuncSetAttribute((const void *)mr::pass1_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-        attr_set = true;
+    // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (96),
+    // 1 = lane-per-item never, 2 = always, 3..5 = the same without tests;
+    // pmode 0 = slice-major (P = 2R), 1 = range-major (one slice; default:
+    // 7.1 vs 8.0 ms at C2)
+    int variant = 0, pmode = 1;
+    if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
+    using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
+    const K kern[8] = {mr::pass1_kernel<96, true>, mr::pass1_kernel<0, true>,
+                       mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
+                       mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
+                       mr::pass1_kernel<96, false, true>, mr::pass1_kernel<96, true, true>};
+    const int vi = variant >= 0 && variant < 8 ? variant : 0;
+    const K k1 = kern[vi];
+    static bool attr_set[8] = {false, false, false, false, false, false, false, false};
+    if (!attr_set[vi]) {
+        SYZ_HIP(hipFuncSetAttribute((const void *)k1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    128 * 1024));
+        attr_set[vi] = true;
+    }
+    if (const char *e = getenv("SYZCOV_MR_CHUNK")) {  // tuning: "first,growth"
+        unsigned long fc = 0, gr = 0;
+        if (sscanf(e, "%lu,%lu", &fc, &gr) == 2) {
+            first_chunk = fc;
+            growth = (uint32_t)gr;
+        }
     }
     if (first_chunk == 0) first_chunk = 64;
     if (growth < 2) growth = 4;
-    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 18;
+    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 17;
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     uint64_t a = 0, step = first_chunk;
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
-        uint64_t G = (b - a) * avg_len / pcs_per_wg_hint;
-        G = std::max<uint64_t>(G, std::max<uint64_t>(4 * nrange, 1024));
-        G = std::min<uint64_t>(G, 8192);
-        hipLaunchKernelGGL(mr::pass1_kernel, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A,
-                           (uint32_t)a, (uint32_t)b, (int)(a != 0));
+        // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
+        // P = 2R workgroups per item slice
+        uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
+        G = std::min<uint64_t>(std::max<uint64_t>(G, 256), 8192);
+        uint64_t P = 2 * nrange;
+        if (pmode == 1) P = G;
+        G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
+        hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
+                           (uint32_t)b, (uint32_t)P, (int)(a != 0));
         hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s,
                            (const unsigned long long *)rec, rec_cap,
                            (const unsigned long long *)rec_cnt, (const unsigned long long *)done,
