@@ -25,6 +25,23 @@ def main():
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n = a.inputs
+    if a.what == "order":  # Go sort.Sort order over n synthetic lengths only
+        import ctypes as C
+        from syzkaller_amd._lib import check, lib
+        L = lib()
+        lens = torch.empty(n, dtype=torch.int32, device="cuda")
+        check(L.syzcov_dev_synth_lens(0x5EED0002, 0, n, a.mean, a.sigma, C.c_void_p(lens.data_ptr()),
+                                      C.c_void_p(torch.cuda.current_stream().cuda_stream)), "synth")
+        lo, span = synth_window(a.log2_space)
+        eng = CorpusEngine(n, 1, 1, lo, span)
+        for _ in range(a.reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            eng.sort_order(lens, n)
+            e.record()
+            torch.cuda.synchronize()
+            print(f"order: {s.elapsed_time(e):.3f} ms  n={n}", flush=True)
+        return
     lo, span = synth_window(a.log2_space)
     off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
                                          log2_space=a.log2_space)
