@@ -102,11 +102,17 @@ def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev_idx = local if world > 1 else 0
+    backend = "nccl"  # RCCL over xGMI
+    ngpu = torch.cuda.device_count()
+    if world > ngpu:
+        # rehearsal of the N-rank path on fewer GPUs (e.g. 2 ranks on the 1-GPU
+        # test box): ranks share devices and the collectives go through gloo
+        dev_idx, backend = local % ngpu, "gloo"
+    dev = torch.device("cuda", dev_idx)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group(backend)
     return world, rank, dev
 
 

@@ -112,6 +112,10 @@ class ShardedEngine(CorpusEngine):
                                    self.L.syzcov_dev_compact_ws_size(n * world)),
                                dtype=torch.uint8, device=self.dev)
 
+    # "exchange": the covered OR, the dictionary, the first-rank MIN merge,
+    # pass 2 and the kept merge (the only phase with collectives besides order)
+    PHASES = ("canon", "order", "minimize", "exchange", "compact", "union", "merge")
+
     def _or_into(self, dst, src):
         check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
               "dev_bitmap_op")
@@ -138,6 +142,7 @@ class ShardedEngine(CorpusEngine):
         items, ranks = local_items(self.order[:N], self.rank, n)
         m = items.numel()
         self.minimize(off, items, ranks, m, do_pass2=False)
+        mark_ev()
         merge_covered(self.covered[:self.nwords], self.world, self._or_into)
         self.build_dict(self.ws2)
         n_ids = int(self.scal[1].item()) & 0xFFFFFFFF
