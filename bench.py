@@ -37,6 +37,7 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED = 0x5EED0002
 SEED_PRIO = 0x5EED0004
+SEED_NEWCOV = 0x5EED0005
 
 
 def parse():
@@ -44,7 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["corpus", "prio"], default="corpus")
+    ap.add_argument("--workload", choices=["corpus", "prio", "newcov"], default="corpus")
+    ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
+    ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
+    ap.add_argument("--history", type=int, default=32,
+                    help="newcov: batches streamed through the check before the bench")
     ap.add_argument("--inputs", type=int, default=1_000_000, help="inputs (programs) per GPU")
     ap.add_argument("--mean", type=int, default=2048)
     ap.add_argument("--sigma", type=int, default=512)
@@ -246,9 +251,150 @@ def bench_prio(args):
     return rank, world, out
 
 
+def cpu_baseline_newcov(args, nrec: int, nhist: int = 16384):
+    """Oracle (sequential fuzzer.go:456-480 loop: Difference x2 + Union per
+    record, C restatement): `nhist` history records bring maxCover up
+    (untimed), then the next `nrec` records are timed."""
+    from oracle import oracle as orc
+    import numpy as np
+    orc.lib()
+    off, pcs = orc.synth_corpus(SEED_NEWCOV, nhist + nrec, args.mean, args.sigma,
+                                args.log2_space)
+    c_off, c_pcs = orc.canonicalize_csr(off, pcs)
+    recs = [c_pcs[c_off[i]:c_off[i + 1]] for i in range(nhist + nrec)]
+    rng = np.random.default_rng(SEED_NEWCOV)
+    cids = rng.integers(0, args.ncalls, size=nhist + nrec)
+    fo, fp = orc.synth_corpus(SEED_NEWCOV ^ 0xF1A4E, 1, 1 << (args.log2_space - 7), 1,
+                              args.log2_space)
+    flakes = orc.canonicalize(fp[:int(fo[1])])
+    _, mc = orc.newcov_batch([[] for _ in range(args.ncalls)], flakes, cids[:nhist],
+                             recs[:nhist])
+    t0 = time.perf_counter()
+    orc.newcov_batch(mc, flakes, cids[nhist:], recs[nhist:])
+    dt = time.perf_counter() - t0
+    npc = int(c_off[-1] - c_off[nhist])
+    return {"value": npc / dt, "unit": "record-PCs/s", "cores": 1, "kind": "port",
+            "sample": f"{nrec} records ({npc} PCs) after {nhist} history records (untimed), "
+                      f"sequential Difference/Difference/Union per record against per-call "
+                      f"maxCover lists, oracle/ C restatement of syz-fuzzer/fuzzer.go:456-480, "
+                      f"1 thread"}
+
+
+def bench_newcov(args):
+    """C5: streaming new-coverage check (syz-fuzzer execute, fuzzer.go:456-480)
+    of batches of call records against the resident per-CallID maxCover and
+    the global flakes set.  Every step is a FRESH batch (W + K distinct batches
+    are generated into HBM up front), so maxCover evolves as in a fuzzer."""
+    import ctypes as C
+    import torch
+    world, rank, dev = init_dist()
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import synth_corpus, synth_window
+    from syzkaller_amd.fuzzer import CoverState
+    L = _lib.lib()
+    s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    lo, span = synth_window(args.log2_space)
+    nrec, nb = args.records, args.warmup + args.steps
+    gen = torch.Generator(device="cpu").manual_seed(SEED_NEWCOV + rank)
+
+    def make_batch(b):
+        first = (rank * (nb + args.history) + b) * nrec
+        off, raw, lens, total = synth_corpus(nrec, SEED_NEWCOV, first=first, mean=args.mean,
+                                             sigma=args.sigma, log2_space=args.log2_space,
+                                             device=dev)
+        new_len = torch.empty(nrec + 1, dtype=torch.int32, device=dev)
+        err = torch.zeros(4, dtype=torch.int32, device=dev)
+        wsz = L.syzcov_dev_canon_split_ws_size(nrec)
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        _lib.check(L.syzcov_dev_canon_split(P(off), P(raw), P(raw), P(new_len), nrec,
+                                            int(lens.max().item()), lo, span, 20, None, None,
+                                            P(err), P(ws), wsz, s()), "canon_split")
+        # compact the canonical prefixes into a record CSR (setup, untimed)
+        nl = new_len[:nrec].to(torch.int64)
+        roff = torch.zeros(nrec + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(nl, 0, out=roff[1:])
+        npc = int(roff[-1].item())
+        seg = torch.repeat_interleave(torch.arange(nrec, device=dev), nl)
+        src = off[:-1][seg] + (torch.arange(npc, device=dev) - roff[:-1][seg])
+        pcs = raw[src].contiguous()
+        cid = torch.randint(0, args.ncalls, (nrec,), generator=gen, dtype=torch.int32).to(dev)
+        return cid, roff, pcs, npc
+
+    st = CoverState(args.ncalls, lo, span)
+    fo, fp, _, _ = synth_corpus(1, SEED_NEWCOV ^ 0xF1A4E, mean=1 << (args.log2_space - 7),
+                                sigma=1, log2_space=args.log2_space, device=dev)
+    import numpy as np
+    st.set_flakes(np.unique(fp[:int(fo[1].item())].cpu().numpy().view(np.uint32)))
+    # a fuzzer that has been running: `history` batches streamed through the
+    # same check before the bench (maxCover near saturation, as in steady state)
+    hist_new = 0
+    for h in range(args.history):
+        cid, roff, pcs, npc = make_batch(nb + h)
+        wsz = L.syzcov_state_newcov_ws_size(nrec, npc)
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        flags = torch.zeros(nrec, dtype=torch.uint8, device=dev)
+        _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc, P(flags),
+                                             None, P(ws), wsz, s()), "state_newcov_dev")
+        hist_new += int(flags.sum().item())
+        del ws, pcs
+    batches = [make_batch(b) for b in range(nb)]
+    max_npc = max(b[3] for b in batches)
+    wsz = L.syzcov_state_newcov_ws_size(nrec, max_npc)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    is_new = torch.zeros(nrec, dtype=torch.uint8, device=dev)
+    stats = torch.zeros(nb, 2, dtype=torch.int32, device=dev)
+    nnew = torch.zeros(nb, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    it = [0]
+
+    def run_step(ev):
+        b = it[0]
+        cid, roff, pcs, npc = batches[b]
+        if ev is not None:
+            ev[0].record()
+        _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc, P(is_new),
+                                             P(stats[b]), P(ws), wsz, s()), "state_newcov_dev")
+        if ev is not None:
+            ev[1].record()
+        nnew[b] = is_new.sum()
+        it[0] += 1
+    dt, phl = timed(run_step, 1, args, world, dev)
+    sc = stats.cpu().tolist()
+    if any(x[0] for x in sc):
+        raise RuntimeError(f"newcov batch rejected: {sc}")
+    timed_pcs = sum(b[3] for b in batches[args.warmup:])
+    value = timed_pcs * world / dt
+    achieved = timed_pcs / args.steps * 4 / (phl[0] * 1e-3) / 1e9
+    out = {
+        "metric": "record-PCs checked/sec, streaming new-coverage check (fuzzer.go:456-480)",
+        "value": value, "unit": "record-PCs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic canonical call records (SURVEY §8d C5), fresh batch every step",
+        "config": {"workload": f"C5: {nrec} call records per batch vs resident maxCover",
+                   "records_per_batch": nrec, "calls": args.ncalls,
+                   "pcs_per_batch": timed_pcs // args.steps, "pc_space": 1 << args.log2_space,
+                   "flakes": f"unique PCs of one synthetic {1 << (args.log2_space - 7)}-PC draw",
+                   "maxcover_bytes": args.ncalls * span // 8,
+                   "history_batches": args.history, "history_new_records": hist_new},
+        "phases_ms": {"newcov": round(phl[0], 4)},
+        "results": {"candidates_per_batch": [x[1] for x in sc[args.warmup:]],
+                    "new_records_per_batch": nnew.cpu().tolist()[args.warmup:],
+                    "records_per_s": nrec * args.steps * world / dt},
+        "roofline": {"bound": "hbm", "kernel": "newcov (cand+hash)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "alg_bytes_per_launch": timed_pcs // args.steps * 4},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, nrec))
+    st.close()
+    return rank, world, out
+
+
 def main():
     args = parse()
-    fn = bench_prio if args.workload == "prio" else bench_corpus
+    fn = {"prio": bench_prio, "newcov": bench_newcov}.get(args.workload, bench_corpus)
     rank, world, out = fn(args)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -88,6 +88,18 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
 int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
                         const int32_t *order, int sort_variant, int32_t *out_idx);
 
+/* Manager.minimizeCorpus (syz-manager/manager.go:504-524): the corpus is
+ * grouped by call (call[i] = any int32 key of RpcInput.Call; corpus order is
+ * kept inside a group, :511-516) and cover.Minimize runs on every group
+ * (:519-523), each with its own Go sort.Sort order (Go >= 1.19 pdqsort,
+ * sort_variant 0, or Go 1.8-1.18 quickSort, 1).  out_idx (capacity n)
+ * receives the kept CORPUS indices, groups in ascending call value, each
+ * group in its Minimize output order; returns their count.  The reference
+ * concatenates groups in Go map order (random), so the shim may reorder
+ * whole groups freely. */
+int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                               size_t n, int sort_variant, int32_t *out_idx);
+
 /* Go sort.Sort(minInputArray) restatement: order[r] for inputs of the given
  * lengths (len(cov) including duplicates).  Computed on the GPU. */
 int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order);
@@ -148,6 +160,18 @@ int64_t syzcov_state_get(syzcov_cover_state st, int call, uint32_t *out, size_t 
  * maxCover as it would.  Returns the number of new records. */
 int64_t syzcov_newcov_batch(syzcov_cover_state st, const int32_t *callid, const uint64_t *rec_off,
                             const uint32_t *rec_pcs, size_t nrec, uint8_t *is_new);
+
+/* Device-resident form of syzcov_newcov_batch for batches already in HBM
+ * (callid, rec_off, pcs, is_new are device pointers; rec_off[0] == 0 and
+ * rec_off[nrec] == npc, the host-side total that sizes the workspace).  Launches
+ * asynchronously on `stream`; stats (device u32[2], nullable) receives
+ * [0] error (1 PC outside the window, 2 call id out of range, 3 unsorted
+ * record: the batch then changes nothing) and [1] the candidates left after
+ * the maxCover/flakes bitmap filter. */
+size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc);
+int syzcov_state_newcov_dev(syzcov_cover_state st, const int32_t *callid, const uint64_t *rec_off,
+                            const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
+                            uint32_t *stats, void *ws, size_t ws_size, void *stream);
 
 /* =================== 2. device-resident launch API ==================== */
 /* All pointers below are device pointers; `stream` is a hipStream_t.
@@ -272,6 +296,14 @@ int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n,
 size_t syzcov_dev_sort_ws_size(size_t n);
 int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order,
                           void *ws, size_t ws_size, void *stream);
+/* Segmented form: an independent Go sort.Sort per group, group g = lens
+ * [goff[g], goff[g+1]) (device u64, ngroups >= 1, every group non-empty,
+ * lengths < 0xFFFFFFFF).  order[i] for i in group g is a grouped index inside
+ * group g, exactly the order Go gives that group as its own slice. */
+size_t syzcov_dev_sort_seg_ws_size(size_t n, size_t ngroups);
+int syzcov_dev_sort_order_segmented(const int64_t *lens, const uint64_t *goff, size_t ngroups,
+                                    size_t n, int sort_variant, int32_t *order, void *ws,
+                                    size_t ws_size, void *stream);
 
 /* Bitmap/byte-map set algebra over a PC window (coalesced, ballot-packed):
  * op 0: dst |= src  (Union)      op 1: dst &= src  (Intersection)

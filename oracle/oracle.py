@@ -130,6 +130,38 @@ def minimize(covers, variant: int = PDQSORT) -> np.ndarray:
     return minimize_csr(off, pcs, variant)
 
 
+def minimize_corpus(calls, covers, variant: int = PDQSORT) -> list:
+    """Manager.minimizeCorpus (syz-manager/manager.go:504-524): group the
+    corpus by call in corpus order (:511-516), cover.Minimize per group
+    (:519-523).  Returns kept corpus indices, groups in ascending call order
+    (the reference walks its `calls` map in Go's random order)."""
+    groups = {}
+    for i, c in enumerate(calls):
+        groups.setdefault(int(c), []).append(i)
+    out = []
+    for c in sorted(groups):
+        members = groups[c]
+        for idx in minimize([covers[i] for i in members], variant):
+            out.append(members[int(idx)])
+    return out
+
+
+def new_inputs(corpus_cover: dict, calls, covers) -> list:
+    """Manager.NewInput (syz-manager/manager.go:596-621), sequentially: an
+    input is accepted iff Difference(cover, corpusCover[call]) is non-empty;
+    then corpusCover[call] = Union(corpusCover[call], cover).  Mutates
+    corpus_cover (call -> sorted uint32 array); returns accepted flags."""
+    acc = []
+    for c, cov in zip(calls, covers):
+        cur = corpus_cover.get(int(c), np.zeros(0, dtype=np.uint32))
+        if len(difference(cov, cur)) == 0:
+            acc.append(False)
+            continue
+        corpus_cover[int(c)] = union(cur, cov)
+        acc.append(True)
+    return acc
+
+
 def union_fold_csr(off, pcs) -> np.ndarray:
     off = np.ascontiguousarray(off, dtype=np.uint64)
     pcs = _u32(pcs)

@@ -46,6 +46,7 @@ _SIGS = {
     "syzcov_intersection": (i64, [p_, sz, p_, sz, p_]),
     "syzcov_minimize": (i64, [p_, p_, sz, p_, C.c_int, p_]),
     "syzcov_sort_order": (C.c_int, [p_, sz, C.c_int, p_]),
+    "syzcov_minimize_corpus": (i64, [p_, p_, p_, sz, C.c_int, p_]),
     "syzcov_union_all": (i64, [p_, p_, sz, p_]),
     "syzcov_calculate_priorities": (C.c_int, [p_, p_, sz, C.c_int, C.c_int, p_, p_, p_]),
     "syzcov_static_priorities": (C.c_int, [p_, p_, p_, sz, p_, p_, p_, C.c_int, p_]),
@@ -58,6 +59,8 @@ _SIGS = {
     "syzcov_state_set_flakes": (C.c_int, [u64, p_, sz]),
     "syzcov_state_get": (i64, [u64, C.c_int, p_, sz]),
     "syzcov_newcov_batch": (i64, [u64, p_, p_, p_, sz, p_]),
+    "syzcov_state_newcov_ws_size": (sz, [sz, u64]),
+    "syzcov_state_newcov_dev": (C.c_int, [u64, p_, p_, p_, sz, u64, p_, p_, p_, sz, p_]),
     # device tier
     "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
     "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
@@ -82,6 +85,8 @@ _SIGS = {
     "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),
     "syzcov_dev_sort_ws_size": (sz, [sz]),
     "syzcov_dev_sort_order": (C.c_int, [p_, sz, C.c_int, p_, p_, sz, p_]),
+    "syzcov_dev_sort_seg_ws_size": (sz, [sz, sz]),
+    "syzcov_dev_sort_order_segmented": (C.c_int, [p_, p_, sz, sz, C.c_int, p_, p_, sz, p_]),
     "syzcov_dev_bytemap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),
     "syzcov_dev_synth_lens": (C.c_int, [u64, u64, sz, u32, u32, p_, p_]),
     "syzcov_dev_synth_pcs": (C.c_int, [u64, u64, sz, p_, u32, C.c_int, p_, p_]),

@@ -130,3 +130,21 @@ def UnionAllCSR(off, pcs) -> np.ndarray:
 def UnionAll(corpus) -> np.ndarray:
     """The `total = Union(total, cov)` fold over a corpus, in one pass."""
     return UnionAllCSR(*to_csr(corpus))
+
+
+def MinimizeCorpus(calls, corpus, variant: int = 0) -> list:
+    """Manager.minimizeCorpus's grouping + per-call cover.Minimize
+    (syz-manager/manager.go:504-524) in one engine call: kept corpus indices,
+    groups in ascending call value (the reference's group order is Go map
+    order, i.e. random), each group in its Minimize output order."""
+    off, pcs = to_csr(corpus)
+    n = off.size - 1
+    if n <= 0:
+        return []
+    cid = np.ascontiguousarray(np.asarray(calls, dtype=np.int32))
+    if cid.size != n:
+        raise ValueError("one call id per corpus input")
+    out = np.empty(n, dtype=np.int32)
+    k = check(lib().syzcov_minimize_corpus(_ptr(cid), _ptr(off), _ptr(pcs), n, variant,
+                                           _ptr(out)), "MinimizeCorpus")
+    return out[:k].tolist()

@@ -214,6 +214,13 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
 // ------------------------------------------------------------------ corpus
 namespace syz {
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
+int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
+                          uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
+                          hipStream_t s);
+int minimize_groups_batch(const uint64_t *off, const uint32_t *pcs, const int32_t *order_c,
+                          const uint32_t *rank_grp, uint32_t r0, uint32_t r1, uint32_t g0,
+                          uint32_t nids, const uint64_t *tab, uint32_t pc_lo, int32_t *first,
+                          size_t first_n, uint8_t *cand, uint8_t *kept, hipStream_t s);
 
 // Stage a CSR corpus and build its dense dictionary.  Fills device pointers.
 struct CorpusDev {
@@ -379,6 +386,86 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
         }
         rc = (int)k;
     } while (0);
+    hipStreamSynchronize(c->s);
+    free_all(owned);
+    return rc;
+}
+
+// Manager.minimizeCorpus (syz-manager/manager.go:504-524): group the corpus by
+// call (corpus order inside a group, :511-516), cover.Minimize each group
+// (:519-523).  The kept corpus indices come out grouped by ascending call
+// value; the reference walks its groups in Go map order, which is random, so
+// every group order is one the reference can produce.
+static int64_t minimize_corpus_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
+                                    const uint32_t *pcs, size_t n, int sort_variant,
+                                    int32_t *out_idx, std::vector<void *> &owned) {
+    // host grouping: stable by call value (the reference's append order)
+    std::vector<int32_t> perm(n);
+    for (size_t i = 0; i < n; i++) perm[i] = (int32_t)i;
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](int32_t a, int32_t b) { return call[a] < call[b]; });
+    std::vector<uint64_t> goff;
+    std::vector<int64_t> lens(n);
+    for (size_t i = 0; i < n; i++) {
+        if (i == 0 || call[perm[i]] != call[perm[i - 1]]) goff.push_back(i);
+        lens[i] = (int64_t)(offsets[perm[i] + 1] - offsets[perm[i]]);
+        if (lens[i] >= 0xFFFFFFFFll) return SYZCOV_ERANGE;
+    }
+    goff.push_back(n);
+    const size_t G = goff.size() - 1;
+    CorpusDev cd;
+    RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    const uint32_t nids = std::max<uint32_t>(cd.n_ids, 1);
+    // first-cover slabs for as many groups as fit 1 GiB (at least one)
+    const size_t per = (size_t)nids * 4;
+    size_t gb = std::max<size_t>(1, std::min<size_t>(G, (1ull << 30) / per));
+    Plan p;
+    size_t i_len = p.add(n * 8), i_goff = p.add((G + 1) * 8), i_perm = p.add(n * 4),
+           i_ordg = p.add(n * 4), i_ordc = p.add(n * 4), i_rg = p.add(n * 4),
+           i_first = p.add(gb * per), i_cand = p.add(n), i_kept = p.add(n), i_out = p.add(n * 4),
+           i_cnt = p.add(4),
+           i_ws = p.add(std::max(syzcov_dev_compact_ws_size(n), syzcov_dev_sort_seg_ws_size(n, G)));
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_len], lens.data(), n * 8, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_goff], goff.data(), (G + 1) * 8, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_perm], perm.data(), n * 4, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_sort_order_segmented((int64_t *)b[i_len], (uint64_t *)b[i_goff], G, n,
+                                       sort_variant, (int32_t *)b[i_ordg], b[i_ws], p.sizes[i_ws],
+                                       c->s));
+    RC(minimize_groups_order((int32_t *)b[i_ordg], (int32_t *)b[i_perm], (uint64_t *)b[i_goff],
+                             (uint32_t)G, (uint32_t)n, (int32_t *)b[i_ordc], (uint32_t *)b[i_rg],
+                             c->s));
+    CK(hipMemsetAsync(b[i_kept], 0, n, c->s));
+    for (size_t g0 = 0; g0 < G; g0 += gb) {
+        const size_t g1 = std::min(G, g0 + gb);
+        RC(minimize_groups_batch(cd.off, cd.pcs, (int32_t *)b[i_ordc], (uint32_t *)b[i_rg],
+                                 (uint32_t)goff[g0], (uint32_t)goff[g1], (uint32_t)g0, nids, cd.tab,
+                                 cd.pc_lo, (int32_t *)b[i_first], (g1 - g0) * nids, b[i_cand],
+                                 b[i_kept], c->s));
+    }
+    RC(syzcov_dev_compact_kept(b[i_kept], (int32_t *)b[i_ordc], n, (int32_t *)b[i_out],
+                               (uint32_t *)b[i_cnt], b[i_ws], c->s));
+    uint32_t k = 0;
+    CK(hipMemcpyAsync(&k, b[i_cnt], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (k) {
+        CK(hipMemcpyAsync(out_idx, b[i_out], (size_t)k * 4, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    return (int64_t)k;
+}
+
+int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                               size_t n, int sort_variant, int32_t *out_idx) {
+    if (n == 0) return 0;
+    if (!call || !offsets || !out_idx || n > 0x7FFFFFFF || (sort_variant != 0 && sort_variant != 1))
+        return SYZCOV_EINVAL;
+    if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    std::vector<void *> owned;
+    const int64_t rc = minimize_corpus_impl(c, call, offsets, pcs, n, sort_variant, out_idx, owned);
     hipStreamSynchronize(c->s);
     free_all(owned);
     return rc;

@@ -120,6 +120,58 @@ __global__ void seed_kernel(uint32_t n, Ctl c) {
     push_seg(c, Seg{0, (int)n, gocore::bits_len(n), 3});
 }
 
+// Segmented form (one independent Go sort.Sort per group, as
+// manager.minimizeCorpus runs cover.Minimize per call, manager.go:516-524):
+// group g occupies positions [goff[g] + g, goff[g+1] + g) and the position
+// after it holds a GAP key 0xFFFFFFFF.  pdqsort reads outside its segment
+// only at a-1 (`a > 0 && !less(data[a-1], pivot)`, the partitionEqual test):
+// at a group start that reads the gap, and less(gap, pivot) is true for every
+// real length (< 0xFFFFFFFF), which is exactly the reference's a == 0 branch
+// of a separate slice.  Gaps are never inside a segment, so never move.
+__global__ void seg_init_kernel(const int64_t *__restrict__ lens, const uint64_t *__restrict__ goff,
+                                uint32_t ngroups, uint32_t *__restrict__ K,
+                                int32_t *__restrict__ I, uint32_t *__restrict__ err) {
+    const uint32_t n = (uint32_t)goff[ngroups];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = ngroups;  // group of i: last g with goff[g] <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (goff[mid] <= i) lo = mid; else hi = mid;
+        }
+        const int64_t l = lens[i];
+        if (l < 0 || l >= 0xFFFFFFFFll) *err = 1u;
+        K[i + lo] = (uint32_t)l;
+        I[i + lo] = (int32_t)i;
+        if (i + 1 == goff[lo + 1] && lo + 1 < ngroups) {
+            K[i + lo + 1] = 0xFFFFFFFFu;
+            I[i + lo + 1] = -1;
+        }
+    }
+}
+
+__global__ void seg_seed_kernel(const uint64_t *__restrict__ goff, uint32_t ngroups, Ctl c) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += gridDim.x * blockDim.x) {
+        const uint32_t a = (uint32_t)goff[g] + g, b = (uint32_t)goff[g + 1] + g;
+        push_seg(c, Seg{(int)a, (int)b, gocore::bits_len(b - a), 3});
+    }
+}
+
+// order[p - g] = I[p] for every non-gap position p of group g (an element
+// never leaves its group, so g is the group of the grouped index I[p])
+__global__ void seg_gather_kernel(const int32_t *__restrict__ I, const uint64_t *__restrict__ goff,
+                                  uint32_t ngroups, uint32_t npos, int32_t *__restrict__ order) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npos; p += gridDim.x * blockDim.x) {
+        const int32_t v = I[p];
+        if (v < 0) continue;
+        uint32_t lo = 0, hi = ngroups;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (goff[mid] <= (uint64_t)v) lo = mid; else hi = mid;
+        }
+        order[p - lo] = v;
+    }
+}
+
 // one lane per segment: control steps of one pdqsort loop iteration
 __global__ void plan_kernel(Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
                             uint32_t *__restrict__ K, int32_t *__restrict__ I, Ctl c) {
@@ -660,9 +712,9 @@ struct SortWs {
     uint32_t seg_cap, small_cap, cc_stride;
 };
 
-static size_t ws_layout(size_t n, SortWs *w, uint8_t *base) {
+static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
     const uint32_t seg_cap = (uint32_t)(2 * (n / SMALL) + 16);
-    const uint32_t small_cap = (uint32_t)(2 * (n / SMALL + 1) * 64 + 64);
+    const uint32_t small_cap = (uint32_t)(2 * (n / SMALL + 1) * 64 + 64 + ngroups);
     const uint32_t cc_stride = (uint32_t)(n / CH + 2);
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -692,46 +744,52 @@ static size_t ws_layout(size_t n, SortWs *w, uint8_t *base) {
     return o;
 }
 
-extern "C" size_t syzcov_dev_sort_ws_size(size_t n) { return ws_layout(n ? n : 1, nullptr, nullptr); }
+extern "C" size_t syzcov_dev_sort_ws_size(size_t n) {
+    return ws_layout(n ? n : 1, 0, nullptr, nullptr);
+}
 
-static int legacy_host(const int64_t *lens, size_t n, int32_t *order, hipStream_t s) {
+extern "C" size_t syzcov_dev_sort_seg_ws_size(size_t n, size_t ngroups) {
+    return ws_layout((n ? n : 1) + ngroups, ngroups, nullptr, nullptr);
+}
+
+// Go 1.8-1.18 quickSort of lens[a, b) into order[a, b) (values a..b-1)
+static void legacy_range(const int64_t *hl, int32_t *ho, long a, long b) {
+    for (long i = a; i < b; i++) ho[i] = (int32_t)(i - a);  // HArr indexes relative to its base
+    HArr d{ho + a, hl + a};
+    int depth = 0;
+    for (long i = b - a; i > 0; i >>= 1) depth++;
+    quick(d, 0, b - a, 2 * depth);
+    for (long i = a; i < b; i++) ho[i] += (int32_t)a;
+}
+
+static int legacy_host(const int64_t *lens, size_t n, const uint64_t *goff, size_t ngroups,
+                       int32_t *order, hipStream_t s) {
     std::vector<int64_t> hl(n);
     std::vector<int32_t> ho(n);
+    std::vector<uint64_t> hg(ngroups + 1);
     SYZ_HIP(hipMemcpyAsync(hl.data(), lens, n * 8, hipMemcpyDeviceToHost, s));
+    if (goff) SYZ_HIP(hipMemcpyAsync(hg.data(), goff, (ngroups + 1) * 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
-    for (size_t i = 0; i < n; i++) ho[i] = (int32_t)i;
-    HArr d{ho.data(), hl.data()};
-    int depth = 0;
-    for (long i = (long)n; i > 0; i >>= 1) depth++;
-    quick(d, 0, (long)n, 2 * depth);
+    if (!goff) {
+        hg[0] = 0;
+        hg[1] = n;
+    }
+    for (size_t g = 0; g < ngroups; g++) legacy_range(hl.data(), ho.data(), (long)hg[g], (long)hg[g + 1]);
     SYZ_HIP(hipMemcpyAsync(order, ho.data(), n * 4, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipStreamSynchronize(s));
     return 0;
 }
 
-extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
-                                     int32_t *order, void *ws, size_t ws_size, void *stream) {
-    if (n == 0) return 0;
-    if (!lens || !order || (sort_variant != 0 && sort_variant != 1) || n > 0x7FFFFFFF)
-        return SYZCOV_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
-    if (sort_variant == 1) return legacy_host(lens, n, order, s);
-    if (!ws || ws_size < syzcov_dev_sort_ws_size(n)) return SYZCOV_EINVAL;
-    SortWs w;
-    ws_layout(n, &w, (uint8_t *)ws);
-    SYZ_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
-    hipLaunchKernelGGL(init_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, lens, (uint32_t)n,
-                       w.K, w.I, w.ctl);
+// Level-synchronous pdqsort rounds over the segments already seeded into
+// segA / small (ctl[1], ctl[3]); the result is left in w.I.
+static int run_rounds(SortWs &w, hipStream_t s) {
     Seg *cur = w.segA, *nxt = w.segB;
     uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
-    Ctl c{cur, ccount, cmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
-    if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
-    SYZ_LAUNCH_CHECK();
     uint32_t h[6];
     SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
     uint32_t ncur = h[1], maxlen = h[4];
-    for (int round = 0; ncur > 0; round++) {
+    for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
         // the children of this round go to nxt
         SYZ_HIP(hipMemsetAsync(ncount, 0, 4, s));
@@ -756,7 +814,6 @@ extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_var
         SYZ_LAUNCH_CHECK();
         SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
         SYZ_HIP(hipStreamSynchronize(s));
-        if (h[0]) break;
         ncur = h[ncount - w.ctl];
         maxlen = h[nmax - w.ctl];
         std::swap(cur, nxt);
@@ -774,6 +831,54 @@ extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_var
         set_error("device sort: internal error %u", h[0]);
         return h[0] == 1 ? SYZCOV_EINVAL : SYZCOV_EHIP;
     }
+    return 0;
+}
+
+extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
+                                     int32_t *order, void *ws, size_t ws_size, void *stream) {
+    if (n == 0) return 0;
+    if (!lens || !order || (sort_variant != 0 && sort_variant != 1) || n > 0x7FFFFFFF)
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (sort_variant == 1) return legacy_host(lens, n, nullptr, 1, order, s);
+    if (!ws || ws_size < syzcov_dev_sort_ws_size(n)) return SYZCOV_EINVAL;
+    SortWs w;
+    ws_layout(n, 0, &w, (uint8_t *)ws);
+    SYZ_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
+    hipLaunchKernelGGL(init_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, lens, (uint32_t)n,
+                       w.K, w.I, w.ctl);
+    Ctl c{w.segA, w.ctl + 1, w.ctl + 4, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
+    if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
+    SYZ_LAUNCH_CHECK();
+    if (int rc = run_rounds(w, s)) return rc;
     SYZ_HIP(hipMemcpyAsync(order, w.I, n * 4, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+extern "C" int syzcov_dev_sort_order_segmented(const int64_t *lens, const uint64_t *goff,
+                                               size_t ngroups, size_t n, int sort_variant,
+                                               int32_t *order, void *ws, size_t ws_size,
+                                               void *stream) {
+    if (n == 0) return 0;
+    if (!lens || !goff || !order || ngroups == 0 || (sort_variant != 0 && sort_variant != 1) ||
+        n + ngroups > 0x7FFFFFFF)
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (sort_variant == 1) return legacy_host(lens, n, goff, ngroups, order, s);
+    if (!ws || ws_size < syzcov_dev_sort_seg_ws_size(n, ngroups)) return SYZCOV_EINVAL;
+    const size_t npos = n + ngroups - 1;
+    SortWs w;
+    ws_layout(npos + 1, ngroups, &w, (uint8_t *)ws);
+    SYZ_HIP(hipMemsetAsync(w.ctl, 0, 64, s));
+    hipLaunchKernelGGL(seg_init_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, lens, goff,
+                       (uint32_t)ngroups, w.K, w.I, w.ctl);
+    Ctl c{w.segA, w.ctl + 1, w.ctl + 4, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
+    hipLaunchKernelGGL(seg_seed_kernel, dim3(grid_for(ngroups, 256, 1024)), dim3(256), 0, s, goff,
+                       (uint32_t)ngroups, c);
+    SYZ_LAUNCH_CHECK();
+    if (int rc = run_rounds(w, s)) return rc;
+    hipLaunchKernelGGL(seg_gather_kernel, dim3(grid_for(npos, 256, 8192)), dim3(256), 0, s,
+                       (const int32_t *)w.I, goff, (uint32_t)ngroups, (uint32_t)npos, order);
+    SYZ_LAUNCH_CHECK();
     return 0;
 }

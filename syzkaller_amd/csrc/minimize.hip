@@ -118,6 +118,72 @@ __global__ __launch_bounds__(CMP_THREADS) void compact_scatter_kernel(
         if (base + q < n && f[base + q]) out[p++] = order ? order[base + q] : (int32_t)(base + q);
 }
 
+// ---------------------------------------------------------------------
+// Manager.minimizeCorpus (syz-manager/manager.go:504-524): cover.Minimize
+// runs once per call group, so first-cover is keyed by (group, pc).  Ranks
+// are grouped (group g owns ranks [goff[g], goff[g+1]), each group in its own
+// Go sort.Sort order) and a batch of groups [g0, g1) gets a first-cover slab
+// first[(g - g0) * nids + id].  ord_g[j] is the grouped index of rank j and
+// perm[] maps grouped indices to corpus indices.
+__global__ void grp_order_kernel(const int32_t *__restrict__ ord_g, const int32_t *__restrict__ perm,
+                                 const uint64_t *__restrict__ goff, uint32_t ngroups, uint32_t n,
+                                 int32_t *__restrict__ order_c, uint32_t *__restrict__ rank_grp) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        order_c[j] = perm[ord_g[j]];
+        uint32_t lo = 0, hi = ngroups;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (goff[mid] <= j) lo = mid; else hi = mid;
+        }
+        rank_grp[j] = lo;
+    }
+}
+
+__global__ __launch_bounds__(MINI_THREADS) void grp_pass1_kernel(
+    const uint64_t *__restrict__ off, const uint32_t *__restrict__ pcs,
+    const int32_t *__restrict__ order, const uint32_t *__restrict__ rank_grp, uint32_t r0,
+    uint32_t r1, uint32_t g0, uint32_t nids, const uint64_t *__restrict__ tab, uint32_t pc_lo,
+    int32_t *__restrict__ first, uint8_t *__restrict__ cand) {
+    for (uint32_t j = r0 + blockIdx.x; j < r1; j += gridDim.x) {
+        const int32_t idx = order[j];
+        int32_t *fg = first + (size_t)(rank_grp[j] - g0) * nids;
+        const int32_t r = (int32_t)j;
+        const uint64_t b = off[idx];
+        const uint32_t l = (uint32_t)(off[idx + 1] - b);
+        bool won = false;
+        for (uint32_t k = threadIdx.x; k < l; k += MINI_THREADS) {
+            const uint32_t id = dense_id(tab, pcs[b + k], pc_lo);
+            if (fg[id] > r) won |= atomicMin(&fg[id], r) > r;
+        }
+        won = __syncthreads_or(won);
+        if (threadIdx.x == 0) cand[j] = won ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(MINI_THREADS) void grp_pass2_kernel(
+    const uint64_t *__restrict__ off, const uint32_t *__restrict__ pcs,
+    const int32_t *__restrict__ order, const uint32_t *__restrict__ rank_grp, uint32_t r0,
+    uint32_t r1, uint32_t g0, uint32_t nids, const uint64_t *__restrict__ tab, uint32_t pc_lo,
+    const int32_t *__restrict__ first, const uint8_t *__restrict__ cand, uint8_t *__restrict__ kept) {
+    for (uint32_t j = r0 + blockIdx.x; j < r1; j += gridDim.x) {
+        if (!cand[j]) continue;
+        const int32_t idx = order[j];
+        const int32_t *fg = first + (size_t)(rank_grp[j] - g0) * nids;
+        const uint64_t b = off[idx];
+        const uint32_t l = (uint32_t)(off[idx + 1] - b);
+        bool found = false;
+        for (uint32_t k0 = 0; k0 < l; k0 += MINI_THREADS) {
+            const uint32_t k = k0 + threadIdx.x;
+            const bool f = k < l && fg[dense_id(tab, pcs[b + k], pc_lo)] == (int32_t)j;
+            if (__syncthreads_or(f)) {
+                found = true;
+                break;
+            }
+        }
+        if (threadIdx.x == 0 && found) kept[j] = 1;
+    }
+}
+
 static unsigned mini_grid(size_t n) {
     // enough workgroups to fill 256 CUs several times over while keeping the
     // in-flight rank window narrow (read-before-atomic filtering)
@@ -183,3 +249,33 @@ extern "C" int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order
     SYZ_LAUNCH_CHECK();
     return 0;
 }
+
+namespace syz {
+// Grouped Minimize over ranks [r0, r1) whose groups are [g0, g1); `first`
+// holds (g1 - g0) * nids entries.  kept[] must be zeroed by the caller.
+// order_c[j] = corpus index of rank j, rank_grp[j] = its group
+int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
+                          uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(grp_order_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, ord_g, perm,
+                       goff_dev, ngroups, n, order_c, rank_grp);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+int minimize_groups_batch(const uint64_t *off, const uint32_t *pcs, const int32_t *order_c,
+                          const uint32_t *rank_grp, uint32_t r0, uint32_t r1, uint32_t g0,
+                          uint32_t nids, const uint64_t *tab, uint32_t pc_lo, int32_t *first,
+                          size_t first_n, uint8_t *cand, uint8_t *kept, hipStream_t s) {
+    if (r1 <= r0) return 0;
+    SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)first, 0x7FFFFFFF, first_n, s));
+    const unsigned g = mini_grid(r1 - r0);
+    hipLaunchKernelGGL(grp_pass1_kernel, dim3(g), dim3(MINI_THREADS), 0, s, off, pcs, order_c,
+                       rank_grp, r0, r1, g0, nids, tab, pc_lo, first, cand);
+    hipLaunchKernelGGL(grp_pass2_kernel, dim3(g), dim3(MINI_THREADS), 0, s, off, pcs, order_c,
+                       rank_grp, r0, r1, g0, nids, tab, pc_lo, (const int32_t *)first,
+                       (const uint8_t *)cand, kept);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+}  // namespace syz

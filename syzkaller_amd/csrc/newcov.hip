@@ -10,10 +10,10 @@
 //              record j < k with c_j = c_k holds pc,
 //   M1[c]  =  M0[c] ∪ (∪_{j: c_j = c} cov_j \ F),
 // i.e. first-cover on the key (CallID, pc) after masking F ∪ M0.  Pass 1
-// tests every PC against the cache-resident bitmaps and compacts the
-// survivors (few once maxCover saturates); a hash table keyed by
+// tests every PC against the bitmaps and compacts each record's survivors
+// into its own slots (few once maxCover saturates); a hash table keyed by
 // (CallID, pc) takes an atomicMin of the record index; pass 2 marks a record
-// new iff it owns one of its keys; the survivors are OR-ed into maxCover.
+// new iff it owns one of its keys and ORs the owned keys into maxCover.
 #include "common.h"
 
 namespace syz {
@@ -23,86 +23,148 @@ __device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64
 }
 
 constexpr int NC_THREADS = 256;
+constexpr int NC_WPB = NC_THREADS / 64;
+constexpr int NC_U = 8;  // rows of 64 PCs in flight per wave
 
-// per record: count candidates
-__global__ __launch_bounds__(NC_THREADS) void newcov_count_kernel(
-    const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
-    const uint32_t *__restrict__ pcs, uint32_t nrec, const uint32_t *__restrict__ maxcov,
-    uint64_t words_per_call, const uint32_t *__restrict__ flakes, uint32_t pc_lo,
-    uint64_t pc_span, int ncalls, uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ err) {
-    __shared__ uint32_t tmp[NC_THREADS / 64 + 1];
-    for (uint32_t k = blockIdx.x; k < nrec; k += gridDim.x) {
-        const int c = callid[k];
-        const uint64_t b = rec_off[k], n = rec_off[k + 1] - b;
-        uint32_t cnt = 0;
-        if (c < 0 || c >= ncalls) {
-            if (threadIdx.x == 0) *err = 2u;
-        } else {
-            const uint32_t *M = maxcov + (uint64_t)c * words_per_call;
-            for (uint64_t q = threadIdx.x; q < n; q += NC_THREADS) {
-                const uint32_t pc = pcs[b + q];
-                const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
-                if (pc < pc_lo || o >= pc_span) {
-                    *err = 1u;
-                    continue;
-                }
-                if (q > 0 && pcs[b + q - 1] > pc) *err = 3u;  // not sorted
-                cnt += !bit_test(flakes, o) && !bit_test(M, o);
-            }
-        }
-        uint32_t total;
-        block_excl_scan<NC_THREADS>(cnt, tmp, &total);
-        if (threadIdx.x == 0) rec_cnt[k] = total;
-    }
-}
+// Records grouped by CallID (counting sort in one workgroup): the candidate
+// pass walks them in this order so the records of one call run together on
+// one XCD and share its L2 copy of maxCover[call] (the probes of one record
+// touch ~2k random lines of an 8 MB bitmap; a call's records hit mostly the
+// same hot lines).  perm[] is only a visiting order: ownership still uses
+// the batch index k.
+constexpr int GRP_MAX_CALLS = 16384;
 
-// exclusive scan of rec_cnt in one workgroup; total -> *tot
-__global__ __launch_bounds__(1024) void newcov_scan_kernel(uint32_t *__restrict__ a, uint32_t n,
-                                                            uint32_t *__restrict__ tot) {
+__global__ __launch_bounds__(1024) void newcov_group_kernel(const int32_t *__restrict__ callid,
+                                                             uint32_t nrec, int ncalls,
+                                                             uint32_t *__restrict__ perm) {
+    __shared__ uint32_t h[GRP_MAX_CALLS];
     __shared__ uint32_t tmp[1024 / 64 + 1];
-    uint32_t carry = 0;
-    for (uint32_t c = 0; c < n; c += 1024) {
-        const uint32_t i = c + threadIdx.x;
-        const uint32_t v = i < n ? a[i] : 0u;
+    const uint32_t t = threadIdx.x;
+    if (ncalls > GRP_MAX_CALLS) {
+        for (uint32_t k = t; k < nrec; k += 1024) perm[k] = k;
+        return;
+    }
+    for (int c = t; c < ncalls; c += 1024) h[c] = 0;
+    __syncthreads();
+    for (uint32_t k = t; k < nrec; k += 1024) {
+        const int c = callid[k];
+        if (c >= 0 && c < ncalls) atomicAdd(&h[c], 1u);
+    }
+    __syncthreads();
+    uint32_t carry = 0;  // exclusive scan; bad call ids go last
+    for (int c0 = 0; c0 < ncalls; c0 += 1024) {
+        const int c = c0 + (int)t;
+        const uint32_t v = c < ncalls ? h[c] : 0u;
         uint32_t total;
         const uint32_t p = block_excl_scan<1024>(v, tmp, &total);
-        if (i < n) a[i] = carry + p;
+        __syncthreads();
+        if (c < ncalls) h[c] = carry + p;
         carry += total;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) *tot = carry;
+    __shared__ uint32_t bad_pos;
+    if (t == 0) bad_pos = carry;
+    __syncthreads();
+    for (uint32_t k = t; k < nrec; k += 1024) {
+        const int c = callid[k];
+        const uint32_t pos = (c >= 0 && c < ncalls) ? atomicAdd(&h[c], 1u) : atomicAdd(&bad_pos, 1u);
+        perm[pos] = k;
+    }
 }
 
-// per record: write candidate (key, record) pairs at rec_base[k] + rank
-__global__ __launch_bounds__(NC_THREADS) void newcov_compact_kernel(
+// stats[0] = error (1 window, 2 call id, 3 unsorted), stats[1] = candidates.
+// One WAVEFRONT per record: coalesced 64-PC rows, both bitmap probes per PC,
+// ballot compaction of the survivors into the record's OWN slots of cpc
+// (cpc is indexed like pcs), so no global atomics per row; one atomic per
+// wave for the batch total.  Once maxCover saturates (a fuzzer's steady
+// state) almost every record has zero survivors.
+__global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
     const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
     const uint32_t *__restrict__ pcs, uint32_t nrec, const uint32_t *__restrict__ maxcov,
     uint64_t words_per_call, const uint32_t *__restrict__ flakes, uint32_t pc_lo,
-    uint64_t pc_span, int ncalls, const uint32_t *__restrict__ rec_base,
-    uint64_t *__restrict__ ckey, uint32_t *__restrict__ crec) {
-    __shared__ uint32_t tmp[NC_THREADS / 64 + 1];
-    for (uint32_t k = blockIdx.x; k < nrec; k += gridDim.x) {
+    uint64_t pc_span, int ncalls, const uint32_t *__restrict__ perm, uint8_t *__restrict__ is_new,
+    uint32_t *__restrict__ cpc, uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ stats) {
+    const uint32_t l = __lane_id();
+    const uint64_t lt = (1ull << l) - 1ull;
+    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
+    // the workgroups of XCD x (blockIdx % 8 == x) take the x-th eighth of
+    // the call-grouped records
+    const uint32_t x = blockIdx.x & 7, nbx = gridDim.x >> 3;
+    const uint32_t j0 = (uint32_t)((uint64_t)nrec * x / 8), j1 = (uint32_t)((uint64_t)nrec * (x + 1) / 8);
+    const uint32_t nw = nbx * NC_WPB;
+    uint32_t wave_tot = 0;
+    for (uint32_t j = j0 + (blockIdx.x >> 3) * NC_WPB + (threadIdx.x >> 6); j < j1; j += nw) {
+        const uint32_t k = perm[j];
         const int c = callid[k];
-        if (c < 0 || c >= ncalls) continue;  // block-uniform
+        if (l == 0) is_new[k] = 0;
+        if (c < 0 || c >= ncalls) {
+            if (l == 0) {
+                stats[0] = 2u;
+                rec_cnt[k] = 0;
+            }
+            continue;
+        }
         const uint32_t *M = maxcov + (uint64_t)c * words_per_call;
         const uint64_t b = rec_off[k], n = rec_off[k + 1] - b;
-        uint32_t wpos = rec_base[k];
-        for (uint64_t q0 = 0; q0 < n; q0 += NC_THREADS) {
-            const uint64_t q = q0 + threadIdx.x;
-            bool cand = false;
-            uint32_t pc = 0;
-            if (q < n) {
-                pc = pcs[b + q];
-                const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
-                cand = pc >= pc_lo && o < pc_span && !bit_test(flakes, o) && !bit_test(M, o);
+        uint32_t bad = 0, cnt = 0, carry = 0;
+        // NC_U rows per step: all their loads and maxCover probes in flight together
+        for (uint64_t q0 = 0; q0 < n; q0 += 64 * NC_U) {
+            uint32_t pc[NC_U], w[NC_U];
+            bool ok[NC_U];
+#pragma unroll
+            for (int u = 0; u < NC_U; u++) {
+                const uint64_t q = q0 + u * 64 + l;
+                pc[u] = q < n ? pcs[b + q] : 0u;
             }
-            uint32_t total;
-            const uint32_t p = block_excl_scan<NC_THREADS>(cand ? 1u : 0u, tmp, &total);
-            if (cand) {
-                ckey[wpos + p] = ((uint64_t)(uint32_t)c << 32) | pc;
-                crec[wpos + p] = k;
+#pragma unroll
+            for (int u = 0; u < NC_U; u++) {
+                const uint64_t q = q0 + u * 64 + l;
+                const uint64_t o = (uint64_t)(uint32_t)(pc[u] - pc_lo);
+                const bool inw = pc[u] >= pc_lo && o < pc_span;
+                ok[u] = q < n && inw;
+                bad |= (uint32_t)(q < n && !inw);
+                w[u] = ok[u] ? M[o >> 5] : 0xFFFFFFFFu;
             }
-            wpos += total;
+#pragma unroll
+            for (int u = 0; u < NC_U; u++) {
+                const uint64_t q = q0 + u * 64 + l;
+                // sortedness: the previous PC is lane l-1 of this row, or the
+                // last PC of the previous row for lane 0
+                uint32_t prev = __shfl_up(pc[u], 1, 64);
+                if (l == 0) prev = carry;
+                carry = __builtin_amdgcn_readlane(pc[u], 63);
+                if (q < n && q > 0 && prev > pc[u]) bad |= 2u;
+                const uint32_t o = pc[u] - pc_lo;
+                // maxCover first: once it saturates, flakes are rarely probed
+                const bool cand = ok[u] && !((w[u] >> (o & 31)) & 1u) && !bit_test(flakes, o);
+                const uint64_t m = __ballot(cand);
+                if (cand) cpc[b + cnt + (uint32_t)__popcll(m & lt)] = pc[u];
+                cnt += (uint32_t)__popcll(m);
+            }
         }
+        if (bad) stats[0] = (bad & 1u) ? 1u : 3u;
+        if (l == 0) rec_cnt[k] = cnt;
+        wave_tot += cnt;
+    }
+    if (l == 0 && wave_tot) atomicAdd(&stats[1], wave_tot);
+}
+
+// table capacity for ncand candidates (power of two, load <= 1/2)
+__device__ __forceinline__ uint64_t hash_cap(uint32_t ncand) {
+    uint64_t cap = 1024;
+    while (cap < 2ull * ncand) cap <<= 1;
+    return cap;
+}
+
+__global__ void hash_clear_kernel(const uint32_t *__restrict__ stats,
+                                  unsigned long long *__restrict__ hkey,
+                                  uint32_t *__restrict__ hval) {
+    if (stats[0] || !stats[1]) return;  // rejected batch / nothing to insert
+    const uint64_t cap = hash_cap(stats[1]);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        hkey[i] = ~0ull;
+        hval[i] = 0xFFFFFFFFu;
     }
 }
 
@@ -117,40 +179,64 @@ __device__ __forceinline__ uint64_t hash64(uint64_t k) {
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
 
-__global__ void newcov_insert_kernel(const uint64_t *__restrict__ ckey,
-                                     const uint32_t *__restrict__ crec, uint32_t ncand,
-                                     unsigned long long *__restrict__ hkey,
-                                     uint32_t *__restrict__ hval, uint64_t mask) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncand;
-         i += gridDim.x * blockDim.x) {
-        const uint64_t key = ckey[i];
-        uint64_t h = hash64(key) & mask;
-        for (;;) {
-            const unsigned long long prev = atomicCAS(&hkey[h], EMPTY_KEY, key);
-            if (prev == EMPTY_KEY || prev == key) {
-                atomicMin(&hval[h], crec[i]);
-                break;
+// first-cover of every candidate key (CallID, pc): hval = min record index
+__global__ __launch_bounds__(NC_THREADS) void newcov_insert_kernel(
+    const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
+    const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
+    const uint32_t *__restrict__ stats, unsigned long long *__restrict__ hkey,
+    uint32_t *__restrict__ hval) {
+    if (stats[0] || !stats[1]) return;
+    const uint64_t mask = hash_cap(stats[1]) - 1;
+    const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
+    for (uint32_t k = blockIdx.x * NC_WPB + (threadIdx.x >> 6); k < nrec; k += nw) {
+        const uint32_t cnt = rec_cnt[k];
+        if (!cnt) continue;
+        const uint64_t hi = (uint64_t)(uint32_t)callid[k] << 32, b = rec_off[k];
+        for (uint32_t i = l; i < cnt; i += 64) {
+            const uint64_t key = hi | cpc[b + i];
+            uint64_t h = hash64(key) & mask;
+            for (;;) {
+                const unsigned long long prev = atomicCAS(&hkey[h], EMPTY_KEY, key);
+                if (prev == EMPTY_KEY || prev == key) {
+                    atomicMin(&hval[h], k);
+                    break;
+                }
+                h = (h + 1) & mask;
             }
-            h = (h + 1) & mask;
         }
     }
 }
 
-__global__ void newcov_own_kernel(const uint64_t *__restrict__ ckey,
-                                  const uint32_t *__restrict__ crec, uint32_t ncand,
-                                  const unsigned long long *__restrict__ hkey,
-                                  const uint32_t *__restrict__ hval, uint64_t mask,
-                                  uint8_t *__restrict__ is_new, uint32_t *__restrict__ maxcov,
-                                  uint64_t words_per_call, uint32_t pc_lo) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ncand;
-         i += gridDim.x * blockDim.x) {
-        const uint64_t key = ckey[i];
-        uint64_t h = hash64(key) & mask;
-        while (hkey[h] != key) h = (h + 1) & mask;
-        if (hval[h] == crec[i]) is_new[crec[i]] = 1;
-        const uint32_t c = (uint32_t)(key >> 32), pc = (uint32_t)key;
-        const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
-        atomicOr(&maxcov[(uint64_t)c * words_per_call + (o >> 5)], 1u << (o & 31));
+// record k is new iff it owns (first-covers) one of its keys; each owned key
+// is OR-ed into maxCover once
+__global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
+    const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
+    const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
+    const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
+    const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
+    uint32_t *__restrict__ maxcov, uint64_t words_per_call, uint32_t pc_lo) {
+    if (stats[0] || !stats[1]) return;
+    const uint64_t mask = hash_cap(stats[1]) - 1;
+    const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
+    for (uint32_t k = blockIdx.x * NC_WPB + (threadIdx.x >> 6); k < nrec; k += nw) {
+        const uint32_t cnt = rec_cnt[k];
+        if (!cnt) continue;
+        const uint32_t c = (uint32_t)callid[k];
+        const uint64_t hi = (uint64_t)c << 32, b = rec_off[k];
+        uint32_t *M = maxcov + (uint64_t)c * words_per_call;
+        bool own = false;
+        for (uint32_t i = l; i < cnt; i += 64) {
+            const uint32_t pc = cpc[b + i];
+            const uint64_t key = hi | pc;
+            uint64_t h = hash64(key) & mask;
+            while (hkey[h] != key) h = (h + 1) & mask;
+            if (hval[h] == k) {
+                own = true;
+                const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
+                atomicOr(&M[o >> 5], 1u << (o & 31));
+            }
+        }
+        if (__ballot(own) && l == 0) is_new[k] = 1;
     }
 }
 
@@ -172,8 +258,10 @@ __global__ void bits_set_kernel(const uint32_t *__restrict__ pcs, uint64_t n,
 }  // namespace syz
 
 // ------------------------------------------------ host-side orchestration
+#include <algorithm>
 #include <mutex>
 #include <new>
+#include <vector>
 
 using namespace syz;
 
@@ -300,6 +388,82 @@ extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *ou
     return rc ? rc : count;
 }
 
+// device workspace: cpc u32[npc] | rec_cnt u32[nrec] | perm u32[nrec] | hkey u64[cap] |
+//                   hval u32[cap] | stats
+static void nc_layout(size_t nrec, uint64_t npc, size_t *o_cnt, size_t *o_hkey, size_t *o_hval,
+                      size_t *o_stats, size_t *end) {
+    uint64_t cap = 1024;
+    while (cap < 2ull * npc) cap <<= 1;
+    *o_cnt = align_up(npc * 4 + 4, 256);
+    *o_hkey = align_up(*o_cnt + 2 * align_up(nrec * 4 + 4, 256), 256);
+    *o_hval = align_up(*o_hkey + cap * 8, 256);
+    *o_stats = align_up(*o_hval + cap * 4, 256);
+    *end = *o_stats + 256;
+}
+
+extern "C" size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc) {
+    size_t a, b, c, d, e;
+    nc_layout(nrec, npc, &a, &b, &c, &d, &e);
+    return e;
+}
+
+static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
+                         const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
+                         uint8_t *ws, uint32_t **stats_out, hipStream_t s) {
+    size_t o_cnt, o_hkey, o_hval, o_stats, end;
+    nc_layout(nrec, npc, &o_cnt, &o_hkey, &o_hval, &o_stats, &end);
+    uint32_t *cpc = (uint32_t *)ws;
+    uint32_t *cnt = (uint32_t *)(ws + o_cnt);
+    uint32_t *perm = (uint32_t *)(ws + o_cnt + align_up(nrec * 4 + 4, 256));
+    unsigned long long *hkey = (unsigned long long *)(ws + o_hkey);
+    uint32_t *hval = (uint32_t *)(ws + o_hval);
+    uint32_t *stats = (uint32_t *)(ws + o_stats);
+    *stats_out = stats;
+    SYZ_HIP(hipMemsetAsync(stats, 0, 16, s));
+    const unsigned gr = grid_for(nrec, NC_WPB, 4096);
+    hipLaunchKernelGGL(newcov_group_kernel, dim3(1), dim3(1024), 0, s, callid, (uint32_t)nrec,
+                       st->ncalls, perm);
+    const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
+    hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off, pcs,
+                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->pc_lo, st->pc_span,
+                       st->ncalls, (const uint32_t *)perm, is_new, cpc, cnt, stats);
+    const unsigned gh = grid_for(std::max<uint64_t>(npc, 512), 256, 8192);
+    hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats, hkey,
+                       hval);
+    hipLaunchKernelGGL(newcov_insert_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
+                       (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
+                       (const uint32_t *)stats, hkey, hval);
+    hipLaunchKernelGGL(newcov_own_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
+                       (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
+                       (const uint32_t *)stats, (const unsigned long long *)hkey,
+                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->pc_lo);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+// Device-resident batch (all pointers device memory; rec_off[0] == 0,
+// rec_off[nrec] == npc).
+// stats (device u32[2], nullable): [0] error code (1 PC outside the window,
+// 2 call id out of range, 3 unsorted record), [1] candidates after the
+// bitmap filter.  Errors are reported there, not returned: the launch is
+// asynchronous on `stream`.
+extern "C" int syzcov_state_newcov_dev(syzcov_cover_state h, const int32_t *callid,
+                                       const uint64_t *rec_off, const uint32_t *pcs, size_t nrec,
+                                       uint64_t npc, uint8_t *is_new, uint32_t *stats, void *ws,
+                                       size_t ws_size, void *stream) {
+    CoverState *st = (CoverState *)(uintptr_t)h;
+    if (!st || !callid || !rec_off || !is_new || !ws || nrec > 0x7FFFFFFF || npc > 0xFFFFFFFFull)
+        return SYZCOV_EINVAL;
+    if (ws_size < syzcov_state_newcov_ws_size(nrec, npc)) return SYZCOV_EINVAL;
+    if (nrec == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *dstats = nullptr;
+    int rc = newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws, &dstats, s);
+    if (rc) return rc;
+    if (stats) SYZ_HIP(hipMemcpyAsync(stats, dstats, 8, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
 extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *callid,
                                        const uint64_t *rec_off, const uint32_t *rec_pcs,
                                        size_t nrec, uint8_t *is_new) {
@@ -312,84 +476,34 @@ extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *call
     const uint64_t base0 = rec_off[0];
     const uint64_t npc = rec_off[nrec] - base0;
     if (npc && !rec_pcs) return SYZCOV_EINVAL;
-    // layout: callid | off | pcs | rec_cnt | err,tot | is_new | ckey | crec | hkey | hval
-    size_t o_cid = 0, o_off = align_up(o_cid + nrec * 4, 256),
-           o_pcs = align_up(o_off + (nrec + 1) * 8, 256), o_cnt = align_up(o_pcs + npc * 4 + 4, 256),
-           o_misc = align_up(o_cnt + nrec * 4, 256), o_new = align_up(o_misc + 16, 256),
-           o_ckey = align_up(o_new + nrec, 256), o_crec = align_up(o_ckey + npc * 8 + 8, 256),
-           o_end = align_up(o_crec + npc * 4 + 4, 256);
+    if (npc > 0xFFFFFFFFull) return SYZCOV_EINVAL;
+    // staging: callid | off | pcs | is_new | newcov workspace
+    const size_t o_off = align_up(nrec * 4, 256), o_pcs = align_up(o_off + (nrec + 1) * 8, 256),
+                 o_new = align_up(o_pcs + npc * 4 + 4, 256), o_ws = align_up(o_new + nrec, 256),
+                 o_end = o_ws + syzcov_state_newcov_ws_size(nrec, npc);
     int rc = grow(st, o_end);
     if (rc) return rc;
     uint8_t *S = (uint8_t *)st->scratch;
-    int32_t *d_cid = (int32_t *)(S + o_cid);
-    uint64_t *d_off = (uint64_t *)(S + o_off);
-    uint32_t *d_pcs = (uint32_t *)(S + o_pcs), *d_cnt = (uint32_t *)(S + o_cnt);
-    uint32_t *d_err = (uint32_t *)(S + o_misc), *d_tot = d_err + 1;
-    uint8_t *d_new = S + o_new;
-    uint64_t *d_ckey = (uint64_t *)(S + o_ckey);
-    uint32_t *d_crec = (uint32_t *)(S + o_crec);
     hipStream_t s = st->s;
-    // offsets rebased to 0
-    uint64_t *hoff = (uint64_t *)malloc((nrec + 1) * 8);
-    if (!hoff) return SYZCOV_ENOMEM;
+    std::vector<uint64_t> hoff(nrec + 1);  // offsets rebased to 0
     for (size_t k = 0; k <= nrec; k++) hoff[k] = rec_off[k] - base0;
-    SYZ_HIP(hipMemsetAsync(d_err, 0, 16, s));
-    SYZ_HIP(hipMemsetAsync(d_new, 0, nrec, s));
-    SYZ_HIP(hipMemcpyAsync(d_cid, callid, nrec * 4, hipMemcpyHostToDevice, s));
-    SYZ_HIP(hipMemcpyAsync(d_off, hoff, (nrec + 1) * 8, hipMemcpyHostToDevice, s));
-    if (npc) SYZ_HIP(hipMemcpyAsync(d_pcs, rec_pcs + base0, npc * 4, hipMemcpyHostToDevice, s));
-    const unsigned gr = grid_for(nrec, 1, 8192);
-    hipLaunchKernelGGL(newcov_count_kernel, dim3(gr), dim3(NC_THREADS), 0, s, d_cid, d_off, d_pcs,
-                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->pc_lo, st->pc_span,
-                       st->ncalls, d_cnt, d_err);
-    hipLaunchKernelGGL(newcov_scan_kernel, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)nrec, d_tot);
-    hipLaunchKernelGGL(newcov_compact_kernel, dim3(gr), dim3(NC_THREADS), 0, s, d_cid, d_off, d_pcs,
-                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->pc_lo, st->pc_span,
-                       st->ncalls, d_cnt, d_ckey, d_crec);
-    SYZ_LAUNCH_CHECK();
-    uint32_t hmisc[2];
-    SYZ_HIP(hipMemcpyAsync(hmisc, d_err, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(S, callid, nrec * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(S + o_off, hoff.data(), (nrec + 1) * 8, hipMemcpyHostToDevice, s));
+    if (npc) SYZ_HIP(hipMemcpyAsync(S + o_pcs, rec_pcs + base0, npc * 4, hipMemcpyHostToDevice, s));
+    uint32_t *dstats = nullptr;
+    rc = newcov_launch(st, (const int32_t *)S, (const uint64_t *)(S + o_off),
+                       (const uint32_t *)(S + o_pcs), nrec, npc, S + o_new, S + o_ws, &dstats, s);
+    if (rc) return rc;
+    uint32_t hs[2];
+    SYZ_HIP(hipMemcpyAsync(hs, dstats, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(is_new, S + o_new, nrec, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
-    free(hoff);
-    if (hmisc[0]) {
-        set_error(hmisc[0] == 1 ? "PC outside the state's PC window"
-                  : hmisc[0] == 2 ? "call id out of range"
-                                  : "record cover not sorted");
-        return hmisc[0] == 1 ? SYZCOV_ERANGE : hmisc[0] == 2 ? SYZCOV_EINVAL : SYZCOV_ENOTSORTED;
+    if (hs[0]) {
+        set_error(hs[0] == 1 ? "PC outside the state's PC window"
+                  : hs[0] == 2 ? "call id out of range"
+                               : "record cover not sorted");
+        return hs[0] == 1 ? SYZCOV_ERANGE : hs[0] == 2 ? SYZCOV_EINVAL : SYZCOV_ENOTSORTED;
     }
-    const uint32_t ncand = hmisc[1];
-    if (ncand) {
-        uint64_t cap = 1024;
-        while (cap < 2ull * ncand) cap <<= 1;
-        const size_t o_hkey = o_end, o_hval = align_up(o_hkey + cap * 8, 256),
-                     o_fin = align_up(o_hval + cap * 4, 256);
-        // grow preserving the candidate arrays: allocate fresh if needed
-        if (o_fin > st->scap) {
-            void *nb = nullptr;
-            if (hipMalloc(&nb, o_fin + o_fin / 2) != hipSuccess) return SYZCOV_ENOMEM;
-            SYZ_HIP(hipMemcpyAsync(nb, st->scratch, o_end, hipMemcpyDeviceToDevice, s));
-            SYZ_HIP(hipStreamSynchronize(s));
-            hipFree(st->scratch);
-            st->scratch = nb;
-            st->scap = o_fin + o_fin / 2;
-            S = (uint8_t *)nb;
-            d_new = S + o_new;
-            d_ckey = (uint64_t *)(S + o_ckey);
-            d_crec = (uint32_t *)(S + o_crec);
-        }
-        unsigned long long *d_hkey = (unsigned long long *)(S + o_hkey);
-        uint32_t *d_hval = (uint32_t *)(S + o_hval);
-        SYZ_HIP(hipMemsetAsync(d_hkey, 0xFF, cap * 8, s));
-        SYZ_HIP(hipMemsetAsync(d_hval, 0xFF, cap * 4, s));
-        hipLaunchKernelGGL(newcov_insert_kernel, dim3(grid_for(ncand, 256, 8192)), dim3(256), 0, s,
-                           d_ckey, d_crec, ncand, d_hkey, d_hval, cap - 1);
-        hipLaunchKernelGGL(newcov_own_kernel, dim3(grid_for(ncand, 256, 8192)), dim3(256), 0, s,
-                           d_ckey, d_crec, ncand, d_hkey, d_hval, cap - 1, d_new, st->maxcov,
-                           st->words, st->pc_lo);
-        SYZ_LAUNCH_CHECK();
-    }
-    SYZ_HIP(hipMemcpyAsync(is_new, d_new, nrec, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
     int64_t nnew = 0;
     for (size_t k = 0; k < nrec; k++) nnew += is_new[k];
     return nnew;

@@ -1,0 +1,142 @@
+"""GPU parity of the manager-side callers (syz-manager/manager.go):
+minimizeCorpus (:504-524, per-call Minimize with its own Go sort.Sort per
+group, one engine call) and NewInput's corpusCover merge (:596-621), against
+the CPU oracle.  Bit-exact (index/integer work)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cover():
+    from syzkaller_amd import cover as c
+    return c
+
+
+def _corpus(rng, n, ncalls, hi, maxlen):
+    calls = rng.integers(0, ncalls, size=n).astype(np.int32)
+    covs = [orc.canonicalize(rng.integers(0, hi, size=int(rng.integers(0, maxlen)),
+                                          dtype=np.uint64).astype(np.uint32))
+            for _ in range(n)]
+    return calls, covs
+
+
+def test_minimize_corpus_kat(cover):
+    # cover_test.go:139-147 corpora as two call groups + a third interleaved
+    covs = [[1, 2, 3, 4], [5], [1, 2], [3, 4, 5, 6, 7], [5, 6], [3, 7]]
+    calls = [4, 9, 4, 4, 9, 4]
+    assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
+    assert cover.MinimizeCorpus(calls, covs) == [3, 0, 4]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_minimize_corpus_random(cover, variant):
+    rng = np.random.default_rng(31 + variant)
+    for trial in range(25):
+        n = int(rng.integers(0, 3000))
+        ncalls = int(rng.choice([1, 3, 293, 5000]))
+        calls, covs = _corpus(rng, n, ncalls, int(rng.choice([40, 3000, 1 << 32])), 30)
+        assert cover.MinimizeCorpus(calls, covs, variant) == \
+            orc.minimize_corpus(calls, covs, variant), (trial, n, ncalls)
+
+
+def test_minimize_corpus_tie_heavy_large_groups(cover):
+    """Groups above the sort's one-workgroup size (4096) with few distinct
+    lengths: exercises the global pdqsort rounds, partitionEqual at group
+    starts (the gap key) and the insertion-sort leaves."""
+    rng = np.random.default_rng(33)
+    n = 30000
+    calls = rng.choice([2, 5, 7], size=n, p=[0.6, 0.3, 0.1]).astype(np.int32)
+    covs = [np.unique(rng.integers(0, 5000, size=int(rng.integers(1, 5)))).astype(np.uint32)
+            for _ in range(n)]
+    assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
+
+
+def test_minimize_corpus_synthetic(cover):
+    off, pcs = orc.synth_corpus(0x5EED0001, 4000, mean=256, sigma=64, log2_space=16)
+    coff, cpcs = orc.canonicalize_csr(off, pcs)
+    covs = [cpcs[coff[i]:coff[i + 1]] for i in range(4000)]
+    calls = (np.arange(4000) * 2654435761 % 293).astype(np.int32)
+    assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
+
+
+def test_minimize_corpus_manager_mirror():
+    from syzkaller_amd.manager import RpcInput, minimize_corpus
+    covs = [[1, 2, 3, 4], [5], [1, 2], [3, 4, 5, 6, 7], [5, 6], [3, 7]]
+    names = ["open", "read", "open", "open", "read", "open"]
+    corpus = [RpcInput(c, bytes([i]), 0, np.array(v, dtype=np.uint32))
+              for i, (c, v) in enumerate(zip(names, covs))]
+    new = minimize_corpus(corpus)
+    assert [inp.Prog for inp in new] == [bytes([3]), bytes([0]), bytes([4])]
+
+
+def test_new_inputs_vs_sequential():
+    from syzkaller_amd.manager import CorpusCover
+    rng = np.random.default_rng(34)
+    ncalls, lo, span = 40, 0x81000000, 1 << 18
+    cc = CorpusCover(ncalls, lo, span)
+    ref = {}
+    for batch in range(3):
+        calls = rng.integers(0, ncalls, size=4000)
+        covs = [np.unique(rng.integers(lo, lo + int(rng.choice([300, span])),
+                                       size=int(rng.integers(0, 50)))).astype(np.uint32)
+                for _ in range(4000)]
+        exp = orc.new_inputs(ref, calls, covs)
+        assert cc.new_inputs(calls, covs).tolist() == exp, batch
+        for c in range(ncalls):
+            assert np.array_equal(cc.get(c), ref.get(c, np.zeros(0, np.uint32))), (batch, c)
+    cc.close()
+
+
+def test_newcov_device_api_vs_oracle():
+    """syzcov_state_newcov_dev (batch already in HBM, async on torch's stream)
+    == the sequential reference loop, incl. flakes and a rejected batch."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    from syzkaller_amd.fuzzer import CoverState
+    L = _lib.lib()
+    rng = np.random.default_rng(35)
+    ncalls, lo, span = 17, 0x81000000, 1 << 20
+    st = CoverState(ncalls, lo, span)
+    flakes = np.unique(rng.integers(lo, lo + span, size=2000)).astype(np.uint32)
+    st.set_flakes(flakes)
+    mc = [[] for _ in range(ncalls)]
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    dev = torch.device("cuda")
+    for batch in range(3):
+        nrec = 5000
+        cids = rng.integers(0, ncalls, size=nrec).astype(np.int32)
+        recs = [np.unique(rng.integers(lo, lo + int(rng.choice([2000, span])),
+                                       size=int(rng.integers(0, 300)))).astype(np.uint32)
+                for _ in range(nrec)]
+        exp, mc = orc.newcov_batch(mc, flakes, cids, recs)
+        off, pcs = orc.to_csr(recs)
+        d_cid = torch.from_numpy(cids).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_pcs = torch.from_numpy(pcs.view(np.int32)).to(dev)
+        d_new = torch.empty(nrec, dtype=torch.uint8, device=dev)
+        stats = torch.zeros(2, dtype=torch.int32, device=dev)
+        wsz = L.syzcov_state_newcov_ws_size(nrec, int(off[-1]))
+        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(L.syzcov_state_newcov_dev(st.h, P(d_cid), P(d_off), P(d_pcs), nrec,
+                                             int(off[-1]), P(d_new), P(stats), P(ws), wsz, s),
+                   "state_newcov_dev")
+        torch.cuda.synchronize()
+        assert stats[0].item() == 0
+        assert np.array_equal(d_new.cpu().numpy(), exp), batch
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
+    # an unsorted record rejects the whole batch and leaves maxCover untouched
+    before = [st.max_cover(c).copy() for c in range(ncalls)]
+    from syzkaller_amd import SyzcovError
+    with pytest.raises(SyzcovError):
+        st.new_coverage([1, 2], [np.array([lo + 5, lo + 9], np.uint32),
+                                 np.array([lo + 9, lo + 5], np.uint32)])
+    for c in range(ncalls):
+        assert np.array_equal(st.max_cover(c), before[c])
+    st.close()

@@ -164,3 +164,37 @@ def test_synth_deterministic():
     lens = np.diff(off)
     assert 1000 < lens.mean() < 3000
     assert pcs.min() >= 0x81000000 and pcs.max() <= 0x84FFFFFF
+
+
+def test_minimize_corpus_groups_vs_python():
+    """manager.go:504-524: per-call Minimize in corpus order, restated twice."""
+    rng = np.random.default_rng(21)
+    for _ in range(40):
+        n = int(rng.integers(0, 300))
+        calls = rng.integers(0, 7, size=n)
+        covs = [list(orc.canonicalize(rng.integers(0, 200, size=int(rng.integers(0, 10)))))
+                for _ in range(n)]
+        exp = []
+        for c in sorted(set(calls.tolist())):
+            members = [i for i in range(n) if calls[i] == c]
+            exp += [members[k] for k in pyref.minimize([covs[i] for i in members])]
+        assert orc.minimize_corpus(calls, covs) == exp
+
+
+def test_new_input_is_newcov_without_flakes():
+    """Manager.NewInput (manager.go:605-610) == the fuzzer's batched
+    new-coverage check (fuzzer.go:456-480) with an empty flakes set, applied
+    in arrival order; the sentinel-only cover is dropped by both."""
+    rng = np.random.default_rng(22)
+    ncalls = 5
+    for _ in range(20):
+        calls = rng.integers(0, ncalls, size=200)
+        covs = [orc.canonicalize(rng.integers(0, 400, size=int(rng.integers(0, 8))))
+                for _ in range(200)]
+        covs[3] = np.array([0xFFFFFFFF], dtype=np.uint32)
+        cc = {}
+        acc = orc.new_inputs(cc, calls, covs)
+        is_new, mc = orc.newcov_batch([[] for _ in range(ncalls)], [], calls, covs)
+        assert acc == [bool(x) for x in is_new]
+        for c in range(ncalls):
+            assert list(mc[c]) == list(cc.get(c, []))
