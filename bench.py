@@ -38,6 +38,7 @@ I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MIC
 SEED = 0x5EED0002
 SEED_PRIO = 0x5EED0004
 SEED_NEWCOV = 0x5EED0005
+FLAKE_INPUT = 1 << 40  # synthetic input index the C5 flakes set is drawn as
 
 
 def parse():
@@ -48,6 +49,9 @@ def parse():
     ap.add_argument("--workload", choices=["corpus", "prio", "newcov"], default="corpus")
     ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
     ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
+    ap.add_argument("--universe", action="store_true",
+                    help="newcov: maxCover over dense ids of the synthetic PC universe "
+                         "(16x less memory; measured slower: two probed lines per PC)")
     ap.add_argument("--history", type=int, default=32,
                     help="newcov: batches streamed through the check before the bench")
     ap.add_argument("--inputs", type=int, default=1_000_000, help="inputs (programs) per GPU")
@@ -264,8 +268,8 @@ def cpu_baseline_newcov(args, nrec: int, nhist: int = 16384):
     recs = [c_pcs[c_off[i]:c_off[i + 1]] for i in range(nhist + nrec)]
     rng = np.random.default_rng(SEED_NEWCOV)
     cids = rng.integers(0, args.ncalls, size=nhist + nrec)
-    fo, fp = orc.synth_corpus(SEED_NEWCOV ^ 0xF1A4E, 1, 1 << (args.log2_space - 7), 1,
-                              args.log2_space)
+    fo, fp = orc.synth_corpus(SEED_NEWCOV, 1, 1 << (args.log2_space - 7), 1, args.log2_space,
+                              first=FLAKE_INPUT)
     flakes = orc.canonicalize(fp[:int(fo[1])])
     _, mc = orc.newcov_batch([[] for _ in range(args.ncalls)], flakes, cids[:nhist],
                              recs[:nhist])
@@ -321,10 +325,17 @@ def bench_newcov(args):
         cid = torch.randint(0, args.ncalls, (nrec,), generator=gen, dtype=torch.int32).to(dev)
         return cid, roff, pcs, npc
 
-    st = CoverState(args.ncalls, lo, span)
-    fo, fp, _, _ = synth_corpus(1, SEED_NEWCOV ^ 0xF1A4E, mean=1 << (args.log2_space - 7),
-                                sigma=1, log2_space=args.log2_space, device=dev)
     import numpy as np
+    st = CoverState(args.ncalls, lo, span)
+    if args.universe:  # SURVEY §8d C5 variant: per-call bitmaps over the 2^22 PC ids
+        univ = torch.empty(1 << args.log2_space, dtype=torch.int32, device=dev)
+        _lib.check(L.syzcov_dev_synth_universe(SEED_NEWCOV, args.log2_space, P(univ), s()),
+                   "synth_universe")
+        st.set_universe(univ.cpu().numpy().view(np.uint32))
+        del univ
+    # flakes: one synthetic draw from the same universe (input index 2^40)
+    fo, fp, _, _ = synth_corpus(1, SEED_NEWCOV, first=FLAKE_INPUT, mean=1 << (args.log2_space - 7),
+                                sigma=1, log2_space=args.log2_space, device=dev)
     st.set_flakes(np.unique(fp[:int(fo[1].item())].cpu().numpy().view(np.uint32)))
     # a fuzzer that has been running: `history` batches streamed through the
     # same check before the bench (maxCover near saturation, as in steady state)
@@ -376,7 +387,11 @@ def bench_newcov(args):
                    "records_per_batch": nrec, "calls": args.ncalls,
                    "pcs_per_batch": timed_pcs // args.steps, "pc_space": 1 << args.log2_space,
                    "flakes": f"unique PCs of one synthetic {1 << (args.log2_space - 7)}-PC draw",
-                   "maxcover_bytes": args.ncalls * span // 8,
+                   "maxcover": ("dense ids over the synthetic 2^%d-PC universe"
+                                % args.log2_space if args.universe
+                                else "window bitmaps (1 bit per PC offset)"),
+                   "maxcover_bytes": args.ncalls * ((1 << args.log2_space) if args.universe
+                                                    else span) // 8,
                    "history_batches": args.history, "history_new_records": hist_new},
         "phases_ms": {"newcov": round(phl[0], 4)},
         "results": {"candidates_per_batch": [x[1] for x in sc[args.warmup:]],

@@ -151,6 +151,12 @@ int syzcov_state_destroy(syzcov_cover_state st);
 /* maxCover[call] = Union(maxCover[call], pcs) (sorted list). */
 int syzcov_state_add(syzcov_cover_state st, int call, const uint32_t *pcs, size_t n);
 int syzcov_state_set_flakes(syzcov_cover_state st, const uint32_t *pcs, size_t n);
+/* Optional, before the first add/newcov: the PC universe (the reference's
+ * allCoverPCs, syz-manager/cover.go:57-69 — the __sanitizer_cov_trace_pc call
+ * sites).  maxCover of universe PCs is then kept over dense universe ids
+ * (1 bit per known PC instead of per window offset); other PCs still work
+ * through the window bitmaps.  Results are identical either way. */
+int syzcov_state_set_universe(syzcov_cover_state st, const uint32_t *pcs, size_t n);
 /* Reads maxCover[call] back as a sorted list (out capacity: pc_span or the
  * count from a NULL-out call); returns its length. */
 int64_t syzcov_state_get(syzcov_cover_state st, int call, uint32_t *out, size_t cap);
@@ -319,6 +325,8 @@ int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean
                           uint32_t *lens, void *stream);
 int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
                          uint32_t log2_space, int uniform, uint32_t *pcs, void *stream);
+/* The synthetic PC universe U[k], k < 2^log2_space (sorted). */
+int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out, void *stream);
 
 /* Dynamic priority counts as a dense contraction on i8 MFMA with i32
  * accumulation: counts = AᵀA over the key-major matrix AT[key][program]

@@ -59,6 +59,7 @@ _SIGS = {
     "syzcov_state_set_flakes": (C.c_int, [u64, p_, sz]),
     "syzcov_state_get": (i64, [u64, C.c_int, p_, sz]),
     "syzcov_newcov_batch": (i64, [u64, p_, p_, p_, sz, p_]),
+    "syzcov_state_set_universe": (C.c_int, [u64, p_, sz]),
     "syzcov_state_newcov_ws_size": (sz, [sz, u64]),
     "syzcov_state_newcov_dev": (C.c_int, [u64, p_, p_, p_, sz, u64, p_, p_, p_, sz, p_]),
     # device tier
@@ -90,6 +91,7 @@ _SIGS = {
     "syzcov_dev_bytemap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),
     "syzcov_dev_synth_lens": (C.c_int, [u64, u64, sz, u32, u32, p_, p_]),
     "syzcov_dev_synth_pcs": (C.c_int, [u64, u64, sz, p_, u32, C.c_int, p_, p_]),
+    "syzcov_dev_synth_universe": (C.c_int, [u64, u32, p_, p_]),
     "syzcov_dev_prio_rows": (sz, [C.c_int]),
     "syzcov_dev_prio_ldp": (sz, [sz]),
     "syzcov_dev_prio_build_at": (C.c_int, [C.c_int, p_, p_, p_, sz, C.c_int, p_, sz, p_, p_]),

@@ -22,6 +22,29 @@ __device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64
     return (bm[o >> 5] >> (o & 31)) & 1u;
 }
 
+// Universe mode (syzcov_state_set_universe): PCs of a known universe (the
+// reference's allCoverPCs, syz-manager/cover.go:57-69: every
+// __sanitizer_cov_trace_pc call site) are tested against per-call bitmaps
+// over DENSE universe ids (utab: the {prefix:32 | bits:32} dictionary per
+// 32-offset window word), 16x smaller than window bitmaps at C5 and
+// L2-resident per call; other PCs keep the window bitmaps.  Returns the word
+// to probe and sets *bit to the bit inside it.
+__device__ __forceinline__ const uint32_t *probe_word(const uint64_t *__restrict__ utab,
+                                                      const uint32_t *DM, const uint32_t *M,
+                                                      uint32_t o, uint32_t *bit) {
+    if (utab) {
+        const uint64_t e = utab[o >> 5];
+        const uint32_t ub = (uint32_t)(e >> 32);
+        if ((ub >> (o & 31)) & 1u) {
+            const uint32_t id = (uint32_t)e + (uint32_t)__popc(ub & ((1u << (o & 31)) - 1u));
+            *bit = id & 31;
+            return DM + (id >> 5);
+        }
+    }
+    *bit = o & 31;
+    return M + (o >> 5);
+}
+
 constexpr int NC_THREADS = 256;
 constexpr int NC_WPB = NC_THREADS / 64;
 constexpr int NC_U = 8;  // rows of 64 PCs in flight per wave
@@ -82,8 +105,10 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
     const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
     const uint32_t *__restrict__ pcs, uint32_t nrec, const uint32_t *__restrict__ maxcov,
     uint64_t words_per_call, const uint32_t *__restrict__ flakes, uint32_t pc_lo,
-    uint64_t pc_span, int ncalls, const uint32_t *__restrict__ perm, uint8_t *__restrict__ is_new,
-    uint32_t *__restrict__ cpc, uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ stats) {
+    uint64_t pc_span, int ncalls, const uint64_t *__restrict__ utab,
+    const uint32_t *__restrict__ dmax, uint64_t dwords, const uint32_t *__restrict__ perm,
+    uint8_t *__restrict__ is_new, uint32_t *__restrict__ cpc, uint32_t *__restrict__ rec_cnt,
+    uint32_t *__restrict__ stats) {
     const uint32_t l = __lane_id();
     const uint64_t lt = (1ull << l) - 1ull;
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
@@ -105,11 +130,12 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
             continue;
         }
         const uint32_t *M = maxcov + (uint64_t)c * words_per_call;
+        const uint32_t *DM = dmax + (uint64_t)c * dwords;
         const uint64_t b = rec_off[k], n = rec_off[k + 1] - b;
         uint32_t bad = 0, cnt = 0, carry = 0;
         // NC_U rows per step: all their loads and maxCover probes in flight together
         for (uint64_t q0 = 0; q0 < n; q0 += 64 * NC_U) {
-            uint32_t pc[NC_U], w[NC_U];
+            uint32_t pc[NC_U], w[NC_U], bt[NC_U];
             bool ok[NC_U];
 #pragma unroll
             for (int u = 0; u < NC_U; u++) {
@@ -123,7 +149,9 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 const bool inw = pc[u] >= pc_lo && o < pc_span;
                 ok[u] = q < n && inw;
                 bad |= (uint32_t)(q < n && !inw);
-                w[u] = ok[u] ? M[o >> 5] : 0xFFFFFFFFu;
+                w[u] = 0xFFFFFFFFu;
+                bt[u] = 0;
+                if (ok[u]) w[u] = *probe_word(utab, DM, M, (uint32_t)o, &bt[u]);
             }
 #pragma unroll
             for (int u = 0; u < NC_U; u++) {
@@ -136,7 +164,7 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 if (q < n && q > 0 && prev > pc[u]) bad |= 2u;
                 const uint32_t o = pc[u] - pc_lo;
                 // maxCover first: once it saturates, flakes are rarely probed
-                const bool cand = ok[u] && !((w[u] >> (o & 31)) & 1u) && !bit_test(flakes, o);
+                const bool cand = ok[u] && !((w[u] >> bt[u]) & 1u) && !bit_test(flakes, o);
                 const uint64_t m = __ballot(cand);
                 if (cand) cpc[b + cnt + (uint32_t)__popcll(m & lt)] = pc[u];
                 cnt += (uint32_t)__popcll(m);
@@ -214,7 +242,8 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
     const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
     const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
-    uint32_t *__restrict__ maxcov, uint64_t words_per_call, uint32_t pc_lo) {
+    uint32_t *__restrict__ maxcov, uint64_t words_per_call, uint32_t pc_lo,
+    const uint64_t *__restrict__ utab, uint32_t *__restrict__ dmax, uint64_t dwords) {
     if (stats[0] || !stats[1]) return;
     const uint64_t mask = hash_cap(stats[1]) - 1;
     const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
@@ -224,6 +253,7 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
         const uint32_t c = (uint32_t)callid[k];
         const uint64_t hi = (uint64_t)c << 32, b = rec_off[k];
         uint32_t *M = maxcov + (uint64_t)c * words_per_call;
+        uint32_t *DM = dmax + (uint64_t)c * dwords;
         bool own = false;
         for (uint32_t i = l; i < cnt; i += 64) {
             const uint32_t pc = cpc[b + i];
@@ -232,8 +262,9 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
             while (hkey[h] != key) h = (h + 1) & mask;
             if (hval[h] == k) {
                 own = true;
-                const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
-                atomicOr(&M[o >> 5], 1u << (o & 31));
+                uint32_t bit;
+                uint32_t *wp = const_cast<uint32_t *>(probe_word(utab, DM, M, pc - pc_lo, &bit));
+                atomicOr(wp, 1u << bit);
             }
         }
         if (__ballot(own) && l == 0) is_new[k] = 1;
@@ -242,7 +273,8 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
 
 __global__ void bits_set_kernel(const uint32_t *__restrict__ pcs, uint64_t n,
                                 uint32_t *__restrict__ bm, uint32_t pc_lo, uint64_t pc_span,
-                                uint32_t *__restrict__ err) {
+                                uint32_t *__restrict__ err, const uint64_t *__restrict__ utab,
+                                uint32_t *__restrict__ dm) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t pc = pcs[i];
@@ -251,7 +283,26 @@ __global__ void bits_set_kernel(const uint32_t *__restrict__ pcs, uint64_t n,
             *err = 1u;
             continue;
         }
-        atomicOr(&bm[o >> 5], 1u << (o & 31));
+        uint32_t bit;
+        uint32_t *wp = const_cast<uint32_t *>(probe_word(utab, dm, bm, (uint32_t)o, &bit));
+        atomicOr(wp, 1u << bit);
+    }
+}
+
+// window bitmap |= the dense bits of one call (universe mode), for reads
+__global__ void dense_to_window_kernel(const uint64_t *__restrict__ utab, uint64_t nwords,
+                                       const uint32_t *__restrict__ dm, uint32_t *__restrict__ bm) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = utab[w];
+        uint32_t ub = (uint32_t)(e >> 32), id = (uint32_t)e, out = 0;
+        while (ub) {
+            const uint32_t b = (uint32_t)__builtin_ctz(ub);
+            if ((dm[id >> 5] >> (id & 31)) & 1u) out |= 1u << b;
+            id++;
+            ub &= ub - 1;
+        }
+        if (out) bm[w] |= out;
     }
 }
 
@@ -273,6 +324,12 @@ struct CoverState {
     uint64_t pc_span = 0, words = 0;
     uint32_t *maxcov = nullptr;  // ncalls x words
     uint32_t *flakes = nullptr;  // words
+    // universe mode: dictionary over the window + per-call dense bitmaps
+    uint64_t *utab = nullptr;    // words entries
+    uint32_t *dmax = nullptr;    // ncalls x dwords
+    uint64_t dwords = 0;
+    uint32_t nuniv = 0;
+    bool dirty = false;          // maxCover touched: the universe can no longer change
     hipStream_t s = nullptr;
     std::mutex mu;  // the reference's coverMu
     // grow-only scratch
@@ -332,13 +389,16 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     hipStreamSynchronize(st->s);
     hipFree(st->maxcov);
     hipFree(st->flakes);
+    if (st->utab) hipFree(st->utab);
+    if (st->dmax) hipFree(st->dmax);
     if (st->scratch) hipFree(st->scratch);
     hipStreamDestroy(st->s);
     delete st;
     return 0;
 }
 
-static int set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n) {
+// bm: a window bitmap; dm (universe mode, nullable): the matching dense bitmap
+static int set_bits(CoverState *st, uint32_t *bm, uint32_t *dm, const uint32_t *pcs, size_t n) {
     if (n == 0) return 0;
     size_t need = align_up(n * 4, 256) + 256;
     int rc = grow(st, need);
@@ -348,7 +408,8 @@ static int set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n)
     SYZ_HIP(hipMemsetAsync(derr, 0, 4, st->s));
     SYZ_HIP(hipMemcpyAsync(dp, pcs, n * 4, hipMemcpyHostToDevice, st->s));
     hipLaunchKernelGGL(bits_set_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st->s, dp,
-                       (uint64_t)n, bm, st->pc_lo, st->pc_span, derr);
+                       (uint64_t)n, bm, st->pc_lo, st->pc_span, derr,
+                       (const uint64_t *)(dm ? st->utab : nullptr), dm);
     SYZ_LAUNCH_CHECK();
     uint32_t herr = 0;
     SYZ_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st->s));
@@ -365,7 +426,67 @@ extern "C" int syzcov_state_add(syzcov_cover_state h, int call, const uint32_t *
     if (!st || call < 0 || call >= st->ncalls || (n && !pcs)) return SYZCOV_EINVAL;
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
-    return set_bits(st, st->maxcov + (size_t)call * st->words, pcs, n);
+    st->dirty = true;
+    return set_bits(st, st->maxcov + (size_t)call * st->words,
+                    st->dmax ? st->dmax + (size_t)call * st->dwords : nullptr, pcs, n);
+}
+
+// Universe mode (see probe_word): PCs of `pcs` (inside the window, any order,
+// duplicates allowed) get dense ids; allowed only while maxCover is empty.
+extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *pcs, size_t n) {
+    CoverState *st = (CoverState *)(uintptr_t)h;
+    if (!st || (n && !pcs)) return SYZCOV_EINVAL;
+    std::lock_guard<std::mutex> g(st->mu);
+    hipSetDevice(st->dev);
+    if (st->dirty) {
+        set_error("set_universe after maxCover was filled");
+        return SYZCOV_EINVAL;
+    }
+    if (st->utab) hipFree(st->utab);
+    if (st->dmax) hipFree(st->dmax);
+    st->utab = nullptr;
+    st->dmax = nullptr;
+    st->nuniv = 0;
+    st->dwords = 0;
+    if (n == 0) return 0;
+    uint32_t *bm = nullptr, *dn = nullptr;
+    void *ws = nullptr;
+    const size_t wsz = syzcov_dev_dict_ws_size(st->pc_span);
+    if (hipMalloc(&st->utab, st->words * 8) != hipSuccess || hipMalloc(&bm, st->words * 4) != hipSuccess ||
+        hipMalloc(&ws, wsz + 256) != hipSuccess) {
+        if (bm) hipFree(bm);
+        if (ws) hipFree(ws);
+        return SYZCOV_ENOMEM;
+    }
+    dn = (uint32_t *)((uint8_t *)ws + wsz);
+    int rc = 0;
+    uint32_t hn = 0;
+    do {
+        if (hipMemsetAsync(bm, 0, st->words * 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if ((rc = set_bits(st, bm, nullptr, pcs, n))) break;
+        if ((rc = syzcov_dev_dict_build_bits(bm, st->pc_span, st->utab, dn, ws, st->s))) break;
+        if (hipMemcpyAsync(&hn, dn, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        st->nuniv = hn;
+        st->dwords = (hn + 31) / 32 + 1;
+        if (hipMalloc(&st->dmax, (size_t)st->ncalls * st->dwords * 4) != hipSuccess) {
+            rc = SYZCOV_ENOMEM;
+            break;
+        }
+        if (hipMemsetAsync(st->dmax, 0, (size_t)st->ncalls * st->dwords * 4, st->s) != hipSuccess ||
+            hipStreamSynchronize(st->s) != hipSuccess) rc = SYZCOV_EHIP;
+    } while (0);
+    hipFree(bm);
+    hipFree(ws);
+    if (rc) {
+        if (st->utab) hipFree(st->utab);
+        if (st->dmax) hipFree(st->dmax);
+        st->utab = nullptr;
+        st->dmax = nullptr;
+        st->nuniv = 0;
+        st->dwords = 0;
+    }
+    return rc;
 }
 
 extern "C" int syzcov_state_set_flakes(syzcov_cover_state h, const uint32_t *pcs, size_t n) {
@@ -374,7 +495,7 @@ extern "C" int syzcov_state_set_flakes(syzcov_cover_state h, const uint32_t *pcs
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     SYZ_HIP(hipMemsetAsync(st->flakes, 0, st->words * 4, st->s));
-    return set_bits(st, st->flakes, pcs, n);
+    return set_bits(st, st->flakes, nullptr, pcs, n);
 }
 
 extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *out, size_t cap) {
@@ -383,8 +504,21 @@ extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *ou
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     int64_t count = 0;
-    int rc = bitmap_to_list(st->maxcov + (size_t)call * st->words, st->pc_span, st->pc_lo, out,
-                            cap, &count, st->s);
+    const uint32_t *bm = st->maxcov + (size_t)call * st->words;
+    uint32_t *tmp = nullptr;
+    if (st->dmax) {  // window bits | dense bits mapped back to their PCs
+        if (hipMalloc(&tmp, st->words * 4) != hipSuccess) return SYZCOV_ENOMEM;
+        SYZ_HIP(hipMemcpyAsync(tmp, bm, st->words * 4, hipMemcpyDeviceToDevice, st->s));
+        hipLaunchKernelGGL(dense_to_window_kernel, dim3(grid_for(st->words, 256, 16384)), dim3(256), 0,
+                           st->s, (const uint64_t *)st->utab, st->words,
+                           (const uint32_t *)(st->dmax + (size_t)call * st->dwords), tmp);
+        bm = tmp;
+    }
+    int rc = bitmap_to_list(bm, st->pc_span, st->pc_lo, out, cap, &count, st->s);
+    if (tmp) {
+        hipStreamSynchronize(st->s);
+        hipFree(tmp);
+    }
     return rc ? rc : count;
 }
 
@@ -426,7 +560,8 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
     hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off, pcs,
                        (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->pc_lo, st->pc_span,
-                       st->ncalls, (const uint32_t *)perm, is_new, cpc, cnt, stats);
+                       st->ncalls, (const uint64_t *)st->utab, (const uint32_t *)st->dmax,
+                       st->dwords, (const uint32_t *)perm, is_new, cpc, cnt, stats);
     const unsigned gh = grid_for(std::max<uint64_t>(npc, 512), 256, 8192);
     hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats, hkey,
                        hval);
@@ -436,7 +571,8 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     hipLaunchKernelGGL(newcov_own_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
                        (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
                        (const uint32_t *)stats, (const unsigned long long *)hkey,
-                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->pc_lo);
+                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->pc_lo,
+                       (const uint64_t *)st->utab, st->dmax, st->dwords);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
@@ -457,6 +593,7 @@ extern "C" int syzcov_state_newcov_dev(syzcov_cover_state h, const int32_t *call
     if (ws_size < syzcov_state_newcov_ws_size(nrec, npc)) return SYZCOV_EINVAL;
     if (nrec == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
+    st->dirty = true;
     uint32_t *dstats = nullptr;
     int rc = newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws, &dstats, s);
     if (rc) return rc;
@@ -485,6 +622,7 @@ extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *call
     if (rc) return rc;
     uint8_t *S = (uint8_t *)st->scratch;
     hipStream_t s = st->s;
+    st->dirty = true;
     std::vector<uint64_t> hoff(nrec + 1);  // offsets rebased to 0
     for (size_t k = 0; k <= nrec; k++) hoff[k] = rec_off[k] - base0;
     SYZ_HIP(hipMemcpyAsync(S, callid, nrec * 4, hipMemcpyHostToDevice, s));

@@ -51,9 +51,24 @@ __global__ void synth_pcs_kernel(uint64_t seed, uint64_t first, uint64_t n,
     }
 }
 
+__global__ void synth_universe_kernel(uint64_t seed, uint32_t n, uint32_t *__restrict__ out) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+        out[k] = synth_universe(seed, k);
+}
+
 }  // namespace syz
 
 using namespace syz;
+
+extern "C" int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out,
+                                         void *stream) {
+    if (!out || log2_space < 1 || log2_space > 26) return SYZCOV_EINVAL;
+    const uint32_t n = 1u << log2_space;
+    hipLaunchKernelGGL(synth_universe_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, seed, n, out);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean,
                                      uint32_t sigma, uint32_t *lens, void *stream) {

@@ -36,6 +36,12 @@ class CoverState:
         a = np.ascontiguousarray(pcs, dtype=np.uint32)
         check(lib().syzcov_state_add(self.h, call, _ptr(a), a.size), "state_add")
 
+    def set_universe(self, pcs):
+        """Known PC universe (allCoverPCs, syz-manager/cover.go:57-69) before
+        the first add/check: maxCover of those PCs is kept over dense ids."""
+        a = np.ascontiguousarray(pcs, dtype=np.uint32)
+        check(lib().syzcov_state_set_universe(self.h, _ptr(a), a.size), "state_set_universe")
+
     def set_flakes(self, pcs):
         a = np.ascontiguousarray(pcs, dtype=np.uint32)
         check(lib().syzcov_state_set_flakes(self.h, _ptr(a), a.size), "state_set_flakes")
