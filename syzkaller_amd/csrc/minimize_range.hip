@@ -20,11 +20,12 @@
 // items' sub-runs inside the range (canonical lists are sorted, so a sub-run
 // is contiguous: split[] from canon_wave.hip).  Ranges get workgroups in
 // proportion to their PC counts (range_tot), so a hot range is cut into many
-// short item slices.  A wave takes 64 items at a time: short sub-runs (the
-// cold ranges) are read one lane per item in 16-byte chunks, U chunks in
-// flight per lane; long sub-runs (the hot ranges) by the whole wave, 256 PCs
-// per row and UB rows in flight.  Either way one VMEM instruction carries up
-// to 1 KB and the per-PC work is a subtract, a shift and one LDS bit test.
+// short item slices.  A wave takes 64 items at a time and reads each item's
+// sub-run with a group of 4 lanes (16 items per step, 16-byte chunks, 4 in
+// flight per lane), so a load instruction covers 16 sub-runs in 64-B pieces
+// instead of 64 scattered 16-B pieces; the per-PC work is a subtract, a shift
+// and one LDS bit test.  (A whole-wave path for long
+// sub-runs remains for the SMALL_M variants.)
 //
 // Record overflow (more uncovered occurrences than rec_cap, only for
 // adversarial corpora) is detected on the device; the fallback kernels then
@@ -41,7 +42,6 @@ namespace mr {
 
 constexpr int THREADS = 1024;
 constexpr int NWAVE = THREADS / 64;
-constexpr int U = 8;             // 16-byte chunks in flight per lane (short sub-runs)
 constexpr int UB = 4;            // 256-PC rows in flight per wave (long sub-runs)
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
@@ -138,7 +138,7 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint
 // SMALL_M: sub-runs up to this length take the lane-per-item path.
 // TEST = false is a tuning variant that streams the data without the
 // covered tests (not exact; selected only through SYZCOV_MR_CFG).
-template <uint32_t SMALL_M, bool TEST, bool WHOLE = false>
+template <uint32_t SMALL_M, bool TEST, bool WHOLE = false, int GS = 8, int UG = 4>
 __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b, uint32_t P,
                                                         int load_cov) {
     extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
@@ -180,27 +180,42 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
             st = A.base_r[item] + s0;
             m = s1 - s0;
         }
-        // ---- (1) short sub-runs: one lane per item, 16-byte chunks, U in flight
-        {
-            const bool mine = m > 0 && m <= SMALL_M;
-            const uint64_t a0 = st & ~3ull;
-            const uint32_t head = (uint32_t)(st - a0), end = head + m;
+        // ---- (1) sub-runs up to SMALL_M PCs: GS lanes per item, 64 / GS
+        // items per step.  A lane group reads its sub-run in consecutive
+        // 16-byte chunks (GS * 16 B per load instruction and item), so one
+        // instruction touches a few whole lines instead of 64 scattered ones;
+        // UG chunks per lane are in flight.  Default GS = 4, UG = 4 (256 B
+        // per item and step): minimize 7.0 -> 4.6 ms at C2 against one lane
+        // per item (sweep: tools/sweep_mr_parity.sh).
+        for (uint32_t pss = 0; pss < (uint32_t)GS; pss++) {  // 64 / GS items per step
+            const uint32_t gi = l / GS, gl = l % GS, sl = pss * (64 / GS) + gi;
+            const uint32_t st_lo = __shfl((uint32_t)st, sl, 64);
+            const uint32_t st_hi = __shfl((uint32_t)(st >> 32), sl, 64);
+            const uint32_t mi = __shfl(m, sl, 64);
+            const int32_t rki = __shfl(rk, sl, 64);
+            const uint64_t sti = (uint64_t)st_lo | ((uint64_t)st_hi << 32);
+            const bool mine = mi > 0 && mi <= SMALL_M;
+            const uint64_t a0 = sti & ~3ull;
+            const uint32_t head = (uint32_t)(sti - a0), end = head + mi;
             const uint32_t nch = mine ? (end + 3) >> 2 : 0u;
             const uint32_t maxch = wave_max(nch);
             const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
-            for (uint32_t c0 = 0; c0 < maxch; c0 += U) {
-                uint4 v[U];
+            for (uint32_t c0 = 0; c0 < maxch; c0 += GS * UG) {
+                uint4 v[UG];
 #pragma unroll
-                for (int u = 0; u < U; u++)
-                    v[u] = c0 + u < nch ? src[c0 + u] : make_uint4(0, 0, 0, 0);
+                for (int u = 0; u < UG; u++) {
+                    const uint32_t ch = c0 + u * GS + gl;
+                    v[u] = ch < nch ? src[ch] : make_uint4(0, 0, 0, 0);
+                }
                 uint32_t um = 0;
 #pragma unroll
-                for (int u = 0; u < U; u++) {
+                for (int u = 0; u < UG; u++) {
+                    const uint32_t ch = c0 + u * GS + gl;
                     const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t idx = (c0 + u) * 4 + k;
-                        const bool valid = c0 + u < nch && idx >= head && idx < end;
+                        const uint32_t idx = ch * 4 + k;
+                        const bool valid = ch < nch && idx >= head && idx < end;
                         const uint32_t bit = valid ? vv[k] - A.pc_lo - rbase : 0u;
                         if (TEST && WHOLE) {  // probe: window-wide test in global memory
                             const uint32_t wo = valid ? vv[k] - A.pc_lo : 0u;
@@ -222,17 +237,17 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                     if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)tot);
                     uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
                     if (um) {
-                        A.cand[item] = 1;
+                        A.cand[ib + sl] = 1;
 #pragma unroll
-                        for (int u = 0; u < U; u++) {
+                        for (int u = 0; u < UG; u++) {
                             const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                             for (int k = 0; k < 4; k++)
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = vv[k] - A.pc_lo;
-                                    atomicMin(&A.first_w[wo], rk);
+                                    atomicMin(&A.first_w[wo], rki);
                                     if (slot < A.rec_cap)
-                                        A.rec[slot] = ((unsigned long long)(uint32_t)rk << 32) | wo;
+                                        A.rec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
                                     slot++;
                                 }
                         }
@@ -511,20 +526,28 @@ extern "C" int syzcov_dev_minimize_range(
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
-    // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (96),
+    // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (32-lane groups),
     // 1 = lane-per-item never, 2 = always, 3..5 = the same without tests;
     // pmode 0 = slice-major (P = 2R), 1 = range-major (one slice; default:
     // 7.1 vs 8.0 ms at C2)
     int variant = 0, pmode = 1;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    const K kern[8] = {mr::pass1_kernel<96, true>, mr::pass1_kernel<0, true>,
-                       mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
-                       mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
-                       mr::pass1_kernel<96, false, true>, mr::pass1_kernel<96, true, true>};
-    const int vi = variant >= 0 && variant < 8 ? variant : 0;
+    // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
+    // minimize ms: (4,4) 4.6, (2,8) 4.9, (4,8) 5.0, (4,2) 5.05, (2,4) 5.05,
+    // (8,2) 5.7, (8,4) 5.9, (16,2) 8.4, one lane per item (old) 7.0
+    constexpr int NVAR = 12;
+    const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>, mr::pass1_kernel<0, true>,
+                          mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
+                          mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
+                          mr::pass1_kernel<96, false, true>, mr::pass1_kernel<96, true, true>,
+                          mr::pass1_kernel<0x40000000, true, false, 2, 8>,
+                          mr::pass1_kernel<0x40000000, true, false, 4, 2>,
+                          mr::pass1_kernel<0x40000000, true, false, 4, 8>,
+                          mr::pass1_kernel<0x40000000, true, false, 2, 4>};
+    const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
-    static bool attr_set[8] = {false, false, false, false, false, false, false, false};
+    static bool attr_set[NVAR] = {};
     if (!attr_set[vi]) {
         SYZ_HIP(hipFuncSetAttribute((const void *)k1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     128 * 1024));
