@@ -231,7 +231,11 @@ def bench_prio(args):
                "synth_lens")
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
-    dt, phl = timed(lambda ev: eng.step(lens, ev), len(phases), args, world, dev)
+    reduce = None
+    if world > 1:  # sharded by program: int32 SUM all-reduce of the counts
+        from syzkaller_amd.dist import merge_counts
+        reduce = merge_counts
+    dt, phl = timed(lambda ev: eng.step(lens, ev, reduce), len(phases), args, world, dev)
     ph = dict(zip(phases, phl))
     ops = eng.gemm_ops()
     achieved = ops / (ph["gemm"] * 1e-3) / 1e12
@@ -243,7 +247,9 @@ def bench_prio(args):
         "data": "synthetic program lengths ~ N(30, 8) (SURVEY §8d C4)",
         "config": {"workload": "C4: CalculatePriorities, positional (reference-exact) keys",
                    "programs_per_gpu": nprog, "calls": eng.C, "at_rows": eng.rows,
-                   "at_cols": eng.ldp},
+                   "at_cols": eng.ldp,
+                   "parallelism": f"shard-by-program x{world}"
+                                  + (", int32 SUM all-reduce of counts" if world > 1 else "")},
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},
         "roofline": {"bound": "mfma", "kernel": "prio_gemm", "achieved": achieved,
                      "peak": I8_PEAK_TOPS, "unit": "TOPS", "frac": achieved / I8_PEAK_TOPS,

@@ -53,6 +53,13 @@ def merge_first(first: torch.Tensor) -> None:
     _all_reduce(first, dist.ReduceOp.MIN)
 
 
+def merge_counts(counts: torch.Tensor) -> None:
+    """CalculatePriorities sharded by program: each rank's
+    int32 co-occurrence counts AᵀA of its own programs; the global counts are
+    their SUM (exact: the contraction is linear in the programs)."""
+    _all_reduce(counts, dist.ReduceOp.SUM)
+
+
 def merge_kept(kept: torch.Tensor) -> None:
     """kept[] is indexed by global rank; each rank set only its own items."""
     _all_reduce(kept, dist.ReduceOp.MAX)

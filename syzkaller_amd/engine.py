@@ -245,7 +245,9 @@ class PrioEngine:
         nt = self.rows // 128
         return nt * (nt + 1) // 2 * 128 * 128 * 2 * self.ldp
 
-    def step(self, lens: torch.Tensor, ev=None):
+    def step(self, lens: torch.Tensor, ev=None, reduce=None):
+        """`reduce(counts)` (sharded by program: dist.merge_counts) runs
+        between the contraction and the normalisation."""
         L, s = self.L, _stream()
 
         def mark_ev(i):
@@ -263,6 +265,8 @@ class PrioEngine:
         mark_ev(2)
         check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
                                        _p(self.counts), s), "dev_prio_counts")
+        if reduce is not None:
+            reduce(self.counts)
         mark_ev(3)
         check(L.syzcov_dev_prio_finish(_p(self.counts), self.C, _p(self.static), _p(self.out),
                                        None, s), "dev_prio_finish")

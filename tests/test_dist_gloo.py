@@ -85,3 +85,36 @@ def test_sharded_range_exchange_matches_oracle(world):
     for rank, kept_idx, union in res:
         assert kept_idx == exp_kept, rank
         assert union == exp_union, rank
+
+
+def _worker_prio(rank, world, port, q):
+    """CalculatePriorities sharded by program: each rank's raw co-occurrence
+    counts (emulated by the oracle) merged with the product's merge_counts."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from syzkaller_amd import dist as sdist
+        lens = orc.synth_lens(0x5EED0004, 500, 30, 8, first=rank * 500).astype(np.int32)
+        counts = torch.from_numpy(orc.dynamic_raw(lens, 64).astype(np.int32))
+        sdist.merge_counts(counts)
+        q.put((rank, counts.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_prio_counts_sum():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_prio, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    lens = orc.synth_lens(0x5EED0004, 500 * world, 30, 8).astype(np.int32)
+    exp = orc.dynamic_raw(lens, 64).astype(np.int32)
+    for rank, c in res:
+        assert np.array_equal(c, exp), rank
