@@ -109,6 +109,17 @@ int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *
  * out must hold the total PC count; returns |union|. */
 int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n, uint32_t *out);
 
+/* Manager.uniqueCover (syz-manager/html.go:213-238): the sorted PCs counted
+ * exactly once over the corpus.  call == NULL is uniqueCover(false): every
+ * occurrence counts, duplicates inside a cover included.  call != NULL
+ * (one int32 key per input, INT32_MIN reserved) is uniqueCover(true): a PC
+ * counts once per call group, so it is unique iff one group holds it.
+ * out capacity: the corpus' distinct PC count (<= total PCs).  Returns the
+ * count.  UI callers: httpSummary (:86-95), httpCorpus (:155-169), httpCover
+ * (:203-205) intersect per-call or per-input covers with it. */
+int64_t syzcov_unique_cover(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                            size_t n, uint32_t *out);
+
 /* prog.CalculatePriorities (prog/prio.go:29-38) given the static matrix
  * (calcStaticPriorities, :40-135, stays with the caller: it depends only on
  * sys.Calls).  key_mode 0 = positional, exactly the reference's
@@ -178,6 +189,22 @@ size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc);
 int syzcov_state_newcov_dev(syzcov_cover_state st, const int32_t *callid, const uint64_t *rec_off,
                             const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
                             uint32_t *stats, void *ws, size_t ws_size, void *stream);
+
+/* Executor output of one program (writer executor/executor.cc:455-466,
+ * reader ipc/ipc.go:225-291: u32 ncmd, then per completed call u32
+ * call_index, call_num, errno, cover_size, pcs[cover_size], little-endian)
+ * -> the records syz-fuzzer execute() checks (fuzzer.go:456-460): calls in
+ * index order, empty covers skipped.  call_num[i] = p.Calls[i].Meta.ID (the
+ * reader's consistency check), callid_of_num[num] = sys.Calls[num].CallID.
+ * Writes errnos[ncalls] (int64: -1 = not executed, else the u32 value) and, per record, rec_callid,
+ * rec_call_index and CSR rec_off[nrec+1] / rec_pcs (capacity pcs_cap).
+ * Returns nrec; a malformed buffer (the reader's error cases) returns < 0.
+ * Host only: append programs and hand the batch to syzcov_newcov_batch. */
+int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncalls,
+                                 const uint32_t *call_num, const int32_t *callid_of_num,
+                                 size_t nnum, int64_t *errnos, int32_t *rec_callid,
+                                 uint32_t *rec_call_index, uint64_t *rec_off, uint32_t *rec_pcs,
+                                 size_t pcs_cap);
 
 /* =================== 2. device-resident launch API ==================== */
 /* All pointers below are device pointers; `stream` is a hipStream_t.

@@ -1,4 +1,5 @@
-"""Pure-Python literal restatement of cover/cover.go and Go's sort.Sort, used
+"""Pure-Python literal restatement of cover/cover.go, Go's sort.Sort and the
+manager's uniqueCover (syz-manager/html.go:213-238), used
 only to cross-check the C oracle on small cases (two independent
 transcriptions of the same published algorithms).  TEST INFRASTRUCTURE ONLY.
 """
@@ -258,3 +259,49 @@ def minimize(covers):  # cover.go:104-131
             if hit:
                 covered.add(pc)
     return out
+
+
+def unique_cover(calls, covers, per_call):  # syz-manager/html.go:213-238
+    total = {}
+    call_cover = {}
+    for c, cov in zip(calls, covers):
+        if per_call and c not in call_cover:
+            call_cover[c] = set()
+        for pc in cov:
+            pc = int(pc)
+            if per_call:
+                if pc in call_cover[c]:
+                    continue
+                call_cover[c].add(pc)
+            total[pc] = total.get(pc, 0) + 1
+    return canonicalize([pc for pc, n in total.items() if n == 1])
+
+
+def parse_exec_output(out, call_num, callid_of_num):
+    """ipc/ipc.go:225-291 + the fuzzer.go:456-460 walk, literally.  Raises on
+    the reader's error cases (ValueError; IndexError where Go panics)."""
+    import struct
+    pos = 0
+
+    def rd():
+        nonlocal pos
+        if len(out) - pos < 4:
+            raise ValueError("short read")
+        v = struct.unpack_from("<I", out, pos)[0]
+        pos += 4
+        return v
+    ncmd = rd()
+    cov = [None] * len(call_num)
+    errnos = [-1] * len(call_num)
+    for _ in range(ncmd):
+        ci, num, err, sz = rd(), rd(), rd(), rd()
+        if ci > len(cov):
+            raise ValueError("call index")
+        if cov[ci] is not None:  # IndexError for ci == len(cov), as Go panics
+            raise ValueError("double coverage")
+        if call_num[ci] != num:
+            raise ValueError("call num")
+        cov[ci] = [rd() for _ in range(sz)]
+        errnos[ci] = err  # int(uint32) in Go
+    recs = [(callid_of_num[call_num[i]], i, c) for i, c in enumerate(cov) if c]
+    return errnos, recs

@@ -48,6 +48,7 @@ _SIGS = {
     "syzcov_sort_order": (C.c_int, [p_, sz, C.c_int, p_]),
     "syzcov_minimize_corpus": (i64, [p_, p_, p_, sz, C.c_int, p_]),
     "syzcov_union_all": (i64, [p_, p_, sz, p_]),
+    "syzcov_unique_cover": (i64, [p_, p_, p_, sz, p_]),
     "syzcov_calculate_priorities": (C.c_int, [p_, p_, sz, C.c_int, C.c_int, p_, p_, p_]),
     "syzcov_static_priorities": (C.c_int, [p_, p_, p_, sz, p_, p_, p_, C.c_int, p_]),
     "syzcov_dev_static_prio": (C.c_int, [p_, p_, p_, p_, p_, p_, C.c_int, p_, p_]),
@@ -59,6 +60,7 @@ _SIGS = {
     "syzcov_state_set_flakes": (C.c_int, [u64, p_, sz]),
     "syzcov_state_get": (i64, [u64, C.c_int, p_, sz]),
     "syzcov_newcov_batch": (i64, [u64, p_, p_, p_, sz, p_]),
+    "syzcov_parse_exec_output": (i64, [p_, sz, sz, p_, p_, sz, p_, p_, p_, p_, p_, sz]),
     "syzcov_state_set_universe": (C.c_int, [u64, p_, sz]),
     "syzcov_state_newcov_ws_size": (sz, [sz, u64]),
     "syzcov_state_newcov_dev": (C.c_int, [u64, p_, p_, p_, sz, u64, p_, p_, p_, sz, p_]),

@@ -148,3 +148,22 @@ def MinimizeCorpus(calls, corpus, variant: int = 0) -> list:
     k = check(lib().syzcov_minimize_corpus(_ptr(cid), _ptr(off), _ptr(pcs), n, variant,
                                            _ptr(out)), "MinimizeCorpus")
     return out[:k].tolist()
+
+
+def UniqueCover(corpus, calls=None) -> np.ndarray:
+    """Manager.uniqueCover (syz-manager/html.go:213-238): PCs counted exactly
+    once; calls=None is uniqueCover(false) (every occurrence counts), a call
+    key per input is uniqueCover(true) (once per call group)."""
+    off, pcs = to_csr(corpus)
+    n = off.size - 1
+    out = np.empty(max(int(off[-1]) if n > 0 else 0, 1), dtype=np.uint32)
+    if n <= 0:
+        return out[:0]
+    cp = None
+    if calls is not None:
+        cid = np.ascontiguousarray(np.asarray(calls, dtype=np.int32))
+        if cid.size != n:
+            raise ValueError("one call key per corpus input")
+        cp = _ptr(cid)
+    k = check(lib().syzcov_unique_cover(cp, _ptr(off), _ptr(pcs), n, _ptr(out)), "UniqueCover")
+    return out[:k]

@@ -214,6 +214,10 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
 // ------------------------------------------------------------------ corpus
 namespace syz {
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
+int unique_cover_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
+                        const uint64_t *tab, uint64_t span, uint32_t pc_lo, uint32_t nids,
+                        uint32_t *cnt, int32_t *owner, uint8_t *flag, int32_t *pc_of,
+                        hipStream_t s);
 int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
                           uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
                           hipStream_t s);
@@ -466,6 +470,60 @@ int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, con
     if (!c) return SYZCOV_ENODEV;
     std::vector<void *> owned;
     const int64_t rc = minimize_corpus_impl(c, call, offsets, pcs, n, sort_variant, out_idx, owned);
+    hipStreamSynchronize(c->s);
+    free_all(owned);
+    return rc;
+}
+
+// Manager.uniqueCover (syz-manager/html.go:213-238).
+static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
+                                 const uint32_t *pcs, size_t n, uint32_t *out,
+                                 std::vector<void *> &owned) {
+    for (size_t i = 0; call && i < n; i++)
+        if (call[i] == INT32_MIN) {
+            set_error("call key INT32_MIN is reserved");
+            return SYZCOV_EINVAL;
+        }
+    CorpusDev cd;
+    RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    const uint32_t nids = cd.n_ids;
+    if (nids == 0) return 0;
+    Plan p;
+    size_t i_call = p.add(call ? n * 4 : 4), i_cnt = p.add((size_t)nids * 4 + 4),
+           i_own = p.add((size_t)nids * 4 + 4), i_flag = p.add(nids), i_pc = p.add((size_t)nids * 4),
+           i_out = p.add((size_t)nids * 4), i_n = p.add(4),
+           i_ws = p.add(syzcov_dev_compact_ws_size(nids));
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    if (call) CK(hipMemcpyAsync(b[i_call], call, n * 4, hipMemcpyHostToDevice, c->s));
+    RC(unique_cover_launch(cd.off, cd.pcs, (uint32_t)n, call ? (const int32_t *)b[i_call] : nullptr,
+                           cd.tab, cd.span, cd.pc_lo, nids, (uint32_t *)b[i_cnt],
+                           (int32_t *)b[i_own], b[i_flag], (int32_t *)b[i_pc], c->s));
+    RC(syzcov_dev_compact_kept(b[i_flag], (const int32_t *)b[i_pc], nids, (int32_t *)b[i_out],
+                               (uint32_t *)b[i_n], b[i_ws], c->s));
+    uint32_t k = 0;
+    CK(hipMemcpyAsync(&k, b[i_n], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (k) {
+        CK(hipMemcpyAsync(out, b[i_out], (size_t)k * 4, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    // the reference ends with cover.Canonicalize (`last := sent`): a lone
+    // 0xFFFFFFFF is dropped
+    if (k == 1 && out[0] == 0xFFFFFFFFu) k = 0;
+    return (int64_t)k;
+}
+
+int64_t syzcov_unique_cover(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                            size_t n, uint32_t *out) {
+    if (n == 0) return 0;
+    if (!offsets || !out || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
+    if (offsets[n] == offsets[0]) return 0;
+    if (!pcs) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    std::vector<void *> owned;
+    const int64_t rc = unique_cover_impl(c, call, offsets, pcs, n, out, owned);
     hipStreamSynchronize(c->s);
     free_all(owned);
     return rc;

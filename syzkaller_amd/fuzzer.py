@@ -71,3 +71,26 @@ class CoverState:
         check(lib().syzcov_newcov_batch(self.h, _ptr(cid), _ptr(off), _ptr(pcs), nrec,
                                         _ptr(is_new)), "newcov_batch")
         return is_new[:nrec]
+
+
+def parse_exec_output(out: bytes, call_num, callid_of_num):
+    """Executor output of one program (ipc/ipc.go:225-291) -> (errnos,
+    records) where records = (callid[], call_index[], off[], pcs[]) are the
+    calls execute() checks (fuzzer.go:456-460), in call order, empty covers
+    skipped.  Host-side parser of libsyzcov (no GPU needed)."""
+    buf = np.frombuffer(out, dtype=np.uint8)
+    buf = np.ascontiguousarray(buf) if buf.size else np.zeros(1, np.uint8)
+    cn = np.ascontiguousarray(call_num, dtype=np.uint32)
+    cmap = np.ascontiguousarray(callid_of_num, dtype=np.int32)
+    nc = cn.size
+    errnos = np.empty(max(nc, 1), np.int64)
+    rcid = np.empty(max(nc, 1), np.int32)
+    rci = np.empty(max(nc, 1), np.uint32)
+    roff = np.zeros(nc + 1, np.uint64)
+    cap = max(len(out) // 4, 1)
+    pcs = np.empty(cap, np.uint32)
+    n = check(lib().syzcov_parse_exec_output(_ptr(buf), len(out), nc, _ptr(cn) if nc else None,
+                                             _ptr(cmap) if cmap.size else None, cmap.size,
+                                             _ptr(errnos), _ptr(rcid), _ptr(rci), _ptr(roff),
+                                             _ptr(pcs), cap), "parse_exec_output")
+    return errnos[:nc], (rcid[:n], rci[:n], roff[:n + 1], pcs[:int(roff[n])])

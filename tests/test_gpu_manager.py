@@ -172,3 +172,63 @@ def test_newcov_universe_mode(frac):
     with pytest.raises(SyzcovError):  # the universe is fixed once maxCover holds data
         st.set_universe(univ)
     st.close()
+
+
+@pytest.mark.parametrize("per_call", [False, True])
+def test_unique_cover_vs_reference(cover, per_call):
+    """Manager.uniqueCover (html.go:213-238) against its literal restatement,
+    with non-canonical covers (duplicates count per occurrence), sentinels
+    and wide PC ranges."""
+    from oracle import pyref
+    rng = np.random.default_rng(37 + per_call)
+    for trial in range(30):
+        n = int(rng.integers(1, 400))
+        hi = int(rng.choice([50, 5000, 1 << 32]))
+        calls = rng.integers(0, int(rng.choice([1, 4, 60])), size=n).astype(np.int32)
+        covs = [rng.integers(0, hi, size=int(rng.integers(0, 30)), dtype=np.uint64)
+                .astype(np.uint32) for _ in range(n)]
+        if trial % 7 == 0:
+            covs[0] = np.append(covs[0], np.uint32(0xFFFFFFFF))
+        exp = pyref.unique_cover(calls.tolist(), covs, per_call)
+        got = cover.UniqueCover(covs, calls if per_call else None)
+        assert got.tolist() == exp, (trial, per_call)
+    assert cover.UniqueCover([[0xFFFFFFFF]]).tolist() == []
+
+
+def test_unique_cover_synthetic(cover):
+    from oracle import pyref
+    off, pcs = orc.synth_corpus(0x5EED0001, 2000, mean=128, sigma=32, log2_space=14)
+    covs = [pcs[off[i]:off[i + 1]] for i in range(2000)]
+    calls = (np.arange(2000) % 37).astype(np.int32)
+    for per_call in (False, True):
+        exp = pyref.unique_cover(calls.tolist(), covs, per_call)
+        assert cover.UniqueCover(covs, calls if per_call else None).tolist() == exp
+
+
+def test_exec_output_to_newcov():
+    """executor output -> parse (host) -> one batched new-coverage check over
+    many programs == ipc.go reader + the sequential execute() loop."""
+    from oracle import pyref
+    from syzkaller_amd.fuzzer import CoverState, parse_exec_output
+    from tests.test_host import _exec_output
+    rng = np.random.default_rng(42)
+    ncalls_total = 293
+    callid_of_num = rng.integers(0, ncalls_total, size=1170).tolist()
+    lo, span = 0x81000000, 1 << 16
+    st = CoverState(ncalls_total, lo, span)
+    mc = [[] for _ in range(ncalls_total)]
+    cids, recs, exp_cids, exp_recs = [], [], [], []
+    for _ in range(300):
+        ncalls = int(rng.integers(1, 10))
+        call_num = rng.integers(0, 1170, size=ncalls).tolist()
+        out = _exec_output(rng, ncalls, call_num, lo=lo, span=span)
+        _, (cid, _ci, off, pcs) = parse_exec_output(out, call_num, callid_of_num)
+        cids += cid.tolist()
+        recs += [pcs[off[k]:off[k + 1]] for k in range(cid.size)]
+        _, r = pyref.parse_exec_output(out, call_num, callid_of_num)
+        exp_cids += [c for c, _, _ in r]
+        exp_recs += [np.array(c, np.uint32) for _, _, c in r]
+    assert cids == exp_cids
+    exp, mc = orc.newcov_batch(mc, [], exp_cids, exp_recs)
+    assert np.array_equal(st.new_coverage(cids, recs), exp)
+    st.close()

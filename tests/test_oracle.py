@@ -198,3 +198,16 @@ def test_new_input_is_newcov_without_flakes():
         assert acc == [bool(x) for x in is_new]
         for c in range(ncalls):
             assert list(mc[c]) == list(cc.get(c, []))
+
+
+def test_unique_cover_restatement():
+    """html.go:213-238 by hand: per input vs per call group."""
+    covs = [[1, 2, 3], [3, 4], [4, 5, 5], [6]]
+    calls = ["a", "a", "b", "b"]
+    # per input: 3 twice, 4 twice, 5 twice (duplicate inside one cover counts)
+    assert pyref.unique_cover(calls, covs, False) == [1, 2, 6]
+    # per call: a = {1,2,3,4}, b = {4,5,6}: 4 is in both
+    assert pyref.unique_cover(calls, covs, True) == [1, 2, 3, 5, 6]
+    # the final Canonicalize drops a lone 0xFFFFFFFF
+    assert pyref.unique_cover(["a"], [[0xFFFFFFFF]], False) == []
+
