@@ -10,7 +10,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsyzcov.so")
+# SYZCOV_LIB: a variant build for tuning sweeps (tools/); default is the in-tree library
+LIB_PATH = os.environ.get("SYZCOV_LIB") or os.path.join(_HERE, "libsyzcov.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "syzcov.h")
 
 OK, EINVAL, ENOTSORTED, ENODEV, EHIP, ERANGE, ENOMEM, ETOOLONG = 0, -1, -2, -3, -4, -5, -6, -7

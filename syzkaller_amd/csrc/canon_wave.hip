@@ -43,6 +43,12 @@ int canon_bitonic_launch(int W, const uint64_t *off, const uint32_t *raw, uint32
                          uint32_t *err, const uint32_t *list, const uint32_t *cnt, uint64_t nseg,
                          hipStream_t s);
 
+#ifndef SYZ_CANON_W32
+#define SYZ_CANON_W32 3
+#endif
+#ifndef SYZ_CANON_W48
+#define SYZ_CANON_W48 3
+#endif
 namespace cw {
 
 constexpr int WPB = 2;        // waves per workgroup (independent segments)
@@ -55,10 +61,19 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Exclusive scan of the 512-entry histogram in place (8 entries per lane).
+// The histogram is PACKED: one u32 per digit holds the current pass's running
+// slot in its low 16 bits and the next pass's digit count in its high 16 bits
+// (a segment holds < 2^16 keys, so neither half overflows into the other).
+// One 2 KB array per wave instead of two raises LDS-limited residency.
+constexpr uint32_t CNT1 = 1u << 16;  // +1 on the high (count) half
+
+// Exclusive scan of the counts (high halves) into slots (low halves), with the
+// high halves cleared for the next pass's counts (8 entries per lane).
 __device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
     uint4 a = h4[2 * l], b = h4[2 * l + 1];
+    a.x >>= 16; a.y >>= 16; a.z >>= 16; a.w >>= 16;
+    b.x >>= 16; b.y >>= 16; b.z >>= 16; b.w >>= 16;
     const uint32_t s = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
     uint32_t p = wave_incl_scan(s) - s;
     uint4 oa, ob;
@@ -73,6 +88,41 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
     h4[2 * l] = make_uint4(0, 0, 0, 0);
     h4[2 * l + 1] = make_uint4(0, 0, 0, 0);
+}
+
+// One radix scatter over the active rows: ranks by ds_add_rtn on the low
+// halves, writes each key to its slot, and counts the next pass's digit into
+// the high halves.  The atomics of BQ row quads are issued before their
+// stores: a store's address depends on its atomic's return, and the compiler
+// does not move a later atomic above an earlier store, so one store per
+// atomic would expose a full LDS round trip per row.  Atomics of a wave apply
+// in program order, so the row-major ranking order (stability) is unchanged.
+#ifndef SYZ_CANON_BQ
+#define SYZ_CANON_BQ 2
+#endif
+template <int NK, int BQ = SYZ_CANON_BQ>
+__device__ __forceinline__ void scatter_rows(const uint32_t (&k)[NK], uint32_t nq, uint32_t *buf,
+                                             uint32_t *hist, uint32_t sh, uint32_t dmask,
+                                             uint32_t dbits, bool count_next) {
+    constexpr int NQ = NK / 4;
+    static_assert(NQ % BQ == 0, "row quads per batch");
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += BQ) {
+        if ((uint32_t)q0 >= nq) continue;
+        uint32_t pos[4 * BQ];
+#pragma unroll
+        for (int j = 0; j < 4 * BQ; j++)
+            if ((uint32_t)(q0 + j / 4) < nq) pos[j] = atomicAdd(&hist[(k[q0 * 4 + j] >> sh) & dmask], 1u);
+#pragma unroll
+        for (int j = 0; j < 4 * BQ; j++)
+            if ((uint32_t)(q0 + j / 4) < nq) buf[pos[j] & 0xFFFFu] = k[q0 * 4 + j];
+        if (count_next) {
+#pragma unroll
+            for (int j = 0; j < 4 * BQ; j++)
+                if ((uint32_t)(q0 + j / 4) < nq)
+                    atomicAdd(&hist[(k[q0 * 4 + j] >> (sh + dbits)) & dmask], CNT1);
+        }
+    }
 }
 
 struct Params {
@@ -159,7 +209,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     constexpr int CAP = 64 * NK;
     constexpr int NQ = NK / 4;  // 16-byte loads per lane = row quads
     __shared__ uint32_t s_buf[WPB][CAP];
-    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][2][HIST];
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
@@ -228,34 +278,23 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
         if (li + nw < nl) issue(li + nw);
         if (__ballot(oob) && l == 0) *P.err = 1u;
         // ------------------------------------------- pass 0 (unstable)
-        hist_zero(s_hist[w][0], l);
-        hist_zero(s_hist[w][1], l);
+        hist_zero(s_hist[w], l);
         wave_sync();
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
 #pragma unroll
-                for (int c = 0; c < 4; c++) atomicAdd(&s_hist[w][0][k[q * 4 + c] & dmask], 1u);
+                for (int c = 0; c < 4; c++) atomicAdd(&s_hist[w][k[q * 4 + c] & dmask], CNT1);
             }
         wave_sync();
-        hist_scan(s_hist[w][0], l);
+        hist_scan(s_hist[w], l);
         wave_sync();
         const bool two = npass > 1;
-#pragma unroll
-        for (int q = 0; q < NQ; q++)
-            if ((uint32_t)q < nq) {
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const uint32_t key = k[q * 4 + c];
-                    buf[atomicAdd(&s_hist[w][0][key & dmask], 1u)] = key;
-                    if (two) atomicAdd(&s_hist[w][1][(key >> dbits) & dmask], 1u);
-                }
-            }
+        scatter_rows<NK>(k, nq, buf, s_hist[w], 0, dmask, dbits, two);
         wave_sync();
         // --------------------------------------------- stable passes
         for (uint32_t p = 1; p < npass; p++) {
             const uint32_t sh = p * dbits;
-            const uint32_t pc = p & 1, pn = pc ^ 1;
             const bool more = p + 1 < npass;
 #pragma unroll
             for (int q = 0; q < NQ; q++)
@@ -263,24 +302,23 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                     for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
                 }
-            hist_scan(s_hist[w][pc], l);
-            if (more) hist_zero(s_hist[w][pn], l);
+            hist_scan(s_hist[w], l);
             wave_sync();
-#pragma unroll
-            for (int q = 0; q < NQ; q++)
-                if ((uint32_t)q < nq) {
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const uint32_t key = k[q * 4 + c];
-                        buf[atomicAdd(&s_hist[w][pc][(key >> sh) & dmask], 1u)] = key;
-                        if (more) atomicAdd(&s_hist[w][pn][(key >> (sh + dbits)) & dmask], 1u);
-                    }
-                }
+            scatter_rows<NK>(k, nq, buf, s_hist[w], sh, dmask, dbits, more);
             wave_sync();
         }
         // --------------------------------- order check + unique + write
         // prev of slot e is slot e-1 (lane l-1 of the row, or lane 63 of the
         // previous row); the reference's `last := sent` for e == 0.
+        // The sorted rows are read once into registers: the LDS writes of the
+        // compaction below may not be reordered ahead of LDS reads, so reading
+        // row by row there would expose one LDS round trip per row.
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
+            }
         uint32_t bad = 0;
         if (inplace) {  // nothing may be written before the order is known
             uint32_t carry = P.sent_key;
@@ -290,7 +328,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                     for (int c = 0; c < 4; c++) {
                         const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
-                        const uint32_t v = buf[e];
+                        const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
                         bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
@@ -309,7 +347,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
-                    const uint32_t v = buf[e];
+                    const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
                     bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
@@ -489,8 +527,8 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
         case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, 3>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<48, 3>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         }
