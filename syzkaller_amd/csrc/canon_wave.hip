@@ -100,27 +100,51 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
 #ifndef SYZ_CANON_BQ
 #define SYZ_CANON_BQ 2
 #endif
-template <int NK, int BQ = SYZ_CANON_BQ>
-__device__ __forceinline__ void scatter_rows(const uint32_t (&k)[NK], uint32_t nq, uint32_t *buf,
+// Only REAL keys take part: slots outside the segment (the aligned head, the
+// tail of the last row quad) are skipped rather than ranked as maximal pads,
+// which would all hit ONE histogram address (serialised same-address LDS
+// atomics).  RAW: the keys are in the raw-load layout (slot (q*64+l)*4+c,
+// real iff in [lo, hi)); otherwise row-major (slot (q*4+c)*64+l, real iff
+// < hi).  Real keys always sort to [0, n), so later passes see them there.
+template <bool RAW, int NK>
+__device__ __forceinline__ bool real_slot(int j, uint32_t l, uint32_t lo, uint32_t hi) {
+    if (RAW) {
+        const uint32_t idx = (uint32_t)(((j >> 2) * 64 + l) * 4 + (j & 3));
+        return idx >= lo && idx < hi;
+    }
+    return (uint32_t)(j * 64) + l < hi;
+}
+
+// Pad slots are sent, branch-free, to a private dummy word of their lane
+// (hist[HIST + l], buf[cap + l]): distinct addresses, so they cost no
+// same-address serialisation, and they never touch the real counters/slots.
+template <bool RAW, int NK, int BQ = SYZ_CANON_BQ>
+__device__ __forceinline__ void scatter_rows(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
+                                             uint32_t lo, uint32_t hi, uint32_t *buf,
                                              uint32_t *hist, uint32_t sh, uint32_t dmask,
                                              uint32_t dbits, bool count_next) {
     constexpr int NQ = NK / 4;
+    constexpr uint32_t CAP = 64 * NK;
     static_assert(NQ % BQ == 0, "row quads per batch");
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += BQ) {
         if ((uint32_t)q0 >= nq) continue;
         uint32_t pos[4 * BQ];
+        bool ok[4 * BQ];
+#pragma unroll
+        for (int j = 0; j < 4 * BQ; j++) {
+            ok[j] = real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
+            if ((uint32_t)(q0 + j / 4) < nq)
+                pos[j] = atomicAdd(&hist[ok[j] ? (k[q0 * 4 + j] >> sh) & dmask : HIST + l], 1u);
+        }
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++)
-            if ((uint32_t)(q0 + j / 4) < nq) pos[j] = atomicAdd(&hist[(k[q0 * 4 + j] >> sh) & dmask], 1u);
-#pragma unroll
-        for (int j = 0; j < 4 * BQ; j++)
-            if ((uint32_t)(q0 + j / 4) < nq) buf[pos[j] & 0xFFFFu] = k[q0 * 4 + j];
+            if ((uint32_t)(q0 + j / 4) < nq) buf[ok[j] ? pos[j] & 0xFFFFu : CAP + l] = k[q0 * 4 + j];
         if (count_next) {
 #pragma unroll
             for (int j = 0; j < 4 * BQ; j++)
                 if ((uint32_t)(q0 + j / 4) < nq)
-                    atomicAdd(&hist[(k[q0 * 4 + j] >> (sh + dbits)) & dmask], CNT1);
+                    atomicAdd(&hist[ok[j] ? (k[q0 * 4 + j] >> (sh + dbits)) & dmask : HIST + l], CNT1);
         }
     }
 }
@@ -198,18 +222,19 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
 
 // NK = keys per lane (CAP = 64 * NK, NK a multiple of 4); MINW = waves per
 // SIMD the register budget must allow (LDS caps residency anyway).  Segments
-// come from a class list.  Slots outside the segment hold PAD (all digits
-// maximal), so every row is full and the sorted real keys are buf[0, n).  Each
-// pass counts the NEXT pass's digits while it scatters (two histograms), so a
-// pass is one read-back and one scatter loop; the keys of the pass being
-// scattered live in registers only between those two loops.
+// come from a class list.  Only the n real keys are ranked (real_slot), so
+// after every pass the sorted keys are buf[0, n); slots past n are stale and
+// never read as keys.  Each pass counts the NEXT pass's digits while it
+// scatters (packed histogram), so a pass is one read-back and one scatter
+// loop; the keys of the pass being scattered live in registers only between
+// those two loops.
 template <int NK, int MINW>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, const uint32_t *list,
                                                                     const uint32_t *count) {
     constexpr int CAP = 64 * NK;
     constexpr int NQ = NK / 4;  // 16-byte loads per lane = row quads
-    __shared__ uint32_t s_buf[WPB][CAP];
-    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST];
+    __shared__ uint32_t s_buf[WPB][CAP + 64];  // + one pad dummy per lane
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST + 64];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
@@ -284,13 +309,15 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
 #pragma unroll
-                for (int c = 0; c < 4; c++) atomicAdd(&s_hist[w][k[q * 4 + c] & dmask], CNT1);
+                for (int c = 0; c < 4; c++)
+                    atomicAdd(&s_hist[w][real_slot<true, NK>(q * 4 + c, l, head, end)
+                                             ? k[q * 4 + c] & dmask : HIST + l], CNT1);
             }
         wave_sync();
         hist_scan(s_hist[w], l);
         wave_sync();
         const bool two = npass > 1;
-        scatter_rows<NK>(k, nq, buf, s_hist[w], 0, dmask, dbits, two);
+        scatter_rows<true, NK>(k, nq, l, head, end, buf, s_hist[w], 0, dmask, dbits, two);
         wave_sync();
         // --------------------------------------------- stable passes
         for (uint32_t p = 1; p < npass; p++) {
@@ -304,7 +331,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                 }
             hist_scan(s_hist[w], l);
             wave_sync();
-            scatter_rows<NK>(k, nq, buf, s_hist[w], sh, dmask, dbits, more);
+            scatter_rows<false, NK>(k, nq, l, 0, n, buf, s_hist[w], sh, dmask, dbits, more);
             wave_sync();
         }
         // --------------------------------- order check + unique + write
