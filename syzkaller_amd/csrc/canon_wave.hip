@@ -46,6 +46,9 @@ int canon_bitonic_launch(int W, const uint64_t *off, const uint32_t *raw, uint32
 #ifndef SYZ_CANON_W32
 #define SYZ_CANON_W32 3
 #endif
+#ifndef SYZ_CANON_W40
+#define SYZ_CANON_W40 3
+#endif
 #ifndef SYZ_CANON_W48
 #define SYZ_CANON_W48 3
 #endif
@@ -555,7 +558,7 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         switch (c) {
         case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<40, 3>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         case 5: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
