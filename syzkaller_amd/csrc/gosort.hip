@@ -173,10 +173,10 @@ __global__ void seg_gather_kernel(const int32_t *__restrict__ I, const uint64_t 
 }
 
 // one lane per segment: control steps of one pdqsort loop iteration
-__global__ void plan_kernel(Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+__global__ void plan_kernel(Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
                             uint32_t *__restrict__ K, int32_t *__restrict__ I, Ctl c) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ncur) return;
+    if (s >= *ncur_p) return;
     Seg g = cur[s];
     Plan p{};
     const int n = g.b - g.a;
@@ -207,18 +207,20 @@ __global__ void plan_kernel(Seg *__restrict__ cur, uint32_t ncur, Plan *__restri
     plan[s] = p;
 }
 
-__global__ void heap_kernel(const Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+__global__ void heap_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
                             uint32_t *__restrict__ K, int32_t *__restrict__ I) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ncur || plan[s].mode != M_HEAP) return;
+    if (s >= *ncur_p || plan[s].mode != M_HEAP) return;
     GAcc d{K, I};
     gocore::heap_sort(d, cur[s].a, cur[s].b);
     plan[s].mode = M_DONE;
 }
 
-__global__ void reverse_kernel(const Seg *__restrict__ cur, const Plan *__restrict__ plan,
-                               uint32_t *__restrict__ K, int32_t *__restrict__ I) {
+__global__ void reverse_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
+                               const Plan *__restrict__ plan, uint32_t *__restrict__ K,
+                               int32_t *__restrict__ I) {
     const uint32_t s = blockIdx.y;
+    if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE || !p.rev) return;
     const Seg g = cur[s];
@@ -248,12 +250,13 @@ __device__ int wg_find_first_descent(const uint32_t *K, int from, int b, int *sh
 }
 
 __global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
+                                                  const uint32_t *__restrict__ ncur_p,
                                                   Plan *__restrict__ plan,
                                                   uint32_t *__restrict__ K,
                                                   int32_t *__restrict__ I) {
     __shared__ int sh[WG / 64 + 2];
     const uint32_t s = blockIdx.x;
-    if (plan[s].mode != M_ACTIVE || !plan[s].pis) return;
+    if (s >= *ncur_p || plan[s].mode != M_ACTIVE || !plan[s].pis) return;
     const Seg g = cur[s];
     const int a = g.a, b = g.b;
     int i = a + 1;
@@ -280,10 +283,10 @@ __global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
     if (threadIdx.x == 0 && sorted) plan[s].mode = M_DONE;
 }
 
-__global__ void eq_kernel(const Seg *__restrict__ cur, uint32_t ncur, Plan *__restrict__ plan,
+__global__ void eq_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
                           uint32_t *__restrict__ K, int32_t *__restrict__ I) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ncur || plan[s].mode != M_ACTIVE) return;
+    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
     const Seg g = cur[s];
     const int pivot = plan[s].pivot;
     GAcc d{K, I};
@@ -299,11 +302,13 @@ __device__ __forceinline__ bool left_group(uint32_t k, uint32_t kp, int eq) {
 }
 
 __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
+                                                    const uint32_t *__restrict__ ncur_p,
                                                     const Plan *__restrict__ plan,
                                                     const uint32_t *__restrict__ K,
                                                     uint32_t *__restrict__ cc, uint32_t stride) {
     __shared__ uint32_t tmp[WG / 64 + 1];
     const uint32_t s = blockIdx.y;
+    if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE) return;
     const Seg g = cur[s];
@@ -318,11 +323,12 @@ __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
 }
 
 __global__ __launch_bounds__(WG) void cscan_kernel(const Seg *__restrict__ cur,
+                                                    const uint32_t *__restrict__ ncur_p,
                                                     Plan *__restrict__ plan,
                                                     uint32_t *__restrict__ cc, uint32_t stride) {
     __shared__ uint32_t tmp[WG / 64 + 1];
     const uint32_t s = blockIdx.x;
-    if (plan[s].mode != M_ACTIVE) return;
+    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
     const Seg g = cur[s];
     const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
     uint32_t carry = 0;
@@ -343,6 +349,7 @@ __global__ __launch_bounds__(WG) void cscan_kernel(const Seg *__restrict__ cur,
 // ranks of the misplaced elements: PL[a + k] / PR[a + k] = position of the
 // k-th left-misplaced (from the left) / right-misplaced (from the right)
 __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
+                                                   const uint32_t *__restrict__ ncur_p,
                                                    Plan *__restrict__ plan,
                                                    const uint32_t *__restrict__ K,
                                                    const uint32_t *__restrict__ cc,
@@ -350,6 +357,7 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    int32_t *__restrict__ PR) {
     __shared__ uint32_t tmp[WG / 64 + 1];
     const uint32_t s = blockIdx.y;
+    if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE) return;
     const Seg g = cur[s];
@@ -378,10 +386,12 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
     if (__lane_id() == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
 }
 
-__global__ void swap_kernel(const Seg *__restrict__ cur, const Plan *__restrict__ plan,
+__global__ void swap_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
+                            const Plan *__restrict__ plan,
                             uint32_t *__restrict__ K, int32_t *__restrict__ I,
                             const int32_t *__restrict__ PL, const int32_t *__restrict__ PR) {
     const uint32_t s = blockIdx.y;
+    if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE) return;
     const Seg g = cur[s];
@@ -391,11 +401,11 @@ __global__ void swap_kernel(const Seg *__restrict__ cur, const Plan *__restrict_
         d.swap(PL[g.a + k], PR[g.a + k]);
 }
 
-__global__ void finish_kernel(const Seg *__restrict__ cur, uint32_t ncur,
+__global__ void finish_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
                               const Plan *__restrict__ plan, uint32_t *__restrict__ K,
                               int32_t *__restrict__ I, Ctl c) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ncur) return;
+    if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE) return;
     const Seg g = cur[s];
@@ -710,6 +720,7 @@ struct SortWs {
     uint32_t *cc;
     uint32_t *ctl;  // [0] err [1] countA [2] countB [3] small count [4] maxA [5] maxB
     uint32_t seg_cap, small_cap, cc_stride;
+    size_t n;  // positions
 };
 
 static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
@@ -740,6 +751,7 @@ static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
         w->seg_cap = seg_cap;
         w->small_cap = small_cap;
         w->cc_stride = cc_stride;
+        w->n = n;
     }
     return o;
 }
@@ -788,6 +800,13 @@ static int run_rounds(SortWs &w, hipStream_t s) {
     uint32_t h[6];
     SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
+    // The kernels read the live segment count from the device (ccount), so
+    // rounds are queued without a host round trip: the host keeps only UPPER
+    // BOUNDS for the grids (a segment has at most two large children, each
+    // shorter than it, and at most total/(SMALL+1) large segments exist) and
+    // reads the true count back every SYNC_EVERY rounds.
+    constexpr int SYNC_EVERY = 4;
+    const uint32_t cap_seg = std::min<uint32_t>(w.seg_cap, w.n / (SMALL + 1) + 1);
     uint32_t ncur = h[1], maxlen = h[4];
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
@@ -797,28 +816,35 @@ static int run_rounds(SortWs &w, hipStream_t s) {
         Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
         const unsigned gs = (ncur + 63) / 64;
         const unsigned nch = (unsigned)((maxlen + CH - 1) / CH);
-        hipLaunchKernelGGL(plan_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I, cn);
-        hipLaunchKernelGGL(heap_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(plan_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I, cn);
+        hipLaunchKernelGGL(heap_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I);
         hipLaunchKernelGGL(reverse_kernel, dim3((nch + 1) / 2 + 1, ncur), dim3(WG), 0, s, cur,
-                           w.plan, w.K, w.I);
-        hipLaunchKernelGGL(pis_kernel, dim3(ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.I);
-        hipLaunchKernelGGL(eq_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I);
-        hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.cc,
+                           ccount, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(pis_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(eq_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+                           w.cc, w.cc_stride);
+        hipLaunchKernelGGL(cscan_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.cc,
                            w.cc_stride);
-        hipLaunchKernelGGL(cscan_kernel, dim3(ncur), dim3(WG), 0, s, cur, w.plan, w.cc, w.cc_stride);
-        hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.cc,
-                           w.cc_stride, w.PL, w.PR);
-        hipLaunchKernelGGL(swap_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, w.plan, w.K, w.I, w.PL,
-                           w.PR);
-        hipLaunchKernelGGL(finish_kernel, dim3(gs), dim3(64), 0, s, cur, ncur, w.plan, w.K, w.I, cn);
+        hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+                           w.cc, w.cc_stride, w.PL, w.PR);
+        hipLaunchKernelGGL(swap_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+                           w.I, w.PL, w.PR);
+        hipLaunchKernelGGL(finish_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I,
+                           cn);
         SYZ_LAUNCH_CHECK();
-        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
-        ncur = h[ncount - w.ctl];
-        maxlen = h[nmax - w.ctl];
         std::swap(cur, nxt);
         std::swap(ccount, ncount);
         std::swap(cmax, nmax);
+        // bounds for the next round (exact after a read-back)
+        ncur = std::min(2 * ncur, cap_seg);
+        maxlen = maxlen > 1 ? maxlen - 1 : 0;
+        if ((round + 1) % SYNC_EVERY == 0 || maxlen <= SMALL) {
+            SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
+            SYZ_HIP(hipStreamSynchronize(s));
+            ncur = h[ccount - w.ctl];
+            maxlen = h[cmax - w.ctl];
+        }
     }
     if (!h[0] && h[3]) {
         hipLaunchKernelGGL(small_kernel, dim3(std::min<uint32_t>(h[3], 8192)), dim3(WG), 0, s, w.small,
