@@ -120,6 +120,23 @@ int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n,
 int64_t syzcov_unique_cover(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
                             size_t n, uint32_t *out);
 
+/* Manager UI statistics over a corpus of CANONICAL covers (the manager's
+ * corpus holds canonical covers; anything else -> SYZCOV_ENOTSORTED).
+ * Replaces the Union fold and Intersection calls of httpSummary
+ * (syz-manager/html.go:67-99) and httpCorpus (:157-175).  call[i] is input
+ * i's call group in [0, ncalls) (RpcInput.Call numbered by the caller).
+ * Per group g (each output nullable, all need call):
+ *   inputs[g]       = CallCov.count                              (:74-75)
+ *   cover[g]        = len(CallCov.cov), the Union fold            (:76)
+ *   unique_cover[g] = len(Intersection(cov, uniqueCover(true)))  (:86-90)
+ * Per input i (nullable; call may be NULL):
+ *   input_unique[i] = len(Intersection(inp.Cover, uniqueCover(false))) (:160-168)
+ * Returns len(Union of all covers), the "cover" stat (:92-97); the sentinel
+ * 0xFFFFFFFF is never counted, as Union/Intersection drop it. */
+int64_t syzcov_ui_stats(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                        size_t n, uint32_t ncalls, uint32_t *inputs, uint32_t *cover,
+                        uint32_t *unique_cover, uint32_t *input_unique);
+
 /* prog.CalculatePriorities (prog/prio.go:29-38) given the static matrix
  * (calcStaticPriorities, :40-135, stays with the caller: it depends only on
  * sys.Calls).  key_mode 0 = positional, exactly the reference's

@@ -277,6 +277,26 @@ def unique_cover(calls, covers, per_call):  # syz-manager/html.go:213-238
     return canonicalize([pc for pc, n in total.items() if n == 1])
 
 
+def summary_stats(calls, covers):  # syz-manager/html.go:67-99, literally
+    cc = {}
+    for c, cov in zip(calls, covers):
+        e = cc.setdefault(c, [0, []])
+        e[0] += 1
+        e[1] = union(e[1], [int(x) for x in cov])
+    total_unique = unique_cover(calls, covers, True)
+    cov_all, rows = [], []
+    for c, (count, ccov) in cc.items():
+        cov_all = union(cov_all, ccov)
+        rows.append((c, count, len(ccov), len(intersection(ccov, total_unique))))
+    return sorted(rows), len(cov_all)
+
+
+def corpus_stats(calls, covers, call):  # syz-manager/html.go:157-175 (before the sort)
+    total_unique = unique_cover(calls, covers, False)
+    return [(i, len(cov), len(intersection([int(x) for x in cov], total_unique)))
+            for i, (c, cov) in enumerate(zip(calls, covers)) if c == call]
+
+
 def parse_exec_output(out, call_num, callid_of_num):
     """ipc/ipc.go:225-291 + the fuzzer.go:456-460 walk, literally.  Raises on
     the reader's error cases (ValueError; IndexError where Go panics)."""

@@ -50,6 +50,7 @@ _SIGS = {
     "syzcov_minimize_corpus": (i64, [p_, p_, p_, sz, C.c_int, p_]),
     "syzcov_union_all": (i64, [p_, p_, sz, p_]),
     "syzcov_unique_cover": (i64, [p_, p_, p_, sz, p_]),
+    "syzcov_ui_stats": (i64, [p_, p_, p_, sz, u32, p_, p_, p_, p_]),
     "syzcov_calculate_priorities": (C.c_int, [p_, p_, sz, C.c_int, C.c_int, p_, p_, p_]),
     "syzcov_static_priorities": (C.c_int, [p_, p_, p_, sz, p_, p_, p_, C.c_int, p_]),
     "syzcov_dev_static_prio": (C.c_int, [p_, p_, p_, p_, p_, p_, C.c_int, p_, p_]),

@@ -167,3 +167,25 @@ def UniqueCover(corpus, calls=None) -> np.ndarray:
         cp = _ptr(cid)
     k = check(lib().syzcov_unique_cover(cp, _ptr(off), _ptr(pcs), n, _ptr(out)), "UniqueCover")
     return out[:k]
+
+
+def UIStats(corpus, calls, ncalls: int):
+    """The manager UI's coverage numbers (syz-manager/html.go) in one device
+    call over canonical covers: per call group g (calls[i] in [0, ncalls)) the
+    input count, len(Union of its covers) and len(Intersection(that union,
+    uniqueCover(true))) of httpSummary (:67-99); per input
+    len(Intersection(cover, uniqueCover(false))) of httpCorpus (:157-175);
+    and the total cover.  Returns (inputs, cover, unique_cover,
+    input_unique, total)."""
+    off, pcs = to_csr(corpus)
+    n = off.size - 1
+    cid = np.ascontiguousarray(np.asarray(calls, dtype=np.int32))
+    if cid.size != max(n, 0):
+        raise ValueError("one call group per corpus input")
+    inputs, cov, ucov = (np.zeros(max(ncalls, 1), dtype=np.uint32) for _ in range(3))
+    inu = np.zeros(max(n, 1), dtype=np.uint32)
+    if n <= 0:
+        return inputs[:ncalls], cov[:ncalls], ucov[:ncalls], inu[:0], 0
+    total = check(lib().syzcov_ui_stats(_ptr(cid), _ptr(off), _ptr(pcs), n, ncalls, _ptr(inputs),
+                                        _ptr(cov), _ptr(ucov), _ptr(inu)), "UIStats")
+    return inputs[:ncalls], cov[:ncalls], ucov[:ncalls], inu[:n], int(total)

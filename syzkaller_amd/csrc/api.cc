@@ -214,6 +214,11 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
 // ------------------------------------------------------------------ corpus
 namespace syz {
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
+int ui_stats_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
+                    uint32_t ncalls, const uint64_t *tab, uint32_t pc_lo, uint32_t nids,
+                    uint32_t sent_id, uint32_t *cnt_all, int32_t *own_all, uint32_t *cnt_call,
+                    int32_t *own_call, uint8_t *flag_all, uint32_t *slab, uint64_t slab_words,
+                    uint32_t *cover, uint32_t *ucov, uint32_t *in_unique, hipStream_t s);
 int unique_cover_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
                         const uint64_t *tab, uint64_t span, uint32_t pc_lo, uint32_t nids,
                         uint32_t *cnt, int32_t *owner, uint8_t *flag, int32_t *pc_of,
@@ -512,6 +517,85 @@ static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *of
     // 0xFFFFFFFF is dropped
     if (k == 1 && out[0] == 0xFFFFFFFFu) k = 0;
     return (int64_t)k;
+}
+
+// Manager UI statistics (html.go:67-99 httpSummary, :157-175 httpCorpus).
+static int64_t ui_stats_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
+                             const uint32_t *pcs, size_t n, uint32_t ncalls, uint32_t *inputs,
+                             uint32_t *cover, uint32_t *ucov, uint32_t *in_unique,
+                             std::vector<void *> &owned) {
+    for (size_t i = 0; i < n; i++) {
+        if (offsets[i + 1] < offsets[i]) return SYZCOV_EINVAL;
+        if (call && (call[i] < 0 || (uint32_t)call[i] >= ncalls)) {
+            set_error("call group %d of input %zu outside [0, %u)", call[i], i, ncalls);
+            return SYZCOV_EINVAL;
+        }
+        for (uint64_t k = offsets[i] + 1; k < offsets[i + 1]; k++)
+            if (pcs[k] <= pcs[k - 1]) {
+                set_error("cover of input %zu is not canonical", i);
+                return SYZCOV_ENOTSORTED;
+            }
+    }
+    if (inputs) {
+        std::fill(inputs, inputs + ncalls, 0u);
+        for (size_t i = 0; i < n; i++) inputs[call[i]]++;
+    }
+    const bool empty = offsets[n] == offsets[0];
+    CorpusDev cd{};
+    if (!empty) RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    const uint32_t nids = empty ? 0 : cd.n_ids;
+    if (nids == 0) {
+        if (cover) std::fill(cover, cover + ncalls, 0u);
+        if (ucov) std::fill(ucov, ucov + ncalls, 0u);
+        if (in_unique) std::fill(in_unique, in_unique + n, 0u);
+        return 0;
+    }
+    // 0xFFFFFFFF is the largest PC: if present, it is the last dense id
+    const bool has_sent = cd.pc_lo + (cd.span - 1) == 0xFFFFFFFFull;
+    const uint32_t sent_id = has_sent ? nids - 1 : 0xFFFFFFFFu;
+    const uint64_t wpg = ((uint64_t)nids + 31) / 32;
+    const uint64_t slab_words = call ? std::min<uint64_t>((uint64_t)ncalls * wpg, 64ull << 20) : 1;
+    Plan p;
+    size_t i_call = p.add(call ? n * 4 : 4), i_ca = p.add((size_t)nids * 4 + 4),
+           i_oa = p.add((size_t)nids * 4 + 4), i_cc = p.add((size_t)nids * 4 + 4),
+           i_oc = p.add((size_t)nids * 4 + 4), i_fl = p.add(nids),
+           i_slab = p.add(std::max<uint64_t>(slab_words, wpg) * 4), i_cov = p.add((size_t)ncalls * 4),
+           i_uc = p.add((size_t)ncalls * 4), i_in = p.add(n * 4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    if (call) CK(hipMemcpyAsync(b[i_call], call, n * 4, hipMemcpyHostToDevice, c->s));
+    RC(ui_stats_launch(cd.off, cd.pcs, (uint32_t)n, call ? (const int32_t *)b[i_call] : nullptr,
+                       ncalls, cd.tab, cd.pc_lo, nids, sent_id, (uint32_t *)b[i_ca],
+                       (int32_t *)b[i_oa], (uint32_t *)b[i_cc], (int32_t *)b[i_oc], b[i_fl],
+                       (uint32_t *)b[i_slab], std::max<uint64_t>(slab_words, wpg),
+                       (uint32_t *)b[i_cov], (uint32_t *)b[i_uc], (uint32_t *)b[i_in], c->s));
+    if (call && cover) CK(hipMemcpyAsync(cover, b[i_cov], (size_t)ncalls * 4, hipMemcpyDeviceToHost, c->s));
+    if (call && ucov) CK(hipMemcpyAsync(ucov, b[i_uc], (size_t)ncalls * 4, hipMemcpyDeviceToHost, c->s));
+    if (in_unique) CK(hipMemcpyAsync(in_unique, b[i_in], n * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    return (int64_t)nids - (has_sent ? 1 : 0);
+}
+
+int64_t syzcov_ui_stats(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                        size_t n, uint32_t ncalls, uint32_t *inputs, uint32_t *cover,
+                        uint32_t *unique_cover, uint32_t *input_unique) {
+    if (!offsets || n > 0x7FFFFFFF || (n && offsets[n] != offsets[0] && !pcs)) return SYZCOV_EINVAL;
+    if ((inputs || cover || unique_cover) && (!call || ncalls == 0)) return SYZCOV_EINVAL;
+    if (!call) ncalls = 0;
+    if (n == 0) {
+        if (inputs) std::fill(inputs, inputs + ncalls, 0u);
+        if (cover) std::fill(cover, cover + ncalls, 0u);
+        if (unique_cover) std::fill(unique_cover, unique_cover + ncalls, 0u);
+        return 0;
+    }
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    std::vector<void *> owned;
+    const int64_t rc = ui_stats_impl(c, call, offsets, pcs, n, ncalls, inputs, cover, unique_cover,
+                                     input_unique, owned);
+    hipStreamSynchronize(c->s);
+    free_all(owned);
+    return rc;
 }
 
 int64_t syzcov_unique_cover(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,

@@ -7,7 +7,9 @@
                     is then Union-ed with it.  A batch of inputs is checked in
                     one device call (syzcov_newcov_batch with an empty flakes
                     set, which is exactly this predicate and update, applied
-                    in batch order).
+                    in batch order);
+  summary_stats     httpSummary's per-call coverage table (html.go:67-99);
+  corpus_stats      httpCorpus's per-input cover / unique-cover (:157-175).
 """
 from __future__ import annotations
 
@@ -56,3 +58,43 @@ class CorpusCover:
 
     def close(self):
         self.state.close()
+
+
+@dataclass
+class UICallType:  # html.go:427-432
+    Name: str
+    Inputs: int
+    Cover: int
+    UniqueCover: int
+
+
+def summary_stats(corpus: list) -> tuple[list, int]:
+    """httpSummary (html.go:67-99): one UICallType per call, sorted by Name
+    (UICallTypeArray.Less, :446), and the "cover" stat (len of the union of
+    every call's cover).  One device call (syzcov_ui_stats)."""
+    names = sorted({inp.Call for inp in corpus})
+    gid = {c: i for i, c in enumerate(names)}
+    inputs, cov, ucov, _, total = cover.UIStats([inp.Cover for inp in corpus],
+                                                [gid[inp.Call] for inp in corpus], len(names))
+    return [UICallType(c, int(inputs[i]), int(cov[i]), int(ucov[i])) for i, c in enumerate(names)], total
+
+
+@dataclass
+class UIInput:  # html.go:434-441 (Short/Full need prog.Deserialize: not coverage work)
+    N: int
+    Cover: int
+    UniqueCover: int
+
+
+def corpus_stats(corpus: list, call: str) -> list:
+    """httpCorpus (html.go:157-175): the inputs of `call` with len(Cover) and
+    len(Intersection(Cover, uniqueCover(false))), in the order Go's
+    sort.Sort(UIInputArray) leaves them (Less = Cover >, :452) -- the same
+    comparator as Minimize's sort, so the device restatement of sort.Sort
+    gives the reference's tie order too."""
+    if not corpus:
+        return []
+    _, _, _, inu, _ = cover.UIStats([inp.Cover for inp in corpus], [0] * len(corpus), 1)
+    data = [UIInput(i, len(inp.Cover), int(inu[i])) for i, inp in enumerate(corpus) if inp.Call == call]
+    order = cover.SortOrder([d.Cover for d in data]) if data else []
+    return [data[j] for j in order]

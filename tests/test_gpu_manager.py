@@ -232,3 +232,45 @@ def test_exec_output_to_newcov():
     exp, mc = orc.newcov_batch(mc, [], exp_cids, exp_recs)
     assert np.array_equal(st.new_coverage(cids, recs), exp)
     st.close()
+
+
+def test_ui_stats_vs_reference(cover):
+    """httpSummary's per-call table + "cover" stat and httpCorpus's per-input
+    unique cover (html.go:67-99, :157-175) against their literal restatement,
+    over canonical covers with sentinels and wide PC ranges."""
+    from oracle import pyref
+    rng = np.random.default_rng(71)
+    for trial in range(24):
+        n = int(rng.integers(1, 300))
+        ncalls = int(rng.choice([1, 3, 40]))
+        calls, covs = _corpus(rng, n, ncalls, int(rng.choice([60, 4000, 1 << 32])), 40)
+        if trial % 5 == 0:
+            covs[0] = np.append(covs[0][covs[0] != 0xFFFFFFFF], np.uint32(0xFFFFFFFF))
+        rows, total = pyref.summary_stats(calls.tolist(), covs)
+        inputs, cov, ucov, inu, tot = cover.UIStats(covs, calls, ncalls)
+        assert tot == total, trial
+        got = [(c, int(inputs[c]), int(cov[c]), int(ucov[c])) for c in range(ncalls) if inputs[c]]
+        assert got == rows, trial
+        for c in range(ncalls):
+            exp = pyref.corpus_stats(calls.tolist(), covs, c)
+            assert [(i, len(covs[i]), int(inu[i])) for i, _, _ in exp] == exp, (trial, c)
+    with pytest.raises(Exception):  # non-canonical covers are rejected
+        cover.UIStats([[3, 1]], [0], 1)
+
+
+def test_ui_stats_synthetic_and_manager_mirror(cover):
+    from oracle import pyref
+    from syzkaller_amd.manager import RpcInput, corpus_stats, summary_stats
+    off, pcs = orc.synth_corpus(0x5EED0001, 3000, mean=96, sigma=24, log2_space=13)
+    c_off, c_pcs = orc.canonicalize_csr(off, pcs)
+    covs = [c_pcs[c_off[i]:c_off[i + 1]] for i in range(3000)]
+    names = [f"call{i % 53}" for i in range(3000)]
+    corpus = [RpcInput(nm, b"", 0, cv) for nm, cv in zip(names, covs)]
+    rows, total = summary_stats(corpus)
+    exp_rows, exp_total = pyref.summary_stats(names, covs)
+    assert total == exp_total
+    assert [(r.Name, r.Inputs, r.Cover, r.UniqueCover) for r in rows] == exp_rows
+    got = corpus_stats(corpus, "call7")
+    exp = pyref.corpus_stats(names, covs, "call7")
+    order = orc.sort_order(np.array([e[1] for e in exp], dtype=np.int64))  # Go sort.Sort, Cover >
+    assert [(u.N, u.Cover, u.UniqueCover) for u in got] == [exp[j] for j in order]

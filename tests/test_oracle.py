@@ -211,3 +211,17 @@ def test_unique_cover_restatement():
     # the final Canonicalize drops a lone 0xFFFFFFFF
     assert pyref.unique_cover(["a"], [[0xFFFFFFFF]], False) == []
 
+
+
+def test_ui_stats_restatement():
+    """httpSummary / httpCorpus (html.go:67-99, :157-175) by hand."""
+    covs = [[1, 2, 3], [3, 4], [4, 5], [6, 0xFFFFFFFF]]
+    calls = ["a", "a", "b", "c"]
+    rows, total = pyref.summary_stats(calls, covs)
+    # a = {1,2,3,4}, b = {4,5}, c = {6} (Union drops the sentinel); unique per
+    # call group: 1,2,3 (a), 5 (b), 6 (c) -- 4 is shared
+    assert rows == [("a", 2, 4, 3), ("b", 1, 2, 1), ("c", 1, 1, 1)]
+    assert total == 6
+    # per input: PCs held by exactly one input (3 and 4 are held twice)
+    assert pyref.corpus_stats(calls, covs, "a") == [(0, 3, 2), (1, 2, 0)]
+    assert pyref.corpus_stats(calls, covs, "c") == [(3, 2, 1)]
