@@ -170,6 +170,16 @@ int syzcov_normalize_prio(float *prios, int C);
  * enabled == NULL enables every call (prio.go:203-208). */
 int syzcov_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run);
 
+/* ChoiceTable.Choose (prog/prio.go:230-249) for nq (call, x) pairs, where
+ * x[k] is the caller's r.Intn(run[call][C-1]) draw (math/rand stays with the
+ * caller).  out[k] = sort.SearchInts(run[call], x) if that call is enabled;
+ * -1 if not (Choose draws again); -2 for call < 0 or a disabled call's nil
+ * row (Choose picks uniformly from enabledCalls).  run/enabled as produced
+ * for syzcov_build_choice_table (enabled == NULL: all).  A call >= C or an x
+ * outside [0, run[call][C-1]) -> SYZCOV_ERANGE. */
+int syzcov_choose_batch(const int64_t *run, const uint8_t *enabled, int C, const int32_t *calls,
+                        const int64_t *x, size_t nq, int32_t *out);
+
 /* Streaming new-coverage check of syz-fuzzer execute() (fuzzer.go:456-480)
  * against resident state.  A handle holds per-CallID maxCover and the global
  * flakes set as device bitmaps over a PC window [pc_lo, pc_lo + pc_span). */
@@ -397,6 +407,8 @@ int syzcov_dev_prio_finish(const int32_t *counts, int C, const float *static_pri
 int syzcov_dev_normalize_prio(float *prios, int C, void *stream);
 int syzcov_dev_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run,
                             void *stream);
+int syzcov_dev_choose(const int64_t *run, const uint8_t *enabled, int C, const int32_t *calls,
+                      const int64_t *x, size_t nq, int32_t *out, uint32_t *err_flag, void *stream);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,7 @@ _SIGS = {
     "syzcov_dev_static_prio": (C.c_int, [p_, p_, p_, p_, p_, p_, C.c_int, p_, p_]),
     "syzcov_normalize_prio": (C.c_int, [p_, C.c_int]),
     "syzcov_build_choice_table": (C.c_int, [p_, p_, C.c_int, p_]),
+    "syzcov_choose_batch": (C.c_int, [p_, p_, C.c_int, p_, p_, sz, p_]),
     "syzcov_state_create": (C.c_int, [C.c_int, u32, u64, p_]),
     "syzcov_state_destroy": (C.c_int, [u64]),
     "syzcov_state_add": (C.c_int, [u64, C.c_int, p_, sz]),
@@ -102,6 +103,7 @@ _SIGS = {
     "syzcov_dev_prio_counts": (C.c_int, [p_, sz, sz, C.c_int, p_, p_]),
     "syzcov_dev_prio_finish": (C.c_int, [p_, C.c_int, p_, p_, p_, p_]),
     "syzcov_dev_normalize_prio": (C.c_int, [p_, C.c_int, p_]),
+    "syzcov_dev_choose": (C.c_int, [p_, p_, C.c_int, p_, p_, sz, p_, p_, p_]),
     "syzcov_dev_choice_table": (C.c_int, [p_, p_, C.c_int, p_, p_]),
 }
 

@@ -773,4 +773,34 @@ int syzcov_build_choice_table(const float *prios, const uint8_t *enabled, int C,
     return 0;
 }
 
+int syzcov_choose_batch(const int64_t *run, const uint8_t *enabled, int C, const int32_t *calls,
+                        const int64_t *x, size_t nq, int32_t *out) {
+    if (nq == 0) return 0;
+    if (C <= 0 || !run || !calls || !x || !out) return SYZCOV_EINVAL;
+    Ctx *c = ctx();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_r = p.add((size_t)C * C * 8), i_e = p.add(C), i_c = p.add(nq * 4), i_x = p.add(nq * 8),
+           i_o = p.add(nq * 4), i_f = p.add(4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    CK(hipMemcpyAsync(b[i_r], run, (size_t)C * C * 8, hipMemcpyHostToDevice, c->s));
+    if (enabled) CK(hipMemcpyAsync(b[i_e], enabled, C, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_c], calls, nq * 4, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_x], x, nq * 8, hipMemcpyHostToDevice, c->s));
+    CK(hipMemsetAsync(b[i_f], 0, 4, c->s));
+    RC(syzcov_dev_choose((const int64_t *)b[i_r], enabled ? b[i_e] : nullptr, C,
+                         (const int32_t *)b[i_c], (const int64_t *)b[i_x], nq, (int32_t *)b[i_o],
+                         (uint32_t *)b[i_f], c->s));
+    uint32_t err = 0;
+    CK(hipMemcpyAsync(out, b[i_o], nq * 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipMemcpyAsync(&err, b[i_f], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (err) {
+        set_error("Choose: call id >= C or draw outside [0, run[call][C-1])");
+        return SYZCOV_ERANGE;
+    }
+    return 0;
+}
+
 }  // extern "C"

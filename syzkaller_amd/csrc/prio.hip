@@ -332,6 +332,47 @@ __global__ __launch_bounds__(FIN_THREADS) void static_prio_kernel(
     for (int j = threadIdx.x; j < C; j += FIN_THREADS) out[(size_t)c0 * C + j] = row[j];
 }
 
+
+// ChoiceTable.Choose (prio.go:230-249) for a batch of (call, x) draws, where
+// x is the caller's r.Intn(run[last]) (Go's math/rand stays with the caller):
+// i = sort.SearchInts(run[call], x), the first i with run[i] >= x.
+//   out = i   the call is enabled (Choose returns i)
+//   out = -1  rejected: Choose draws again (`continue`)
+//   out = -2  call < 0 or a nil (disabled) row: Choose picks uniformly from
+//             enabledCalls
+// An x outside [0, run[call][C-1]) (r.Intn's range) sets *err.
+__global__ void choose_kernel(const int64_t *__restrict__ run, const uint8_t *__restrict__ enabled,
+                              int C, const int32_t *__restrict__ calls,
+                              const int64_t *__restrict__ x, uint64_t nq, int32_t *__restrict__ out,
+                              uint32_t *__restrict__ err) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nq;
+         k += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t c = calls[k];
+        if (c >= C) {
+            *err = 1u;
+            out[k] = -3;
+            continue;
+        }
+        if (c < 0 || (enabled && !enabled[c])) {
+            out[k] = -2;
+            continue;
+        }
+        const int64_t *row = run + (uint64_t)c * C;
+        const int64_t xx = x[k];
+        if (xx < 0 || xx >= row[C - 1]) {
+            *err = 1u;
+            out[k] = -3;
+            continue;
+        }
+        int lo = 0, hi = C - 1;  // row[C-1] > xx, so the answer is < C
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (row[mid] >= xx) hi = mid; else lo = mid + 1;
+        }
+        out[k] = (!enabled || enabled[lo]) ? lo : -1;
+    }
+}
+
 }  // namespace syz
 
 using namespace syz;
@@ -417,6 +458,17 @@ extern "C" int syzcov_dev_choice_table(const float *prios, const uint8_t *enable
     if (C <= 0 || !prios || !run) return SYZCOV_EINVAL;
     hipLaunchKernelGGL(choice_table_kernel, dim3(C), dim3(FIN_THREADS), 0, (hipStream_t)stream,
                        prios, enabled, C, run);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_choose(const int64_t *run, const uint8_t *enabled, int C,
+                                 const int32_t *calls, const int64_t *x, size_t nq, int32_t *out,
+                                 uint32_t *err_flag, void *stream) {
+    if (nq == 0) return 0;
+    if (C <= 0 || !run || !calls || !x || !out || !err_flag) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(choose_kernel, dim3(grid_for(nq, 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, run, enabled, C, calls, x, (uint64_t)nq, out, err_flag);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -123,6 +123,46 @@ class ChoiceTable:
         self.enabledCalls = enabled_calls
         self.enabled = enabled
 
+    def choose_draws(self, calls, x) -> np.ndarray:
+        """One device pass of Choose's search for given draws x[k] =
+        r.Intn(run[call][-1]): the chosen call, -1 (rejected, Choose draws
+        again) or -2 (uniform over enabledCalls).  syzcov_choose_batch."""
+        calls = np.ascontiguousarray(np.asarray(calls, dtype=np.int32))
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.int64))
+        if calls.size != x.size:
+            raise ValueError("one draw per call")
+        out = np.empty(max(calls.size, 1), dtype=np.int32)
+        if calls.size:
+            check(lib().syzcov_choose_batch(_ptr(self._run), _ptr(self._en), self._run.shape[0],
+                                            _ptr(calls), _ptr(x), calls.size, _ptr(out)),
+                  "ChooseBatch")
+        return out[:calls.size]
+
+    def choose_batch(self, rnd, calls) -> list:
+        """Choose (prio.go:230-249) for many calls at once: every call's pick
+        follows Choose exactly (draw, search, redraw on a disabled hit), but
+        the draws are taken round by round over the batch, so for one seed
+        the picks differ from a sequential loop of Choose calls."""
+        calls = [int(c) for c in calls]
+        res = [None] * len(calls)
+        todo = list(range(len(calls)))
+        while todo:
+            xs = []
+            for k in todo:
+                run = self.run[calls[k]] if calls[k] >= 0 else None
+                xs.append(rnd.randrange(int(run[-1])) if run is not None else 0)
+            got = self.choose_draws([calls[k] for k in todo], xs)
+            nxt = []
+            for k, g in zip(todo, got):
+                if g == -2:
+                    res[k] = self.enabledCalls[rnd.randrange(len(self.enabledCalls))]
+                elif g == -1:
+                    nxt.append(k)
+                else:
+                    res[k] = int(g)
+            todo = nxt
+        return res
+
     def Choose(self, rnd, call: int) -> int:  # prio.go:230-249
         if call < 0:
             return self.enabledCalls[rnd.randrange(len(self.enabledCalls))]
@@ -146,4 +186,6 @@ def BuildChoiceTable(prios, enabled=None) -> ChoiceTable:
     check(lib().syzcov_build_choice_table(_ptr(prios), _ptr(en), C_, _ptr(run)),
           "BuildChoiceTable")
     rows = [run[i] if en[i] else None for i in range(C_)]
-    return ChoiceTable(rows, [i for i in range(C_) if en[i]], en.astype(bool))
+    ct = ChoiceTable(rows, [i for i in range(C_) if en[i]], en.astype(bool))
+    ct._run, ct._en = run, en  # device layout for choose_draws
+    return ct

@@ -215,6 +215,46 @@ def test_normalize_and_choice_table(torch):
         assert ct.enabled[ct.Choose(r, i)]
 
 
+def test_choose_batch(torch):
+    """Batched ChoiceTable.Choose (prio.go:230-249): for given draws x the
+    device search equals sort.SearchInts on the row (bisect_left), with the
+    reference's reject (-1) and uniform-fallback (-2) cases."""
+    import random
+    from syzkaller_amd import SyzcovError, prio
+    rng = np.random.default_rng(8)
+    C = 1170
+    p = rng.integers(0, 50, size=(C, C)).astype(np.float32)
+    pr = orc.normalize_prio(p)
+    en = (rng.random(C) < 0.6).astype(np.uint8)
+    ct = prio.BuildChoiceTable(pr, en)
+    exp_run = orc.build_choice_table(pr, en)
+    nq = 200_000
+    calls = rng.integers(-1, C, size=nq).astype(np.int32)
+    x = np.zeros(nq, dtype=np.int64)
+    exp = np.full(nq, -2, dtype=np.int32)
+    for k in range(nq):
+        c = calls[k]
+        if c >= 0 and en[c]:
+            row = exp_run[c]
+            x[k] = rng.integers(0, row[-1])
+            # exact hits on a run value pick its first index (SearchInts)
+            if k % 97 == 0 and row[0] < row[-1]:
+                v = row[rng.integers(0, C - 1)]
+                x[k] = v if v < row[-1] else row[0]
+            i = int(np.searchsorted(row, x[k], side="left"))
+            exp[k] = i if en[i] else -1
+    got = ct.choose_draws(calls, x)
+    assert np.array_equal(got, exp)
+    assert (got == -1).any() and (got >= 0).any() and (got == -2).any()
+    c0 = next(c for c in range(C) if en[c])
+    with pytest.raises(SyzcovError):  # outside r.Intn's range
+        ct.choose_draws([c0], [exp_run[c0][-1]])
+    with pytest.raises(SyzcovError):
+        ct.choose_draws([C], [0])
+    picks = ct.choose_batch(random.Random(1), [c0] * 500 + [-1] * 20)
+    assert all(ct.enabled[i] for i in picks)
+
+
 def test_newcov_batch_vs_sequential(torch):
     from syzkaller_amd.fuzzer import CoverState
     rng = np.random.default_rng(12)
