@@ -383,9 +383,9 @@ int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t
 int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out, void *stream);
 
 /* Dynamic priority counts as a dense contraction on i8 MFMA with i32
- * accumulation: counts = AᵀA over the key-major matrix AT[key][program]
- * (rows = syzcov_dev_prio_rows(C), program stride ldp =
- * syzcov_dev_prio_ldp(nprog), zero padded).  Row C of AT is all ones, so
+ * accumulation: counts = AᵀA over the matrix AT (rows = syzcov_dev_prio_rows(C)
+ * keys x ldp = syzcov_dev_prio_ldp(nprog) programs, zero padded), stored
+ * K-blocked: (key r, program p) at byte (p / 64) * rows * 64 + r * 64 + p % 64.  Row C of AT is all ones, so
  * counts[i][C] = colsum(A)[i] feeds the diagonal correction.
  * key_mode 0 (positional, reference-exact: prio.go:142-150 indexes by call
  * position): AT[k][p] = [k < lens[p]]; key_mode 1: AT[c][p] = number of calls

@@ -8,9 +8,11 @@
 //   key mode 0 (reference-exact): the reference indexes prios by call
 //     POSITION (prio.go:142-150 never reads Meta.ID), so A[p][k] = [k < len(p)];
 //   key mode 1: A[p][c] = number of calls with syscall id c in program p.
-// A is stored key-major (AT[key][program], program stride ldp, zero padded)
-// so an MFMA fragment — 16 consecutive programs of one key — is one 16-byte
-// LDS read.  An all-ones key row at index C makes the GEMM also produce
+// A is stored K-blocked: for each step of PK = 64 programs a contiguous
+// [rows][64] byte block (key-major inside), so an MFMA fragment -- 16
+// consecutive programs of one key -- is one 16-byte read, and one K step of
+// every tile is one contiguous 80 KB region (L2-friendly; a plain key-major
+// AT with a 1 MB row stride made the tiles' rows collide in the same L2 sets).  An all-ones key row at index C makes the GEMM also produce
 // colsum(A) = D[i][C] for the diagonal correction.  Only tiles with I <= J are
 // computed (D is symmetric) and mirrored; K (programs) is split across
 // workgroups with exact int32 atomics in the epilogue.
@@ -21,6 +23,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
@@ -32,30 +36,42 @@ constexpr int PK = 64;   // programs per K-step
 
 __host__ __device__ inline size_t prio_rows(int C) { return ((size_t)C + 1 + PT - 1) / PT * PT; }
 __host__ __device__ inline size_t prio_ldp(size_t nprog) { return (nprog + PK - 1) / PK * PK; }
+// byte offset of (key r, program p) in the K-blocked AT
+__host__ __device__ inline size_t at_off(size_t r, size_t p, size_t rows) {
+    return (p / PK) * (rows * PK) + r * PK + (p % PK);
+}
 
 // ---------------------------------------------------------------- A builders
-// positional: AT[c][p] = (c < len[p]) for c < C, AT[C][p] = (p < nprog)
-__global__ void prio_build_pos_kernel(const int32_t *__restrict__ lens, size_t nprog, int C,
-                                      size_t rows, size_t ldp, int8_t *__restrict__ at) {
-    const size_t nvec = rows * (ldp / 16);
-    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec;
-         v += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = v / (ldp / 16);
-        const size_t p0 = (v % (ldp / 16)) * 16;
-        uint32_t w[4] = {0, 0, 0, 0};
+// positional: AT[c][p] = (c < len[p]) for c < C, AT[C][p] = (p < nprog).
+// One workgroup per K block (64 programs, a contiguous rows x 64 B region):
+// thread t owns program chunk t % 4 (its 16 lengths stay in registers) and
+// rows t / 4 + 64 i, so a wave stores 1 KB contiguous per instruction.
+__global__ __launch_bounds__(256) void prio_build_pos_kernel(const int32_t *__restrict__ lens,
+                                                             size_t nprog, int C, size_t rows,
+                                                             size_t ldp, int8_t *__restrict__ at) {
+    const size_t nkb = ldp / PK;
+    const uint32_t t = threadIdx.x, ch = t & 3u;
+    for (size_t kb = blockIdx.x; kb < nkb; kb += gridDim.x) {
+        const size_t p0 = kb * PK + ch * 16;
+        int32_t ln[16];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const size_t p = p0 + j;
-            uint32_t bit = 0;
-            if (p < nprog) {
-                if ((int)r < C)
-                    bit = (int32_t)r < lens[p];
-                else if ((int)r == C)
-                    bit = 1;
+        for (int j = 0; j < 16; j++) ln[j] = p0 + j < nprog ? lens[p0 + j] : -1;  // -1: no program
+        int8_t *blk = at + kb * (rows * PK) + ch * 16;
+        for (size_t r = t >> 2; r < rows; r += 64) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const int32_t L = ln[q * 4 + c];
+                    const bool bit = (int)r < C ? (int32_t)r < L : ((int)r == C && L >= 0);
+                    v |= (uint32_t)bit << (8 * c);
+                }
+                w[q] = v;
             }
-            w[j >> 2] |= bit << (8 * (j & 3));
+            *(uint4 *)(blk + r * PK) = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        ((uint4 *)at)[v] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
 
@@ -63,7 +79,7 @@ __global__ void prio_build_pos_kernel(const int32_t *__restrict__ lens, size_t n
 // per program is checked by the host wrapper's caller contract)
 __global__ void prio_build_id_kernel(const uint64_t *__restrict__ prog_off,
                                      const uint16_t *__restrict__ ids, size_t nprog, int C,
-                                     size_t ldp, int8_t *__restrict__ at,
+                                     size_t rows, int8_t *__restrict__ at,
                                      uint32_t *__restrict__ err) {
     for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < nprog;
          p += (size_t)gridDim.x * blockDim.x) {
@@ -73,10 +89,10 @@ __global__ void prio_build_id_kernel(const uint64_t *__restrict__ prog_off,
                 *err = 1u;
                 continue;
             }
-            const size_t byte = c * ldp + p;
+            const size_t byte = at_off(c, p, rows);
             atomicAdd((unsigned int *)(at + (byte & ~(size_t)3)), 1u << (8 * (byte & 3)));
         }
-        const size_t byte = (size_t)C * ldp + p;  // ones row
+        const size_t byte = at_off((size_t)C, p, rows);  // ones row
         atomicAdd((unsigned int *)(at + (byte & ~(size_t)3)), 1u << (8 * (byte & 3)));
     }
 }
@@ -88,14 +104,44 @@ __device__ __forceinline__ uint32_t lds_off(uint32_t row, uint32_t chunk) {
     return row * PK + ((chunk ^ ((row >> 2) & 3u)) << 4);
 }
 
+// One K step (64 programs) of a wave's 64x64 sub-tile: 2 x 2 MFMA 32x32x32.
+__device__ __forceinline__ void mfma_step(const int8_t *Asrc, const int8_t *Bsrc, uint32_t l,
+                                          uint32_t wr, uint32_t wc, v16i (&acc)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+        const uint32_t ch = ks * 2 + (l >> 5);
+        v4i fa[2], fb[2];
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+            fa[mi] = *(const v4i *)(Asrc + lds_off(wr * 64 + mi * 32 + (l & 31), ch));
+#pragma unroll
+        for (int ni = 0; ni < 2; ni++)
+            fb[ni] = *(const v4i *)(Bsrc + lds_off(wc * 64 + ni * 32 + (l & 31), ch));
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+            for (int ni = 0; ni < 2; ni++)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+    }
+}
+
+// Workgroup -> (tile, K split).  Splits are grouped by XCD: consecutive
+// workgroup ids go to the 8 XCDs round-robin, so workgroup b runs on XCD
+// b % 8 and the `gpx` K splits of an XCD run there with ALL their tiles at
+// the same time.  The tiles of one split stream the same A rows over the same
+// K range, so each operand chunk comes from HBM once per XCD and is re-read
+// by the other tiles from that XCD's L2 (K splits spread over XCDs instead
+// made every XCD fetch every chunk).
 __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict__ at, size_t ldp,
                                                         size_t kchunk, int ntile_dim,
-                                                        int ntiles, int32_t *__restrict__ counts,
+                                                        int ntiles, int gpx,
+                                                        int32_t *__restrict__ counts,
                                                         size_t rows) {
-    __shared__ __attribute__((aligned(16))) int8_t As[PT * PK];
-    __shared__ __attribute__((aligned(16))) int8_t Bs[PT * PK];
-    const int tile = blockIdx.x % ntiles;
-    const size_t split = blockIdx.x / ntiles;
+    __shared__ __attribute__((aligned(16))) int8_t As[2][PT * PK];
+    __shared__ __attribute__((aligned(16))) int8_t Bs[2][PT * PK];
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    const int tile = (int)(slot % (uint32_t)ntiles);
+    const size_t split = (size_t)xcd * gpx + slot / (uint32_t)ntiles;
     // tile -> (I, J) with I <= J, row-major over the upper triangle
     int I = 0, rem = tile;
     while (rem >= ntile_dim - I) {
@@ -116,44 +162,46 @@ __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[a][b][r] = 0;
 
-    for (size_t kb = kb0; kb < kb1; kb += PK) {
-        // stage: 128 rows x 4 chunks = 512 chunks per operand, 2 per thread
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const uint32_t q = t + 256u * s;
-            const uint32_t row = q >> 2, ch = q & 3u;
-            const uint4 va = *(const uint4 *)(at + (i0 + row) * ldp + kb + ch * 16);
-            *(uint4 *)(As + lds_off(row, ch)) = va;
-            if (!diag) {
-                const uint4 vb = *(const uint4 *)(at + (j0 + row) * ldp + kb + ch * 16);
-                *(uint4 *)(Bs + lds_off(row, ch)) = vb;
-            }
-        }
-        __syncthreads();
-        const int8_t *Bsrc = diag ? As : Bs;
-#pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-            const uint32_t ch = ks * 2 + (l >> 5);
-            v4i fa[2], fb[2];
-#pragma unroll
-            for (int mi = 0; mi < 2; mi++) {
-                const uint32_t row = wr * 64 + mi * 32 + (l & 31);
-                fa[mi] = *(const v4i *)(As + lds_off(row, ch));
-            }
-#pragma unroll
-            for (int ni = 0; ni < 2; ni++) {
-                const uint32_t row = wc * 64 + ni * 32 + (l & 31);
-                fb[ni] = *(const v4i *)(Bsrc + lds_off(row, ch));
-            }
-#pragma unroll
-            for (int mi = 0; mi < 2; mi++)
-#pragma unroll
-                for (int ni = 0; ni < 2; ni++)
-                    acc[mi][ni] =
-                        __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
-        }
-        __syncthreads();
+    // software pipeline, two K steps deep: step i+2's operands are loaded
+    // into registers (set i % 2, just stored to LDS) while step i's MFMAs
+    // run, so a load has two compute phases to arrive; two LDS buffers, one
+    // barrier per step.  The loop is unrolled by two with named register sets
+    // (arrays indexed by the set went to scratch).
+    const uint32_t row0 = t >> 2, row1 = (t + 256u) >> 2, chq = t & 3u;  // chunk of both rows
+    const uint32_t lo0 = lds_off(row0, chq), lo1 = lds_off(row1, chq);
+    auto ld = [&](size_t kb, uint32_t base, uint32_t row) -> uint4 {
+        return *(const uint4 *)(at + (kb / PK) * (rows * PK) + chq * 16 + (base + row) * PK);
+    };
+    uint4 a00, a01, b00, b01, a10, a11, b10, b11;
+#define PRIO_LOAD(SET, KB)                                   \
+    do {                                                     \
+        a##SET##0 = ld((KB), (uint32_t)i0, row0);            \
+        a##SET##1 = ld((KB), (uint32_t)i0, row1);            \
+        if (!diag) {                                         \
+            b##SET##0 = ld((KB), (uint32_t)j0, row0);        \
+            b##SET##1 = ld((KB), (uint32_t)j0, row1);        \
+        }                                                    \
+    } while (0)
+#define PRIO_STEP(SET, KB)                                                          \
+    do {                                                                            \
+        *(uint4 *)(As[SET] + lo0) = a##SET##0;                                      \
+        *(uint4 *)(As[SET] + lo1) = a##SET##1;                                      \
+        if (!diag) {                                                                \
+            *(uint4 *)(Bs[SET] + lo0) = b##SET##0;                                  \
+            *(uint4 *)(Bs[SET] + lo1) = b##SET##1;                                  \
+        }                                                                           \
+        __syncthreads();                                                            \
+        if ((KB) + 2 * PK < kb1) PRIO_LOAD(SET, (KB) + 2 * PK);                     \
+        mfma_step(As[SET], diag ? As[SET] : Bs[SET], l, wr, wc, acc);               \
+    } while (0)
+    if (kb0 < kb1) PRIO_LOAD(0, kb0);
+    if (kb0 + PK < kb1) PRIO_LOAD(1, kb0 + PK);
+    for (size_t kb = kb0; kb < kb1; kb += 2 * PK) {
+        PRIO_STEP(0, kb);
+        if (kb + PK < kb1) PRIO_STEP(1, kb + PK);
     }
+#undef PRIO_STEP
+#undef PRIO_LOAD
     // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
     for (int mi = 0; mi < 2; mi++)
@@ -402,8 +450,7 @@ extern "C" int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens,
     const size_t rows = prio_rows(C);
     if (key_mode == 0) {
         if (nprog && !lens) return SYZCOV_EINVAL;
-        const size_t nvec = rows * (ldp / 16);
-        hipLaunchKernelGGL(prio_build_pos_kernel, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
+        hipLaunchKernelGGL(prio_build_pos_kernel, dim3(grid_for(ldp / PK, 1, 16384)), dim3(256), 0,
                            s, lens, nprog, C, rows, ldp, at);
         SYZ_LAUNCH_CHECK();
         return 0;
@@ -412,7 +459,7 @@ extern "C" int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens,
     SYZ_HIP(hipMemsetAsync(at, 0, rows * ldp, s));
     if (nprog) {
         hipLaunchKernelGGL(prio_build_id_kernel, dim3(grid_for(nprog, 256, 8192)), dim3(256), 0, s,
-                           prog_off, call_ids, nprog, C, ldp, at, err_flag);
+                           prog_off, call_ids, nprog, C, rows, at, err_flag);
         SYZ_LAUNCH_CHECK();
     }
     return 0;
@@ -425,13 +472,16 @@ extern "C" int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog
     const size_t rows = prio_rows(C);
     const int nt = (int)(rows / PT);
     const int ntiles = nt * (nt + 1) / 2;
-    // K split: enough workgroups to fill the chip ~3x over
-    size_t nk = ldp / PK;
-    size_t splits = std::max<size_t>(1, std::min<size_t>(nk, (768 + ntiles - 1) / ntiles));
-    size_t kchunk = (nk + splits - 1) / splits * PK;
-    splits = (ldp + kchunk - 1) / kchunk;
+    // K splits: a multiple of the 8 XCDs, gpx per XCD, enough workgroups to
+    // fill the chip ~3x over.  Splits past the end of K have empty ranges.
+    const size_t nk = ldp / PK;
+    int gpx = (int)std::max<size_t>(1, std::min<size_t>((nk + 7) / 8,
+                                                              (768 / 8 + ntiles - 1) / ntiles));
+    if (const char *e = getenv("SYZCOV_PRIO_GPX")) gpx = std::max(1, atoi(e));  // tuning sweeps
+    const size_t splits = 8 * (size_t)gpx;
+    const size_t kchunk = (nk + splits - 1) / splits * PK;
     hipLaunchKernelGGL(prio_gemm_kernel, dim3((unsigned)(ntiles * splits)), dim3(256), 0,
-                       (hipStream_t)stream, at, ldp, kchunk, nt, ntiles, counts, rows);
+                       (hipStream_t)stream, at, ldp, kchunk, nt, ntiles, gpx, counts, rows);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
