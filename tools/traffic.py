@@ -3,8 +3,7 @@
 WRITE_SIZE in separate runs, MI355X_MICROARCH.md 'HBM'):
   bytes_read  = 2 * FETCH_SIZE[KB] * 1024   (gfx950 tallies 128-B requests at 64 B)
   bytes_write = WRITE_SIZE[KB] * 1024
-per launch of each phase = sum over the phase's kernels of the per-dispatch
-average.  Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json]"""
+per step of each phase = sum over the phase's kernels of their per-step totals.  Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json]"""
 import collections
 import csv
 import glob
@@ -24,7 +23,11 @@ PHASES = {
 }
 
 
-def per_dispatch(d, counter):
+def per_step(d, counter):
+    """Counter total per bench step for each kernel name: a kernel may run
+    several times per step (pass1_kernel once per rank chunk), so the total is
+    divided by the number of steps, counted as the dispatches of bin_kernel
+    (canon bins once per step)."""
     tot = collections.defaultdict(float)
     disp = collections.defaultdict(set)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -34,7 +37,8 @@ def per_dispatch(d, counter):
             k = r["Kernel_Name"]
             tot[k] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
-    return {k: tot[k] / len(disp[k]) for k in tot}
+    steps = max([len(v) for k, v in disp.items() if "bin_kernel" in k] or [1])
+    return {k: tot[k] / steps for k in tot}
 
 
 def phase_of(name):
@@ -45,8 +49,8 @@ def phase_of(name):
 
 
 def main(fd, wd, out=None):
-    fetch = per_dispatch(fd, "FETCH_SIZE")
-    write = per_dispatch(wd, "WRITE_SIZE")
+    fetch = per_step(fd, "FETCH_SIZE")
+    write = per_step(wd, "WRITE_SIZE")
     res = {}
     for name in set(fetch) | set(write):
         ph = phase_of(name)
