@@ -528,9 +528,10 @@ extern "C" int syzcov_dev_minimize_range(
     const size_t lds = ((size_t)1 << range_shift) / 8;
     // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (32-lane groups),
     // 1 = lane-per-item never, 2 = always, 3..5 = the same without tests;
-    // pmode 0 = slice-major (P = 2R), 1 = range-major (one slice; default:
-    // 7.1 vs 8.0 ms at C2)
-    int variant = 0, pmode = 1;
+    // pmode 0 = slice-major (P = 2R; default: 4.47 vs 4.60 ms at C2 with the
+    // 4-lane-group kernel), 1 = range-major (one slice; it was faster with the
+    // lane-per-item kernel, 7.1 vs 8.0 ms), k >= 3 = P = kR (4.6 ms)
+    int variant = 0, pmode = 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
     // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
@@ -573,6 +574,7 @@ extern "C" int syzcov_dev_minimize_range(
         G = std::min<uint64_t>(std::max<uint64_t>(G, 256), 8192);
         uint64_t P = 2 * nrange;
         if (pmode == 1) P = G;
+        else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // tuning: wider slices
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
