@@ -477,6 +477,27 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
 
 using namespace syz;
 
+// Workgroups that fit on the whole chip at once for a class kernel: the grid
+// is never larger, so every wave owns an equal share of the class (+-1
+// segment) instead of a fixed 1/4096 of it run in 2-3 partly empty rounds.
+template <int NK, int MW>
+static unsigned resident_grid(uint64_t nseg) {
+    static unsigned cap = 0;
+    if (!cap) {
+        int dev = 0, ncu = 256, nb = 0;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            hipDeviceProp_t pr;
+            if (hipGetDeviceProperties(&pr, dev) == hipSuccess) ncu = pr.multiProcessorCount;
+        }
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void *>(cw::canon_wave_kernel<NK, MW>), 64 * cw::WPB,
+                0) != hipSuccess || nb < 1)
+            nb = 1;
+        cap = (unsigned)(nb * ncu);
+    }
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, cap));
+}
+
 extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
     // counters | redo list | big list | class lists
     return 256 + (2 + cw::NCLS) * align_up(nseg * sizeof(uint32_t), 256);
@@ -544,7 +565,6 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     SYZ_HIP(hipMemsetAsync(ccnt, 0, cw::NCLS * sizeof(uint32_t), s));
     hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 2048)), dim3(256), 0, s, off,
                        (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1);
-    const unsigned grid = (unsigned)std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, 4096);
     for (int c = 0; bitonic && c < 3; c++) {
         if (max_seg_len < C.lo[c]) break;
         int rc = canon_bitonic_launch(1 << c, off, raw, out, new_len, pc_lo, pc_span, P.sent_key,
@@ -556,12 +576,12 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
-        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 5: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(grid), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(resident_grid<16, 5>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(resident_grid<32, SYZ_CANON_W32>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(resident_grid<40, SYZ_CANON_W40>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(resident_grid<48, SYZ_CANON_W48>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(resident_grid<64, 2>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 5: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(resident_grid<128, 1>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         }
         SYZ_LAUNCH_CHECK();
     }
