@@ -40,10 +40,11 @@ constexpr int WG = 256;
 struct Seg {
     int a, b, limit, flags;  // flags: bit0 wasBalanced, bit1 wasPartitioned
 };
-enum { M_DONE = 0, M_HEAP = 1, M_ACTIVE = 2 };
+enum { M_DONE = 0, M_ACTIVE = 2 };
 struct Plan {
     int mode, pivot, rev, pis, eq, cnt, m;
     uint32_t kp;
+    uint32_t done_c, done_s;  // blocks of count_kernel / swap_kernel finished this round
 };
 
 // accessor over the global key/index arrays
@@ -176,6 +177,10 @@ __global__ void seg_gather_kernel(const int32_t *__restrict__ I, const uint64_t 
 __global__ void plan_kernel(Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
                             uint32_t *__restrict__ K, int32_t *__restrict__ I, Ctl c) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0) {  // the children of this round are pushed by swap_kernel (after this grid)
+        *c.next_count = 0u;
+        *c.next_maxlen = 0u;
+    }
     if (s >= *ncur_p) return;
     Seg g = cur[s];
     Plan p{};
@@ -184,8 +189,9 @@ __global__ void plan_kernel(Seg *__restrict__ cur, const uint32_t *__restrict__ 
     if (n <= SMALL) {  // (only the seed can be small here)
         push_seg(c, g);
         p.mode = M_DONE;
-    } else if (g.limit == 0) {
-        p.mode = M_HEAP;
+    } else if (g.limit == 0) {  // `if limit == 0 { heapSort(data, a, b); return }`
+        gocore::heap_sort(d, g.a, g.b);
+        p.mode = M_DONE;
     } else {
         const bool wb = g.flags & 1, wp = g.flags & 2;
         if (!wb) {
@@ -207,15 +213,6 @@ __global__ void plan_kernel(Seg *__restrict__ cur, const uint32_t *__restrict__ 
     plan[s] = p;
 }
 
-__global__ void heap_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
-                            uint32_t *__restrict__ K, int32_t *__restrict__ I) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *ncur_p || plan[s].mode != M_HEAP) return;
-    GAcc d{K, I};
-    gocore::heap_sort(d, cur[s].a, cur[s].b);
-    plan[s].mode = M_DONE;
-}
-
 __global__ void reverse_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
                                const Plan *__restrict__ plan, uint32_t *__restrict__ K,
                                int32_t *__restrict__ I) {
@@ -231,7 +228,8 @@ __global__ void reverse_kernel(const Seg *__restrict__ cur, const uint32_t *__re
         d.swap(g.a + i, g.b - 1 - i);
 }
 
-// WG-cooperative partialInsertionSort (cover: gosort_core.h's sequential form)
+// WG-cooperative partialInsertionSort (cover: gosort_core.h's sequential form),
+// then on lane 0 the partitionEqual test and the partition's Swap(a, pivot)
 __device__ int wg_find_first_descent(const uint32_t *K, int from, int b, int *sh) {
     // first i in [from, b) with K[i] > K[i-1], or b
     for (int c0 = from; c0 < b; c0 += WG) {
@@ -256,12 +254,12 @@ __global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
                                                   int32_t *__restrict__ I) {
     __shared__ int sh[WG / 64 + 2];
     const uint32_t s = blockIdx.x;
-    if (s >= *ncur_p || plan[s].mode != M_ACTIVE || !plan[s].pis) return;
+    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
     const Seg g = cur[s];
     const int a = g.a, b = g.b;
     int i = a + 1;
     bool sorted = false;
-    for (int step = 0; step < 5; step++) {
+    for (int step = 0; plan[s].pis && step < 5; step++) {
         i = wg_find_first_descent(K, i, b, sh);
         if (i == b) {
             sorted = true;
@@ -280,19 +278,18 @@ __global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
         __threadfence_block();
         __syncthreads();
     }
-    if (threadIdx.x == 0 && sorted) plan[s].mode = M_DONE;
-}
-
-__global__ void eq_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
-                          uint32_t *__restrict__ K, int32_t *__restrict__ I) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
-    const Seg g = cur[s];
+    if (threadIdx.x != 0) return;
+    if (sorted) {
+        plan[s].mode = M_DONE;
+        return;
+    }
+    // the partitionEqual test, then Swap(a, pivot) that both partition forms
+    // start with (same lane as the moves above: no fence needed)
     const int pivot = plan[s].pivot;
     GAcc d{K, I};
-    plan[s].eq = g.a > 0 && !d.less(g.a - 1, pivot);
-    d.swap(g.a, pivot);  // both partition forms start with Swap(a, pivot)
-    plan[s].kp = K[g.a];
+    plan[s].eq = a > 0 && !d.less(a - 1, pivot);
+    d.swap(a, pivot);
+    plan[s].kp = K[a];
 }
 
 // f(x): x belongs to the left group (partition: Less(x, a) = K[x] > kp;
@@ -303,7 +300,7 @@ __device__ __forceinline__ bool left_group(uint32_t k, uint32_t kp, int eq) {
 
 __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
                                                     const uint32_t *__restrict__ ncur_p,
-                                                    const Plan *__restrict__ plan,
+                                                    Plan *__restrict__ plan,
                                                     const uint32_t *__restrict__ K,
                                                     uint32_t *__restrict__ cc, uint32_t stride) {
     __shared__ uint32_t tmp[WG / 64 + 1];
@@ -319,26 +316,27 @@ __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
     for (int x = x0 + threadIdx.x; x < x1; x += WG) c += left_group(K[x], p.kp, p.eq);
     uint32_t total;
     block_excl_scan<WG>(c, tmp, &total);
-    if (threadIdx.x == 0) cc[(size_t)s * stride + blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(WG) void cscan_kernel(const Seg *__restrict__ cur,
-                                                    const uint32_t *__restrict__ ncur_p,
-                                                    Plan *__restrict__ plan,
-                                                    uint32_t *__restrict__ cc, uint32_t stride) {
-    __shared__ uint32_t tmp[WG / 64 + 1];
-    const uint32_t s = blockIdx.x;
-    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
-    const Seg g = cur[s];
+    // The last block of the segment to finish scans the block counts (the
+    // counts of the other blocks are released by their fences before the
+    // atomic; this block's fence after it acquires them).
     const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
+    __shared__ uint32_t last;
+    if (threadIdx.x == 0) {
+        cc[(size_t)s * stride + blockIdx.x] = total;
+        __threadfence();
+        last = atomicAdd(&plan[s].done_c, 1u) == nch - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
     uint32_t carry = 0;
     for (uint32_t c0 = 0; c0 < nch; c0 += WG) {
         const uint32_t c = c0 + threadIdx.x;
         const uint32_t v = c < nch ? cc[(size_t)s * stride + c] : 0u;
-        uint32_t total;
-        const uint32_t pre = block_excl_scan<WG>(v, tmp, &total);
+        uint32_t sum;
+        const uint32_t pre = block_excl_scan<WG>(v, tmp, &sum);
         if (c < nch) cc[(size_t)s * stride + c] = carry + pre;
-        carry += total;
+        carry += sum;
     }
     if (threadIdx.x == 0) {
         plan[s].cnt = (int)carry;
@@ -386,35 +384,36 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
     if (__lane_id() == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
 }
 
-__global__ void swap_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
-                            const Plan *__restrict__ plan,
-                            uint32_t *__restrict__ K, int32_t *__restrict__ I,
-                            const int32_t *__restrict__ PL, const int32_t *__restrict__ PR) {
+// The m swaps of the partition, then (last block of the segment) the tail of
+// the loop iteration: partitionEqual's `a = mid` continue, or the pivot swap
+// and the two recursions (smaller side first, as Go recurses on it).
+__global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
+                                                   const uint32_t *__restrict__ ncur_p,
+                                                   Plan *__restrict__ plan, uint32_t *__restrict__ K,
+                                                   int32_t *__restrict__ I,
+                                                   const int32_t *__restrict__ PL,
+                                                   const int32_t *__restrict__ PR, Ctl c) {
     const uint32_t s = blockIdx.y;
     if (s >= *ncur_p) return;
     const Plan p = plan[s];
     if (p.mode != M_ACTIVE) return;
+    const uint32_t nparts = p.m > 0 ? (uint32_t)((p.m + CH - 1) / CH) : 1u;
+    if (blockIdx.x >= nparts) return;
     const Seg g = cur[s];
     GAcc d{K, I};
     for (int k = blockIdx.x * CH + threadIdx.x; k < min(p.m, (int)(blockIdx.x + 1) * CH);
          k += blockDim.x)
         d.swap(PL[g.a + k], PR[g.a + k]);
-}
-
-__global__ void finish_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
-                              const Plan *__restrict__ plan, uint32_t *__restrict__ K,
-                              int32_t *__restrict__ I, Ctl c) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *ncur_p) return;
-    const Plan p = plan[s];
-    if (p.mode != M_ACTIVE) return;
-    const Seg g = cur[s];
+    __threadfence();  // release this thread's swaps at device scope
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (atomicAdd(&plan[s].done_s, 1u) != nparts - 1) return;
+    __threadfence();  // acquire the other blocks' swaps
     if (p.eq) {  // partitionEqual returns a + 1 + cnt; the loop continues
         push_seg(c, Seg{g.a + 1 + p.cnt, g.b, g.limit, g.flags});
         return;
     }
     const int mid = g.a + p.cnt;
-    GAcc d{K, I};
     d.swap(mid, g.a);
     const int already = p.m == 0;
     const int n = g.b - g.a, ln = mid - g.a, rn = g.b - mid, thr = n / 8;
@@ -811,27 +810,20 @@ static int run_rounds(SortWs &w, hipStream_t s) {
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
         // the children of this round go to nxt
-        SYZ_HIP(hipMemsetAsync(ncount, 0, 4, s));
-        SYZ_HIP(hipMemsetAsync(nmax, 0, 4, s));
+        // (plan_kernel zeroes ncount / nmax)
         Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
         const unsigned gs = (ncur + 63) / 64;
         const unsigned nch = (unsigned)((maxlen + CH - 1) / CH);
         hipLaunchKernelGGL(plan_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I, cn);
-        hipLaunchKernelGGL(heap_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I);
         hipLaunchKernelGGL(reverse_kernel, dim3((nch + 1) / 2 + 1, ncur), dim3(WG), 0, s, cur,
                            ccount, w.plan, w.K, w.I);
         hipLaunchKernelGGL(pis_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I);
-        hipLaunchKernelGGL(eq_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I);
         hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
                            w.cc, w.cc_stride);
-        hipLaunchKernelGGL(cscan_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.cc,
-                           w.cc_stride);
         hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
                            w.cc, w.cc_stride, w.PL, w.PR);
         hipLaunchKernelGGL(swap_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
-                           w.I, w.PL, w.PR);
-        hipLaunchKernelGGL(finish_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I,
-                           cn);
+                           w.I, w.PL, w.PR, cn);
         SYZ_LAUNCH_CHECK();
         std::swap(cur, nxt);
         std::swap(ccount, ncount);
