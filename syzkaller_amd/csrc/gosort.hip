@@ -793,12 +793,22 @@ static int legacy_host(const int64_t *lens, size_t n, const uint64_t *goff, size
 
 // Level-synchronous pdqsort rounds over the segments already seeded into
 // segA / small (ctl[1], ctl[3]); the result is left in w.I.
-static int run_rounds(SortWs &w, hipStream_t s) {
+// seeded >= 0: the host already knows the seed (one segment of `seeded`
+// elements), so the first read-back is skipped; an input error flagged by the
+// init kernel is then reported by the final read-back.
+static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     Seg *cur = w.segA, *nxt = w.segB;
     uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
-    uint32_t h[6];
-    SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
+    uint32_t h[6] = {0, 0, 0, 0, 0, 0};
+    if (seeded < 0) {
+        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+    } else if (seeded > SMALL) {
+        h[1] = 1;
+        h[4] = (uint32_t)seeded;
+    } else if (seeded > 1) {
+        h[3] = 1;
+    }
     // The kernels read the live segment count from the device (ccount), so
     // rounds are queued without a host round trip: the host keeps only UPPER
     // BOUNDS for the grids (a segment has at most two large children, each
@@ -842,6 +852,8 @@ static int run_rounds(SortWs &w, hipStream_t s) {
         hipLaunchKernelGGL(small_kernel, dim3(std::min<uint32_t>(h[3], 8192)), dim3(WG), 0, s, w.small,
                            w.ctl + 3, w.K, w.I, w.ctl);
         SYZ_LAUNCH_CHECK();
+    }
+    if (!h[0] && (h[3] || seeded >= 0)) {
         SYZ_HIP(hipMemcpyAsync(h, w.ctl, 4, hipMemcpyDeviceToHost, s));
         SYZ_HIP(hipStreamSynchronize(s));
     }
@@ -868,7 +880,7 @@ extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_var
     Ctl c{w.segA, w.ctl + 1, w.ctl + 4, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
     if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
     SYZ_LAUNCH_CHECK();
-    if (int rc = run_rounds(w, s)) return rc;
+    if (int rc = run_rounds(w, s, (int64_t)n)) return rc;
     SYZ_HIP(hipMemcpyAsync(order, w.I, n * 4, hipMemcpyDeviceToDevice, s));
     return 0;
 }
