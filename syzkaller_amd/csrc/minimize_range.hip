@@ -27,7 +27,12 @@
 // and one LDS bit test.  (A whole-wave path for long
 // sub-runs remains for the SMALL_M variants.)
 //
-// Record overflow (more uncovered occurrences than rec_cap, only for
+// Records go to NCTR regions of the record buffer, each with its own counter
+// (workgroup b appends to region b mod NCTR): one counter for the whole chip
+// serialised every wave's reservation on a single address, which dominated the
+// early chunks, where nearly every PC is a record.
+//
+// Record overflow (more uncovered occurrences than a region holds, only for
 // adversarial corpora) is detected on the device; the fallback kernels then
 // rescan candidate items and derive the union from first_w, so the result
 // stays exact for every input.
@@ -50,6 +55,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 constexpr int MAX_R = 256;
+constexpr int NCTR = 64;        // record regions (counters)
+constexpr int CTR_STRIDE = 32;  // u64s between counters (256 B: separate lines)
 
 struct Args {
     const uint64_t *off;
@@ -65,7 +72,10 @@ struct Args {
     int32_t *first_w;          // [span], INT32_MAX outside records
     unsigned long long *rec;   // (rank << 32) | window offset
     uint64_t rec_cap;
-    unsigned long long *rec_cnt;  // may exceed rec_cap (overflow)
+    unsigned long long *rec_cnt;  // total (ABI); > rec_cap if a region overflowed
+    unsigned long long *ctr;   // [NCTR * CTR_STRIDE] records appended per region
+    unsigned long long *done;  // [NCTR * CTR_STRIDE] records already in `covered`
+    uint64_t cap_k;            // records per region: rec[k * cap_k ...]
     uint8_t *cand;             // [items] item had an uncovered PC
     // rank-ordered descriptors (prep_kernel): coalesced per (range, item slice)
     const uint64_t *base_r;    // [items] off[order[j]]
@@ -145,6 +155,9 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
     __shared__ uint32_t s_plan[MAX_R + 1];
     uint32_t rho, i0, i1;
     if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
+    const uint32_t region = blockIdx.x % NCTR;
+    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
+    unsigned long long *const rrec = A.rec + region * A.cap_k;
     const uint32_t nwords = (1u << A.rshift) >> 5;
     {
         const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
@@ -234,7 +247,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                     const uint32_t incl = wave_incl_scan(cnt);
                     const uint32_t tot = __shfl(incl, 63, 64);
                     unsigned long long basei = 0;
-                    if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)tot);
+                    if (l == 0) basei = atomicAdd(rctr, (unsigned long long)tot);
                     uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
                     if (um) {
                         A.cand[ib + sl] = 1;
@@ -246,8 +259,8 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = vv[k] - A.pc_lo;
                                     atomicMin(&A.first_w[wo], rki);
-                                    if (slot < A.rec_cap)
-                                        A.rec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    if (slot < A.cap_k)
+                                        rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
                                     slot++;
                                 }
                         }
@@ -301,7 +314,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                     const uint32_t incl = wave_incl_scan(cnt);
                     const uint32_t tot = __shfl(incl, 63, 64);
                     unsigned long long basei = 0;
-                    if (l == 0) basei = atomicAdd(A.rec_cnt, (unsigned long long)tot);
+                    if (l == 0) basei = atomicAdd(rctr, (unsigned long long)tot);
                     uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
                     if (l == 0) A.cand[ib + i] = 1;
                     if (um) {
@@ -313,8 +326,8 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = vv[k] - A.pc_lo;
                                     atomicMin(&A.first_w[wo], rki);
-                                    if (slot < A.rec_cap)
-                                        A.rec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    if (slot < A.cap_k)
+                                        rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
                                     slot++;
                                 }
                         }
@@ -325,22 +338,40 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
     }
 }
 
-// covered |= records [*done, min(*cnt, cap)); then *done advances (next kernel).
-__global__ void cover_records_kernel(const unsigned long long *rec, uint64_t cap,
-                                     const unsigned long long *cnt, const unsigned long long *done,
-                                     uint32_t *covered) {
-    const uint64_t lo = *done, hi = std::min<uint64_t>(*cnt, cap);
-    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t wo = (uint32_t)rec[i];
+// Region loops: block b serves region b % NCTR (the grid is a multiple of
+// NCTR), records [lo_k, min(ctr_k, cap_k)) of it.
+#define SYZ_FOR_RECORDS(A, LO, i, r)                                                          \
+    const uint32_t k_ = blockIdx.x % NCTR, sub_ = blockIdx.x / NCTR, nsub_ = gridDim.x / NCTR; \
+    const uint64_t hi_ = std::min<uint64_t>((A).ctr[k_ * CTR_STRIDE], (A).cap_k);             \
+    const unsigned long long *rk_ = (A).rec + k_ * (A).cap_k;                                 \
+    for (uint64_t i = (LO) + (uint64_t)sub_ * blockDim.x + threadIdx.x; i < hi_;               \
+         i += (uint64_t)nsub_ * blockDim.x)                                                   \
+        if (const unsigned long long r = rk_[i]; true)
+
+// covered |= the records appended since the last chunk; then done advances.
+__global__ void cover_records_kernel(Args A) {
+    SYZ_FOR_RECORDS(A, A.done[(blockIdx.x % NCTR) * CTR_STRIDE], i, r) {
+        const uint32_t wo = (uint32_t)r;
         const uint32_t mbit = 1u << (wo & 31);
-        if (!(covered[wo >> 5] & mbit)) atomicOr(&covered[wo >> 5], mbit);
+        if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
     }
 }
 
-__global__ void advance_kernel(const unsigned long long *cnt, unsigned long long *done,
-                               uint64_t cap) {
-    if (threadIdx.x == 0) *done = std::min<uint64_t>(*cnt, cap);
+__global__ void advance_kernel(Args A) {
+    const uint32_t k = threadIdx.x;
+    if (k < NCTR)
+        A.done[k * CTR_STRIDE] = std::min<uint64_t>(A.ctr[k * CTR_STRIDE], A.cap_k);
+}
+
+// *rec_cnt = total records, or more than rec_cap if any region overflowed
+// (the overflow fallbacks key on that).
+__global__ void total_kernel(Args A) {
+    const uint32_t k = threadIdx.x;
+    unsigned long long c = k < NCTR ? A.ctr[k * CTR_STRIDE] : 0ull;
+    int ovf = k < NCTR && c > A.cap_k;
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    ovf = __any(ovf);
+    if (k == 0) *A.rec_cnt = ovf ? std::max<unsigned long long>(c, A.rec_cap + 1) : c;
 }
 
 // The first-cover rank of window offset wo: first_w[wo] on one GPU; across
@@ -356,25 +387,16 @@ __device__ __forceinline__ int32_t first_of(const int32_t *first_w, const uint64
 }
 
 // Pass 2 over the records: kept[rank] = 1 iff first(pc) == rank.
-__global__ void pass2_kernel(const unsigned long long *rec, uint64_t cap,
-                             const unsigned long long *cnt, const int32_t *first_w,
-                             const uint64_t *tab, const int32_t *first_d, uint8_t *kept) {
-    const uint64_t hi = std::min<uint64_t>(*cnt, cap);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned long long r = rec[i];
+__global__ void pass2_kernel(Args A, const uint64_t *tab, const int32_t *first_d, uint8_t *kept) {
+    SYZ_FOR_RECORDS(A, 0, i, r) {
         const int32_t rank = (int32_t)(r >> 32);
-        if (first_of(first_w, tab, first_d, (uint32_t)r) == rank) kept[rank] = 1;
+        if (first_of(A.first_w, tab, first_d, (uint32_t)r) == rank) kept[rank] = 1;
     }
 }
 
 // first_w back to INT32_MAX at every recorded offset (after pass 2).
-__global__ void reset_kernel(const unsigned long long *rec, uint64_t cap,
-                             const unsigned long long *cnt, int32_t *first_w) {
-    const uint64_t hi = std::min<uint64_t>(*cnt, cap);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        first_w[(uint32_t)rec[i]] = INT32_MAX;
+__global__ void reset_kernel(Args A) {
+    SYZ_FOR_RECORDS(A, 0, i, r) A.first_w[(uint32_t)r] = INT32_MAX;
 }
 
 // ---- overflow fallbacks (early exit unless *cnt > cap)
@@ -439,7 +461,9 @@ __global__ void first_dense_kernel(const uint64_t *__restrict__ tab, uint64_t nw
 
 using namespace syz;
 
-/* ws: rec_done (u64) | base_r [n_items] u64 | split_t [nrange][n_items] u32 */
+/* ws: region counters ctr | done (NCTR * 256 B each) | base_r [n_items] u64 |
+ *     split_t [nrange][n_items] u32 */
+static constexpr size_t MR_HDR = 2 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t);
 static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
     return (span + (1ull << rshift) - 1) >> rshift;
 }
@@ -447,7 +471,7 @@ static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
 extern "C" size_t syzcov_dev_minimize_range_ws_size(size_t n_items, uint64_t pc_span,
                                                     uint32_t range_shift) {
     if (range_shift > 20) range_shift = 20;
-    return 256 + align_up(n_items * 8, 256) +
+    return MR_HDR + align_up(n_items * 8, 256) +
            align_up(mr_nrange(pc_span, range_shift) * n_items * 4, 256);
 }
 
@@ -482,7 +506,10 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.rec_cnt = (unsigned long long *)rec_cnt;
     A.cand = cand;
     A.n_items = (uint32_t)n_items;
-    A.base_r = (uint64_t *)((uint8_t *)ws + 256);
+    A.ctr = (unsigned long long *)ws;
+    A.done = A.ctr + mr::NCTR * mr::CTR_STRIDE;
+    A.cap_k = rec_cap / mr::NCTR;
+    A.base_r = (uint64_t *)((uint8_t *)ws + MR_HDR);
     A.split_t = (uint32_t *)((uint8_t *)A.base_r + align_up(n_items * 8, 256));
     return 0;
 }
@@ -490,13 +517,11 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
 // pass 2 + resets (first_w back to INT32_MAX)
 static int mr_pass2(const mr::Args &A, uint64_t pc_span, const uint64_t *tab,
                     const int32_t *first_d, uint8_t *kept, hipStream_t s) {
-    const unsigned long long *rec = A.rec, *cnt = A.rec_cnt;
-    hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, rec, A.rec_cap, cnt,
-                       (const int32_t *)A.first_w, tab, first_d, kept);
+    const unsigned long long *cnt = A.rec_cnt;
+    hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, A, tab, first_d, kept);
     hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, A.n_items,
                        (const int32_t *)A.first_w, tab, first_d, kept);
-    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, rec, A.rec_cap, cnt,
-                       A.first_w);
+    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, A);
     hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s, cnt, A.rec_cap, A.first_w,
                        pc_span);
     SYZ_LAUNCH_CHECK();
@@ -520,9 +545,7 @@ extern "C" int syzcov_dev_minimize_range(
                      range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
     if (rc) return rc;
     const uint64_t nrange = A.nrange;
-    unsigned long long *done = (unsigned long long *)ws;
-    SYZ_HIP(hipMemsetAsync(done, 0, sizeof(uint64_t), s));
-    SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
+    SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters and done marks
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
@@ -578,15 +601,12 @@ extern "C" int syzcov_dev_minimize_range(
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
-        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s,
-                           (const unsigned long long *)rec, rec_cap,
-                           (const unsigned long long *)rec_cnt, (const unsigned long long *)done,
-                           covered);
-        hipLaunchKernelGGL(mr::advance_kernel, dim3(1), dim3(64), 0, s,
-                           (const unsigned long long *)rec_cnt, done, rec_cap);
+        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(mr::advance_kernel, dim3(1), dim3(mr::NCTR), 0, s, A);
         a = b;
         step *= growth;
     }
+    hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
     // record overflow: the union comes from first_w instead
     hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
                        (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
