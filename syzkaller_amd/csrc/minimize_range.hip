@@ -85,16 +85,36 @@ struct Args {
 
 // Gather the items' CSR bases and split columns into rank order, transposed
 // so that a workgroup owning range rho reads split_t[rho][i0..i1) contiguously.
+// A tile of 64 items is read row by row (each item's nrange split points are
+// contiguous, so a wave reads whole rows), transposed in LDS (row stride
+// nrange + 1: conflict-free column reads for even nrange) and written one
+// range column of 64 items at a time.  Dynamic LDS: 64 * (nrange + 1) u32.
 __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uint32_t *split_t) {
-    const uint32_t n = A.n_items;
+    extern __shared__ uint32_t s_tile[];
+    __shared__ uint32_t s_seg[64];
+    const uint32_t n = A.n_items, R = A.nrange, ld = R + 1;
     for (uint32_t t0 = blockIdx.x * 64; t0 < n; t0 += gridDim.x * 64) {
-        const uint32_t j = t0 + (threadIdx.x & 63);
-        if (j >= n) continue;
-        const uint32_t seg = (uint32_t)A.order[j];
-        if (threadIdx.x < 64) base_r[j] = A.off[seg];
-        for (uint32_t rho = threadIdx.x >> 6; rho < A.nrange; rho += 4)
-            split_t[(uint64_t)rho * n + j] =
-                A.split ? A.split[(uint64_t)seg * A.nrange + rho] : A.len[seg];
+        const uint32_t rows = min(64u, n - t0);
+        if (threadIdx.x < rows) {
+            const uint32_t seg = (uint32_t)A.order[t0 + threadIdx.x];
+            s_seg[threadIdx.x] = seg;
+            base_r[t0 + threadIdx.x] = A.off[seg];
+        }
+        __syncthreads();
+        if (!A.split) {  // one range: the column is the canonical length
+            if (threadIdx.x < rows) split_t[t0 + threadIdx.x] = A.len[s_seg[threadIdx.x]];
+        } else {
+            for (uint32_t e = threadIdx.x; e < rows * R; e += blockDim.x) {
+                const uint32_t r = e / R, c = e - r * R;
+                s_tile[r * ld + c] = A.split[(uint64_t)s_seg[r] * R + c];
+            }
+            __syncthreads();
+            for (uint32_t e = threadIdx.x; e < 64 * R; e += blockDim.x) {
+                const uint32_t rho = e >> 6, jj = e & 63;
+                if (jj < rows) split_t[(uint64_t)rho * n + t0 + jj] = s_tile[jj * ld + rho];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -546,7 +566,14 @@ extern "C" int syzcov_dev_minimize_range(
     if (rc) return rc;
     const uint64_t nrange = A.nrange;
     SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters and done marks
-    hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256), 0, s, A,
+    static bool prep_attr = false;  // nrange = 256 needs 65.8 KB of dynamic LDS
+    if (!prep_attr) {
+        SYZ_HIP(hipFuncSetAttribute((const void *)mr::prep_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
+        prep_attr = true;
+    }
+    hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256),
+                       split ? 64 * (nrange + 1) * sizeof(uint32_t) : 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / 8;
     // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (32-lane groups),
