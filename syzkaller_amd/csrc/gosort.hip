@@ -33,7 +33,10 @@ namespace syz {
 namespace gsort {
 
 constexpr int SMALL = 4096;  // segment finished in one workgroup's LDS
-constexpr int TINY = 64;     // leaf finished by one lane
+#ifndef SYZ_GSORT_TINY
+#define SYZ_GSORT_TINY 32
+#endif
+constexpr int TINY = SYZ_GSORT_TINY;  // leaf finished by one lane
 constexpr int CH = 4096;     // elements per block in the global rounds
 constexpr int WG = 256;
 
@@ -428,12 +431,134 @@ __global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
 
 // ------------------------------------------------------- in-LDS finisher
 // One workgroup per segment of <= SMALL elements: tasks are popped by lane 0
-// (O(1) control steps), partitions run WG-parallel, leaves of <= TINY
+// (O(1) control steps), partitions of tasks longer than MID run WG-parallel;
+// tasks of TINY < n <= MID are then dealt to the 4 waves, each running its
+// own loop with wave-parallel partitions (no workgroup barriers; tasks are
+// disjoint and read only the finished pivot left of them); leaves of <= TINY
 // elements are collected and finished one per lane at the end.
 struct LTask {
     int16_t a, b;  // relative to the segment start
     int16_t limit, flags;
 };
+#ifndef SYZ_GSORT_MID
+#define SYZ_GSORT_MID 1024
+#endif
+constexpr int MID = SYZ_GSORT_MID;  // tasks up to MID run on one wave
+constexpr int MCAP = SMALL / TINY * 2;  // mid tasks per segment
+constexpr int WSTK = SMALL / TINY / 4 + 32;  // per-wave stack (its share + depth)
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One loop of pdqsort on a wave over the tasks in its stack (lane 0: control
+// steps; all lanes: the Hoare partition with wave prefix sums).  PL / PR are
+// indexed by the task's own positions, so waves never share them.
+__device__ void wave_tasks(LAcc d, int a, LTask *stk, int depth, LTask *tiny, int *ntiny,
+                           int16_t *PL, int16_t *PR, uint32_t *err) {
+    const uint32_t l = __lane_id();
+    int sp = depth;  // stack size (uniform)
+    while (sp > 0) {
+        int mode = 3, ta = 0, tb = 0, limit = 0, flags = 0;
+        if (l == 0) {
+            const LTask lt = stk[--sp];
+            ta = a + lt.a;
+            tb = a + lt.b;
+            const int tn = lt.b - lt.a;
+            limit = lt.limit;
+            flags = lt.flags;
+            if (tn <= TINY) {
+                if (tn > 1) {
+                    const int q = atomicAdd(ntiny, 1);
+                    if (q < SMALL / 2) tiny[q] = lt; else *err = 4u;
+                }
+            } else if (limit == 0) {
+                gocore::heap_sort(d, ta, tb);
+            } else {
+                const bool wb = flags & 1, wp = flags & 2;
+                if (!wb) {
+                    gocore::break_patterns(d, ta, tb);
+                    limit--;
+                }
+                int hint;
+                int pivot = gocore::choose_pivot(d, ta, tb, &hint);
+                if (hint == gocore::kDecreasing) {
+                    gocore::reverse_range(d, ta, tb);
+                    pivot = (tb - 1) - (pivot - ta);
+                    hint = gocore::kIncreasing;
+                }
+                if (!(wb && wp && hint == gocore::kIncreasing &&
+                      gocore::partial_insertion_sort(d, ta, tb))) {
+                    const int eq = ta > 0 && !d.less(ta - 1, pivot);
+                    d.swap(ta, pivot);
+                    mode = eq ? 2 : 1;
+                }
+            }
+        }
+        sp = __shfl(sp, 0, 64);
+        mode = __shfl(mode, 0, 64);
+        wave_sync_lds();
+        if (mode == 3) continue;
+        ta = __shfl(ta, 0, 64);
+        tb = __shfl(tb, 0, 64);
+        const int eq = mode == 2;
+        const uint32_t kp = d.K[ta - a + 1];
+        const int len = tb - ta - 1;
+        const int per = (len + 63) / 64;
+        const int x0 = ta + 1 + (int)l * per, x1 = min(tb, x0 + per);
+        uint32_t c = 0;
+        for (int x = x0; x < x1; x++) c += left_group(d.K[x - a + 1], kp, eq);
+        const uint32_t inc = wave_incl_scan(c);
+        const uint32_t cnt = __shfl(inc, 63, 64);
+        uint32_t pf = inc - c;
+        const int L = ta + (int)cnt;
+        const int base = ta - a;  // this task's PL / PR window
+        uint32_t mine = 0;
+        for (int x = x0; x < x1; x++) {
+            const bool f = left_group(d.K[x - a + 1], kp, eq);
+            if (x > L && f) PR[base + (int)cnt - (int)pf - 1] = (int16_t)(x - a);
+            if (x <= L && !f) {
+                PL[base + (x - (ta + 1)) - (int)pf] = (int16_t)(x - a);
+                mine++;
+            }
+            pf += f;
+        }
+        const uint32_t m = wave_sum(mine);
+        wave_sync_lds();
+        for (int k = (int)l; k < (int)m; k += 64) d.swap(a + PL[base + k], a + PR[base + k]);
+        wave_sync_lds();
+        if (l == 0) {
+            if (eq) {
+                const int na = ta + 1 + (int)cnt;
+                if (tb - na > 1)
+                    stk[sp++] = LTask{(int16_t)(na - a), (int16_t)(tb - a), (int16_t)limit,
+                                      (int16_t)flags};
+            } else {
+                const int mid = ta + (int)cnt;
+                d.swap(mid, ta);
+                const int already = m == 0;
+                const int tn = tb - ta, ln = mid - ta, rn = tb - mid, thr = tn / 8;
+                LTask cont, fresh;
+                if (ln < rn) {
+                    cont = LTask{(int16_t)(mid + 1 - a), (int16_t)(tb - a), (int16_t)limit,
+                                 (int16_t)((ln >= thr) | (already << 1))};
+                    fresh = LTask{(int16_t)(ta - a), (int16_t)(mid - a), (int16_t)limit, 3};
+                } else {
+                    cont = LTask{(int16_t)(ta - a), (int16_t)(mid - a), (int16_t)limit,
+                                 (int16_t)((rn >= thr) | (already << 1))};
+                    fresh = LTask{(int16_t)(mid + 1 - a), (int16_t)(tb - a), (int16_t)limit, 3};
+                }
+                if (cont.b - cont.a > 1 && sp < WSTK) stk[sp++] = cont;
+                else if (cont.b - cont.a > 1) *err = 5u;
+                if (fresh.b - fresh.a > 1 && sp < WSTK) stk[sp++] = fresh;
+                else if (fresh.b - fresh.a > 1) *err = 5u;
+            }
+        }
+        sp = __shfl(sp, 0, 64);
+        wave_sync_lds();
+    }
+}
 
 __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small,
                                                     const uint32_t *__restrict__ nsmall_p,
@@ -443,10 +568,12 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
     constexpr int TCAP = SMALL / 2;
     __shared__ uint32_t K[SMALL + 1];
     __shared__ int32_t I[SMALL + 1];
-    __shared__ int32_t PL[SMALL];
-    __shared__ int32_t PR[SMALL];
+    __shared__ int16_t PL[SMALL];  // positions relative to the segment start
+    __shared__ int16_t PR[SMALL];  // (int16: two workgroups per CU fit in LDS)
     __shared__ LTask tiny[TCAP];
     __shared__ LTask stk[40];
+    __shared__ LTask mids[MCAP];
+    __shared__ LTask wstk[WG / 64][WSTK];
     __shared__ int sh[8];
     __shared__ uint32_t tmp[WG / 64 + 1];
     const uint32_t nsmall = *nsmall_p;
@@ -463,6 +590,7 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
             stk[0] = LTask{0, (int16_t)n, (int16_t)g.limit, (int16_t)g.flags};
             sh[0] = 1;  // stack size
             sh[1] = 0;  // tiny count
+            sh[7] = 0;  // mid count
         }
         __syncthreads();
         LAcc d{K, I, a};
@@ -483,6 +611,11 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
                             else
                                 *err = 4u;
                         }
+                    } else if (tn <= MID) {  // to the wave phase
+                        if (sh[7] < MCAP)
+                            mids[sh[7]++] = lt;
+                        else
+                            *err = 4u;
                     } else if (limit == 0) {
                         gocore::heap_sort(d, ta, tb);
                     } else {
@@ -530,16 +663,16 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
             uint32_t mine = 0;
             for (int x = x0; x < x1; x++) {
                 const bool f = left_group(K[x - a + 1], kp, eq);
-                if (x > L && f) PR[(int)cnt - (int)pf - 1] = x;
+                if (x > L && f) PR[(int)cnt - (int)pf - 1] = (int16_t)(x - a);
                 if (x <= L && !f) {
-                    PL[(x - (ta + 1)) - (int)pf] = x;
+                    PL[(x - (ta + 1)) - (int)pf] = (int16_t)(x - a);
                     mine++;
                 }
                 pf += f;
             }
             uint32_t m;
             block_excl_scan<WG>(mine, tmp, &m);  // total misplaced pairs (barriers)
-            for (int k = threadIdx.x; k < (int)m; k += WG) d.swap(PL[k], PR[k]);
+            for (int k = threadIdx.x; k < (int)m; k += WG) d.swap(a + PL[k], a + PR[k]);
             __syncthreads();
             if (threadIdx.x == 0) {
                 const int limit = sh[4], flags = sh[5];
@@ -570,6 +703,23 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
             }
             __syncthreads();
         }
+        // ---- mid tasks: dealt round-robin to the waves, one loop per wave
+        {
+            const uint32_t w = threadIdx.x >> 6;
+            const int nm = sh[7];
+            int depth = 0;
+            for (int q = (int)w; q < nm; q += WG / 64) {
+                if (depth < WSTK) {
+                    if (__lane_id() == 0) wstk[w][depth] = mids[q];
+                } else if (__lane_id() == 0) {
+                    *err = 5u;
+                }
+                depth++;
+            }
+            wave_sync_lds();
+            wave_tasks(d, a, wstk[w], min(depth, WSTK), tiny, &sh[1], PL, PR, err);
+        }
+        __syncthreads();
         // ---- leaves: one lane each, Go's sequential loop
         const int nt = sh[1];
         for (int q = threadIdx.x; q < nt; q += WG) {
