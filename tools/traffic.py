@@ -15,7 +15,7 @@ PHASES = {
     "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
               "large_"),
     "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel", "advance_kernel",
-                 "pass2_kernel", "ovf_", "reset_kernel"),
+                 "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
     "order": ("gsort::",),
     "compact": ("compact_", "scan_blocks"),
     "union": ("dict_",),
