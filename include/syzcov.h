@@ -321,7 +321,7 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
  * handled exactly by fallback kernels).  cand: u8 per item (pre-zeroed).
  * kept: u8 per rank (pre-zeroed) receives kept[rank] = 1 (do_pass2).  first_chunk /
  * growth / pcs_per_wg_hint tune the chunk schedule (0 = defaults: 64, 4,
- * 2^17); any values give the same result.
+ * 2^19); any values give the same result.
  * ws: syzcov_dev_minimize_range_ws_size(n_items, pc_span, range_shift). */
 size_t syzcov_dev_minimize_range_ws_size(size_t n_items, uint64_t pc_span, uint32_t range_shift);
 int syzcov_dev_minimize_range(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,

@@ -368,19 +368,20 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
          i += (uint64_t)nsub_ * blockDim.x)                                                   \
         if (const unsigned long long r = rk_[i]; true)
 
-// covered |= the records appended since the last chunk; then done advances.
-__global__ void cover_records_kernel(Args A) {
-    SYZ_FOR_RECORDS(A, A.done[(blockIdx.x % NCTR) * CTR_STRIDE], i, r) {
+// covered |= the records appended since the last chunk.  The done marks are
+// double-buffered: chunk c reads set c % 2 and one thread per region writes
+// the new mark into the other set, so no separate advance launch is needed.
+__global__ void cover_records_kernel(Args A, int par) {
+    const unsigned long long *done_in = A.done + (par ? 1 : 0) * NCTR * CTR_STRIDE;
+    unsigned long long *done_out = A.done + (par ? 0 : 1) * NCTR * CTR_STRIDE;
+    if (blockIdx.x < NCTR && threadIdx.x == 0)
+        done_out[blockIdx.x * CTR_STRIDE] =
+            std::min<uint64_t>(A.ctr[blockIdx.x * CTR_STRIDE], A.cap_k);
+    SYZ_FOR_RECORDS(A, done_in[(blockIdx.x % NCTR) * CTR_STRIDE], i, r) {
         const uint32_t wo = (uint32_t)r;
         const uint32_t mbit = 1u << (wo & 31);
         if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
     }
-}
-
-__global__ void advance_kernel(Args A) {
-    const uint32_t k = threadIdx.x;
-    if (k < NCTR)
-        A.done[k * CTR_STRIDE] = std::min<uint64_t>(A.ctr[k * CTR_STRIDE], A.cap_k);
 }
 
 // *rec_cnt = total records, or more than rec_cap if any region overflowed
@@ -481,9 +482,9 @@ __global__ void first_dense_kernel(const uint64_t *__restrict__ tab, uint64_t nw
 
 using namespace syz;
 
-/* ws: region counters ctr | done (NCTR * 256 B each) | base_r [n_items] u64 |
+/* ws: region counters ctr | done marks x 2 (NCTR * 256 B each) | base_r [n_items] u64 |
  *     split_t [nrange][n_items] u32 */
-static constexpr size_t MR_HDR = 2 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t);
+static constexpr size_t MR_HDR = 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t);
 static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
     return (span + (1ull << rshift) - 1) >> rshift;
 }
@@ -613,9 +614,11 @@ extern "C" int syzcov_dev_minimize_range(
     }
     if (first_chunk == 0) first_chunk = 64;
     if (growth < 2) growth = 4;
-    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 17;
+    if (const char *e = getenv("SYZCOV_MR_WG")) pcs_per_wg_hint = strtoull(e, nullptr, 0);  // tuning
+    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;  // sweep: 2^17 4.03, 2^19 4.00, 2^20 4.40 ms
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     uint64_t a = 0, step = first_chunk;
+    int par = 0;  // done-mark set of this chunk
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
         // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
@@ -628,8 +631,8 @@ extern "C" int syzcov_dev_minimize_range(
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
-        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A);
-        hipLaunchKernelGGL(mr::advance_kernel, dim3(1), dim3(mr::NCTR), 0, s, A);
+        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A, par);
+        par ^= 1;
         a = b;
         step *= growth;
     }

@@ -14,7 +14,7 @@ import sys
 PHASES = {
     "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
               "large_"),
-    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel", "advance_kernel",
+    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
     "order": ("gsort::",),
     "compact": ("compact_", "scan_blocks"),
