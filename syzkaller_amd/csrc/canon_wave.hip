@@ -172,7 +172,7 @@ struct Params {
 
 // Wave-aggregated binning of segments into capacity classes (one atomic per
 // wave and class): lists[c][..] = segments with cls_lo[c] <= n <= cls_hi[c].
-constexpr int NCLS = 6;
+constexpr int NCLS = 5;
 struct Classes { uint32_t lo[NCLS], hi[NCLS]; };
 
 __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ off, uint64_t nseg,
@@ -551,13 +551,16 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     bool bitonic = false;
     if (const char *e = getenv("SYZCOV_CANON")) bitonic = strcmp(e, "bitonic") == 0;
     cw::Classes C;
-    const uint32_t nk[cw::NCLS] = {16, 32, 40, 48, 64, 128};
+    // (a 1024-key class for the segments of <= 1021 keys measured slower than
+    // sending them to the 2048-key class: 7.85 vs 7.79 ms at C2; its short
+    // kernel was mostly ramp and tail)
+    const uint32_t nk[cw::NCLS] = {32, 40, 48, 64, 128};
     for (int c = 0; c < cw::NCLS; c++) {
         C.lo[c] = c ? nk[c - 1] * 64 - 2 : 0;  // CAP - 3 + 1 of the previous class
         C.hi[c] = nk[c] * 64 - 3;
     }
     if (bitonic) {  // 1, 2, 4 waves of 2048 keys
-        const uint32_t bl[cw::NCLS] = {0, 2046, 4094, 1, 1, 1}, bh[cw::NCLS] = {2045, 4093, 8189, 0, 0, 0};
+        const uint32_t bl[cw::NCLS] = {0, 2046, 4094, 1, 1}, bh[cw::NCLS] = {2045, 4093, 8189, 0, 0};
         for (int c = 0; c < cw::NCLS; c++) C.lo[c] = bl[c], C.hi[c] = bh[c];
     }
     uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
@@ -576,12 +579,11 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
-        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<16, 5>), dim3(resident_grid<16, 5>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(resident_grid<32, SYZ_CANON_W32>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(resident_grid<40, SYZ_CANON_W40>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(resident_grid<48, SYZ_CANON_W48>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(resident_grid<64, 2>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 5: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(resident_grid<128, 1>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(resident_grid<32, SYZ_CANON_W32>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(resident_grid<40, SYZ_CANON_W40>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(resident_grid<48, SYZ_CANON_W48>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(resident_grid<64, 2>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(resident_grid<128, 1>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
         }
         SYZ_LAUNCH_CHECK();
     }
