@@ -129,15 +129,21 @@ class CorpusEngine:
 
     def sort_order(self, lens32: torch.Tensor, n: int):
         """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
-        self.lens64[:n].copy_(lens32[:n].to(torch.int64))
+        self.lens64[:n].copy_(lens32[:n])  # int32 -> int64 in the copy kernel
         check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
                                            _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
 
-    def minimize(self, off, order, ranks, n_items, do_pass2=True):
-        """Range-partitioned first-cover Minimize; leaves the union in covered."""
+    def minimize_clear(self, n_items):
+        """Zero minimize's inputs (covered, cand, kept)."""
         self.covered.zero_()
         self.cand[:n_items].zero_()
         self.kept.zero_()
+
+    def minimize(self, off, order, ranks, n_items, do_pass2=True, cleared=False):
+        """Range-partitioned first-cover Minimize; leaves the union in covered.
+        cleared: minimize_clear() already ran on this stream."""
+        if not cleared:
+            self.minimize_clear(n_items)
         check(self.L.syzcov_dev_minimize_range(
             _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
             n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
@@ -184,9 +190,12 @@ class CorpusEngine:
         mark_ev()
         self.canonicalize(off, raw, n)
         mark_ev()
+        # queued ahead of the sort, whose final read-back leaves the GPU idle
+        # while the host issues the next launches
+        self.minimize_clear(n)
         self.sort_order(self.new_len, n)
         mark_ev()
-        self.minimize(off, self.order, None, n)
+        self.minimize(off, self.order, None, n, cleared=True)
         mark_ev()
         self.compact(n)
         mark_ev()
