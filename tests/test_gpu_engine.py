@@ -61,6 +61,29 @@ def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
     assert res2.max_cover == exp_union.size
 
 
+@pytest.mark.parametrize("rec_cap", [64, 64 * 300, 64 * 5000])
+def test_engine_record_overflow(torch, rec_cap):
+    """Records overflowing their region (all regions at 64, some at 64 * 300)
+    take the exact fallbacks: same kept list and union, and first_w is left
+    all INT32_MAX (a second step gives the same result)."""
+    from syzkaller_amd.engine import INT32_MAX, CorpusEngine, synth_corpus, synth_window
+    n, seed, log2 = 3000, 0x5EED0007, 14
+    off, raw, lens, total = synth_corpus(n, seed, mean=400, sigma=150, log2_space=log2)
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, rec_cap=rec_cap)
+    o_off, o_pcs = orc.synth_corpus(seed, n, mean=400, sigma=150, log2_space=log2)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    exp_kept = list(orc.minimize_csr(c_off, c_pcs))
+    exp_union = orc.union_fold_csr(c_off, c_pcs)
+    for _ in range(2):
+        res = eng.step(off, raw, n)
+        assert res.kept_idx.cpu().numpy().tolist() == exp_kept
+        assert np.array_equal(_to_np_u32(res.union), exp_union)
+        assert bool((eng.first == INT32_MAX).all().item())
+    if rec_cap == 64:
+        assert int(eng.rec_cnt.item()) > rec_cap  # the fallback path ran
+
+
 def test_engine_sentinel_window(torch):
     """Window touching 0xFFFFFFFF: inputs made only of the sentinel canonicalize
     to empty, otherwise it is an ordinary PC (cover.go:36-52, 104-131)."""
