@@ -348,7 +348,10 @@ __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
 }
 
 // ranks of the misplaced elements: PL[a + k] / PR[a + k] = position of the
-// k-th left-misplaced (from the left) / right-misplaced (from the right)
+// k-th left-misplaced (from the left) / right-misplaced (from the right).
+// Each wave owns a contiguous quarter of the block's chunk: it counts its
+// left-group elements, one barrier gives the waves' offsets, and it then
+// ranks its rows with ballots (no block scans inside the loop).
 __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    const uint32_t *__restrict__ ncur_p,
                                                    Plan *__restrict__ plan,
@@ -356,7 +359,8 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    const uint32_t *__restrict__ cc,
                                                    uint32_t stride, int32_t *__restrict__ PL,
                                                    int32_t *__restrict__ PR) {
-    __shared__ uint32_t tmp[WG / 64 + 1];
+    constexpr int NW = WG / 64, WCH = CH / NW;  // elements per wave
+    __shared__ uint32_t wcnt[NW];
     const uint32_t s = blockIdx.y;
     if (s >= *ncur_p) return;
     const Plan p = plan[s];
@@ -365,15 +369,24 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
     const int x0 = g.a + 1 + (int)blockIdx.x * CH;
     if (x0 >= g.b) return;
     const int x1 = min(g.b, x0 + CH);
-    const int L = g.a + p.cnt;  // left region [a+1, L]
+    const uint32_t w = threadIdx.x >> 6, l = __lane_id();
+    const uint64_t lt = (1ull << l) - 1ull;
+    const int w0 = x0 + (int)w * WCH, w1 = min(x1, w0 + WCH);
+    uint32_t c = 0;
+    for (int x = w0 + (int)l; x < w1; x += 64) c += left_group(K[x], p.kp, p.eq);
+    c = wave_sum(c);
+    if (l == 0) wcnt[w] = c;
+    __syncthreads();
     uint32_t base = cc[(size_t)s * stride + blockIdx.x];
+    for (uint32_t v = 0; v < w; v++) base += wcnt[v];
+    const int L = g.a + p.cnt;  // left region [a+1, L]
     uint32_t mloc = 0;
-    for (int c0 = x0; c0 < x1; c0 += WG) {
-        const int x = c0 + threadIdx.x;
-        const bool in = x < x1;
+    for (int c0 = w0; c0 < w1; c0 += 64) {
+        const int x = c0 + (int)l;
+        const bool in = x < w1;
         const bool f = in && left_group(K[x], p.kp, p.eq);
-        uint32_t total;
-        const uint32_t pf = base + block_excl_scan<WG>(f ? 1u : 0u, tmp, &total);
+        const uint64_t m = __ballot(f);
+        const uint32_t pf = base + (uint32_t)__popcll(m & lt);
         if (in) {
             if (x > L && f) PR[g.a + (p.cnt - (int)pf - 1)] = x;
             if (x <= L && !f) {
@@ -381,10 +394,10 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                 mloc++;
             }
         }
-        base += total;
+        base += (uint32_t)__popcll(m);
     }
     mloc = wave_sum(mloc);
-    if (__lane_id() == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
+    if (l == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
 }
 
 // The m swaps of the partition, then (last block of the segment) the tail of

@@ -615,6 +615,8 @@ extern "C" int syzcov_dev_minimize_range(
     if (first_chunk == 0) first_chunk = 64;
     if (growth < 2) growth = 4;
     if (const char *e = getenv("SYZCOV_MR_WG")) pcs_per_wg_hint = strtoull(e, nullptr, 0);  // tuning
+    uint64_t g_min = 256;  // at least one workgroup per CU
+    if (const char *e = getenv("SYZCOV_MR_GMIN")) g_min = strtoull(e, nullptr, 0);  // tuning
     if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;  // sweep: 2^17 4.03, 2^19 4.00, 2^20 4.40 ms
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     uint64_t a = 0, step = first_chunk;
@@ -624,7 +626,7 @@ extern "C" int syzcov_dev_minimize_range(
         // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
         // P = 2R workgroups per item slice
         uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
-        G = std::min<uint64_t>(std::max<uint64_t>(G, 256), 8192);
+        G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
         uint64_t P = 2 * nrange;
         if (pmode == 1) P = G;
         else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // tuning: wider slices
