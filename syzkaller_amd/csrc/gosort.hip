@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 
@@ -977,7 +978,8 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     // BOUNDS for the grids (a segment has at most two large children, each
     // shorter than it, and at most total/(SMALL+1) large segments exist) and
     // reads the true count back every SYNC_EVERY rounds.
-    constexpr int SYNC_EVERY = 4;
+    int SYNC_EVERY = 4;
+    if (const char *e = getenv("SYZCOV_SORT_SYNC")) SYNC_EVERY = std::max(1, atoi(e));  // tuning
     const uint32_t cap_seg = std::min<uint32_t>(w.seg_cap, w.n / (SMALL + 1) + 1);
     uint32_t ncur = h[1], maxlen = h[4];
     for (int round = 0; ncur > 0 && !h[0]; round++) {
