@@ -48,7 +48,7 @@ enum { M_DONE = 0, M_ACTIVE = 2 };
 struct Plan {
     int mode, pivot, rev, pis, eq, cnt, m;
     uint32_t kp;
-    uint32_t done_c, done_s;  // blocks of count_kernel / swap_kernel finished this round
+    uint32_t done_c;  // blocks of count_kernel finished this round
 };
 
 // accessor over the global key/index arrays
@@ -401,9 +401,13 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
     if (l == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
 }
 
-// The m swaps of the partition, then (last block of the segment) the tail of
-// the loop iteration: partitionEqual's `a = mid` continue, or the pivot swap
-// and the two recursions (smaller side first, as Go recurses on it).
+// The m swaps of the partition, then the tail of the loop iteration:
+// partitionEqual's `a = mid` continue, or the pivot swap and the two
+// recursions (smaller side first, as Go recurses on it).  The tail touches
+// only positions a (never swapped: PL, PR lie in (a, b)) and mid = a + cnt,
+// which a swap moves only if it is the last left-misplaced element
+// (PL[m - 1] == mid).  So the block that owns swap m - 1 runs the tail after
+// its own swaps (block 0 if mid does not move): no cross-block hand-off.
 __global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
                                                    const uint32_t *__restrict__ ncur_p,
                                                    Plan *__restrict__ plan, uint32_t *__restrict__ K,
@@ -421,16 +425,16 @@ __global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
     for (int k = blockIdx.x * CH + threadIdx.x; k < min(p.m, (int)(blockIdx.x + 1) * CH);
          k += blockDim.x)
         d.swap(PL[g.a + k], PR[g.a + k]);
-    __threadfence();  // release this thread's swaps at device scope
-    __syncthreads();
+    const int mid = g.a + p.cnt;
+    const bool moved = !p.eq && p.m > 0 && PL[g.a + p.m - 1] == mid;
+    const uint32_t owner = moved ? (uint32_t)((p.m - 1) / CH) : 0u;
+    if (blockIdx.x != owner) return;
+    __syncthreads();  // this block's swaps (incl. the one moving mid) before the tail
     if (threadIdx.x != 0) return;
-    if (atomicAdd(&plan[s].done_s, 1u) != nparts - 1) return;
-    __threadfence();  // acquire the other blocks' swaps
     if (p.eq) {  // partitionEqual returns a + 1 + cnt; the loop continues
         push_seg(c, Seg{g.a + 1 + p.cnt, g.b, g.limit, g.flags});
         return;
     }
-    const int mid = g.a + p.cnt;
     d.swap(mid, g.a);
     const int already = p.m == 0;
     const int n = g.b - g.a, ln = mid - g.a, rn = g.b - mid, thr = n / 8;
