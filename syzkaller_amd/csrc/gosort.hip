@@ -48,7 +48,6 @@ enum { M_DONE = 0, M_ACTIVE = 2 };
 struct Plan {
     int mode, pivot, rev, pis, eq, cnt, m;
     uint32_t kp;
-    uint32_t done_c;  // blocks of count_kernel finished this round
 };
 
 // accessor over the global key/index arrays
@@ -304,7 +303,7 @@ __device__ __forceinline__ bool left_group(uint32_t k, uint32_t kp, int eq) {
 
 __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
                                                     const uint32_t *__restrict__ ncur_p,
-                                                    Plan *__restrict__ plan,
+                                                    const Plan *__restrict__ plan,
                                                     const uint32_t *__restrict__ K,
                                                     uint32_t *__restrict__ cc, uint32_t stride) {
     __shared__ uint32_t tmp[WG / 64 + 1];
@@ -320,39 +319,16 @@ __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
     for (int x = x0 + threadIdx.x; x < x1; x += WG) c += left_group(K[x], p.kp, p.eq);
     uint32_t total;
     block_excl_scan<WG>(c, tmp, &total);
-    // The last block of the segment to finish scans the block counts (the
-    // counts of the other blocks are released by their fences before the
-    // atomic; this block's fence after it acquires them).
-    const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
-    __shared__ uint32_t last;
-    if (threadIdx.x == 0) {
-        cc[(size_t)s * stride + blockIdx.x] = total;
-        __threadfence();
-        last = atomicAdd(&plan[s].done_c, 1u) == nch - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    uint32_t carry = 0;
-    for (uint32_t c0 = 0; c0 < nch; c0 += WG) {
-        const uint32_t c = c0 + threadIdx.x;
-        const uint32_t v = c < nch ? cc[(size_t)s * stride + c] : 0u;
-        uint32_t sum;
-        const uint32_t pre = block_excl_scan<WG>(v, tmp, &sum);
-        if (c < nch) cc[(size_t)s * stride + c] = carry + pre;
-        carry += sum;
-    }
-    if (threadIdx.x == 0) {
-        plan[s].cnt = (int)carry;
-        plan[s].m = 0;
-    }
+    if (threadIdx.x == 0) cc[(size_t)s * stride + blockIdx.x] = total;
 }
 
 // ranks of the misplaced elements: PL[a + k] / PR[a + k] = position of the
 // k-th left-misplaced (from the left) / right-misplaced (from the right).
-// Each wave owns a contiguous quarter of the block's chunk: it counts its
-// left-group elements, one barrier gives the waves' offsets, and it then
-// ranks its rows with ballots (no block scans inside the loop).
+// The block sums the segment's block counts itself (its prefix and the total
+// cnt; block 0 stores cnt for swap_kernel).  Each wave owns a contiguous
+// quarter of the block's chunk: it counts its left-group elements, one
+// barrier gives the waves' offsets, and it then ranks its rows with ballots
+// (no block scans inside the loop).
 __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    const uint32_t *__restrict__ ncur_p,
                                                    Plan *__restrict__ plan,
@@ -361,7 +337,7 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    uint32_t stride, int32_t *__restrict__ PL,
                                                    int32_t *__restrict__ PR) {
     constexpr int NW = WG / 64, WCH = CH / NW;  // elements per wave
-    __shared__ uint32_t wcnt[NW];
+    __shared__ uint32_t wcnt[NW], wpre[NW], wtot[NW];
     const uint32_t s = blockIdx.y;
     if (s >= *ncur_p) return;
     const Plan p = plan[s];
@@ -376,11 +352,28 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
     uint32_t c = 0;
     for (int x = w0 + (int)l; x < w1; x += 64) c += left_group(K[x], p.kp, p.eq);
     c = wave_sum(c);
-    if (l == 0) wcnt[w] = c;
+    const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t q = threadIdx.x; q < nch; q += WG) {
+        const uint32_t v = cc[(size_t)s * stride + q];
+        tot += v;
+        pre += q < blockIdx.x ? v : 0u;
+    }
+    pre = wave_sum(pre);
+    tot = wave_sum(tot);
+    if (l == 0) {
+        wcnt[w] = c;
+        wpre[w] = pre;
+        wtot[w] = tot;
+    }
     __syncthreads();
-    uint32_t base = cc[(size_t)s * stride + blockIdx.x];
-    for (uint32_t v = 0; v < w; v++) base += wcnt[v];
-    const int L = g.a + p.cnt;  // left region [a+1, L]
+    uint32_t base = 0, cnt = 0;
+    for (uint32_t v = 0; v < (uint32_t)NW; v++) {
+        base += wpre[v] + (v < w ? wcnt[v] : 0u);
+        cnt += wtot[v];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) plan[s].cnt = (int)cnt;
+    const int L = g.a + (int)cnt;  // left region [a+1, L]
     uint32_t mloc = 0;
     for (int c0 = w0; c0 < w1; c0 += 64) {
         const int x = c0 + (int)l;
@@ -389,7 +382,7 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
         const uint64_t m = __ballot(f);
         const uint32_t pf = base + (uint32_t)__popcll(m & lt);
         if (in) {
-            if (x > L && f) PR[g.a + (p.cnt - (int)pf - 1)] = x;
+            if (x > L && f) PR[g.a + ((int)cnt - (int)pf - 1)] = x;
             if (x <= L && !f) {
                 PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
                 mloc++;
