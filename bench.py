@@ -2,8 +2,10 @@
 """Benchmarks of the syzkaller coverage hot path on MI355X.
 
 Default (the driver's headline line): input-PCs processed/sec for
-Canonicalize + Minimize + maxCover Union (BASELINE.json metric; config C2 at
-N=1, the same per-GPU shard with RCCL merges at N>1 — weak scaling).
+Canonicalize + Minimize + maxCover Union (BASELINE.json metric).  N=1 runs
+config C2 (1M inputs, one GPU); N>1 runs config C3 (10M global inputs sharded
+by input over the ranks, RCCL merges; total work fixed, so "strong" scaling
+across N >= 2); --global-inputs overrides the corpus size.
 
 One step = one pass of the hot path over one synthetic corpus already
 resident in HBM (raw KCOV lists, CSR):
@@ -35,7 +37,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # this same bench command (tools/profile.sh -> tools/traffic.py), committed per round
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
-SEED = 0x5EED0002
+SEED_C1 = 0x5EED0001  # BASELINE.json configs[0]: the CPU (reference) config
+SEED = 0x5EED0002     # configs[1]: 1M inputs, one GPU
+SEED_C3 = 0x5EED0003  # configs[2]: 10M inputs over the GPUs of one node
+C3_INPUTS = 10_000_000
 SEED_PRIO = 0x5EED0004
 SEED_NEWCOV = 0x5EED0005
 FLAKE_INPUT = 1 << 40  # synthetic input index the C5 flakes set is drawn as
@@ -54,41 +59,81 @@ def parse():
                          "(16x less memory; measured slower: two probed lines per PC)")
     ap.add_argument("--history", type=int, default=32,
                     help="newcov: batches streamed through the check before the bench")
-    ap.add_argument("--inputs", type=int, default=1_000_000, help="inputs (programs) per GPU")
+    ap.add_argument("--inputs", type=int, default=1_000_000,
+                    help="inputs (programs) per GPU at N=1 (config C2)")
+    ap.add_argument("--global-inputs", type=int, default=None,
+                    help="corpus inputs over all ranks, sharded by input (default at N>1: "
+                         "config C3's 10M inputs, seed 0x5EED0003)")
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=None)
     ap.add_argument("--mean", type=int, default=2048)
     ap.add_argument("--sigma", type=int, default=512)
     ap.add_argument("--log2-space", type=int, default=22)
-    ap.add_argument("--cpu-sample", type=int, default=2000,
-                    help="inputs timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=10_000,
+                    help="inputs of config C1 timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
 def cpu_baseline(args):
     """Oracle (literal C restatement of cover.go; Go toolchain absent) on the
-    host: Canonicalize + Minimize + Union fold over a bounded sample."""
+    host, on BASELINE.json configs[0] = C1: the 10k-input synthetic corpus
+    (seed 0x5EED0001), Canonicalize + Minimize + the Union fold, timed
+    separately."""
     from oracle import oracle as orc
     orc.lib()
     n = args.cpu_sample
-    off, pcs = orc.synth_corpus(SEED, n, args.mean, args.sigma, args.log2_space)
+    off, pcs = orc.synth_corpus(SEED_C1, n, args.mean, args.sigma, args.log2_space)
     raw_pcs = int(off[-1])
     t0 = time.perf_counter()
     c_off, c_pcs = orc.canonicalize_csr(off, pcs)
     t1 = time.perf_counter()
-    orc.minimize_csr(c_off, c_pcs)
+    kept = orc.minimize_csr(c_off, c_pcs)
     t2 = time.perf_counter()
-    orc.union_fold_csr(c_off, c_pcs)
+    union = orc.union_fold_csr(c_off, c_pcs)
     t3 = time.perf_counter()
+    canon_pcs = int(c_off[-1])
     return {
         "value": raw_pcs / (t3 - t0), "unit": "input-PCs/s", "cores": 1, "kind": "port",
-        "sample": (f"first {n} inputs of the same synthetic corpus ({raw_pcs} raw PCs): "
-                   f"Canonicalize {t1 - t0:.2f}s + Minimize {t2 - t1:.2f}s + Union fold "
-                   f"{t3 - t2:.2f}s, 1 thread, oracle/ C restatement of cover/cover.go "
-                   f"(Go toolchain absent); the reference's Union fold is O(N*|U|), so the "
-                   f"CPU rate falls further as N grows"),
+        "sample": (f"config C1: {n} inputs of the seed-{SEED_C1:#x} synthetic corpus "
+                   f"({raw_pcs} raw PCs): Canonicalize {t1 - t0:.2f}s + Minimize {t2 - t1:.2f}s "
+                   f"+ Union fold {t3 - t2:.2f}s, 1 thread, oracle/ C restatement of "
+                   f"cover/cover.go (Go toolchain absent)"),
+        "phases_s": {"canonicalize": t1 - t0, "minimize": t2 - t1, "union_fold": t3 - t2},
+        "minimize_canonical_pcs_per_s": canon_pcs / (t2 - t1),
+        "union_fold_canonical_pcs_per_s": canon_pcs / (t3 - t2),
+        "results": {"kept": int(len(kept)), "union": int(union.size)},
         "host": platform.processor() or platform.machine(),
         "nproc": os.cpu_count(),
     }
+
+
+def stream_peak(dev, nbytes: int = 4 << 30, reps: int = 10) -> float:
+    """Measured HBM copy rate (GB/s, read + write bytes) of the 16-B streaming
+    copy kernel, next to the 8 TB/s vendor figure."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def copy():
+        _lib.check(L.syzcov_dev_stream_copy(C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()),
+                                            nbytes, s), "stream_copy")
+    copy()
+    copy()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        copy()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline_prio(nprog: int, C: int):
@@ -160,9 +205,20 @@ def bench_corpus(args):
     import torch
     world, rank, dev = init_dist()
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
-    n = args.inputs
+    # N=1: config C2 (1M inputs); N>1: config C3 (10M global inputs, sharded
+    # by input: rank r holds [r*n, (r+1)*n)), unless --global-inputs says otherwise
+    glob = args.global_inputs
+    if glob is None and world > 1:
+        glob = C3_INPUTS
+    if glob is None:
+        n, seed, cname = args.inputs, SEED, "C2"
+    else:
+        n = -(-glob // world)
+        seed, cname = (SEED_C3, "C3") if glob == C3_INPUTS else (SEED, "custom")
+    if args.seed is not None:
+        seed = args.seed
     lo, span = synth_window(args.log2_space)
-    off, raw, lens, total = synth_corpus(n, SEED, first=rank * n, mean=args.mean,
+    off, raw, lens, total = synth_corpus(n, seed, first=rank * n, mean=args.mean,
                                          sigma=args.sigma, log2_space=args.log2_space, device=dev)
     max_len = int(lens.max().item())
     if world > 1:
@@ -191,11 +247,14 @@ def bench_corpus(args):
         "metric": "input-PCs processed/sec for Canonicalize+Minimize+Union (maxCover merge)",
         "value": value, "unit": "input-PCs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "weak" if glob is None else "strong",
+        "vs_baseline": None,
         "dtype": "u32", "data": "synthetic (counter-based generator, SURVEY §8d)",
-        "config": {"workload": "C2: Canonicalize + Minimize + maxCover union"
-                               + (" (C3 sharding)" if world > 1 else ""),
-                   "inputs_per_gpu": n, "global_inputs": n * world, "raw_pcs_per_gpu": total,
+        "config": {"workload": f"{cname}: Canonicalize + Minimize + maxCover union, "
+                               f"{n * world} inputs" + (f" sharded over {world} GPUs"
+                                                        if world > 1 else ""),
+                   "seed": seed, "inputs_per_gpu": n, "global_inputs": n * world,
+                   "raw_pcs_per_gpu": total,
                    "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
                    "len_mean": args.mean, "len_sigma": args.sigma,
                    "parallelism": f"shard-by-input x{world}"},
@@ -209,9 +268,15 @@ def bench_corpus(args):
         "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph["compact"]
                                                           + ph["union"] + ph["merge"]) * 1e-3),
     }
+    if world == 1:
+        pk = stream_peak(dev)
+        out["roofline"]["peak_measured"] = pk
+        out["roofline"]["frac_of_measured"] = achieved / pk
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(args)
-        out["vs_cpu"] = value / out["cpu_baseline"]["value"]
+        cb = out["cpu_baseline"] = cpu_baseline(args)
+        out["vs_cpu"] = value / cb["value"]
+        out["vs_cpu_minimize_union"] = (out["minimize_union_pcs_per_s"]
+                                        / cb["minimize_canonical_pcs_per_s"])
     return rank, world, out
 
 
@@ -408,7 +473,7 @@ def bench_newcov(args):
                      "traffic": None, "alg_bytes_per_launch": timed_pcs // args.steps * 4},
     }
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, nrec))
+        out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, 2000, nrec))
     st.close()
     return rank, world, out
 

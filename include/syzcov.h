@@ -49,6 +49,10 @@ extern "C" {
 #define SYZCOV_ENOMEM -6      /* device allocation failed */
 #define SYZCOV_ETOOLONG -7    /* program longer than the call table (Go would panic) */
 
+/* bits of a device err_flag word (engine kernels) */
+#define SYZCOV_ERR_WINDOW 1u  /* a PC outside the configured PC window */
+#define SYZCOV_ERR_SEGLEN 2u  /* a segment longer than the declared max_seg_len */
+
 /* Version / build identification: "syzcov <ver> gfx950". */
 const char *syzcov_version(void);
 /* Human-readable text for the last error on this thread. */
@@ -300,7 +304,8 @@ int syzcov_dev_first_dense(const uint64_t *tab, uint64_t pc_span, int32_t *first
  * Canonicalize (cover.go:27-40) with ONE wavefront per segment (LDS radix
  * sort over window offsets, unique, PCs written to out[off[i] ..), in place
  * allowed when max_seg_len <= 16384).  PCs outside [pc_lo, pc_lo + pc_span)
- * set *err_flag.  If split != NULL (nrange = ceil(pc_span / 2^range_shift)
+ * set SYZCOV_ERR_WINDOW in *err_flag, a segment longer than max_seg_len sets
+ * SYZCOV_ERR_SEGLEN (it is not canonicalized).  If split != NULL (nrange = ceil(pc_span / 2^range_shift)
  * <= 256 columns per segment), split[i * nrange + j] = number of canonical
  * PCs of segment i below pc_lo + ((j + 1) << range_shift) and range_tot[j]
  * (u64, pre-zeroed) accumulates the canonical PCs of range j.
@@ -381,6 +386,9 @@ int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t
                          uint32_t log2_space, int uniform, uint32_t *pcs, void *stream);
 /* The synthetic PC universe U[k], k < 2^log2_space (sorted). */
 int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out, void *stream);
+/* dst <- src, 16-byte aligned, nbytes % 16 == 0: the streaming-copy kernel
+ * whose rate the bench reports as the measured HBM peak. */
+int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes, void *stream);
 
 /* Dynamic priority counts as a dense contraction on i8 MFMA with i32
  * accumulation: counts = AᵀA over the matrix AT (rows = syzcov_dev_prio_rows(C)

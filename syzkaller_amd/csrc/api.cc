@@ -513,9 +513,8 @@ static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *of
         CK(hipMemcpyAsync(out, b[i_out], (size_t)k * 4, hipMemcpyDeviceToHost, c->s));
         CK(hipStreamSynchronize(c->s));
     }
-    // the reference ends with cover.Canonicalize (`last := sent`): a lone
-    // 0xFFFFFFFF is dropped
-    if (k == 1 && out[0] == 0xFFFFFFFFu) k = 0;
+    // html.go:236 calls cover.Canonicalize(cov) but returns cov itself: the
+    // sorted slice in full, so a lone 0xFFFFFFFF is kept
     return (int64_t)k;
 }
 

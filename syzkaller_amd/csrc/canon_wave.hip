@@ -37,11 +37,6 @@ int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
                      uint64_t pc_span, uint32_t *err, hipStream_t s);
-int canon_bitonic_launch(int W, const uint64_t *off, const uint32_t *raw, uint32_t *out,
-                         uint32_t *new_len, uint32_t pc_lo, uint64_t pc_span, uint32_t sent_key,
-                         uint32_t *split, uint32_t nrange, uint32_t rshift, uint64_t *range_tot,
-                         uint32_t *err, const uint32_t *list, const uint32_t *cnt, uint64_t nseg,
-                         hipStream_t s);
 
 #ifndef SYZ_CANON_W32
 #define SYZ_CANON_W32 3
@@ -179,7 +174,8 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
                                                   Classes C, uint32_t *__restrict__ counts,
                                                   uint32_t *__restrict__ lists, uint64_t stride,
                                                   uint32_t *__restrict__ big_list,
-                                                  uint32_t *__restrict__ big_cnt) {
+                                                  uint32_t *__restrict__ big_cnt,
+                                                  uint64_t max_len, uint32_t *__restrict__ err) {
     // block-aggregated: LDS counts per class, ONE global atomic per block and class
     __shared__ uint32_t s_cnt[NCLS + 1], s_base[NCLS + 1];
     const uint32_t l = __lane_id();
@@ -192,6 +188,9 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
         int c = -1;
         if (i < nseg) {
             const uint64_t n = off[i + 1] - off[i];
+            // the host launches only the classes the declared bound reaches:
+            // a longer segment would be left uncanonicalized, so it fails loudly
+            if (n > max_len) atomicOr(err, SYZCOV_ERR_SEGLEN);
             c = n > WAVE_MAX ? NCLS : -1;  // NCLS = big list
 #pragma unroll
             for (int k = 0; k < NCLS; k++)
@@ -304,7 +303,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
             }
         }
         if (li + nw < nl) issue(li + nw);
-        if (__ballot(oob) && l == 0) *P.err = 1u;
+        if (__ballot(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
         // ------------------------------------------- pass 0 (unstable)
         hist_zero(s_hist[w], l);
         wave_sync();
@@ -545,11 +544,8 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     P.big_cnt = cnts + 1;
     P.err = err_flag;
     // bin by capacity class (wave-aggregated atomics), one launch per class
-    // algorithm: the LDS radix sort (default; 11.9 ms at C2) or the register
-    // bitonic network (SYZCOV_CANON=bitonic; 20.3 ms at C2: 147 VALU ops per
-    // key at 2 waves/SIMD lose to ~13 LDS ops per 64 keys).  Both are exact.
-    bool bitonic = false;
-    if (const char *e = getenv("SYZCOV_CANON")) bitonic = strcmp(e, "bitonic") == 0;
+    // (a register bitonic network measured 20.3 ms at C2 against the LDS
+    // radix's 7.8: 147 VALU ops per key)
     cw::Classes C;
     // (a 1024-key class for the segments of <= 1021 keys measured slower than
     // sending them to the 2048-key class: 7.85 vs 7.79 ms at C2; its short
@@ -559,23 +555,13 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         C.lo[c] = c ? nk[c - 1] * 64 - 2 : 0;  // CAP - 3 + 1 of the previous class
         C.hi[c] = nk[c] * 64 - 3;
     }
-    if (bitonic) {  // 1, 2, 4 waves of 2048 keys
-        const uint32_t bl[cw::NCLS] = {0, 2046, 4094, 1, 1}, bh[cw::NCLS] = {2045, 4093, 8189, 0, 0};
-        for (int c = 0; c < cw::NCLS; c++) C.lo[c] = bl[c], C.hi[c] = bh[c];
-    }
     uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
     uint32_t *ccnt = cnts + 2;
     SYZ_HIP(hipMemsetAsync(ccnt, 0, cw::NCLS * sizeof(uint32_t), s));
     hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 2048)), dim3(256), 0, s, off,
-                       (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1);
-    for (int c = 0; bitonic && c < 3; c++) {
-        if (max_seg_len < C.lo[c]) break;
-        int rc = canon_bitonic_launch(1 << c, off, raw, out, new_len, pc_lo, pc_span, P.sent_key,
-                                      split, (uint32_t)nrange, range_shift, range_tot, err_flag,
-                                      clists + (size_t)c * nseg, ccnt + c, nseg, s);
-        if (rc) return rc;
-    }
-    for (int c = 0; !bitonic && c < cw::NCLS; c++) {
+                       (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1,
+                       (uint64_t)max_seg_len, err_flag);
+    for (int c = 0; c < cw::NCLS; c++) {
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {

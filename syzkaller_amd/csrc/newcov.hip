@@ -147,8 +147,11 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 const uint64_t q = q0 + u * 64 + l;
                 const uint64_t o = (uint64_t)(uint32_t)(pc[u] - pc_lo);
                 const bool inw = pc[u] >= pc_lo && o < pc_span;
-                ok[u] = q < n && inw;
-                bad |= (uint32_t)(q < n && !inw);
+                // 0xFFFFFFFF is Difference's end sentinel: never part of a
+                // diff (cover.go:43-48,97), so never a candidate, never an error
+                const bool sent = pc[u] == 0xFFFFFFFFu;
+                ok[u] = q < n && inw && !sent;
+                bad |= (uint32_t)(q < n && !inw && !sent);
                 w[u] = 0xFFFFFFFFu;
                 bt[u] = 0;
                 if (ok[u]) w[u] = *probe_word(utab, DM, M, (uint32_t)o, &bt[u]);
@@ -279,6 +282,7 @@ __global__ void bits_set_kernel(const uint32_t *__restrict__ pcs, uint64_t n,
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t pc = pcs[i];
         const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
+        if (pc == 0xFFFFFFFFu) continue;  // Union drops the sentinel (cover.go:97)
         if (pc < pc_lo || o >= pc_span) {
             *err = 1u;
             continue;

@@ -29,6 +29,7 @@ import torch
 from ._lib import check, lib
 
 INT32_MAX = 0x7FFFFFFF
+SYZCOV_ERR_WINDOW, SYZCOV_ERR_SEGLEN = 1, 2  # err_flag bits (include/syzcov.h)
 RANGE_SHIFT = 20  # 2^20 PCs per LDS-resident range (128 KB covered bitmap)
 
 
@@ -64,7 +65,7 @@ class CorpusEngine:
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  device="cuda", n_global: int | None = None, sort_variant: int = 0,
-                 rec_cap: int = 0):
+                 rec_cap: int = 0, canon_in_place: bool = False):
         L = lib()
         dev = torch.device(device)
         self.dev, self.L = dev, L
@@ -78,7 +79,12 @@ class CorpusEngine:
             raise ValueError("PC window too wide for the range engine (> 256 ranges of 2^20)")
         nwords = (pc_span + 31) // 32
         self.nwords = nwords
-        self.canon = _u32(p_max + 1, dev)
+        # canonical covers: their own buffer, or the raw CSR slots themselves
+        # (canon_in_place: halves the corpus footprint; the raw lists are consumed)
+        self.canon_in_place = canon_in_place
+        if canon_in_place and max_seg_len > 16384:
+            raise ValueError("in-place canonicalization needs max_seg_len <= 16384")
+        self.canon = None if canon_in_place else _u32(p_max + 1, dev)
         self.new_len = _u32(n_max + 1, dev)
         # split points (columns per segment) and PCs per range, from canon
         self.split = (torch.empty(n_max * self.nrange, dtype=torch.int32, device=dev)
@@ -121,6 +127,8 @@ class CorpusEngine:
         """Wavefront canonicalize + per-range split points and range totals."""
         self.scal.zero_()
         self.range_tot.zero_()
+        if self.canon_in_place:
+            self.canon = raw
         check(self.L.syzcov_dev_canon_split(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
                                             self.max_seg, self.pc_lo, self.span, self.rshift,
                                             _p(self.split), _p(self.range_tot), _p(self.scal),
@@ -176,6 +184,11 @@ class CorpusEngine:
                                              _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
 
     def merge_max_cover(self):
+        """maxCover |= union.  The union (Union fold) drops 0xFFFFFFFF
+        (cover.go:97): if the window holds it, its covered bit goes first."""
+        so = 0xFFFFFFFF - self.pc_lo
+        if so < self.span:
+            self.covered[so >> 5] &= ~(1 << (so & 31)) if (so & 31) != 31 else 0x7FFFFFFF
         check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered), self.nwords,
                                           _p(self.scal[4:5]), _stream()), "dev_bitmap_op")
 
@@ -208,8 +221,12 @@ class CorpusEngine:
 
     def result(self) -> StepResult:
         sc = self.scal.cpu().tolist()
-        if sc[0] & 0xFFFFFFFF:
+        if sc[0] & SYZCOV_ERR_WINDOW:
             raise RuntimeError("a PC fell outside the engine's PC window")
+        if sc[0] & SYZCOV_ERR_SEGLEN:
+            raise RuntimeError(f"an input is longer than max_seg_len={self.max_seg}")
+        if sc[0] & 0xFFFFFFFF:
+            raise RuntimeError(f"engine error flags {sc[0] & 0xFFFFFFFF:#x}")
         n_ids, n_kept, n_union = (int(x) & 0xFFFFFFFF for x in sc[1:4])
         return StepResult(self.out_idx[:n_kept], n_kept, self.union[:n_union], n_union, n_ids,
                           int(sc[4]))

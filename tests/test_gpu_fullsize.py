@@ -1,0 +1,148 @@
+"""Full-size parity: the engine at BASELINE.json's own sizes against the CPU
+oracle's digests (tests/golden/fullsize_digests.json, written by
+tools/gen_golden_fullsize.py from oracle/fullsize.c).
+
+  C2  1M inputs, one GPU                      kept / union / order / lens digests
+  C3  10M inputs (82 GB raw), one GPU         kept / union / order / lens digests
+  C3  canonical lengths in 1M chunks + the 10M Go sort order on the device
+  C2  world-8 sharded rehearsal on one GPU    kept / union / order digests
+  C4  1M programs: raw co-occurrence counts against the closed form
+      D[i][j] = #{p : len(p) > max(i, j)}, D[i][i] = 0 (prio.go:137-154)
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def golden(name):
+    with open(os.path.join(HERE, "golden", "fullsize_digests.json")) as f:
+        return json.load(f)[name]
+
+
+def sha(t) -> str:
+    return hashlib.sha256(t.cpu().numpy().astype("<i4").tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def _engine_vs_digest(torch, name, inplace):
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    g = golden(name)
+    n = g["n"]
+    off, raw, lens, total = synth_corpus(n, g["seed"], mean=g["mean"], sigma=g["sigma"],
+                                         log2_space=g["log2_space"])
+    assert total == g["raw_pcs"]
+    lo, span = synth_window(g["log2_space"])
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, canon_in_place=inplace)
+    res = eng.step(off, raw, n)
+    assert int(eng.new_len[:n].to(torch.int64).sum().item()) == g["canonical_pcs"]
+    assert sha(eng.new_len[:n]) == g["lens_sha256"]
+    assert sha(eng.order[:n]) == g["order_sha256"]
+    assert res.n_kept == g["n_kept"]
+    assert res.kept_idx[:16].cpu().tolist() == g["kept_head"]
+    assert sha(res.kept_idx) == g["kept_sha256"]
+    assert res.n_union == g["n_union"] and res.max_cover == g["n_union"]
+    assert sha(res.union) == g["union_sha256"]
+    return eng, off, raw
+
+
+def test_c2_fullsize_digest(torch):
+    """Config C2 (1M inputs, 2.05 G raw PCs) on one GPU: bit-exact kept list,
+    union, canonical lengths and Go sort order; a second step (engine state
+    reused, maxCover saturated) gives the same."""
+    eng, off, raw = _engine_vs_digest(torch, "C2", inplace=False)
+    g = golden("C2")
+    res = eng.step(off, raw, g["n"])
+    assert sha(res.kept_idx) == g["kept_sha256"] and sha(res.union) == g["union_sha256"]
+
+
+def test_c3_fullsize_digest(torch):
+    """Config C3 (10M inputs, 20.5 G raw PCs = 82 GB) on ONE 288 GB GPU,
+    canonicalized in place: bit-exact against the oracle's digests."""
+    free, _ = torch.cuda.mem_get_info()
+    if free < 120 << 30:
+        pytest.skip(f"C3 needs ~100 GB of HBM, {free >> 30} GB free")
+    eng, off, raw = _engine_vs_digest(torch, "C3", inplace=True)
+    del eng, off, raw
+    torch.cuda.empty_cache()
+
+
+def test_c3_order_chunked(torch):
+    """C3's 10M canonical lengths, canonicalized 1M inputs at a time, and the
+    device restatement of Go's sort.Sort over all 10M of them."""
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    g = golden("C3")
+    n, chunk = g["n"], 1_000_000
+    lo, span = synth_window(g["log2_space"])
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    eng = None
+    for c0 in range(0, n, chunk):
+        off, raw, l_, total = synth_corpus(chunk, g["seed"], first=c0, mean=g["mean"],
+                                           sigma=g["sigma"], log2_space=g["log2_space"])
+        if eng is None:
+            eng = CorpusEngine(chunk, int(total * 1.01), 65535, lo, span, n_global=n)
+        eng.canonicalize(off, raw, chunk)
+        lens[c0:c0 + chunk].copy_(eng.new_len[:chunk])
+        del off, raw
+    assert sha(lens) == g["lens_sha256"]
+    eng.sort_order(lens, n)
+    assert sha(eng.order[:n]) == g["order_sha256"]
+
+
+def test_world8_rehearsal_c2(torch):
+    """Eight ranks of the sharded engine on one GPU (gloo collectives) over C2,
+    checked against the ORACLE's digests (not against the single-GPU engine)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "8", "C2"],
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and r.stdout.count("OK") == 8, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_c4_closed_form_1m(torch):
+    """C4: 1M programs with lengths ~ N(30, 8) (the bench's own generator):
+    the raw co-occurrence counts of the i8-MFMA AᵀA are exactly
+    D[i][j] = #{p : len(p) > max(i, j)} (i != j), D[i][i] = 0; the normalised
+    priorities equal the oracle's normalizePrio of that matrix."""
+    import ctypes as C
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import PrioEngine, _stream
+    L = _lib.lib()
+    nprog, seed = 1_000_000, 0x5EED0004
+    eng = PrioEngine(nprog)
+    lens = torch.empty(nprog, dtype=torch.int32, device="cuda")
+    _lib.check(L.syzcov_dev_synth_lens(seed, 0, nprog, 30, 8, C.c_void_p(lens.data_ptr()),
+                                       _stream()), "synth_lens")
+    out = eng.step(lens)
+    Cn = eng.C
+    raw = torch.empty(Cn * Cn, dtype=torch.int32, device="cuda")
+    _lib.check(L.syzcov_dev_prio_finish(C.c_void_p(eng.counts.data_ptr()), Cn, None,
+                                        C.c_void_p(eng.out.data_ptr()), C.c_void_p(raw.data_ptr()),
+                                        _stream()), "prio_finish")
+    hl = lens.cpu().numpy()
+    assert np.array_equal(hl[:2000], orc.synth_lens(seed, 2000, 30, 8).astype(np.int32))
+    gt = np.zeros(Cn + 1, np.int64)  # gt[m] = #{p : len(p) > m}
+    h = np.bincount(hl, minlength=Cn + 1)
+    gt[:Cn + 1] = nprog - np.cumsum(h)[:Cn + 1]
+    idx = np.arange(Cn)
+    D = gt[np.maximum(idx[:, None], idx[None, :])]
+    np.fill_diagonal(D, 0)
+    got = raw.cpu().numpy().astype(np.int64).reshape(Cn, Cn)
+    assert np.array_equal(got, D)
+    # normalised (no static factor) == normalizePrio of the exact float32 counts
+    exp = orc.normalize_prio(D.astype(np.float32))
+    assert np.array_equal(eng.out.cpu().numpy().reshape(Cn, Cn), exp)
+    assert out is eng.out

@@ -142,6 +142,35 @@ def test_newcov_device_api_vs_oracle():
     st.close()
 
 
+def test_newcov_sentinel_full_window():
+    """Full 2^32 window (the CoverState default): a record whose only new PC
+    is 0xFFFFFFFF is NOT new (Difference drops the sentinel, cover.go:43-48,
+    97), and the sentinel never enters maxCover / corpusCover (Union drops it)."""
+    from syzkaller_amd.fuzzer import CoverState
+    from syzkaller_amd.manager import CorpusCover
+    S = 0xFFFFFFFF
+    ncalls = 3
+    st = CoverState(ncalls)
+    mc = [[] for _ in range(ncalls)]
+    st.add(1, np.array([5, S], np.uint32))
+    mc[1] = orc.union([], [5, S])
+    cids = [0, 0, 1, 1, 2, 2]
+    recs = [np.array(r, np.uint32) for r in
+            ([S], [7, S], [5, S], [5, 6, S], [0, S], [0])]
+    exp, mc = orc.newcov_batch(mc, [], cids, recs)
+    assert exp.tolist() == [0, 1, 0, 1, 1, 0]
+    assert np.array_equal(st.new_coverage(cids, recs), exp)
+    for c in range(ncalls):
+        assert np.array_equal(st.max_cover(c), mc[c]) and S not in st.max_cover(c).tolist()
+    st.close()
+    cc = CorpusCover(ncalls, 0, 1 << 32)
+    ref = {}
+    assert cc.new_inputs(cids, recs).tolist() == orc.new_inputs(ref, cids, recs)
+    for c in range(ncalls):
+        assert np.array_equal(cc.get(c), ref.get(c, np.zeros(0, np.uint32)))
+    cc.close()
+
+
 @pytest.mark.parametrize("frac", [1.0, 0.7])
 def test_newcov_universe_mode(frac):
     """Dense-id maxCover (state_set_universe) gives the reference's results,
@@ -192,7 +221,9 @@ def test_unique_cover_vs_reference(cover, per_call):
         exp = pyref.unique_cover(calls.tolist(), covs, per_call)
         got = cover.UniqueCover(covs, calls if per_call else None)
         assert got.tolist() == exp, (trial, per_call)
-    assert cover.UniqueCover([[0xFFFFFFFF]]).tolist() == []
+    # html.go:236 ignores Canonicalize's return value: a lone sentinel survives
+    assert cover.UniqueCover([[0xFFFFFFFF]]).tolist() == [0xFFFFFFFF]
+    assert cover.UniqueCover([[7, 0xFFFFFFFF], [7]]).tolist() == [0xFFFFFFFF]
 
 
 def test_unique_cover_synthetic(cover):

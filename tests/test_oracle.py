@@ -208,8 +208,9 @@ def test_unique_cover_restatement():
     assert pyref.unique_cover(calls, covs, False) == [1, 2, 6]
     # per call: a = {1,2,3,4}, b = {4,5,6}: 4 is in both
     assert pyref.unique_cover(calls, covs, True) == [1, 2, 3, 5, 6]
-    # the final Canonicalize drops a lone 0xFFFFFFFF
-    assert pyref.unique_cover(["a"], [[0xFFFFFFFF]], False) == []
+    # html.go:236 ignores Canonicalize's return value: a lone 0xFFFFFFFF stays
+    assert pyref.unique_cover(["a"], [[0xFFFFFFFF]], False) == [0xFFFFFFFF]
+    assert pyref.unique_cover(["a", "b"], [[7, 0xFFFFFFFF], [7]], False) == [0xFFFFFFFF]
 
 
 

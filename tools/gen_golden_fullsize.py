@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/fullsize_digests.json: the CPU oracle's results on the
+full-size synthetic corpora of BASELINE.json's configs, as
+digests the GPU tests compare the engine against.
+
+  C1  10k inputs   seed 0x5EED0001   (CPU-only config)
+  C2  1M inputs    seed 0x5EED0002   (one MI355X; also the world-8 rehearsal)
+  C3  10M inputs   seed 0x5EED0003   (the 8-GPU config; 82 GB of raw PCs)
+
+Each run is oracle/build/fullsize (oracle/fullsize.c): the reference's
+Canonicalize + sort.Sort + Minimize loop + Union fold, restated so the corpus
+is regenerated instead of held in memory.  TEST INFRASTRUCTURE: run once in
+the build container (C3 takes ~15 min on 8 threads); the digests are data.
+
+usage: python tools/gen_golden_fullsize.py [C1 C2 C3 ...]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "tests", "golden", "fullsize_digests.json")
+CONFIGS = {
+    "C1": dict(seed=0x5EED0001, n=10_000),
+    "C2": dict(seed=0x5EED0002, n=1_000_000),
+    "C3": dict(seed=0x5EED0003, n=10_000_000),
+}
+MEAN, SIGMA, LOG2 = 2048, 512, 22
+
+
+def sha(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def run(name: str, threads: int) -> dict:
+    cfg = CONFIGS[name]
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    exe = os.path.join(ROOT, "oracle", "build", "fullsize")
+    with tempfile.TemporaryDirectory() as d:
+        t0 = time.time()
+        r = subprocess.run([exe, hex(cfg["seed"]), str(cfg["n"]), str(MEAN), str(SIGMA), str(LOG2),
+                            str(threads), d], check=True, capture_output=True, text=True)
+        summary = json.loads(r.stdout)
+        kept = np.fromfile(os.path.join(d, "kept.i32"), dtype=np.int32)
+        union = np.fromfile(os.path.join(d, "union.u32"), dtype=np.uint32)
+        out = dict(seed=cfg["seed"], n=cfg["n"], mean=MEAN, sigma=SIGMA, log2_space=LOG2,
+                   raw_pcs=summary["raw_pcs"], canonical_pcs=summary["canonical_pcs"],
+                   n_kept=summary["n_kept"], kept_sha256=sha(os.path.join(d, "kept.i32")),
+                   kept_head=kept[:16].tolist(), kept_tail=kept[-16:].tolist(),
+                   n_union=summary["n_union"], union_sha256=sha(os.path.join(d, "union.u32")),
+                   union_head=union[:4].tolist(), union_tail=union[-4:].tolist(),
+                   order_sha256=sha(os.path.join(d, "order.i32")),
+                   lens_sha256=sha(os.path.join(d, "lens.u32")),
+                   sort="pdqsort (Go >= 1.19)", oracle_seconds=round(time.time() - t0, 1),
+                   oracle_threads=threads)
+    return out
+
+
+def main():
+    names = sys.argv[1:] or list(CONFIGS)
+    data = {}
+    if os.path.exists(OUT):
+        with open(OUT) as f:
+            data = json.load(f)
+    data["_about"] = ("CPU oracle digests (oracle/fullsize.c via tools/gen_golden_fullsize.py) of "
+                      "Canonicalize + Minimize + Union over the synthetic corpora of SURVEY §8d: "
+                      "kept = original indices in processing order (int32 LE), union = sorted "
+                      "PCs (uint32 LE), order = Go sort.Sort processing order over the canonical "
+                      "lengths, lens = canonical lengths (uint32 LE)")
+    for name in names:
+        print(f"{name} ...", flush=True)
+        data[name] = run(name, os.cpu_count() or 8)
+        print(json.dumps(data[name]), flush=True)
+        with open(OUT, "w") as f:
+            json.dump(data, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
