@@ -57,6 +57,13 @@ extern "C" {
 const char *syzcov_version(void);
 /* Human-readable text for the last error on this thread. */
 const char *syzcov_last_error(void);
+/* Device contexts (stream + arenas) the pool has created on `device`: calls
+ * lease one for their duration, so this is the peak number of concurrent
+ * callers, independent of how many OS threads ever called in. */
+int64_t syzcov_pool_contexts(int device);
+/* Free the arenas of every idle pooled context (a call keeps up to 3 x 32 MB
+ * of arena per context between calls; larger ones are freed as it returns). */
+int syzcov_pool_trim(void);
 
 /* ======================= 1. drop-in host API ========================= */
 
@@ -86,8 +93,9 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
  * processing order — order[r] = index of the r-th input after Go's
  * sort.Sort(minInputArray) (cover.go:113).  The Go shim passes the order its
  * own sort.Sort produced (exact by construction); NULL makes the engine
- * compute it with its restatement of Go >= 1.19 pdqsort (sort_variant 0) or
- * the Go 1.8-1.18 quickSort (sort_variant 1).  Writes the kept input indices
+ * compute it on the GPU with its restatement of Go >= 1.19 pdqsort
+ * (sort_variant must be 0; for Go 1.8-1.18's quickSort order the caller passes
+ * `order`: the library has no host sort).  Writes the kept input indices
  * in processing order to out_idx (capacity n) and returns their count. */
 int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
                         const int32_t *order, int sort_variant, int32_t *out_idx);
@@ -95,8 +103,8 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
 /* Manager.minimizeCorpus (syz-manager/manager.go:504-524): the corpus is
  * grouped by call (call[i] = any int32 key of RpcInput.Call; corpus order is
  * kept inside a group, :511-516) and cover.Minimize runs on every group
- * (:519-523), each with its own Go sort.Sort order (Go >= 1.19 pdqsort,
- * sort_variant 0, or Go 1.8-1.18 quickSort, 1).  out_idx (capacity n)
+ * (:519-523), each with its own Go sort.Sort order (Go >= 1.19 pdqsort;
+ * sort_variant must be 0).  out_idx (capacity n)
  * receives the kept CORPUS indices, groups in ascending call value, each
  * group in its Minimize output order; returns their count.  The reference
  * concatenates groups in Go map order (random), so the shim may reorder

@@ -274,7 +274,9 @@ def unique_cover(calls, covers, per_call):  # syz-manager/html.go:213-238
                     continue
                 call_cover[c].add(pc)
             total[pc] = total.get(pc, 0) + 1
-    return canonicalize([pc for pc, n in total.items() if n == 1])
+    cov = sorted(pc for pc, n in total.items() if n == 1)
+    canonicalize(list(cov))  # :236 `cover.Canonicalize(cov)`, return value ignored:
+    return cov               # the full sorted slice (a lone 0xFFFFFFFF survives)
 
 
 def summary_stats(calls, covers):  # syz-manager/html.go:67-99, literally

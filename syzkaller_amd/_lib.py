@@ -39,6 +39,8 @@ u32, u64, i32, i64 = C.c_uint32, C.c_uint64, C.c_int32, C.c_int64
 _SIGS = {
     "syzcov_version": (C.c_char_p, []),
     "syzcov_last_error": (C.c_char_p, []),
+    "syzcov_pool_contexts": (i64, [C.c_int]),
+    "syzcov_pool_trim": (C.c_int, []),
     "syzcov_restore_pc": (u64, [u32, u32]),
     "syzcov_canonicalize": (i64, [p_, sz]),
     "syzcov_difference": (i64, [p_, sz, p_, sz, p_]),

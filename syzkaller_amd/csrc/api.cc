@@ -9,6 +9,9 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <memory>
+#include <mutex>
+#include <new>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -33,44 +36,95 @@ int dev_setop(int op, const uint32_t *a, size_t na, const uint32_t *b, size_t nb
 
 static inline size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
+// A grow-only device arena.  Growth frees the old block after the stream has
+// drained; a block larger than kKeepBytes is released at the end of the call
+// that needed it (corpus-level calls), so an idle thread pins at most that.
+struct Arena {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+constexpr size_t kKeepBytes = 32ull << 20;
+
+// A device context: a stream and three arenas (staged corpus, its
+// dictionary, the call's work buffers).  Contexts live in a process-wide pool
+// per device: a call leases one for its duration and returns it, so the
+// number of contexts is the peak number of CONCURRENT callers (the fuzzer's
+// <= 32 goroutines), not the number of OS threads that ever called in (cgo
+// moves goroutines across many threads, and thread-exit destructors cannot be
+// relied on to run before the HIP runtime is torn down).
 struct Ctx {
     int dev = -1;
     hipStream_t s = nullptr;
-    void *arena = nullptr;
-    size_t cap = 0;
-    ~Ctx() {
-        if (arena) hipFree(arena);
-        if (s) hipStreamDestroy(s);
-    }
+    Arena a[3];
 };
+enum { A_STAGE = 0, A_DICT = 1, A_WORK = 2 };
 
-static thread_local Ctx *g_ctx[16];
-
-// Current device's per-thread context; nullptr + error if no device.
-static Ctx *ctx() {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-        set_error("no HIP device (libsyzcov has no CPU path)");
-        return nullptr;
-    }
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (dev < 0 || dev >= 16) return nullptr;
-    Ctx *c = g_ctx[dev];
-    if (!c) {
-        c = new Ctx();
-        c->dev = dev;
-        if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
-            set_error("hipStreamCreate failed");
-            delete c;
-            return nullptr;
-        }
-        g_ctx[dev] = c;
-    }
-    return c;
+static int device_count() {
+    static std::once_flag once;
+    static int n = 0;
+    std::call_once(once, [] {
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    });
+    return n;
 }
 
-// Bump allocator over the arena: plan sizes first, then reserve once.
+struct CtxPool {
+    std::mutex mu;
+    std::vector<Ctx *> idle[16];
+    size_t created[16] = {};
+};
+static CtxPool &pool() {
+    static CtxPool *p = new CtxPool();  // never destroyed: outlives every caller
+    return *p;
+}
+
+// RAII lease of the current device's context; get() == nullptr + error if none.
+class CtxLease {
+  public:
+    CtxLease() {
+        if (device_count() == 0) {
+            set_error("no HIP device (libsyzcov has no CPU path)");
+            return;
+        }
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return;
+        CtxPool &P = pool();
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            if (!P.idle[dev].empty()) {
+                c_ = P.idle[dev].back();
+                P.idle[dev].pop_back();
+                return;
+            }
+        }
+        Ctx *n = new (std::nothrow) Ctx();
+        if (!n) return;
+        n->dev = dev;
+        if (hipStreamCreateWithFlags(&n->s, hipStreamNonBlocking) != hipSuccess) {
+            set_error("hipStreamCreate failed");
+            delete n;
+            return;
+        }
+        std::lock_guard<std::mutex> g(P.mu);
+        P.created[dev]++;
+        c_ = n;
+    }
+    ~CtxLease() {
+        if (!c_) return;
+        hipStreamSynchronize(c_->s);
+        CtxPool &P = pool();
+        std::lock_guard<std::mutex> g(P.mu);
+        P.idle[c_->dev].push_back(c_);
+    }
+    Ctx *get() const { return c_; }
+    CtxLease(const CtxLease &) = delete;
+    CtxLease &operator=(const CtxLease &) = delete;
+
+  private:
+    Ctx *c_ = nullptr;
+};
+
+// Bump allocator over an arena: plan sizes first, then reserve once.
 struct Plan {
     std::vector<size_t> sizes;
     size_t add(size_t bytes) {
@@ -84,29 +138,44 @@ struct Plan {
     }
 };
 
-static int reserve(Ctx *c, const Plan &p, std::vector<uint8_t *> &ptrs) {
+static int reserve(Ctx *c, int which, const Plan &p, std::vector<uint8_t *> &ptrs) {
+    Arena &A = c->a[which];
     const size_t need = p.total();
-    if (need > c->cap) {
-        if (c->arena) {
+    if (need > A.cap) {
+        if (A.p) {
             hipStreamSynchronize(c->s);
-            hipFree(c->arena);
+            hipFree(A.p);
         }
-        c->arena = nullptr;
-        c->cap = 0;
+        A.p = nullptr;
+        A.cap = 0;
         size_t cap = need + need / 4;
-        if (hipMalloc(&c->arena, cap) != hipSuccess) {
+        if (hipMalloc(&A.p, cap) != hipSuccess) {
             set_error("hipMalloc(%zu) failed", cap);
             return SYZCOV_ENOMEM;
         }
-        c->cap = cap;
+        A.cap = cap;
     }
     ptrs.clear();
-    uint8_t *b = (uint8_t *)c->arena;
+    uint8_t *b = (uint8_t *)A.p;
     for (size_t s : p.sizes) {
         ptrs.push_back(b);
         b += s;
     }
     return 0;
+}
+static int reserve(Ctx *c, const Plan &p, std::vector<uint8_t *> &ptrs) {
+    return reserve(c, A_WORK, p, ptrs);
+}
+
+// End of a corpus-level call: drain, and give back arenas above kKeepBytes.
+static void release_large(Ctx *c) {
+    hipStreamSynchronize(c->s);
+    for (Arena &x : c->a)
+        if (x.cap > kKeepBytes) {
+            hipFree(x.p);
+            x.p = nullptr;
+            x.cap = 0;
+        }
 }
 
 #define CK(expr)                                                                         \
@@ -129,7 +198,34 @@ using namespace syz;
 
 extern "C" {
 
-const char *syzcov_version(void) { return "syzcov 0.1 gfx950"; }
+const char *syzcov_version(void) { return "syzcov 0.2 gfx950"; }
+
+int syzcov_pool_trim(void) {
+    CtxPool &P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (int d = 0; d < 16; d++)
+        for (Ctx *c : P.idle[d]) {
+            hipSetDevice(d);
+            hipStreamSynchronize(c->s);
+            for (Arena &x : c->a)
+                if (x.p) {
+                    hipFree(x.p);
+                    x.p = nullptr;
+                    x.cap = 0;
+                }
+        }
+    hipSetDevice(cur);
+    return 0;
+}
+
+int64_t syzcov_pool_contexts(int device) {
+    if (device < 0 || device >= 16) return SYZCOV_EINVAL;
+    CtxPool &P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    return (int64_t)P.created[device];
+}
 const char *syzcov_last_error(void) { return g_err; }
 
 uint64_t syzcov_restore_pc(uint32_t pc, uint32_t base) {
@@ -139,7 +235,8 @@ uint64_t syzcov_restore_pc(uint32_t pc, uint32_t base) {
 int64_t syzcov_canonicalize(uint32_t *cov, size_t n) {
     if (n == 0) return 0;
     if (!cov) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_off = p.add(2 * 8), i_pcs = p.add(n * 4), i_len = p.add(4),
@@ -166,7 +263,8 @@ static int64_t setop(int op, const uint32_t *a, size_t na, const uint32_t *b_, s
                      uint32_t *out) {
     if ((na && !a) || (nb && !b_) || !out) return SYZCOV_EINVAL;
     if (na + nb == 0) return 0;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_a = p.add(na * 4), i_b = p.add(nb * 4), i_o = p.add((na + nb) * 4), i_n = p.add(8),
@@ -243,47 +341,42 @@ struct CorpusDev {
 };
 
 static int stage_corpus(Ctx *c, const uint64_t *offsets, const uint32_t *pcs, size_t n,
-                        CorpusDev &cd, std::vector<void *> &owned) {
+                        CorpusDev &cd) {
     const uint64_t base = offsets[0];
     const uint64_t P = offsets[n] - base;
     std::vector<uint64_t> hoff(n + 1);
     for (size_t i = 0; i <= n; i++) hoff[i] = offsets[i] - base;
-    void *d_off = nullptr, *d_pcs = nullptr;
-    if (hipMalloc(&d_off, (n + 1) * 8) != hipSuccess || hipMalloc(&d_pcs, P * 4 + 4) != hipSuccess)
-        return SYZCOV_ENOMEM;
-    owned.push_back(d_off);
-    owned.push_back(d_pcs);
-    CK(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->s));
-    if (P) CK(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, c->s));
-    cd.off = (uint64_t *)d_off;
-    cd.pcs = (uint32_t *)d_pcs;
+    Plan p0;
+    const size_t i_off = p0.add((n + 1) * 8), i_pcs = p0.add(P * 4 + 4), i_mm = p0.add(256);
+    std::vector<uint8_t *> b0;
+    RC(reserve(c, A_STAGE, p0, b0));
+    CK(hipMemcpyAsync(b0[i_off], hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->s));
+    if (P) CK(hipMemcpyAsync(b0[i_pcs], pcs + base, P * 4, hipMemcpyHostToDevice, c->s));
+    cd.off = (uint64_t *)b0[i_off];
+    cd.pcs = (uint32_t *)b0[i_pcs];
     // PC window from a device min/max reduction
-    void *d_mm = nullptr;
-    if (hipMalloc(&d_mm, 256) != hipSuccess) return SYZCOV_ENOMEM;
-    owned.push_back(d_mm);
+    uint32_t *d_mm = (uint32_t *)b0[i_mm];
     uint32_t mm[2] = {0, 0};
     if (P) {
-        RC(minmax_pcs(cd.pcs, P, (uint32_t *)d_mm, c->s));
+        RC(minmax_pcs(cd.pcs, P, d_mm, c->s));
         CK(hipMemcpyAsync(mm, d_mm, 8, hipMemcpyDeviceToHost, c->s));
         CK(hipStreamSynchronize(c->s));
     }
     cd.pc_lo = mm[0];
     cd.span = (uint64_t)mm[1] - mm[0] + 1;
-    void *d_pres = nullptr, *d_tab = nullptr, *d_ws = nullptr;
     const uint64_t nwords = (cd.span + 31) / 32;
-    if (hipMalloc(&d_pres, al(cd.span)) != hipSuccess || hipMalloc(&d_tab, nwords * 8) != hipSuccess ||
-        hipMalloc(&d_ws, syzcov_dev_dict_ws_size(cd.span) + 256) != hipSuccess)
-        return SYZCOV_ENOMEM;
-    owned.push_back(d_pres);
-    owned.push_back(d_tab);
-    owned.push_back(d_ws);
-    cd.pres = (uint8_t *)d_pres;
-    cd.tab = (uint64_t *)d_tab;
-    uint32_t *d_err = (uint32_t *)d_mm + 4, *d_nids = (uint32_t *)d_mm + 8;
-    CK(hipMemsetAsync(d_pres, 0, al(cd.span), c->s));
+    Plan p1;
+    const size_t i_pres = p1.add(al(cd.span)), i_tab = p1.add(nwords * 8),
+                 i_ws = p1.add(syzcov_dev_dict_ws_size(cd.span) + 256);
+    std::vector<uint8_t *> b1;
+    RC(reserve(c, A_DICT, p1, b1));
+    cd.pres = b1[i_pres];
+    cd.tab = (uint64_t *)b1[i_tab];
+    uint32_t *d_err = d_mm + 4, *d_nids = d_mm + 8;
+    CK(hipMemsetAsync(cd.pres, 0, al(cd.span), c->s));
     CK(hipMemsetAsync(d_err, 0, 4, c->s));
     RC(syzcov_dev_mark(cd.off, nullptr, cd.pcs, n, cd.pres, cd.pc_lo, cd.span, d_err, c->s));
-    RC(syzcov_dev_dict_build(cd.pres, cd.span, cd.tab, d_nids, d_ws, c->s));
+    RC(syzcov_dev_dict_build(cd.pres, cd.span, cd.tab, d_nids, b1[i_ws], c->s));
     uint32_t h[2];
     CK(hipMemcpyAsync(h, d_err, 4, hipMemcpyDeviceToHost, c->s));
     CK(hipMemcpyAsync(h + 1, d_nids, 4, hipMemcpyDeviceToHost, c->s));
@@ -295,11 +388,6 @@ static int stage_corpus(Ctx *c, const uint64_t *offsets, const uint32_t *pcs, si
     cd.n_ids = h[1];
     return 0;
 }
-
-static void free_all(std::vector<void *> &v) {
-    for (void *p : v) hipFree(p);
-    v.clear();
-}
 }  // namespace syz
 
 extern "C" {
@@ -307,7 +395,8 @@ extern "C" {
 int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order) {
     if (n == 0) return 0;
     if (!lens || !order) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_l = p.add(n * 8), i_o = p.add(n * 4), i_ws = p.add(syzcov_dev_sort_ws_size(n));
@@ -326,13 +415,13 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
     if (n == 0) return 0;
     if (!offsets || !out_idx || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
-    std::vector<void *> owned;
     CorpusDev cd;
-    int rc = stage_corpus(c, offsets, pcs, n, cd, owned);
+    int rc = stage_corpus(c, offsets, pcs, n, cd);
     if (rc) {
-        free_all(owned);
+        release_large(c);
         return rc;
     }
     Plan p;
@@ -342,7 +431,7 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
     std::vector<uint8_t *> b;
     rc = reserve(c, p, b);
     if (rc) {
-        free_all(owned);
+        release_large(c);
         return rc;
     }
     int32_t *d_ord = (int32_t *)b[i_ord];
@@ -396,7 +485,7 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
         rc = (int)k;
     } while (0);
     hipStreamSynchronize(c->s);
-    free_all(owned);
+    release_large(c);
     return rc;
 }
 
@@ -407,7 +496,7 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
 // every group order is one the reference can produce.
 static int64_t minimize_corpus_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
                                     const uint32_t *pcs, size_t n, int sort_variant,
-                                    int32_t *out_idx, std::vector<void *> &owned) {
+                                    int32_t *out_idx) {
     // host grouping: stable by call value (the reference's append order)
     std::vector<int32_t> perm(n);
     for (size_t i = 0; i < n; i++) perm[i] = (int32_t)i;
@@ -423,7 +512,7 @@ static int64_t minimize_corpus_impl(Ctx *c, const int32_t *call, const uint64_t 
     goff.push_back(n);
     const size_t G = goff.size() - 1;
     CorpusDev cd;
-    RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    RC(stage_corpus(c, offsets, pcs, n, cd));
     const uint32_t nids = std::max<uint32_t>(cd.n_ids, 1);
     // first-cover slabs for as many groups as fit 1 GiB (at least one)
     const size_t per = (size_t)nids * 4;
@@ -468,29 +557,28 @@ static int64_t minimize_corpus_impl(Ctx *c, const int32_t *call, const uint64_t 
 int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
                                size_t n, int sort_variant, int32_t *out_idx) {
     if (n == 0) return 0;
-    if (!call || !offsets || !out_idx || n > 0x7FFFFFFF || (sort_variant != 0 && sort_variant != 1))
+    if (!call || !offsets || !out_idx || n > 0x7FFFFFFF || sort_variant != 0)
         return SYZCOV_EINVAL;
     if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
-    std::vector<void *> owned;
-    const int64_t rc = minimize_corpus_impl(c, call, offsets, pcs, n, sort_variant, out_idx, owned);
+    const int64_t rc = minimize_corpus_impl(c, call, offsets, pcs, n, sort_variant, out_idx);
     hipStreamSynchronize(c->s);
-    free_all(owned);
+    release_large(c);
     return rc;
 }
 
 // Manager.uniqueCover (syz-manager/html.go:213-238).
 static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
-                                 const uint32_t *pcs, size_t n, uint32_t *out,
-                                 std::vector<void *> &owned) {
+                                 const uint32_t *pcs, size_t n, uint32_t *out) {
     for (size_t i = 0; call && i < n; i++)
         if (call[i] == INT32_MIN) {
             set_error("call key INT32_MIN is reserved");
             return SYZCOV_EINVAL;
         }
     CorpusDev cd;
-    RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    RC(stage_corpus(c, offsets, pcs, n, cd));
     const uint32_t nids = cd.n_ids;
     if (nids == 0) return 0;
     Plan p;
@@ -521,8 +609,7 @@ static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *of
 // Manager UI statistics (html.go:67-99 httpSummary, :157-175 httpCorpus).
 static int64_t ui_stats_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,
                              const uint32_t *pcs, size_t n, uint32_t ncalls, uint32_t *inputs,
-                             uint32_t *cover, uint32_t *ucov, uint32_t *in_unique,
-                             std::vector<void *> &owned) {
+                             uint32_t *cover, uint32_t *ucov, uint32_t *in_unique) {
     for (size_t i = 0; i < n; i++) {
         if (offsets[i + 1] < offsets[i]) return SYZCOV_EINVAL;
         if (call && (call[i] < 0 || (uint32_t)call[i] >= ncalls)) {
@@ -541,7 +628,7 @@ static int64_t ui_stats_impl(Ctx *c, const int32_t *call, const uint64_t *offset
     }
     const bool empty = offsets[n] == offsets[0];
     CorpusDev cd{};
-    if (!empty) RC(stage_corpus(c, offsets, pcs, n, cd, owned));
+    if (!empty) RC(stage_corpus(c, offsets, pcs, n, cd));
     const uint32_t nids = empty ? 0 : cd.n_ids;
     if (nids == 0) {
         if (cover) std::fill(cover, cover + ncalls, 0u);
@@ -587,13 +674,13 @@ int64_t syzcov_ui_stats(const int32_t *call, const uint64_t *offsets, const uint
         if (unique_cover) std::fill(unique_cover, unique_cover + ncalls, 0u);
         return 0;
     }
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
-    std::vector<void *> owned;
     const int64_t rc = ui_stats_impl(c, call, offsets, pcs, n, ncalls, inputs, cover, unique_cover,
-                                     input_unique, owned);
+                                     input_unique);
     hipStreamSynchronize(c->s);
-    free_all(owned);
+    release_large(c);
     return rc;
 }
 
@@ -603,12 +690,12 @@ int64_t syzcov_unique_cover(const int32_t *call, const uint64_t *offsets, const 
     if (!offsets || !out || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (offsets[n] == offsets[0]) return 0;
     if (!pcs) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
-    std::vector<void *> owned;
-    const int64_t rc = unique_cover_impl(c, call, offsets, pcs, n, out, owned);
+    const int64_t rc = unique_cover_impl(c, call, offsets, pcs, n, out);
     hipStreamSynchronize(c->s);
-    free_all(owned);
+    release_large(c);
     return rc;
 }
 
@@ -617,21 +704,19 @@ int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n,
     if (!offsets || !out) return SYZCOV_EINVAL;
     if (offsets[n] == offsets[0]) return 0;
     if (!pcs) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
-    std::vector<void *> owned;
     CorpusDev cd;
-    int64_t rc = stage_corpus(c, offsets, pcs, n, cd, owned);
+    int64_t rc = stage_corpus(c, offsets, pcs, n, cd);
     if (!rc) {
-        void *d_out = nullptr, *d_n = nullptr;
-        if (hipMalloc(&d_out, (size_t)cd.n_ids * 4 + 4) != hipSuccess ||
-            hipMalloc(&d_n, 256) != hipSuccess) {
-            rc = SYZCOV_ENOMEM;
-        } else {
-            owned.push_back(d_out);
-            owned.push_back(d_n);
-            rc = syzcov_dev_dict_to_list(cd.tab, cd.span, cd.pc_lo, (uint32_t *)d_out,
-                                         (uint32_t *)d_n, c->s);
+        Plan p;
+        const size_t i_out = p.add((size_t)cd.n_ids * 4 + 4), i_n = p.add(256);
+        std::vector<uint8_t *> b;
+        rc = reserve(c, p, b);
+        if (!rc) {
+            uint32_t *d_out = (uint32_t *)b[i_out], *d_n = (uint32_t *)b[i_n];
+            rc = syzcov_dev_dict_to_list(cd.tab, cd.span, cd.pc_lo, d_out, d_n, c->s);
             uint32_t k = 0;
             if (!rc && (hipMemcpyAsync(&k, d_n, 4, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
                         hipStreamSynchronize(c->s) != hipSuccess))
@@ -645,7 +730,7 @@ int64_t syzcov_union_all(const uint64_t *offsets, const uint32_t *pcs, size_t n,
         }
     }
     hipStreamSynchronize(c->s);
-    free_all(owned);
+    release_large(c);
     return rc;
 }
 
@@ -671,7 +756,8 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
         lens[p] = (int32_t)l;
     }
     for (size_t p = 0; p <= nprog; p++) hoff[p] = nprog ? prog_off[p] - base : 0;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     const size_t rows = syzcov_dev_prio_rows(C), ldp = syzcov_dev_prio_ldp(nprog ? nprog : 1);
     Plan p;
@@ -716,7 +802,8 @@ int syzcov_static_priorities(const uint32_t *id_off, const uint16_t *id_calls, c
     if (C <= 0 || !id_off || !call_off || !out) return SYZCOV_EINVAL;
     const size_t nm = id_off[nids], nc = call_off[C];
     if ((nm && (!id_calls || !id_w)) || (nc && (!call_ids || !call_w))) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_io = p.add((nids + 1) * 4), i_ic = p.add(nm * 2), i_iw = p.add(nm * 4),
@@ -740,7 +827,8 @@ int syzcov_static_priorities(const uint32_t *id_off, const uint16_t *id_calls, c
 
 int syzcov_normalize_prio(float *prios, int C) {
     if (C <= 0 || !prios) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_p = p.add((size_t)C * C * 4);
@@ -755,7 +843,8 @@ int syzcov_normalize_prio(float *prios, int C) {
 
 int syzcov_build_choice_table(const float *prios, const uint8_t *enabled, int C, int64_t *run) {
     if (C <= 0 || !prios || !run) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_p = p.add((size_t)C * C * 4), i_e = p.add(C), i_r = p.add((size_t)C * C * 8);
@@ -776,7 +865,8 @@ int syzcov_choose_batch(const int64_t *run, const uint8_t *enabled, int C, const
                         const int64_t *x, size_t nq, int32_t *out) {
     if (nq == 0) return 0;
     if (C <= 0 || !run || !calls || !x || !out) return SYZCOV_EINVAL;
-    Ctx *c = ctx();
+    CtxLease lease;
+    Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     Plan p;
     size_t i_r = p.add((size_t)C * C * 8), i_e = p.add(C), i_c = p.add(nq * 4), i_x = p.add(nq * 8),

@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <atomic>
+
 #include "../../include/syzcov.h"
 
 #define SYZ_SENT 0xFFFFFFFFu
@@ -35,6 +37,19 @@ void set_error(const char *fmt, ...);
     } while (0)
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// `done` holds one bit per device (function attributes are per device, and
+// the C-ABI serves up to 16 devices from concurrent threads).
+static inline int set_dyn_lds_once(const void *fn, int bytes, std::atomic<uint32_t> &done) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return SYZCOV_EHIP;
+    const uint32_t bit = 1u << (dev & 31);
+    if (done.load(std::memory_order_acquire) & bit) return 0;
+    SYZ_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.fetch_or(bit, std::memory_order_release);
+    return 0;
+}
 static inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 16) {
     size_t g = (n + block - 1) / block;
     if (g < 1) g = 1;

@@ -17,9 +17,10 @@
 // touch anything outside [a, b) but the finished pivot at a-1, so their
 // processing order does not change the result.
 //
-// The legacy variant (Go 1.8-1.18 quickSort) is a host restatement at the end
-// of this file: its doPivot is a sequential 3-way scan and it is not the
-// default Go behaviour any more.
+// Only Go >= 1.19's pdqsort is restated.  The legacy Go 1.8-1.18 quickSort
+// order is not computed here (sort_variant 1 -> SYZCOV_EINVAL): a caller on
+// an old Go passes its own sort.Sort order (`order` of syzcov_minimize), as
+// the drop-in Go shim does anyway.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -745,126 +746,6 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
     }
 }
 
-// ---------------------------------------------------------------- legacy
-// Go 1.8-1.18 sort.Sort (quickSort + gap-6 ShellSort pass), host restatement.
-struct HArr {
-    int32_t *idx;
-    const int64_t *len;
-    bool less(long i, long j) const { return len[idx[i]] > len[idx[j]]; }
-    void swap(long i, long j) const { std::swap(idx[i], idx[j]); }
-};
-
-static void h_insertion(const HArr &d, long a, long b) {
-    for (long i = a + 1; i < b; i++)
-        for (long j = i; j > a && d.less(j, j - 1); j--) d.swap(j, j - 1);
-}
-
-static void h_sift(const HArr &d, long lo, long hi, long first) {
-    for (long root = lo;;) {
-        long child = 2 * root + 1;
-        if (child >= hi) return;
-        if (child + 1 < hi && d.less(first + child, first + child + 1)) child++;
-        if (!d.less(first + root, first + child)) return;
-        d.swap(first + root, first + child);
-        root = child;
-    }
-}
-
-static void h_heap(const HArr &d, long a, long b) {
-    long hi = b - a;
-    for (long i = (hi - 1) / 2; i >= 0; i--) h_sift(d, i, hi, a);
-    for (long i = hi - 1; i >= 0; i--) {
-        d.swap(a, a + i);
-        h_sift(d, 0, i, a);
-    }
-}
-
-static void median3(const HArr &d, long m1, long m0, long m2) {
-    if (d.less(m1, m0)) d.swap(m1, m0);
-    if (d.less(m2, m1)) {
-        d.swap(m2, m1);
-        if (d.less(m1, m0)) d.swap(m1, m0);
-    }
-}
-
-static void do_pivot(const HArr &d, long lo, long hi, long &midlo, long &midhi) {
-    long m = (long)((unsigned long)(lo + hi) >> 1);
-    if (hi - lo > 40) {
-        long s = (hi - lo) / 8;
-        median3(d, lo, lo + s, lo + 2 * s);
-        median3(d, m, m - s, m + s);
-        median3(d, hi - 1, hi - 1 - s, hi - 1 - 2 * s);
-    }
-    median3(d, lo, m, hi - 1);
-    long pivot = lo, a = lo + 1, c = hi - 1;
-    while (a < c && d.less(a, pivot)) a++;
-    long b = a;
-    for (;;) {
-        while (b < c && !d.less(pivot, b)) b++;
-        while (b < c && d.less(pivot, c - 1)) c--;
-        if (b >= c) break;
-        d.swap(b, c - 1);
-        b++;
-        c--;
-    }
-    bool protect = hi - c < 5;
-    if (!protect && hi - c < (hi - lo) / 4) {
-        int dups = 0;
-        if (!d.less(pivot, hi - 1)) {
-            d.swap(c, hi - 1);
-            c++;
-            dups++;
-        }
-        if (!d.less(b - 1, pivot)) {
-            b--;
-            dups++;
-        }
-        if (!d.less(m, pivot)) {
-            d.swap(m, b - 1);
-            b--;
-            dups++;
-        }
-        protect = dups > 1;
-    }
-    if (protect) {
-        for (;;) {
-            while (a < b && !d.less(b - 1, pivot)) b--;
-            while (a < b && d.less(a, pivot)) a++;
-            if (a >= b) break;
-            d.swap(a, b - 1);
-            a++;
-            b--;
-        }
-    }
-    d.swap(pivot, b - 1);
-    midlo = b - 1;
-    midhi = c;
-}
-
-static void quick(const HArr &d, long a, long b, int depth) {
-    while (b - a > 12) {
-        if (depth == 0) {
-            h_heap(d, a, b);
-            return;
-        }
-        depth--;
-        long mlo, mhi;
-        do_pivot(d, a, b, mlo, mhi);
-        if (mlo - a < b - mhi) {
-            quick(d, a, mlo, depth);
-            a = mhi;
-        } else {
-            quick(d, mhi, b, depth);
-            b = mlo;
-        }
-    }
-    if (b - a > 1) {
-        for (long i = a + 6; i < b; i++)
-            if (d.less(i, i - 6)) d.swap(i, i - 6);
-        h_insertion(d, a, b);
-    }
-}
-
 }  // namespace gsort
 }  // namespace syz
 
@@ -922,34 +803,6 @@ extern "C" size_t syzcov_dev_sort_ws_size(size_t n) {
 
 extern "C" size_t syzcov_dev_sort_seg_ws_size(size_t n, size_t ngroups) {
     return ws_layout((n ? n : 1) + ngroups, ngroups, nullptr, nullptr);
-}
-
-// Go 1.8-1.18 quickSort of lens[a, b) into order[a, b) (values a..b-1)
-static void legacy_range(const int64_t *hl, int32_t *ho, long a, long b) {
-    for (long i = a; i < b; i++) ho[i] = (int32_t)(i - a);  // HArr indexes relative to its base
-    HArr d{ho + a, hl + a};
-    int depth = 0;
-    for (long i = b - a; i > 0; i >>= 1) depth++;
-    quick(d, 0, b - a, 2 * depth);
-    for (long i = a; i < b; i++) ho[i] += (int32_t)a;
-}
-
-static int legacy_host(const int64_t *lens, size_t n, const uint64_t *goff, size_t ngroups,
-                       int32_t *order, hipStream_t s) {
-    std::vector<int64_t> hl(n);
-    std::vector<int32_t> ho(n);
-    std::vector<uint64_t> hg(ngroups + 1);
-    SYZ_HIP(hipMemcpyAsync(hl.data(), lens, n * 8, hipMemcpyDeviceToHost, s));
-    if (goff) SYZ_HIP(hipMemcpyAsync(hg.data(), goff, (ngroups + 1) * 8, hipMemcpyDeviceToHost, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    if (!goff) {
-        hg[0] = 0;
-        hg[1] = n;
-    }
-    for (size_t g = 0; g < ngroups; g++) legacy_range(hl.data(), ho.data(), (long)hg[g], (long)hg[g + 1]);
-    SYZ_HIP(hipMemcpyAsync(order, ho.data(), n * 4, hipMemcpyHostToDevice, s));
-    SYZ_HIP(hipStreamSynchronize(s));
-    return 0;
 }
 
 // Level-synchronous pdqsort rounds over the segments already seeded into
@@ -1029,10 +882,12 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
 extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
                                      int32_t *order, void *ws, size_t ws_size, void *stream) {
     if (n == 0) return 0;
-    if (!lens || !order || (sort_variant != 0 && sort_variant != 1) || n > 0x7FFFFFFF)
+    if (!lens || !order || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
+    if (sort_variant != 0) {
+        set_error("only Go >= 1.19 pdqsort order is computed; pass the caller's order instead");
         return SYZCOV_EINVAL;
+    }
     hipStream_t s = (hipStream_t)stream;
-    if (sort_variant == 1) return legacy_host(lens, n, nullptr, 1, order, s);
     if (!ws || ws_size < syzcov_dev_sort_ws_size(n)) return SYZCOV_EINVAL;
     SortWs w;
     ws_layout(n, 0, &w, (uint8_t *)ws);
@@ -1052,11 +907,13 @@ extern "C" int syzcov_dev_sort_order_segmented(const int64_t *lens, const uint64
                                                int32_t *order, void *ws, size_t ws_size,
                                                void *stream) {
     if (n == 0) return 0;
-    if (!lens || !goff || !order || ngroups == 0 || (sort_variant != 0 && sort_variant != 1) ||
-        n + ngroups > 0x7FFFFFFF)
+    if (!lens || !goff || !order || ngroups == 0 || n + ngroups > 0x7FFFFFFF)
         return SYZCOV_EINVAL;
+    if (sort_variant != 0) {
+        set_error("only Go >= 1.19 pdqsort order is computed");
+        return SYZCOV_EINVAL;
+    }
     hipStream_t s = (hipStream_t)stream;
-    if (sort_variant == 1) return legacy_host(lens, n, goff, ngroups, order, s);
     if (!ws || ws_size < syzcov_dev_sort_seg_ws_size(n, ngroups)) return SYZCOV_EINVAL;
     const size_t npos = n + ngroups - 1;
     SortWs w;

@@ -567,12 +567,8 @@ extern "C" int syzcov_dev_minimize_range(
     if (rc) return rc;
     const uint64_t nrange = A.nrange;
     SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters and done marks
-    static bool prep_attr = false;  // nrange = 256 needs 65.8 KB of dynamic LDS
-    if (!prep_attr) {
-        SYZ_HIP(hipFuncSetAttribute((const void *)mr::prep_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
-        prep_attr = true;
-    }
+    static std::atomic<uint32_t> prep_attr{0};  // nrange = 256 needs 65.8 KB of dynamic LDS
+    if ((rc = set_dyn_lds_once((const void *)mr::prep_kernel, 80 * 1024, prep_attr))) return rc;
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256),
                        split ? 64 * (nrange + 1) * sizeof(uint32_t) : 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
@@ -599,12 +595,8 @@ extern "C" int syzcov_dev_minimize_range(
                           mr::pass1_kernel<0x40000000, true, false, 2, 4>};
     const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
-    static bool attr_set[NVAR] = {};
-    if (!attr_set[vi]) {
-        SYZ_HIP(hipFuncSetAttribute((const void *)k1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    128 * 1024));
-        attr_set[vi] = true;
-    }
+    static std::atomic<uint32_t> attr_set[NVAR];
+    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[vi]))) return rc;
     if (const char *e = getenv("SYZCOV_MR_CHUNK")) {  // tuning: "first,growth"
         unsigned long fc = 0, gr = 0;
         if (sscanf(e, "%lu,%lu", &fc, &gr) == 2) {

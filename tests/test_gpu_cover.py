@@ -112,9 +112,11 @@ def test_sort_order_matches_go(cover):
                 rng.integers(0, 1 << 16, size=n) if kind == 1 else
                 np.sort(rng.integers(0, 100, size=n)) if kind == 2 else
                 rng.normal(2048, 512, size=n).astype(np.int64).clip(1, 65535))
-        for variant in (orc.PDQSORT, orc.LEGACY):
-            assert np.array_equal(cover.SortOrder(lens, variant), orc.sort_order(lens, variant)), \
-                (trial, variant)
+        assert np.array_equal(cover.SortOrder(lens), orc.sort_order(lens)), trial
+    # the legacy Go <= 1.18 order is the caller's to pass (no host path in the library)
+    from syzkaller_amd import SyzcovError
+    with pytest.raises(SyzcovError):
+        cover.SortOrder(lens, orc.LEGACY)
     # C2-sized: 1M canonical lengths ~ N(2048, 512) (deep global rounds + LDS finisher)
     lens = rng.normal(2048, 512, size=1_000_000).astype(np.int64).clip(1, 65535)
     assert np.array_equal(cover.SortOrder(lens), orc.sort_order(lens))
@@ -131,9 +133,10 @@ def test_minimize_random_vs_oracle(cover):
         covs = [orc.canonicalize(rng.integers(0, hi, size=int(rng.integers(0, 40)),
                                               dtype=np.uint64).astype(np.uint32))
                 for _ in range(n)]
-        for variant in (orc.PDQSORT, orc.LEGACY):
-            assert cover.Minimize(covs, variant=variant) == list(orc.minimize(covs, variant)), \
-                (trial, variant)
+        assert cover.Minimize(covs) == list(orc.minimize(covs)), trial
+        # Go 1.8-1.18: the caller's legacy sort.Sort order, Minimize on the GPU
+        legacy = orc.sort_order([len(c) for c in covs], orc.LEGACY)
+        assert cover.Minimize(covs, order=legacy) == list(orc.minimize(covs, orc.LEGACY)), trial
 
 
 def test_minimize_non_canonical_covers(cover):
@@ -194,3 +197,50 @@ def test_concurrent_callers(cover):
     [t.start() for t in ts]
     [t.join() for t in ts]
     assert not errors
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_bitmap_and_bytemap_ops(op):
+    """The bitmap / byte-map set algebra of the north star (OR = Union, AND =
+    Intersection, ANDNOT = Difference, XOR = SymmetricDifference over a PC
+    window, cover.go:42-79 on set operands) + popcount, against numpy and
+    against the oracle's list set ops on the same sets."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(50 + op)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    npf = [np.bitwise_or, np.bitwise_and, lambda a, b: a & ~b, np.bitwise_xor][op]
+    for nwords in (1, 3, 17, 4097, (1 << 20) + 5):
+        dens = rng.choice([0.01, 0.5])
+        a = (rng.random(nwords * 32) < dens)
+        b = (rng.random(nwords * 32) < 0.3)
+        aw = np.packbits(a, bitorder="little").view(np.uint32)
+        bw = np.packbits(b, bitorder="little").view(np.uint32)
+        d = torch.from_numpy(aw.view(np.int32).copy()).cuda()
+        src = torch.from_numpy(bw.view(np.int32).copy()).cuda()
+        pop = torch.zeros(1, dtype=torch.int64, device="cuda")
+        _lib.check(L.syzcov_dev_bitmap_op(op, P(d), P(src), nwords, P(pop), s), "bitmap_op")
+        exp = npf(aw, bw)
+        got = d.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, exp), (op, nwords)
+        assert int(pop.item()) == int(np.unpackbits(exp.view(np.uint8)).sum())
+        if nwords == 17:  # the same sets as sorted PC lists through the oracle
+            la = np.nonzero(a)[0].astype(np.uint32)
+            lb = np.nonzero(b)[0].astype(np.uint32)
+            ref = orc.setop({0: orc.UNION, 1: orc.INTERSECTION, 2: orc.DIFFERENCE,
+                            3: orc.SYMDIFF}[op], la, lb)
+            assert np.array_equal(np.nonzero(np.unpackbits(got.view(np.uint8),
+                                                           bitorder="little"))[0], ref)
+    for nbytes in (1, 15, 16, 33, 4099, (1 << 22) + 7):
+        a = (rng.random(nbytes) < 0.4) * rng.integers(1, 256, size=nbytes)
+        b = (rng.random(nbytes) < 0.4) * rng.integers(1, 256, size=nbytes)
+        d = torch.from_numpy(a.astype(np.uint8)).cuda()
+        src = torch.from_numpy(b.astype(np.uint8)).cuda()
+        pop = torch.zeros(1, dtype=torch.int64, device="cuda")
+        _lib.check(L.syzcov_dev_bytemap_op(op, P(d), P(src), nbytes, P(pop), s), "bytemap_op")
+        exp = npf((a != 0).astype(np.uint8), (b != 0).astype(np.uint8)) & 1
+        assert np.array_equal(d.cpu().numpy(), exp.astype(np.uint8)), (op, nbytes)
+        assert int(pop.item()) == int(exp.sum())

@@ -1,0 +1,45 @@
+"""Host-code sanitizer runs (the C-ABI parses untrusted executor
+output and is called from many threads).
+
+  * ingest.cc (the ipc.go:225-291 reader) under ASan + UBSan with malformed
+    executor outputs (CPU, tests/native/ingest_fuzz.cc);
+  * the whole C-ABI's host code under ASan + UBSan (-Xarch_host only: GPU
+    sanitizers are not available) driven by 32 concurrent threads of mixed
+    set ops / Canonicalize / Minimize checked against the oracle, with device
+    memory back to its starting level once the threads have exited
+    (tests/native/abi_stress.cc, built by tools/build_asan.sh; GPU)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+ASAN_ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+
+def test_ingest_asan_ubsan(tmp_path):
+    if not shutil.which("g++"):
+        pytest.skip("g++ absent")
+    exe = tmp_path / "ingest_fuzz"
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-o", str(exe),
+                    os.path.join(HERE, "native", "ingest_fuzz.cc"),
+                    os.path.join(ROOT, "syzkaller_amd", "csrc", "ingest.cc")], check=True)
+    r = subprocess.run([str(exe), "30000"], capture_output=True, text=True, timeout=120,
+                       env=ASAN_ENV)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ok, rej = (int(x) for x in r.stdout.split()[1::2])
+    assert ok > 1000 and rej > 1000  # both branches exercised
+
+
+@pytest.mark.gpu
+def test_abi_concurrent_asan():
+    exe = os.path.join(ROOT, "tests", "native", "build", "abi_stress_asan")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} not built (tools/build_asan.sh, run by __graft_entry__.build())")
+    r = subprocess.run([exe, "32", "8"], capture_output=True, text=True, timeout=240,
+                       env=ASAN_ENV)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-3000:] + r.stderr[-5000:]
