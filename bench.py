@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
 # this same bench command (tools/profile.sh -> tools/traffic.py), committed per round
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED_C1 = 0x5EED0001  # BASELINE.json configs[0]: the CPU (reference) config
 SEED = 0x5EED0002     # configs[1]: 1M inputs, one GPU
@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=10_000,
                     help="inputs of config C1 timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-universe", action="store_true",
+                    help="corpus: window-offset keys instead of the dense keys of the registered "
+                         "PC universe (keys.hip)")
     return ap.parse_args()
 
 
@@ -204,7 +207,7 @@ def timed(run_step, nphase, args, world, dev):
 def bench_corpus(args):
     import torch
     world, rank, dev = init_dist()
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     # N=1: config C2 (1M inputs); N>1: config C3 (10M global inputs, sharded
     # by input: rank r holds [r*n, (r+1)*n)), unless --global-inputs says otherwise
     glob = args.global_inputs
@@ -221,11 +224,15 @@ def bench_corpus(args):
     off, raw, lens, total = synth_corpus(n, seed, first=rank * n, mean=args.mean,
                                          sigma=args.sigma, log2_space=args.log2_space, device=dev)
     max_len = int(lens.max().item())
+    # the PC universe (allCoverPCs, syz-manager/cover.go:57-69) is registered once,
+    # outside the timed steps, like the resident maxCover
+    univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev)
     if world > 1:
         from syzkaller_amd.dist import ShardedEngine
-        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev)
+        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev, universe=univ)
     else:
-        eng = CorpusEngine(n, total, max_len, lo, span, device=dev)
+        eng = CorpusEngine(n, total, max_len, lo, span, device=dev, universe=univ)
+    del univ
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
     dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), args,
@@ -257,6 +264,9 @@ def bench_corpus(args):
                    "raw_pcs_per_gpu": total,
                    "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
                    "len_mean": args.mean, "len_sigma": args.sigma,
+                   "keys": (f"dense keys of the registered PC universe: (pc >> {eng.kshift}) - "
+                            f"{eng.kbase:#x}, {eng.span} keys" if eng.key_mode
+                            else f"window offsets pc - {lo:#x}, {span} keys"),
                    "parallelism": f"shard-by-input x{world}"},
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},
         "results": {"kept": res.n_kept, "union": res.n_union, "max_cover": res.max_cover,

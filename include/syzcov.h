@@ -324,6 +324,30 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
                            uint64_t pc_span, uint32_t range_shift, uint32_t *split,
                            uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
                            void *stream);
+/* Key mode (keys.hip): key(pc) = (pc >> kshift) - kbase over a registered PC
+ * universe (allCoverPCs) with kshift = the largest collision-free shift:
+ * Canonicalize writes sorted unique KEYS (nkeys = key range; the contract is
+ * that every PC belongs to the universe, which KCOV guarantees for the
+ * kernel the universe was taken from).  Otherwise as syzcov_dev_canon_split. */
+int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                                uint32_t *new_len, size_t nseg, size_t max_seg_len,
+                                uint32_t kshift, uint32_t kbase, uint64_t nkeys,
+                                uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
+                                uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+/* pc_of_key[key(univ[i])] = univ[i] (univ sorted, collision-free under
+ * kshift, else *err_flag |= 1). */
+int syzcov_dev_universe_keymap(const uint32_t *univ, size_t n, uint32_t kshift, uint32_t kbase,
+                               uint64_t nkeys, uint32_t *pc_of_key, uint32_t *err_flag,
+                               void *stream);
+/* out[i] = pc_of_key[keys[i]] for i < min(*n_dev, n_max) (n_dev: device count,
+ * nullable); keys >= nkeys give 0xFFFFFFFF; in place allowed. */
+int syzcov_dev_keys_to_pcs(const uint32_t *pc_of_key, uint64_t nkeys, const uint32_t *keys,
+                           uint32_t *out, const uint32_t *n_dev, size_t n_max, void *stream);
+
+/* covered[w] = bits of first[] < INT32_MAX over [0, span) (the union of a
+ * sharded step from its MIN all-reduced first-cover array). */
+int syzcov_dev_first_to_bits(const int32_t *first, uint64_t span, uint32_t *covered, void *stream);
+
 /* Minimize (cover.go:104-131) over canonical covers with split[] from
  * syzcov_dev_canon_split.  Item j (processing order) is input order[j] with
  * rank ranks[j] (NULL: j).  covered: window bitmap of nrange << range_shift

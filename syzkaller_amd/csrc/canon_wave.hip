@@ -1,9 +1,15 @@
 // canon_wave.hip — corpus-scale cover.Canonicalize (cover/cover.go:27-40):
 // one WAVEFRONT per segment, no workgroup barriers.
 //
-// A segment of n <= 8189 raw PCs is sorted by an LSD radix sort over its
-// window offsets (key = pc - pc_lo, nbits = bit_length(span-1), <= 9-bit
-// digits) entirely in the wave's private LDS slice:
+// A segment of n <= 8189 raw PCs is sorted by an LSD radix sort over its keys
+// entirely in the wave's private LDS slice.  Key = (pc >> kshift) - kbase:
+// kshift = 0, kbase = pc_lo gives window offsets (exact for any PC in the
+// window); with a registered PC universe (engine key mode) kshift is the
+// largest shift that keeps the universe collision-free, which maps it onto a
+// dense key space (the synthetic universe: 2^22 keys instead of 2^26 window
+// offsets).  nbits = bit_length(nkeys - 1); digits of <= 9 bits (512-entry
+// histogram), or 11 bits (2048 entries) when that saves a pass (19..22-bit
+// keys: 2 passes instead of 3):
 //   load     16-byte vector loads of the raw list (head/tail masked);
 //   pass 0   lowest digit, unstable: count (ds_add), exclusive scan of the
 //            512-entry histogram, scatter with ds_add_rtn positions;
@@ -17,8 +23,8 @@
 //            to the workgroup bitonic fallback (canon.hip) instead.
 //   unique   the reference loop (`last := sent`: the key of PC 0xFFFFFFFF is
 //            dropped only in first position), ballot-compacted, written back
-//            as PCs to the segment's own CSR slots (in place is safe: the
-//            wave holds its keys before it writes).
+//            to the segment's own CSR slots (in place is safe: the wave holds
+//            its keys before it writes) as PCs, or as keys in key mode.
 // Optional outputs for the range-partitioned Minimize (minimize_range.hip):
 //   split[seg * R + j] = number of canonical PCs with offset < (j+1) << rshift
 //   range_tot[j]      += canonical PCs of range j over the corpus.
@@ -50,7 +56,6 @@ int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uin
 namespace cw {
 
 constexpr int WPB = 2;        // waves per workgroup (independent segments)
-constexpr int HIST = 512;     // 9-bit digits
 constexpr int MAX_RPL = 4;    // ranges per lane (R <= 256)
 constexpr uint32_t WAVE_MAX = 8192 - 3;  // a CAP-slot wave holds head (<= 3) + n keys
 
@@ -66,26 +71,34 @@ __device__ __forceinline__ void wave_sync() {
 constexpr uint32_t CNT1 = 1u << 16;  // +1 on the high (count) half
 
 // Exclusive scan of the counts (high halves) into slots (low halves), with the
-// high halves cleared for the next pass's counts (8 entries per lane).
+// high halves cleared for the next pass's counts (HIST / 64 entries per lane).
+template <int HIST>
 __device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
+    constexpr int PL = HIST / 256;  // uint4 chunks per lane
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
-    uint4 a = h4[2 * l], b = h4[2 * l + 1];
-    a.x >>= 16; a.y >>= 16; a.z >>= 16; a.w >>= 16;
-    b.x >>= 16; b.y >>= 16; b.z >>= 16; b.w >>= 16;
-    const uint32_t s = a.x + a.y + a.z + a.w + b.x + b.y + b.z + b.w;
-    uint32_t p = wave_incl_scan(s) - s;
-    uint4 oa, ob;
-    oa.x = p; p += a.x; oa.y = p; p += a.y; oa.z = p; p += a.z; oa.w = p; p += a.w;
-    ob.x = p; p += b.x; ob.y = p; p += b.y; ob.z = p; p += b.z; ob.w = p;
-    h4[2 * l] = oa;
-    h4[2 * l + 1] = ob;
+    uint4 v[PL];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PL; q++) {
+        v[q] = h4[PL * l + q];
+        v[q].x >>= 16; v[q].y >>= 16; v[q].z >>= 16; v[q].w >>= 16;
+        sum += v[q].x + v[q].y + v[q].z + v[q].w;
+    }
+    uint32_t p = wave_incl_scan(sum) - sum;
+#pragma unroll
+    for (int q = 0; q < PL; q++) {
+        uint4 o;
+        o.x = p; p += v[q].x; o.y = p; p += v[q].y; o.z = p; p += v[q].z; o.w = p; p += v[q].w;
+        h4[PL * l + q] = o;
+    }
 }
 
-
+template <int HIST>
 __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
+    constexpr int PL = HIST / 256;
     uint4 *h4 = reinterpret_cast<uint4 *>(hist);
-    h4[2 * l] = make_uint4(0, 0, 0, 0);
-    h4[2 * l + 1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < PL; q++) h4[PL * l + q] = make_uint4(0, 0, 0, 0);
 }
 
 // One radix scatter over the active rows: ranks by ds_add_rtn on the low
@@ -116,7 +129,7 @@ __device__ __forceinline__ bool real_slot(int j, uint32_t l, uint32_t lo, uint32
 // Pad slots are sent, branch-free, to a private dummy word of their lane
 // (hist[HIST + l], buf[cap + l]): distinct addresses, so they cost no
 // same-address serialisation, and they never touch the real counters/slots.
-template <bool RAW, int NK, int BQ = SYZ_CANON_BQ>
+template <bool RAW, int NK, int HIST, int BQ = SYZ_CANON_BQ>
 __device__ __forceinline__ void scatter_rows(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
                                              uint32_t lo, uint32_t hi, uint32_t *buf,
                                              uint32_t *hist, uint32_t sh, uint32_t dmask,
@@ -156,7 +169,9 @@ struct Params {
     uint32_t pc_lo;
     uint64_t span;
     uint32_t nbits;
-    uint32_t sent_key;        // window offset of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
+    uint32_t kshift, kbase;   // key = (pc >> kshift) - kbase; span = number of keys
+    int key_out;              // write keys (key mode) instead of PCs (kshift == 0)
+    uint32_t sent_key;        // key of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
     uint32_t *split;          // nullable: [nseg][nrange]
     uint32_t nrange, rshift;
     unsigned long long *range_tot;  // nullable: [nrange]
@@ -230,10 +245,11 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
 // scatters (packed histogram), so a pass is one read-back and one scatter
 // loop; the keys of the pass being scattered live in registers only between
 // those two loops.
-template <int NK, int MINW>
+template <int NK, int MINW, int HB>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, const uint32_t *list,
                                                                     const uint32_t *count) {
     constexpr int CAP = 64 * NK;
+    constexpr int HIST = 1 << HB;
     constexpr int NQ = NK / 4;  // 16-byte loads per lane = row quads
     __shared__ uint32_t s_buf[WPB][CAP + 64];  // + one pad dummy per lane
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST + 64];
@@ -241,8 +257,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
     const uint32_t nbits = P.nbits < 1 ? 1 : P.nbits;
-    const uint32_t npass = (nbits + 8) / 9;
-    const uint32_t dbits = (nbits + npass - 1) / npass;  // <= 9
+    const uint32_t npass = (nbits + HB - 1) / HB;
+    const uint32_t dbits = (nbits + npass - 1) / npass;  // <= HB
     const uint32_t dmask = (1u << dbits) - 1u;
     const uint32_t PAD = npass * dbits >= 32 ? 0xFFFFFFFFu : (1u << (npass * dbits)) - 1u;
     const uint64_t lt = (1ull << l) - 1ull;
@@ -295,7 +311,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t idx = e4 + c;
-                    const uint32_t key = vv[c] - P.pc_lo;
+                    const uint32_t key = (vv[c] >> P.kshift) - P.kbase;
                     const bool valid = idx >= head && idx < end;
                     oob |= valid && key > span_m1;
                     k[q * 4 + c] = valid ? key : PAD;
@@ -305,7 +321,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
         if (li + nw < nl) issue(li + nw);
         if (__ballot(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
         // ------------------------------------------- pass 0 (unstable)
-        hist_zero(s_hist[w], l);
+        hist_zero<HIST>(s_hist[w], l);
         wave_sync();
 #pragma unroll
         for (int q = 0; q < NQ; q++)
@@ -316,10 +332,10 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                                              ? k[q * 4 + c] & dmask : HIST + l], CNT1);
             }
         wave_sync();
-        hist_scan(s_hist[w], l);
+        hist_scan<HIST>(s_hist[w], l);
         wave_sync();
         const bool two = npass > 1;
-        scatter_rows<true, NK>(k, nq, l, head, end, buf, s_hist[w], 0, dmask, dbits, two);
+        scatter_rows<true, NK, HIST>(k, nq, l, head, end, buf, s_hist[w], 0, dmask, dbits, two);
         wave_sync();
         // --------------------------------------------- stable passes
         for (uint32_t p = 1; p < npass; p++) {
@@ -331,9 +347,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                     for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
                 }
-            hist_scan(s_hist[w], l);
+            hist_scan<HIST>(s_hist[w], l);
             wave_sync();
-            scatter_rows<false, NK>(k, nq, l, 0, n, buf, s_hist[w], sh, dmask, dbits, more);
+            scatter_rows<false, NK, HIST>(k, nq, l, 0, n, buf, s_hist[w], sh, dmask, dbits, more);
             wave_sync();
         }
         // --------------------------------- order check + unique + write
@@ -380,11 +396,14 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
                     bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
-                    const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
+                    // keys outside [0, span) (flagged at load) sort last and are
+                    // dropped, so nothing downstream indexes past the key range
+                    const uint32_t keep =
+                        (uint32_t)(e < n) & (uint32_t)(v != prev) & (uint32_t)(v <= span_m1);
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        outp[pos] = v + P.pc_lo;
+                        outp[pos] = P.key_out ? v : v + P.kbase;
                         buf[pos] = v;
                     }
                     cnt += (uint32_t)__popcll(m);
@@ -456,7 +475,7 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
                 uint32_t lo = 0, hi = cnt;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (c[mid] - P.pc_lo < b) lo = mid + 1; else hi = mid;
+                    if (c[mid] - (P.key_out ? 0u : P.kbase) < b) lo = mid + 1; else hi = mid;
                 }
                 s = lo;
             }
@@ -471,6 +490,34 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
     }
 }
 
+// Segments canonicalized by the workgroup paths (canon.hip) hold PCs: check
+// them against the key range and, in key mode, turn them into keys (in place)
+// before their split points are taken.  A key outside [0, span) sets
+// SYZCOV_ERR_WINDOW and drops the segment, so Minimize never indexes past the
+// range (the wave path drops such keys itself).
+__global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_t *list,
+                                                         const uint32_t *count, int big_only) {
+    const uint32_t nl = *count;
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint32_t seg = list[li];
+        if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
+        uint32_t *c = P.out + P.off[seg];
+        const uint32_t cnt = P.new_len[seg];
+        bool bad = false;
+        for (uint32_t i = __lane_id(); i < cnt; i += 64) {
+            const uint32_t key = (c[i] >> P.kshift) - P.kbase;
+            bad |= key > (uint32_t)(P.span - 1);
+            if (P.key_out) c[i] = key;
+        }
+        if (__ballot(bad)) {  // flagged; the segment is dropped (memory-safe downstream)
+            if (__lane_id() == 0) {
+                atomicOr(P.err, SYZCOV_ERR_WINDOW);
+                P.new_len[seg] = 0;
+            }
+        }
+    }
+}
+
 }  // namespace cw
 }  // namespace syz
 
@@ -479,7 +526,7 @@ using namespace syz;
 // Workgroups that fit on the whole chip at once for a class kernel: the grid
 // is never larger, so every wave owns an equal share of the class (+-1
 // segment) instead of a fixed 1/4096 of it run in 2-3 partly empty rounds.
-template <int NK, int MW>
+template <int NK, int MW, int HB>
 static unsigned resident_grid(uint64_t nseg) {
     static unsigned cap = 0;
     if (!cap) {
@@ -489,7 +536,7 @@ static unsigned resident_grid(uint64_t nseg) {
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess) ncu = pr.multiProcessorCount;
         }
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void *>(cw::canon_wave_kernel<NK, MW>), 64 * cw::WPB,
+                &nb, reinterpret_cast<const void *>(cw::canon_wave_kernel<NK, MW, HB>), 64 * cw::WPB,
                 0) != hipSuccess || nb < 1)
             nb = 1;
         cap = (unsigned)(nb * ncu);
@@ -502,20 +549,39 @@ extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
     return 256 + (2 + cw::NCLS) * align_up(nseg * sizeof(uint32_t), 256);
 }
 
-extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *out,
-                                      uint32_t *new_len, size_t nseg, size_t max_seg_len,
-                                      uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
-                                      uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
-                                      void *ws, size_t ws_size, void *stream) {
+// One class launch: HB = 11 (2048-entry histograms) when 19..22-bit keys
+// then take 2 passes instead of 3, else HB = 9.
+template <int NK, int MW>
+static void launch_class(bool hb11, const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
+                         uint64_t nseg, hipStream_t s) {
+    // 8 KB histograms: LDS allows 2 waves per SIMD at most
+    constexpr int MW11 = MW > 2 ? 2 : MW;
+    if (hb11)
+        hipLaunchKernelGGL((cw::canon_wave_kernel<NK, MW11, 11>),
+                           dim3(resident_grid<NK, MW11, 11>(nseg)), dim3(64 * cw::WPB), 0, s, P,
+                           lc, cnt);
+    else
+        hipLaunchKernelGGL((cw::canon_wave_kernel<NK, MW, 9>),
+                           dim3(resident_grid<NK, MW, 9>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc,
+                           cnt);
+}
+
+static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                            uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t kshift,
+                            uint32_t kbase, uint64_t nkeys, int key_out, uint32_t range_shift,
+                            uint32_t *split, uint64_t *range_tot, uint32_t *err_flag, void *ws,
+                            size_t ws_size, void *stream) {
     if (nseg == 0) return 0;
     if (!off || !raw || !out || !new_len || !err_flag || !ws) return SYZCOV_EINVAL;
-    if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
+    if (nkeys == 0 || nkeys > (1ull << 32) || kshift > 31 ||
+        (uint64_t)kbase + nkeys > (1ull << (32 - kshift)))
         return SYZCOV_ERANGE;
+    if (kshift && !key_out) return SYZCOV_EINVAL;  // PCs are not recoverable from shifted keys
     if (ws_size < syzcov_dev_canon_split_ws_size(nseg) || nseg > 0xFFFFFFFFull)
         return SYZCOV_EINVAL;
     if (out == raw && max_seg_len > 16384) return SYZCOV_EINVAL;  // large path is out of place
     if (range_shift > 20) return SYZCOV_EINVAL;
-    const uint64_t nrange = (pc_span + (1ull << range_shift) - 1) >> range_shift;
+    const uint64_t nrange = (nkeys + (1ull << range_shift) - 1) >> range_shift;
     if (split && nrange > (uint64_t)cw::MAX_RPL * 64) return SYZCOV_ERANGE;
     hipStream_t s = (hipStream_t)stream;
     uint8_t *w = (uint8_t *)ws;
@@ -529,11 +595,14 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     P.out = out;
     P.new_len = new_len;
     P.nseg = nseg;
-    P.pc_lo = pc_lo;
-    P.span = pc_span;
-    P.nbits = pc_span <= 1 ? 1 : 64 - __builtin_clzll(pc_span - 1);
-    const uint64_t so = (uint64_t)(uint32_t)(0xFFFFFFFFu - pc_lo);
-    P.sent_key = so < pc_span ? (uint32_t)so : 0xFFFFFFFFu;
+    P.pc_lo = kshift ? 0u : kbase;
+    P.span = nkeys;
+    P.kshift = kshift;
+    P.kbase = kbase;
+    P.key_out = key_out;
+    P.nbits = nkeys <= 1 ? 1 : 64 - __builtin_clzll(nkeys - 1);
+    const uint64_t so = (uint64_t)(uint32_t)((0xFFFFFFFFu >> kshift) - kbase);
+    P.sent_key = so < nkeys ? (uint32_t)so : 0xFFFFFFFFu;
     P.split = split;
     P.nrange = (uint32_t)nrange;
     P.rshift = range_shift;
@@ -543,6 +612,7 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
     P.big_list = big;
     P.big_cnt = cnts + 1;
     P.err = err_flag;
+    const bool hb11 = P.nbits >= 19 && P.nbits <= 22;
     // bin by capacity class (wave-aggregated atomics), one launch per class
     // (a register bitonic network measured 20.3 ms at C2 against the LDS
     // radix's 7.8: 147 VALU ops per key)
@@ -565,20 +635,27 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
         switch (c) {
-        case 0: hipLaunchKernelGGL((cw::canon_wave_kernel<32, SYZ_CANON_W32>), dim3(resident_grid<32, SYZ_CANON_W32>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 1: hipLaunchKernelGGL((cw::canon_wave_kernel<40, SYZ_CANON_W40>), dim3(resident_grid<40, SYZ_CANON_W40>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 2: hipLaunchKernelGGL((cw::canon_wave_kernel<48, SYZ_CANON_W48>), dim3(resident_grid<48, SYZ_CANON_W48>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 3: hipLaunchKernelGGL((cw::canon_wave_kernel<64, 2>), dim3(resident_grid<64, 2>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
-        case 4: hipLaunchKernelGGL((cw::canon_wave_kernel<128, 1>), dim3(resident_grid<128, 1>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc, ccnt + c); break;
+        case 0: launch_class<32, SYZ_CANON_W32>(hb11, P, lc, ccnt + c, nseg, s); break;
+        case 1: launch_class<40, SYZ_CANON_W40>(hb11, P, lc, ccnt + c, nseg, s); break;
+        case 2: launch_class<48, SYZ_CANON_W48>(hb11, P, lc, ccnt + c, nseg, s); break;
+        case 3: launch_class<64, 2>(hb11, P, lc, ccnt + c, nseg, s); break;
+        case 4: launch_class<128, 1>(hb11, P, lc, ccnt + c, nseg, s); break;
         }
         SYZ_LAUNCH_CHECK();
     }
+    // the workgroup paths write PCs: keys for them in key mode, then splits
+    auto finish_list = [&](const uint32_t *list, const uint32_t *cnt, int big_only,
+                           unsigned grid) {
+        hipLaunchKernelGGL(cw::keyify_list_kernel, dim3(grid), dim3(64), 0, s, P, list, cnt,
+                           big_only);
+        if (split)
+            hipLaunchKernelGGL(cw::split_list_kernel, dim3(grid), dim3(64), 0, s, P, list, cnt,
+                               big_only);
+    };
     // segments whose wave sort failed the order check (not expected on gfx950)
     int rc = canon_list_path(off, raw, out, new_len, redo, cnts, s);
     if (rc) return rc;
-    if (split)
-        hipLaunchKernelGGL(cw::split_list_kernel, dim3(64), dim3(64), 0, s, P, (const uint32_t *)redo,
-                           (const uint32_t *)cnts, 0);
+    finish_list(redo, cnts, 0, 64);
     if (max_seg_len > cw::WAVE_MAX) {
         if (max_seg_len <= 16384) {
             rc = canon_list_path(off, raw, out, new_len, big, cnts + 1, s);
@@ -588,15 +665,36 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
             SYZ_HIP(hipMemcpyAsync(&nbig, cnts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             SYZ_HIP(hipStreamSynchronize(s));
             if (nbig) {
-                rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr, pc_lo, pc_span,
+                // window check of the PC path: the keys are checked by keyify
+                rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr,
+                                      key_out ? 0u : kbase, key_out ? (1ull << 32) : nkeys,
                                       err_flag, s);
                 if (rc) return rc;
             }
         }
-        if (split)
-            hipLaunchKernelGGL(cw::split_list_kernel, dim3(256), dim3(64), 0, s, P,
-                               (const uint32_t *)big, (const uint32_t *)(cnts + 1), 1);
+        finish_list(big, cnts + 1, 1, 256);
     }
     SYZ_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                                      uint32_t *new_len, size_t nseg, size_t max_seg_len,
+                                      uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+                                      uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
+                                      void *ws, size_t ws_size, void *stream) {
+    if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
+        return nseg ? SYZCOV_ERANGE : 0;
+    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, 0, pc_lo, pc_span, 0,
+                            range_shift, split, range_tot, err_flag, ws, ws_size, stream);
+}
+
+extern "C" int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                                           uint32_t *new_len, size_t nseg, size_t max_seg_len,
+                                           uint32_t kshift, uint32_t kbase, uint64_t nkeys,
+                                           uint32_t range_shift, uint32_t *split,
+                                           uint64_t *range_tot, uint32_t *err_flag, void *ws,
+                                           size_t ws_size, void *stream) {
+    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, kshift, kbase, nkeys, 1,
+                            range_shift, split, range_tot, err_flag, ws, ws_size, stream);
 }

@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .engine import CorpusEngine, _p, _stream
+from .engine import INT32_MAX, CorpusEngine, _p, _stream
 from ._lib import check
 
 
@@ -103,9 +103,9 @@ class ShardedEngine(CorpusEngine):
     (global input i lives on rank i // n)."""
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 rank: int, world: int, device="cuda", sort_variant: int = 0):
+                 rank: int, world: int, device="cuda", sort_variant: int = 0, universe=None):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
-                         n_global=n * world, sort_variant=sort_variant)
+                         n_global=n * world, sort_variant=sort_variant, universe=universe)
         self.rank, self.world, self.n_local = rank, world, n
         self.glens = torch.empty(n * world, dtype=torch.int32, device=self.dev)
         # the merged union can be larger than this shard's PC count
@@ -150,6 +150,24 @@ class ShardedEngine(CorpusEngine):
         m = items.numel()
         self.minimize(off, items, ranks, m, do_pass2=False)
         mark_ev()
+        if self.key_mode:
+            # dense key space: the first-cover array itself is the exchange
+            # (nkeys int32, 16 MB at 2^22 keys; no dictionary, no host sync)
+            merge_first(self.first[:self.span])                  # RCCL int32 MIN
+            check(L.syzcov_dev_first_to_bits(_p(self.first), self.span, _p(self.covered), s),
+                  "dev_first_to_bits")                          # union = keys with a first cover
+            self.minimize_pass2(off, items, ranks, m)            # kept against the global first
+            self.first[:self.span].fill_(INT32_MAX)              # other ranks' entries too
+            merge_kept(self.kept[:N])                            # RCCL uint8 MAX
+            self.build_dict(self.ws2)
+            mark_ev()
+            self.compact(N, self.ws2)
+            mark_ev()
+            self.union_list()
+            mark_ev()
+            self.merge_max_cover()
+            mark_ev()
+            return self.result() if sync else None
         merge_covered(self.covered[:self.nwords], self.world, self._or_into)
         self.build_dict(self.ws2)
         n_ids = int(self.scal[1].item()) & 0xFFFFFFFF

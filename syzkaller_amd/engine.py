@@ -65,12 +65,21 @@ class CorpusEngine:
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  device="cuda", n_global: int | None = None, sort_variant: int = 0,
-                 rec_cap: int = 0, canon_in_place: bool = False):
+                 rec_cap: int = 0, canon_in_place: bool = False, universe=None):
         L = lib()
         dev = torch.device(device)
         self.dev, self.L = dev, L
         self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
+        # Key mode (keys.hip): with the PC universe registered, every phase works
+        # on dense keys (pc >> kshift) - kbase instead of window offsets
+        self.key_mode = universe is not None
+        self.kshift, self.kbase = 0, pc_lo
+        if self.key_mode:
+            self.kshift, self.kbase, nkeys, self.pc_of_key = universe_keymap(universe, dev)
+            pc_lo, pc_span = 0, nkeys  # minimize / union / maxCover window = the key range
         self.pc_lo, self.span = pc_lo, pc_span
+        so = (0xFFFFFFFF >> self.kshift) - self.kbase  # key of the 0xFFFFFFFF sentinel
+        self.sent_key = so if 0 <= so < pc_span else None
         self.sort_variant = sort_variant
         self.n_global = n_global or n_max
         self.rshift = RANGE_SHIFT
@@ -129,6 +138,12 @@ class CorpusEngine:
         self.range_tot.zero_()
         if self.canon_in_place:
             self.canon = raw
+        if self.key_mode:
+            check(self.L.syzcov_dev_canon_split_keys(
+                _p(off), _p(raw), _p(self.canon), _p(self.new_len), n, self.max_seg, self.kshift,
+                self.kbase, self.span, self.rshift, _p(self.split), _p(self.range_tot),
+                _p(self.scal), _p(self.ws), self.ws_size, _stream()), "dev_canon_split_keys")
+            return
         check(self.L.syzcov_dev_canon_split(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
                                             self.max_seg, self.pc_lo, self.span, self.rshift,
                                             _p(self.split), _p(self.range_tot), _p(self.scal),
@@ -182,12 +197,17 @@ class CorpusEngine:
     def union_list(self):
         check(self.L.syzcov_dev_dict_to_list(_p(self.tab), self.span, self.pc_lo, _p(self.union),
                                              _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
+        if self.key_mode:  # sorted keys -> sorted PCs (the key map is monotone)
+            check(self.L.syzcov_dev_keys_to_pcs(_p(self.pc_of_key), self.span, _p(self.union),
+                                                _p(self.union),
+                                                _p(self.scal[3:4]), self.union.numel(), _stream()),
+                  "dev_keys_to_pcs")
 
     def merge_max_cover(self):
         """maxCover |= union.  The union (Union fold) drops 0xFFFFFFFF
         (cover.go:97): if the window holds it, its covered bit goes first."""
-        so = 0xFFFFFFFF - self.pc_lo
-        if so < self.span:
+        so = self.sent_key
+        if so is not None:
             self.covered[so >> 5] &= ~(1 << (so & 31)) if (so & 31) != 31 else 0x7FFFFFFF
         check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered), self.nwords,
                                           _p(self.scal[4:5]), _stream()), "dev_bitmap_op")
@@ -232,8 +252,15 @@ class CorpusEngine:
                           int(sc[4]))
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
-        """The canonical covers as PCs, in the CSR slots of `off`."""
-        return self.canon
+        """The canonical covers as PCs, in the CSR slots of `off` (key mode:
+        mapped back from the keys canon wrote there)."""
+        if not self.key_mode:
+            return self.canon
+        out = torch.empty_like(self.canon)
+        check(self.L.syzcov_dev_keys_to_pcs(_p(self.pc_of_key), self.span, _p(self.canon), _p(out),
+                                            None, int(off[n].item()), _stream()),
+              "dev_keys_to_pcs")
+        return out
 
 
 class PrioEngine:
@@ -319,6 +346,48 @@ def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int
 
 
 SYNTH_PC_LO = 0x81000000
+
+
+def universe_shift(u: np.ndarray) -> int:
+    """Largest kshift with no two neighbouring (sorted, unique) universe PCs
+    sharing pc >> kshift: (a >> s) != (b >> s) iff a ^ b has a bit >= s, so
+    kshift = min over neighbours of the highest differing bit."""
+    u = np.asarray(u, dtype=np.uint32)
+    if u.size < 2:
+        return 0
+    if not np.all(u[1:] > u[:-1]):
+        raise ValueError("the PC universe must be sorted and unique")
+    return int((u[1:] ^ u[:-1]).min()).bit_length() - 1
+
+
+def universe_keymap(universe, dev):
+    """(kshift, kbase, nkeys, pc_of_key) of a registered PC universe
+    (sorted unique uint32 PCs: allCoverPCs, syz-manager/cover.go:57-69)."""
+    if isinstance(universe, torch.Tensor):
+        uh = universe.cpu().numpy().view(np.uint32)
+        ud = universe.to(dev)
+    else:
+        uh = np.ascontiguousarray(universe, dtype=np.uint32)
+        ud = torch.from_numpy(uh.view(np.int32)).to(dev)
+    ks = universe_shift(uh)
+    kbase = int(uh[0]) >> ks
+    nkeys = (int(uh[-1]) >> ks) - kbase + 1
+    pc_of_key = torch.zeros(nkeys, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    L = lib()
+    check(L.syzcov_dev_universe_keymap(_p(ud), uh.size, ks, kbase, nkeys, _p(pc_of_key), _p(err),
+                                       _stream()), "dev_universe_keymap")
+    if int(err.item()):
+        raise ValueError("universe keymap failed (unsorted or colliding universe)")
+    return ks, kbase, nkeys, pc_of_key
+
+
+def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda") -> torch.Tensor:
+    """The synthetic generator's PC universe U[k], k < 2^log2_space (sorted;
+    it depends on the corpus seed)."""
+    u = torch.empty(1 << log2_space, dtype=torch.int32, device=device)
+    check(lib().syzcov_dev_synth_universe(seed, log2_space, _p(u), _stream()), "synth_universe")
+    return u
 
 
 def synth_window(log2_space: int = 22):

@@ -5,7 +5,7 @@ through the host) and process config C2's 1M-input corpus split by input
 and the union with the CPU oracle's full-size digests
 (tests/golden/fullsize_digests.json) and prints OK.
 
-usage: gpu_dist_rehearse.py WORLD [CONFIG]"""
+usage: gpu_dist_rehearse.py WORLD [CONFIG] [keys|window]"""
 import hashlib
 import json
 import os
@@ -15,11 +15,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(rank, world, port, cfg):
+def worker(rank, world, port, cfg, keys):
     import torch
     import torch.distributed as dist
     from syzkaller_amd.dist import ShardedEngine
-    from syzkaller_amd.engine import synth_corpus, synth_window
+    from syzkaller_amd.engine import synth_corpus, synth_universe, synth_window
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
@@ -27,7 +27,8 @@ def worker(rank, world, port, cfg):
     lo, span = synth_window(cfg["log2_space"])
     off, raw, lens, total = synth_corpus(n, cfg["seed"], first=rank * n, mean=cfg["mean"],
                                          sigma=cfg["sigma"], log2_space=cfg["log2_space"])
-    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world)
+    univ = synth_universe(cfg["log2_space"], cfg["seed"]) if keys else None
+    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world, universe=univ)
     for step in range(2):  # the second step must find the engine state clean
         res = eng.step(off, raw, n)
         kept = res.kept_idx.cpu().numpy().astype("<i4").tobytes()
@@ -48,6 +49,7 @@ def main():
     import torch.multiprocessing as mp
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     name = sys.argv[2] if len(sys.argv) > 2 else "C2"
+    keys = (sys.argv[3] if len(sys.argv) > 3 else "keys") == "keys"
     with open(os.path.join(ROOT, "tests", "golden", "fullsize_digests.json")) as f:
         cfg = json.load(f)[name]
     assert cfg["n"] % world == 0
@@ -56,7 +58,7 @@ def main():
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
-    ps = [ctx.Process(target=worker, args=(r, world, port, cfg)) for r in range(world)]
+    ps = [ctx.Process(target=worker, args=(r, world, port, cfg, keys)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:

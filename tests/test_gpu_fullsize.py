@@ -38,15 +38,18 @@ def torch():
     return t
 
 
-def _engine_vs_digest(torch, name, inplace):
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+def _engine_vs_digest(torch, name, inplace, keys=True):
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     g = golden(name)
     n = g["n"]
     off, raw, lens, total = synth_corpus(n, g["seed"], mean=g["mean"], sigma=g["sigma"],
                                          log2_space=g["log2_space"])
     assert total == g["raw_pcs"]
     lo, span = synth_window(g["log2_space"])
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, canon_in_place=inplace)
+    univ = synth_universe(g["log2_space"], g["seed"]) if keys else None
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, canon_in_place=inplace,
+                       universe=univ)
+    assert eng.key_mode == keys
     res = eng.step(off, raw, n)
     assert int(eng.new_len[:n].to(torch.int64).sum().item()) == g["canonical_pcs"]
     assert sha(eng.new_len[:n]) == g["lens_sha256"]
@@ -59,11 +62,13 @@ def _engine_vs_digest(torch, name, inplace):
     return eng, off, raw
 
 
-def test_c2_fullsize_digest(torch):
-    """Config C2 (1M inputs, 2.05 G raw PCs) on one GPU: bit-exact kept list,
-    union, canonical lengths and Go sort order; a second step (engine state
-    reused, maxCover saturated) gives the same."""
-    eng, off, raw = _engine_vs_digest(torch, "C2", inplace=False)
+@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
+def test_c2_fullsize_digest(torch, keys):
+    """Config C2 (1M inputs, 2.05 G raw PCs) on one GPU, dense universe keys
+    and window offsets: bit-exact kept list, union, canonical lengths and Go
+    sort order; a second step (engine state reused, maxCover saturated) gives
+    the same."""
+    eng, off, raw = _engine_vs_digest(torch, "C2", inplace=False, keys=keys)
     g = golden("C2")
     res = eng.step(off, raw, g["n"])
     assert sha(res.kept_idx) == g["kept_sha256"] and sha(res.union) == g["union_sha256"]
@@ -83,7 +88,7 @@ def test_c3_fullsize_digest(torch):
 def test_c3_order_chunked(torch):
     """C3's 10M canonical lengths, canonicalized 1M inputs at a time, and the
     device restatement of Go's sort.Sort over all 10M of them."""
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     g = golden("C3")
     n, chunk = g["n"], 1_000_000
     lo, span = synth_window(g["log2_space"])
@@ -93,7 +98,8 @@ def test_c3_order_chunked(torch):
         off, raw, l_, total = synth_corpus(chunk, g["seed"], first=c0, mean=g["mean"],
                                            sigma=g["sigma"], log2_space=g["log2_space"])
         if eng is None:
-            eng = CorpusEngine(chunk, int(total * 1.01), 65535, lo, span, n_global=n)
+            eng = CorpusEngine(chunk, int(total * 1.01), 16384, lo, span, n_global=n,
+                               universe=synth_universe(g["log2_space"], g["seed"]))
         eng.canonicalize(off, raw, chunk)
         lens[c0:c0 + chunk].copy_(eng.new_len[:chunk])
         del off, raw
@@ -102,13 +108,17 @@ def test_c3_order_chunked(torch):
     assert sha(eng.order[:n]) == g["order_sha256"]
 
 
-def test_world8_rehearsal_c2(torch):
+@pytest.mark.parametrize("keys", ["keys", "window"])
+def test_world8_rehearsal_c2(torch, keys):
     """Eight ranks of the sharded engine on one GPU (gloo collectives) over C2,
-    checked against the ORACLE's digests (not against the single-GPU engine)."""
+    checked against the ORACLE's digests (not against the single-GPU engine).
+    Key mode exchanges the first-cover array (MIN) and kept flags (MAX);
+    window mode the covered bitmaps, first ranks over the merged dictionary
+    and kept flags."""
     import subprocess
     import sys
-    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "8", "C2"],
-                       capture_output=True, text=True, timeout=280)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "8", "C2",
+                        keys], capture_output=True, text=True, timeout=280)
     assert r.returncode == 0 and r.stdout.count("OK") == 8, r.stdout[-3000:] + r.stderr[-3000:]
 
 

@@ -1,0 +1,76 @@
+"""Key mode (keys.hip): the engine over dense keys (pc >> kshift) - kbase of
+a registered PC universe, against the CPU oracle, which works on PCs."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available()
+    return t
+
+
+def test_keymap_roundtrip(torch):
+    from syzkaller_amd.engine import synth_universe, universe_keymap, _p, _stream
+    from syzkaller_amd import _lib
+    u = synth_universe(16, 0x5EED0002)
+    uh = u.cpu().numpy().view(np.uint32)
+    assert np.array_equal(uh, [orc.lib().orc_synth_universe(0x5EED0002, k) for k in range(1 << 16)])
+    ks, kbase, nkeys, pok = universe_keymap(u, "cuda")
+    assert ks == 4 and nkeys == 1 << 16
+    keys = torch.from_numpy(((uh >> ks) - kbase).astype(np.int32)).cuda()
+    out = torch.empty_like(keys)
+    L = _lib.lib()
+    _lib.check(L.syzcov_dev_keys_to_pcs(_p(pok), nkeys, _p(keys), _p(out), None, keys.numel(),
+                                        _stream()), "keys_to_pcs")
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), uh)
+    with pytest.raises(ValueError):  # unsorted universe
+        universe_keymap(np.array([5, 3], np.uint32), "cuda")
+
+
+@pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
+                                               (500, 9000, 6000, 20), (2000, 600, 300, 17)])
+def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2):
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    seed = 0x5EED0002
+    off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span,
+                       universe=synth_universe(log2, seed))
+    assert eng.key_mode and eng.span == 1 << log2 and eng.kshift == 4
+    res = eng.step(off, raw, n)
+    o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    new_len = eng.new_len[:n].cpu().numpy()
+    assert np.array_equal(new_len, np.diff(c_off).astype(np.int32))
+    canon = eng.canonical_pcs(off, n).cpu().numpy().view(np.uint32)
+    offs = off.cpu().numpy()
+    for i in range(0, n, max(1, n // 40)):
+        assert np.array_equal(canon[offs[i]:offs[i] + new_len[i]], c_pcs[c_off[i]:c_off[i + 1]])
+    exp_kept = orc.minimize_csr(c_off, c_pcs)
+    assert res.kept_idx.cpu().numpy().tolist() == list(exp_kept)
+    exp_union = orc.union_fold_csr(c_off, c_pcs)
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
+    assert res.max_cover == exp_union.size
+    res2 = eng.step(off, raw, n)
+    assert res2.kept_idx.cpu().numpy().tolist() == list(exp_kept)
+    assert np.array_equal(res2.union.cpu().numpy().view(np.uint32), exp_union)
+
+
+def test_engine_key_mode_window_error(torch):
+    """A PC below the universe's first key is out of the key range: the
+    step raises instead of returning a wrong result."""
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2 = 300, 14
+    off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=200, sigma=50, log2_space=log2)
+    raw[5] = 0x10  # far below the universe
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span,
+                       universe=synth_universe(log2, 0x5EED0002))
+    with pytest.raises(RuntimeError):
+        eng.step(off, raw, n)
