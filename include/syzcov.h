@@ -325,13 +325,16 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
                            uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
                            void *stream);
 /* Key mode (keys.hip): key(pc) = (pc >> kshift) - kbase over a registered PC
- * universe (allCoverPCs) with kshift = the largest collision-free shift:
- * Canonicalize writes sorted unique KEYS (nkeys = key range; the contract is
- * that every PC belongs to the universe, which KCOV guarantees for the
- * kernel the universe was taken from).  Otherwise as syzcov_dev_canon_split. */
+ * universe (allCoverPCs) with kshift = the largest collision-free shift.
+ * The sort runs on window offsets of [pc_lo, pc_lo + pc_span) as in
+ * syzcov_dev_canon_split; every canonical PC is written as its KEY, and
+ * split[] / range_tot[] count ranges of 2^range_shift keys.  The window must
+ * map into [0, nkeys).  Contract: every PC belongs to the universe (KCOV only
+ * reports call sites of the kernel the universe was taken from); distinct
+ * non-universe PCs may share a key. */
 int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
-                                uint32_t *new_len, size_t nseg, size_t max_seg_len,
-                                uint32_t kshift, uint32_t kbase, uint64_t nkeys,
+                                uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
+                                uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
                                 uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
                                 uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
 /* pc_of_key[key(univ[i])] = univ[i] (univ sorted, collision-free under

@@ -83,8 +83,8 @@ _SIGS = {
     "syzcov_dev_canon_split_ws_size": (sz, [sz]),
     "syzcov_dev_canon_split": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, p_, p_, p_, p_, sz,
                                          p_]),
-    "syzcov_dev_canon_split_keys": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u32, u64, u32, p_,
-                                              p_, p_, p_, sz, p_]),
+    "syzcov_dev_canon_split_keys": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, u32, u64,
+                                              u32, p_, p_, p_, p_, sz, p_]),
     "syzcov_dev_universe_keymap": (C.c_int, [p_, sz, u32, u32, u64, p_, p_, p_]),
     "syzcov_dev_keys_to_pcs": (C.c_int, [p_, u64, p_, p_, p_, sz, p_]),
     "syzcov_dev_first_to_bits": (C.c_int, [p_, u64, p_, p_]),

@@ -1,15 +1,13 @@
 // canon_wave.hip — corpus-scale cover.Canonicalize (cover/cover.go:27-40):
 // one WAVEFRONT per segment, no workgroup barriers.
 //
-// A segment of n <= 8189 raw PCs is sorted by an LSD radix sort over its keys
-// entirely in the wave's private LDS slice.  Key = (pc >> kshift) - kbase:
-// kshift = 0, kbase = pc_lo gives window offsets (exact for any PC in the
-// window); with a registered PC universe (engine key mode) kshift is the
-// largest shift that keeps the universe collision-free, which maps it onto a
-// dense key space (the synthetic universe: 2^22 keys instead of 2^26 window
-// offsets).  nbits = bit_length(nkeys - 1); digits of <= 9 bits (512-entry
-// histogram), or 11 bits (2048 entries) when that saves a pass (19..22-bit
-// keys: 2 passes instead of 3):
+// A segment of n <= 8189 raw PCs is sorted by an LSD radix sort over its
+// window offsets (pc - pc_lo, nbits = bit_length(span - 1), <= 9-bit digits)
+// entirely in the wave's private LDS slice.  Key mode (a registered PC
+// universe, keys.hip) writes each canonical PC as its dense key
+// (pc >> kshift) - kbase: the map is monotone and injective on the universe,
+// so the sorted unique PCs give the sorted unique keys, and the split points
+// are taken over key ranges.  The sort itself stays on window offsets:
 //   load     16-byte vector loads of the raw list (head/tail masked);
 //   pass 0   lowest digit, unstable: count (ds_add), exclusive scan of the
 //            512-entry histogram, scatter with ds_add_rtn positions;
@@ -169,8 +167,9 @@ struct Params {
     uint32_t pc_lo;
     uint64_t span;
     uint32_t nbits;
-    uint32_t kshift, kbase;   // key = (pc >> kshift) - kbase; span = number of keys
-    int key_out;              // write keys (key mode) instead of PCs (kshift == 0)
+    uint32_t kshift, kbase;   // output key = (pc >> kshift) - kbase (key mode)
+    uint64_t nkeys;
+    int key_out;              // write keys (key mode) instead of PCs
     uint32_t sent_key;        // key of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
     uint32_t *split;          // nullable: [nseg][nrange]
     uint32_t nrange, rshift;
@@ -235,6 +234,16 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
         }
         __syncthreads();
     }
+}
+
+// Window offset below which a canonical PC falls in range j of the split
+// (ranges of 2^rshift KEYS in key mode, of window offsets otherwise).
+__device__ __forceinline__ uint32_t split_bound(const Params &P, uint32_t j) {
+    if (!P.key_out) return (j + 1) << P.rshift;
+    const uint64_t pc = ((uint64_t)P.kbase + ((uint64_t)(j + 1) << P.rshift)) << P.kshift;
+    if (pc <= P.pc_lo) return 0;
+    const uint64_t o = pc - P.pc_lo;
+    return o > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)o;
 }
 
 // NK = keys per lane (CAP = 64 * NK, NK a multiple of 4); MINW = waves per
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t idx = e4 + c;
-                    const uint32_t key = (vv[c] >> P.kshift) - P.kbase;
+                    const uint32_t key = vv[c] - P.pc_lo;  // window offset: the sort key
                     const bool valid = idx >= head && idx < end;
                     oob |= valid && key > span_m1;
                     k[q * 4 + c] = valid ? key : PAD;
@@ -403,7 +412,10 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        outp[pos] = P.key_out ? v : v + P.kbase;
+                        // key mode: the dense key of the PC; the key map is
+                        // monotone, so sorted unique PCs give sorted unique keys
+                        outp[pos] = P.key_out ? ((v + P.pc_lo) >> P.kshift) - P.kbase
+                                              : v + P.pc_lo;
                         buf[pos] = v;
                     }
                     cnt += (uint32_t)__popcll(m);
@@ -427,7 +439,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                 if (q * 64 < (int)P.nrange) {
                     uint32_t s = cnt;
                     if (j + 1 < P.nrange) {
-                        const uint32_t b = (j + 1) << P.rshift;
+                        const uint32_t b = split_bound(P, j);
                         uint32_t lo = 0, hi = cnt;  // lower_bound(b) in buf[0, cnt)
                         while (lo < hi) {
                             const uint32_t mid = (lo + hi) >> 1;
@@ -475,7 +487,7 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
                 uint32_t lo = 0, hi = cnt;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (c[mid] - (P.key_out ? 0u : P.kbase) < b) lo = mid + 1; else hi = mid;
+                    if (c[mid] - (P.key_out ? 0u : P.pc_lo) < b) lo = mid + 1; else hi = mid;
                 }
                 s = lo;
             }
@@ -505,9 +517,9 @@ __global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_
         const uint32_t cnt = P.new_len[seg];
         bool bad = false;
         for (uint32_t i = __lane_id(); i < cnt; i += 64) {
-            const uint32_t key = (c[i] >> P.kshift) - P.kbase;
-            bad |= key > (uint32_t)(P.span - 1);
-            if (P.key_out) c[i] = key;
+            const uint32_t pc = c[i];
+            bad |= pc - P.pc_lo > (uint32_t)(P.span - 1);
+            if (P.key_out) c[i] = (pc >> P.kshift) - P.kbase;
         }
         if (__ballot(bad)) {  // flagged; the segment is dropped (memory-safe downstream)
             if (__lane_id() == 0) {
@@ -567,16 +579,21 @@ static void launch_class(bool hb11, const cw::Params &P, const uint32_t *lc, con
 }
 
 static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *out,
-                            uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t kshift,
-                            uint32_t kbase, uint64_t nkeys, int key_out, uint32_t range_shift,
-                            uint32_t *split, uint64_t *range_tot, uint32_t *err_flag, void *ws,
-                            size_t ws_size, void *stream) {
+                            uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
+                            uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
+                            int key_out, uint32_t range_shift, uint32_t *split,
+                            uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
+                            void *stream) {
     if (nseg == 0) return 0;
     if (!off || !raw || !out || !new_len || !err_flag || !ws) return SYZCOV_EINVAL;
-    if (nkeys == 0 || nkeys > (1ull << 32) || kshift > 31 ||
-        (uint64_t)kbase + nkeys > (1ull << (32 - kshift)))
+    if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
         return SYZCOV_ERANGE;
-    if (kshift && !key_out) return SYZCOV_EINVAL;  // PCs are not recoverable from shifted keys
+    if (key_out) {  // every window PC must map into [0, nkeys)
+        const uint64_t k0 = pc_lo >> kshift, k1 = (pc_lo + pc_span - 1) >> kshift;
+        if (kshift > 31 || nkeys == 0 || k0 < kbase || k1 - kbase >= nkeys) return SYZCOV_ERANGE;
+    } else {
+        nkeys = pc_span;
+    }
     if (ws_size < syzcov_dev_canon_split_ws_size(nseg) || nseg > 0xFFFFFFFFull)
         return SYZCOV_EINVAL;
     if (out == raw && max_seg_len > 16384) return SYZCOV_EINVAL;  // large path is out of place
@@ -595,14 +612,15 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.out = out;
     P.new_len = new_len;
     P.nseg = nseg;
-    P.pc_lo = kshift ? 0u : kbase;
-    P.span = nkeys;
+    P.pc_lo = pc_lo;
+    P.span = pc_span;
     P.kshift = kshift;
     P.kbase = kbase;
+    P.nkeys = nkeys;
     P.key_out = key_out;
-    P.nbits = nkeys <= 1 ? 1 : 64 - __builtin_clzll(nkeys - 1);
-    const uint64_t so = (uint64_t)(uint32_t)((0xFFFFFFFFu >> kshift) - kbase);
-    P.sent_key = so < nkeys ? (uint32_t)so : 0xFFFFFFFFu;
+    P.nbits = pc_span <= 1 ? 1 : 64 - __builtin_clzll(pc_span - 1);
+    const uint64_t so = (uint64_t)(uint32_t)(0xFFFFFFFFu - pc_lo);
+    P.sent_key = so < pc_span ? (uint32_t)so : 0xFFFFFFFFu;
     P.split = split;
     P.nrange = (uint32_t)nrange;
     P.rshift = range_shift;
@@ -612,7 +630,12 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.big_list = big;
     P.big_cnt = cnts + 1;
     P.err = err_flag;
-    const bool hb11 = P.nbits >= 19 && P.nbits <= 22;
+    // 2 passes of 11-bit digits (2048-entry histograms) for 19..22-bit keys
+    // measured slower than 3 passes of <= 9 bits (C2 key mode 9.45 vs 7.9 ms:
+    // 8 KB histograms halve the resident waves), so it is a tuning option only
+    bool hb11 = false;
+    if (const char *e = getenv("SYZCOV_CANON_HB"))
+        hb11 = atoi(e) == 11 && P.nbits >= 19 && P.nbits <= 22;
     // bin by capacity class (wave-aggregated atomics), one launch per class
     // (a register bitonic network measured 20.3 ms at C2 against the LDS
     // radix's 7.8: 147 VALU ops per key)
@@ -665,10 +688,9 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
             SYZ_HIP(hipMemcpyAsync(&nbig, cnts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             SYZ_HIP(hipStreamSynchronize(s));
             if (nbig) {
-                // window check of the PC path: the keys are checked by keyify
-                rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr,
-                                      key_out ? 0u : kbase, key_out ? (1ull << 32) : nkeys,
-                                      err_flag, s);
+                // the window is checked by keyify_list_kernel
+                rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr, pc_lo,
+                                      pc_span, err_flag, s);
                 if (rc) return rc;
             }
         }
@@ -683,18 +705,19 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
                                       uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
                                       uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
                                       void *ws, size_t ws_size, void *stream) {
-    if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
-        return nseg ? SYZCOV_ERANGE : 0;
-    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, 0, pc_lo, pc_span, 0,
-                            range_shift, split, range_tot, err_flag, ws, ws_size, stream);
+    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, 0, pc_lo,
+                            pc_span, 0, range_shift, split, range_tot, err_flag, ws, ws_size,
+                            stream);
 }
 
 extern "C" int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                                            uint32_t *new_len, size_t nseg, size_t max_seg_len,
-                                           uint32_t kshift, uint32_t kbase, uint64_t nkeys,
-                                           uint32_t range_shift, uint32_t *split,
-                                           uint64_t *range_tot, uint32_t *err_flag, void *ws,
-                                           size_t ws_size, void *stream) {
-    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, kshift, kbase, nkeys, 1,
-                            range_shift, split, range_tot, err_flag, ws, ws_size, stream);
+                                           uint32_t pc_lo, uint64_t pc_span, uint32_t kshift,
+                                           uint32_t kbase, uint64_t nkeys, uint32_t range_shift,
+                                           uint32_t *split, uint64_t *range_tot,
+                                           uint32_t *err_flag, void *ws, size_t ws_size,
+                                           void *stream) {
+    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, kshift,
+                            kbase, nkeys, 1, range_shift, split, range_tot, err_flag, ws, ws_size,
+                            stream);
 }

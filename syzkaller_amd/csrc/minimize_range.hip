@@ -42,6 +42,12 @@
 #include <cstdio>
 #include <cstdlib>
 
+#define RC_(expr)                 \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ < 0) return r_;    \
+    } while (0)
+
 namespace syz {
 namespace mr {
 
@@ -116,6 +122,29 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
         }
         __syncthreads();
     }
+}
+
+// Drop from `um` every uncovered occurrence whose PC already has a first
+// cover below rank rk: first(pc) <= first_w[pc] < rk, so the record could
+// never make rk kept and the atomicMin cannot lower first_w.  first_w only
+// decreases, so a stale read prunes less, never wrongly.  This takes the
+// same-address atomics of hot PCs out of the early chunks, where nearly every
+// PC is uncovered and the chunk's items share them.
+template <int NU>
+__device__ __forceinline__ uint32_t prune_ranked(uint32_t um, const uint4 (&v)[NU], int32_t rk,
+                                                 const Args &A) {
+    int32_t f[NU * 4];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            f[u * 4 + k] = ((um >> (u * 4 + k)) & 1u) ? A.first_w[vv[k] - A.pc_lo] : INT32_MAX;
+    }
+#pragma unroll
+    for (int q = 0; q < NU * 4; q++)
+        if (f[q] < rk) um &= ~(1u << q);
+    return um;
 }
 
 // Workgroup -> (range, item slice [i0, i1)).  The chunk's items are cut into
@@ -261,6 +290,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
                     }
                 }
+                if (__ballot(um != 0)) um = prune_ranked<UG>(um, v, rki, A);
                 if (__ballot(um != 0)) {
                     // reserve this lane's records, then write them
                     const uint32_t cnt = (uint32_t)__popc(um);
@@ -329,6 +359,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
                     }
                 }
+                if (__ballot(um != 0)) um = prune_ranked<UB>(um, v, rki, A);
                 if (__ballot(um != 0)) {
                     const uint32_t cnt = (uint32_t)__popc(um);
                     const uint32_t incl = wave_incl_scan(cnt);
@@ -578,13 +609,16 @@ extern "C" int syzcov_dev_minimize_range(
     // pmode 0 = slice-major (P = 2R; default: 4.47 vs 4.60 ms at C2 with the
     // 4-lane-group kernel), 1 = range-major (one slice; it was faster with the
     // lane-per-item kernel, 7.1 vs 8.0 ms), k >= 3 = P = kR (4.6 ms)
-    int variant = 0, pmode = 0;
+    // few long sub-runs per item (dense keys: 4 ranges at C2) take the whole
+    // wave above 512 PCs (variant 14: minimize 3.07 vs 3.57 ms, C2 key mode);
+    // many short ones (64 window ranges) the 4-lane groups throughout
+    int variant = nrange <= 16 ? 14 : 0, pmode = 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
     // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
     // minimize ms: (4,4) 4.6, (2,8) 4.9, (4,8) 5.0, (4,2) 5.05, (2,4) 5.05,
     // (8,2) 5.7, (8,4) 5.9, (16,2) 8.4, one lane per item (old) 7.0
-    constexpr int NVAR = 12;
+    constexpr int NVAR = 15;
     const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>, mr::pass1_kernel<0, true>,
                           mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
                           mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
@@ -592,7 +626,11 @@ extern "C" int syzcov_dev_minimize_range(
                           mr::pass1_kernel<0x40000000, true, false, 2, 8>,
                           mr::pass1_kernel<0x40000000, true, false, 4, 2>,
                           mr::pass1_kernel<0x40000000, true, false, 4, 8>,
-                          mr::pass1_kernel<0x40000000, true, false, 2, 4>};
+                          mr::pass1_kernel<0x40000000, true, false, 2, 4>,
+                          // 12..14: lane groups up to 256 / 128 / 512 PCs, whole wave above
+                          mr::pass1_kernel<256, true, false, 4, 4>,
+                          mr::pass1_kernel<128, true, false, 4, 4>,
+                          mr::pass1_kernel<512, true, false, 4, 4>};
     const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
     static std::atomic<uint32_t> attr_set[NVAR];
@@ -611,6 +649,9 @@ extern "C" int syzcov_dev_minimize_range(
     if (const char *e = getenv("SYZCOV_MR_GMIN")) g_min = strtoull(e, nullptr, 0);  // tuning
     if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;  // sweep: 2^17 4.03, 2^19 4.00, 2^20 4.40 ms
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
+    // below 2^24 PCs (64 MB of first_w) the covered set is rebuilt from first_w
+    bool cover_from_first = pc_span <= (1ull << 24);
+    if (const char *e = getenv("SYZCOV_MR_COVER")) cover_from_first = atoi(e) == 1;  // tuning
     uint64_t a = 0, step = first_chunk;
     int par = 0;  // done-mark set of this chunk
     while (a < n_items) {
@@ -625,12 +666,20 @@ extern "C" int syzcov_dev_minimize_range(
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
-        hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A, par);
+        if (cover_from_first) {
+            // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
+            // first_w (16 MB at 2^22 keys) instead of an atomicOr per record
+            // (C2 key mode: 5 vs 74-274 us per early chunk)
+            if (b < n_items) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
+        } else {
+            hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A, par);
+        }
         par ^= 1;
         a = b;
         step *= growth;
     }
     hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
+    if (cover_from_first) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
     // record overflow: the union comes from first_w instead
     hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
                        (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,

@@ -74,8 +74,11 @@ class CorpusEngine:
         # on dense keys (pc >> kshift) - kbase instead of window offsets
         self.key_mode = universe is not None
         self.kshift, self.kbase = 0, pc_lo
+        self.win_lo, self.win_span = pc_lo, pc_span  # Canonicalize's sort window
         if self.key_mode:
-            self.kshift, self.kbase, nkeys, self.pc_of_key = universe_keymap(universe, dev)
+            self.kshift, self.kbase, nkeys, self.pc_of_key, ulo, uhi = universe_keymap(universe,
+                                                                                      dev)
+            self.win_lo, self.win_span = ulo, uhi - ulo + 1  # the universe's extent
             pc_lo, pc_span = 0, nkeys  # minimize / union / maxCover window = the key range
         self.pc_lo, self.span = pc_lo, pc_span
         so = (0xFFFFFFFF >> self.kshift) - self.kbase  # key of the 0xFFFFFFFF sentinel
@@ -140,9 +143,10 @@ class CorpusEngine:
             self.canon = raw
         if self.key_mode:
             check(self.L.syzcov_dev_canon_split_keys(
-                _p(off), _p(raw), _p(self.canon), _p(self.new_len), n, self.max_seg, self.kshift,
-                self.kbase, self.span, self.rshift, _p(self.split), _p(self.range_tot),
-                _p(self.scal), _p(self.ws), self.ws_size, _stream()), "dev_canon_split_keys")
+                _p(off), _p(raw), _p(self.canon), _p(self.new_len), n, self.max_seg, self.win_lo,
+                self.win_span, self.kshift, self.kbase, self.span, self.rshift, _p(self.split),
+                _p(self.range_tot), _p(self.scal), _p(self.ws), self.ws_size, _stream()),
+                "dev_canon_split_keys")
             return
         check(self.L.syzcov_dev_canon_split(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
                                             self.max_seg, self.pc_lo, self.span, self.rshift,
@@ -361,7 +365,7 @@ def universe_shift(u: np.ndarray) -> int:
 
 
 def universe_keymap(universe, dev):
-    """(kshift, kbase, nkeys, pc_of_key) of a registered PC universe
+    """(kshift, kbase, nkeys, pc_of_key, lowest PC, highest PC) of a registered PC universe
     (sorted unique uint32 PCs: allCoverPCs, syz-manager/cover.go:57-69)."""
     if isinstance(universe, torch.Tensor):
         uh = universe.cpu().numpy().view(np.uint32)
@@ -379,7 +383,7 @@ def universe_keymap(universe, dev):
                                        _stream()), "dev_universe_keymap")
     if int(err.item()):
         raise ValueError("universe keymap failed (unsorted or colliding universe)")
-    return ks, kbase, nkeys, pc_of_key
+    return ks, kbase, nkeys, pc_of_key, int(uh[0]), int(uh[-1])
 
 
 def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda") -> torch.Tensor:

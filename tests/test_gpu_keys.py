@@ -21,7 +21,8 @@ def test_keymap_roundtrip(torch):
     u = synth_universe(16, 0x5EED0002)
     uh = u.cpu().numpy().view(np.uint32)
     assert np.array_equal(uh, [orc.lib().orc_synth_universe(0x5EED0002, k) for k in range(1 << 16)])
-    ks, kbase, nkeys, pok = universe_keymap(u, "cuda")
+    ks, kbase, nkeys, pok, ulo, uhi = universe_keymap(u, "cuda")
+    assert (ulo, uhi) == (int(uh[0]), int(uh[-1]))
     assert ks == 4 and nkeys == 1 << 16
     keys = torch.from_numpy(((uh >> ks) - kbase).astype(np.int32)).cuda()
     out = torch.empty_like(keys)
