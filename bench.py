@@ -54,9 +54,6 @@ def parse():
     ap.add_argument("--workload", choices=["corpus", "prio", "newcov"], default="corpus")
     ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
     ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
-    ap.add_argument("--universe", action="store_true",
-                    help="newcov: maxCover over dense ids of the synthetic PC universe "
-                         "(16x less memory; measured slower: two probed lines per PC)")
     ap.add_argument("--history", type=int, default=32,
                     help="newcov: batches streamed through the check before the bench")
     ap.add_argument("--inputs", type=int, default=1_000_000,
@@ -71,9 +68,11 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=10_000,
                     help="inputs of config C1 timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prio-dense", action="store_true",
+                    help="prio: contract over all C keys instead of the active positional keys")
     ap.add_argument("--no-universe", action="store_true",
-                    help="corpus: window-offset keys instead of the dense keys of the registered "
-                         "PC universe (keys.hip)")
+                    help="window offsets instead of the dense keys of the registered PC "
+                         "universe (keys.hip), for the corpus engine and newcov's maxCover")
     return ap.parse_args()
 
 
@@ -298,7 +297,9 @@ def bench_prio(args):
     from syzkaller_amd.engine import PrioEngine
     L = _lib.lib()
     nprog = args.inputs
-    eng = PrioEngine(nprog, device=dev)
+    # default: positional counts over the active keys (reference-exact, prio.go:142-150);
+    # --prio-dense: the full 1170-key contraction (the dense MFMA GEMM)
+    eng = PrioEngine(nprog, device=dev, active_rows=not args.prio_dense)
     lens = torch.empty(nprog, dtype=torch.int32, device=dev)
     _lib.check(L.syzcov_dev_synth_lens(SEED_PRIO, rank * nprog, nprog, 30, 8,
                                        C.c_void_p(lens.data_ptr()),
@@ -320,8 +321,11 @@ def bench_prio(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "i8",
         "data": "synthetic program lengths ~ N(30, 8) (SURVEY §8d C4)",
-        "config": {"workload": "C4: CalculatePriorities, positional (reference-exact) keys",
-                   "programs_per_gpu": nprog, "calls": eng.C, "at_rows": eng.rows,
+        "config": {"workload": "C4: CalculatePriorities, positional (reference-exact) keys"
+                               + (", all C keys contracted" if args.prio_dense
+                                  else f", active keys 0..{eng.max_len - 1}"),
+                   "programs_per_gpu": nprog, "calls": eng.C,
+                   "at_rows": eng.rows if args.prio_dense else -(-eng.max_len // 128) * 128,
                    "at_cols": eng.ldp,
                    "parallelism": f"shard-by-program x{world}"
                                   + (", int32 SUM all-reduce of counts" if world > 1 else "")},
@@ -408,7 +412,7 @@ def bench_newcov(args):
 
     import numpy as np
     st = CoverState(args.ncalls, lo, span)
-    if args.universe:  # SURVEY §8d C5 variant: per-call bitmaps over the 2^22 PC ids
+    if not args.no_universe:  # per-call bitmaps over the 2^22 dense keys
         univ = torch.empty(1 << args.log2_space, dtype=torch.int32, device=dev)
         _lib.check(L.syzcov_dev_synth_universe(SEED_NEWCOV, args.log2_space, P(univ), s()),
                    "synth_universe")
@@ -468,10 +472,10 @@ def bench_newcov(args):
                    "records_per_batch": nrec, "calls": args.ncalls,
                    "pcs_per_batch": timed_pcs // args.steps, "pc_space": 1 << args.log2_space,
                    "flakes": f"unique PCs of one synthetic {1 << (args.log2_space - 7)}-PC draw",
-                   "maxcover": ("dense ids over the synthetic 2^%d-PC universe"
-                                % args.log2_space if args.universe
+                   "maxcover": ("bitmaps over the dense keys of the synthetic 2^%d-PC "
+                                "universe" % args.log2_space if not args.no_universe
                                 else "window bitmaps (1 bit per PC offset)"),
-                   "maxcover_bytes": args.ncalls * ((1 << args.log2_space) if args.universe
+                   "maxcover_bytes": args.ncalls * ((1 << args.log2_space) if not args.no_universe
                                                     else span) // 8,
                    "history_batches": args.history, "history_new_records": hist_new},
         "phases_ms": {"newcov": round(phl[0], 4)},

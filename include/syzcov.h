@@ -442,6 +442,15 @@ int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens, const uint64_t *
                              size_t ldp, uint32_t *err_flag, void *stream);
 int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog, int C, int32_t *counts,
                            void *stream);
+/* Positional counts (key_mode 0) over the ACTIVE keys only: A[p][k] is zero
+ * for k >= max_len, so AT is built for the first roundup(max_len, 128) keys,
+ * the MFMA tiles are K-split with partial tiles + a reduction, and the
+ * colsum column counts[i][C] comes from a length histogram.  counts
+ * (prio_rows(C)^2 int32) must be zeroed by the caller; max_len = max(lens)
+ * (<= C).  ws: syzcov_dev_prio_pos_ws_size(nprog, C, max_len). */
+size_t syzcov_dev_prio_pos_ws_size(size_t nprog, int C, int max_len);
+int syzcov_dev_prio_counts_pos(const int32_t *lens, size_t nprog, int C, int max_len,
+                               int32_t *counts, void *ws, size_t ws_size, void *stream);
 /* counts -> D = AᵀA - diag(colsum) -> float32 exactly as Go's repeated
  * `+= 1.0` would hold it (min(n, 2^24)) -> normalizePrio -> * static
  * (nullable).  raw_out (nullable, C*C uint32) receives D. */

@@ -760,6 +760,33 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
     Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;
     const size_t rows = syzcov_dev_prio_rows(C), ldp = syzcov_dev_prio_ldp(nprog ? nprog : 1);
+    int max_len = 0;
+    for (size_t q = 0; q < nprog; q++) max_len = std::max(max_len, lens[q]);
+    if (key_mode == 0) {  // positional: the active keys only (prio.hip)
+        Plan p;
+        size_t i_len = p.add(lens.size() * 4), i_cnt = p.add(rows * rows * 4),
+               i_st = p.add((size_t)C * C * 4), i_out = p.add((size_t)C * C * 4),
+               i_raw = p.add(raw_counts ? (size_t)C * C * 4 : 0),
+               i_ws = p.add(syzcov_dev_prio_pos_ws_size(nprog ? nprog : 1, C, max_len));
+        std::vector<uint8_t *> b;
+        RC(reserve(c, p, b));
+        CK(hipMemcpyAsync(b[i_len], lens.data(), lens.size() * 4, hipMemcpyHostToDevice, c->s));
+        if (static_prios)
+            CK(hipMemcpyAsync(b[i_st], static_prios, (size_t)C * C * 4, hipMemcpyHostToDevice,
+                              c->s));
+        CK(hipMemsetAsync(b[i_cnt], 0, rows * rows * 4, c->s));
+        RC(syzcov_dev_prio_counts_pos((int32_t *)b[i_len], nprog, C, max_len, (int32_t *)b[i_cnt],
+                                      b[i_ws], p.sizes[i_ws], c->s));
+        RC(syzcov_dev_prio_finish((int32_t *)b[i_cnt], C,
+                                  static_prios ? (float *)b[i_st] : nullptr, (float *)b[i_out],
+                                  raw_counts ? (uint32_t *)b[i_raw] : nullptr, c->s));
+        CK(hipMemcpyAsync(out, b[i_out], (size_t)C * C * 4, hipMemcpyDeviceToHost, c->s));
+        if (raw_counts)
+            CK(hipMemcpyAsync(raw_counts, b[i_raw], (size_t)C * C * 4, hipMemcpyDeviceToHost,
+                              c->s));
+        CK(hipStreamSynchronize(c->s));
+        return 0;
+    }
     Plan p;
     size_t i_len = p.add(lens.size() * 4), i_off = p.add((nprog + 1) * 8),
            i_ids = p.add(key_mode ? ncalls * 2 : 0), i_at = p.add(rows * ldp),

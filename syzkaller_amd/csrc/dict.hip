@@ -428,8 +428,10 @@ extern "C" int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, u
 namespace syz {
 // Sorted PC list of a bitmap over [pc_lo, pc_lo + pc_span) (sentinel
 // dropped, as a Union result would).  out == NULL: count only.
+// pc_of_key (nullable): the bitmap is over dense keys (keys.hip); the list is
+// mapped back to PCs (monotone, so it stays sorted).
 int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
-                   size_t cap, int64_t *count, hipStream_t s) {
+                   size_t cap, int64_t *count, hipStream_t s, const uint32_t *pc_of_key) {
     const uint64_t nwords = (pc_span + 31) / 32;
     const uint64_t nblk = (nwords + DICT_WPB - 1) / DICT_WPB;
     void *buf = nullptr;
@@ -474,6 +476,9 @@ int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_
                 rc = SYZCOV_EINVAL;
                 break;
             }
+            if (pc_of_key && hn &&
+                (rc = syzcov_dev_keys_to_pcs(pc_of_key, pc_span, dout, dout, nullptr, hn, s)))
+                break;
             if (hn && (hipMemcpyAsync(out, dout, (size_t)hn * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                        hipStreamSynchronize(s) != hipSuccess)) {
                 rc = SYZCOV_EHIP;

@@ -14,6 +14,13 @@
 // into its own slots (few once maxCover saturates); a hash table keyed by
 // (CallID, pc) takes an atomicMin of the record index; pass 2 marks a record
 // new iff it owns one of its keys and ORs the owned keys into maxCover.
+//
+// The bitmaps are indexed by window offset (pc - pc_lo), or, once the PC
+// universe is registered (syzcov_state_set_universe), by the dense key
+// (pc >> kshift) - kbase of keys.hip: one probe per PC into a per-call bitmap
+// of nkeys bits (512 KB at the synthetic 2^22-PC universe instead of 8 MB of
+// window bits), so a call's bitmap stays in its XCD's L2 while that XCD
+// walks the call's records.
 #include "common.h"
 
 namespace syz {
@@ -22,27 +29,23 @@ __device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64
     return (bm[o >> 5] >> (o & 31)) & 1u;
 }
 
-// Universe mode (syzcov_state_set_universe): PCs of a known universe (the
-// reference's allCoverPCs, syz-manager/cover.go:57-69: every
-// __sanitizer_cov_trace_pc call site) are tested against per-call bitmaps
-// over DENSE universe ids (utab: the {prefix:32 | bits:32} dictionary per
-// 32-offset window word), 16x smaller than window bitmaps at C5 and
-// L2-resident per call; other PCs keep the window bitmaps.  Returns the word
-// to probe and sets *bit to the bit inside it.
-__device__ __forceinline__ const uint32_t *probe_word(const uint64_t *__restrict__ utab,
-                                                      const uint32_t *DM, const uint32_t *M,
-                                                      uint32_t o, uint32_t *bit) {
-    if (utab) {
-        const uint64_t e = utab[o >> 5];
-        const uint32_t ub = (uint32_t)(e >> 32);
-        if ((ub >> (o & 31)) & 1u) {
-            const uint32_t id = (uint32_t)e + (uint32_t)__popc(ub & ((1u << (o & 31)) - 1u));
-            *bit = id & 31;
-            return DM + (id >> 5);
-        }
+// Where a PC lives in the bitmaps: its window offset, or its dense key.
+struct Index {
+    int key_mode;
+    uint32_t pc_lo, kshift, kbase;
+    uint64_t span;  // window span, or nkeys
+};
+
+// Bitmap index of pc; false if pc is outside the window / key range.
+__device__ __forceinline__ bool pc_index(const Index &X, uint32_t pc, uint32_t *idx) {
+    if (X.key_mode) {
+        const uint32_t k = (pc >> X.kshift) - X.kbase;  // wraps past span below kbase
+        *idx = k;
+        return k < X.span;
     }
-    *bit = o & 31;
-    return M + (o >> 5);
+    const uint32_t o = pc - X.pc_lo;
+    *idx = o;
+    return pc >= X.pc_lo && (uint64_t)o < X.span;
 }
 
 constexpr int NC_THREADS = 256;
@@ -104,11 +107,9 @@ __global__ __launch_bounds__(1024) void newcov_group_kernel(const int32_t *__res
 __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
     const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
     const uint32_t *__restrict__ pcs, uint32_t nrec, const uint32_t *__restrict__ maxcov,
-    uint64_t words_per_call, const uint32_t *__restrict__ flakes, uint32_t pc_lo,
-    uint64_t pc_span, int ncalls, const uint64_t *__restrict__ utab,
-    const uint32_t *__restrict__ dmax, uint64_t dwords, const uint32_t *__restrict__ perm,
-    uint8_t *__restrict__ is_new, uint32_t *__restrict__ cpc, uint32_t *__restrict__ rec_cnt,
-    uint32_t *__restrict__ stats) {
+    uint64_t words_per_call, const uint32_t *__restrict__ flakes, Index X, int ncalls,
+    const uint32_t *__restrict__ perm, uint8_t *__restrict__ is_new, uint32_t *__restrict__ cpc,
+    uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ stats) {
     const uint32_t l = __lane_id();
     const uint64_t lt = (1ull << l) - 1ull;
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
@@ -130,12 +131,11 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
             continue;
         }
         const uint32_t *M = maxcov + (uint64_t)c * words_per_call;
-        const uint32_t *DM = dmax + (uint64_t)c * dwords;
         const uint64_t b = rec_off[k], n = rec_off[k + 1] - b;
         uint32_t bad = 0, cnt = 0, carry = 0;
         // NC_U rows per step: all their loads and maxCover probes in flight together
         for (uint64_t q0 = 0; q0 < n; q0 += 64 * NC_U) {
-            uint32_t pc[NC_U], w[NC_U], bt[NC_U];
+            uint32_t pc[NC_U], w[NC_U], ix[NC_U];
             bool ok[NC_U];
 #pragma unroll
             for (int u = 0; u < NC_U; u++) {
@@ -145,16 +145,13 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
 #pragma unroll
             for (int u = 0; u < NC_U; u++) {
                 const uint64_t q = q0 + u * 64 + l;
-                const uint64_t o = (uint64_t)(uint32_t)(pc[u] - pc_lo);
-                const bool inw = pc[u] >= pc_lo && o < pc_span;
+                const bool inw = pc_index(X, pc[u], &ix[u]);
                 // 0xFFFFFFFF is Difference's end sentinel: never part of a
                 // diff (cover.go:43-48,97), so never a candidate, never an error
                 const bool sent = pc[u] == 0xFFFFFFFFu;
                 ok[u] = q < n && inw && !sent;
                 bad |= (uint32_t)(q < n && !inw && !sent);
-                w[u] = 0xFFFFFFFFu;
-                bt[u] = 0;
-                if (ok[u]) w[u] = *probe_word(utab, DM, M, (uint32_t)o, &bt[u]);
+                w[u] = ok[u] ? M[ix[u] >> 5] : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int u = 0; u < NC_U; u++) {
@@ -165,9 +162,9 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 if (l == 0) prev = carry;
                 carry = __builtin_amdgcn_readlane(pc[u], 63);
                 if (q < n && q > 0 && prev > pc[u]) bad |= 2u;
-                const uint32_t o = pc[u] - pc_lo;
                 // maxCover first: once it saturates, flakes are rarely probed
-                const bool cand = ok[u] && !((w[u] >> bt[u]) & 1u) && !bit_test(flakes, o);
+                const bool cand =
+                    ok[u] && !((w[u] >> (ix[u] & 31)) & 1u) && !bit_test(flakes, ix[u]);
                 const uint64_t m = __ballot(cand);
                 if (cand) cpc[b + cnt + (uint32_t)__popcll(m & lt)] = pc[u];
                 cnt += (uint32_t)__popcll(m);
@@ -245,8 +242,7 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
     const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
     const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
-    uint32_t *__restrict__ maxcov, uint64_t words_per_call, uint32_t pc_lo,
-    const uint64_t *__restrict__ utab, uint32_t *__restrict__ dmax, uint64_t dwords) {
+    uint32_t *__restrict__ maxcov, uint64_t words_per_call, Index X) {
     if (stats[0] || !stats[1]) return;
     const uint64_t mask = hash_cap(stats[1]) - 1;
     const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
@@ -256,7 +252,6 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
         const uint32_t c = (uint32_t)callid[k];
         const uint64_t hi = (uint64_t)c << 32, b = rec_off[k];
         uint32_t *M = maxcov + (uint64_t)c * words_per_call;
-        uint32_t *DM = dmax + (uint64_t)c * dwords;
         bool own = false;
         for (uint32_t i = l; i < cnt; i += 64) {
             const uint32_t pc = cpc[b + i];
@@ -265,9 +260,9 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
             while (hkey[h] != key) h = (h + 1) & mask;
             if (hval[h] == k) {
                 own = true;
-                uint32_t bit;
-                uint32_t *wp = const_cast<uint32_t *>(probe_word(utab, DM, M, pc - pc_lo, &bit));
-                atomicOr(wp, 1u << bit);
+                uint32_t ix;
+                pc_index(X, pc, &ix);  // candidates are inside (checked by the cand pass)
+                atomicOr(&M[ix >> 5], 1u << (ix & 31));
             }
         }
         if (__ballot(own) && l == 0) is_new[k] = 1;
@@ -275,39 +270,30 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
 }
 
 __global__ void bits_set_kernel(const uint32_t *__restrict__ pcs, uint64_t n,
-                                uint32_t *__restrict__ bm, uint32_t pc_lo, uint64_t pc_span,
-                                uint32_t *__restrict__ err, const uint64_t *__restrict__ utab,
-                                uint32_t *__restrict__ dm) {
+                                uint32_t *__restrict__ bm, Index X, uint32_t *__restrict__ err) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t pc = pcs[i];
-        const uint64_t o = (uint64_t)(uint32_t)(pc - pc_lo);
         if (pc == 0xFFFFFFFFu) continue;  // Union drops the sentinel (cover.go:97)
-        if (pc < pc_lo || o >= pc_span) {
+        uint32_t ix;
+        if (!pc_index(X, pc, &ix)) {
             *err = 1u;
             continue;
         }
-        uint32_t bit;
-        uint32_t *wp = const_cast<uint32_t *>(probe_word(utab, dm, bm, (uint32_t)o, &bit));
-        atomicOr(wp, 1u << bit);
+        atomicOr(&bm[ix >> 5], 1u << (ix & 31));
     }
 }
 
-// window bitmap |= the dense bits of one call (universe mode), for reads
-__global__ void dense_to_window_kernel(const uint64_t *__restrict__ utab, uint64_t nwords,
-                                       const uint32_t *__restrict__ dm, uint32_t *__restrict__ bm) {
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
-         w += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = utab[w];
-        uint32_t ub = (uint32_t)(e >> 32), id = (uint32_t)e, out = 0;
-        while (ub) {
-            const uint32_t b = (uint32_t)__builtin_ctz(ub);
-            if ((dm[id >> 5] >> (id & 31)) & 1u) out |= 1u << b;
-            id++;
-            ub &= ub - 1;
-        }
-        if (out) bm[w] |= out;
-    }
+// kshift of a sorted unique universe: min over neighbours of the highest
+// differing bit (keys.hip); *out pre-set to 31.
+__global__ void universe_shift_kernel(const uint32_t *__restrict__ u, uint32_t n,
+                                      uint32_t *__restrict__ out) {
+    uint32_t m = 31;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n;
+         i += gridDim.x * blockDim.x)
+        m = min(m, 31u - (uint32_t)__clz(u[i] ^ u[i + 1]));
+    for (int d = 32; d >= 1; d >>= 1) m = min(m, (uint32_t)__shfl_xor(m, d, 64));
+    if (__lane_id() == 0) atomicMin(out, m);
 }
 
 }  // namespace syz
@@ -325,14 +311,14 @@ struct CoverState {
     int dev = 0;
     int ncalls = 0;
     uint32_t pc_lo = 0;
-    uint64_t pc_span = 0, words = 0;
+    uint64_t pc_span = 0;
+    // bitmap index space: window offsets, or dense keys of the registered
+    // universe (key mode); words = 32-bit words per bitmap
+    Index X{};
+    uint64_t words = 0;
     uint32_t *maxcov = nullptr;  // ncalls x words
     uint32_t *flakes = nullptr;  // words
-    // universe mode: dictionary over the window + per-call dense bitmaps
-    uint64_t *utab = nullptr;    // words entries
-    uint32_t *dmax = nullptr;    // ncalls x dwords
-    uint64_t dwords = 0;
-    uint32_t nuniv = 0;
+    uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
     bool dirty = false;          // maxCover touched: the universe can no longer change
     hipStream_t s = nullptr;
     std::mutex mu;  // the reference's coverMu
@@ -342,17 +328,35 @@ struct CoverState {
 };
 
 int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
-                   size_t cap, int64_t *count, hipStream_t s);
+                   size_t cap, int64_t *count, hipStream_t s, const uint32_t *pc_of_key);
 }  // namespace syz
 
 static int grow(CoverState *st, size_t need) {
     if (need <= st->scap) return 0;
-    if (st->scratch) hipFree(st->scratch);
+    if (st->scratch) {
+        hipStreamSynchronize(st->s);
+        hipFree(st->scratch);
+    }
     st->scratch = nullptr;
     st->scap = 0;
     size_t cap = need + need / 2;
     if (hipMalloc(&st->scratch, cap) != hipSuccess) return SYZCOV_ENOMEM;
     st->scap = cap;
+    return 0;
+}
+
+// (re)allocate the bitmaps for the current index space, zeroed
+static int alloc_maps(CoverState *st) {
+    if (st->maxcov) hipFree(st->maxcov);
+    if (st->flakes) hipFree(st->flakes);
+    st->maxcov = st->flakes = nullptr;
+    st->words = (st->X.span + 31) / 32;
+    if (hipMalloc(&st->maxcov, (size_t)st->ncalls * st->words * 4) != hipSuccess ||
+        hipMalloc(&st->flakes, st->words * 4) != hipSuccess)
+        return SYZCOV_ENOMEM;
+    SYZ_HIP(hipMemsetAsync(st->maxcov, 0, (size_t)st->ncalls * st->words * 4, st->s));
+    SYZ_HIP(hipMemsetAsync(st->flakes, 0, st->words * 4, st->s));
+    SYZ_HIP(hipStreamSynchronize(st->s));
     return 0;
 }
 
@@ -371,18 +375,16 @@ extern "C" int syzcov_state_create(int ncalls, uint32_t pc_lo, uint64_t pc_span,
     st->ncalls = ncalls;
     st->pc_lo = pc_lo;
     st->pc_span = pc_span;
-    st->words = (pc_span + 31) / 32;
-    if (hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&st->maxcov, (size_t)ncalls * st->words * 4) != hipSuccess ||
-        hipMalloc(&st->flakes, st->words * 4) != hipSuccess) {
+    st->X = Index{0, pc_lo, 0, 0, pc_span};
+    int rc = hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking) == hipSuccess
+                 ? alloc_maps(st) : SYZCOV_EHIP;
+    if (rc) {
         if (st->maxcov) hipFree(st->maxcov);
+        if (st->flakes) hipFree(st->flakes);
         if (st->s) hipStreamDestroy(st->s);
         delete st;
-        return SYZCOV_ENOMEM;
+        return rc;
     }
-    hipMemsetAsync(st->maxcov, 0, (size_t)ncalls * st->words * 4, st->s);
-    hipMemsetAsync(st->flakes, 0, st->words * 4, st->s);
-    if (hipStreamSynchronize(st->s) != hipSuccess) return SYZCOV_EHIP;
     *out = (syzcov_cover_state)(uintptr_t)st;
     return 0;
 }
@@ -393,16 +395,14 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     hipStreamSynchronize(st->s);
     hipFree(st->maxcov);
     hipFree(st->flakes);
-    if (st->utab) hipFree(st->utab);
-    if (st->dmax) hipFree(st->dmax);
+    if (st->pc_of_key) hipFree(st->pc_of_key);
     if (st->scratch) hipFree(st->scratch);
     hipStreamDestroy(st->s);
     delete st;
     return 0;
 }
 
-// bm: a window bitmap; dm (universe mode, nullable): the matching dense bitmap
-static int set_bits(CoverState *st, uint32_t *bm, uint32_t *dm, const uint32_t *pcs, size_t n) {
+static int set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n) {
     if (n == 0) return 0;
     size_t need = align_up(n * 4, 256) + 256;
     int rc = grow(st, need);
@@ -412,14 +412,14 @@ static int set_bits(CoverState *st, uint32_t *bm, uint32_t *dm, const uint32_t *
     SYZ_HIP(hipMemsetAsync(derr, 0, 4, st->s));
     SYZ_HIP(hipMemcpyAsync(dp, pcs, n * 4, hipMemcpyHostToDevice, st->s));
     hipLaunchKernelGGL(bits_set_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st->s, dp,
-                       (uint64_t)n, bm, st->pc_lo, st->pc_span, derr,
-                       (const uint64_t *)(dm ? st->utab : nullptr), dm);
+                       (uint64_t)n, bm, st->X, derr);
     SYZ_LAUNCH_CHECK();
     uint32_t herr = 0;
     SYZ_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st->s));
     SYZ_HIP(hipStreamSynchronize(st->s));
     if (herr) {
-        set_error("PC outside the state's PC window");
+        set_error(st->X.key_mode ? "PC outside the registered universe's key range"
+                                 : "PC outside the state's PC window");
         return SYZCOV_ERANGE;
     }
     return 0;
@@ -431,12 +431,15 @@ extern "C" int syzcov_state_add(syzcov_cover_state h, int call, const uint32_t *
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     st->dirty = true;
-    return set_bits(st, st->maxcov + (size_t)call * st->words,
-                    st->dmax ? st->dmax + (size_t)call * st->dwords : nullptr, pcs, n);
+    return set_bits(st, st->maxcov + (size_t)call * st->words, pcs, n);
 }
 
-// Universe mode (see probe_word): PCs of `pcs` (inside the window, any order,
-// duplicates allowed) get dense ids; allowed only while maxCover is empty.
+// Key mode (keys.hip): the PC universe (allCoverPCs, syz-manager/cover.go:57-69;
+// inside the window, any order, duplicates allowed) fixes kshift / kbase /
+// nkeys; maxCover and flakes become bitmaps over its dense keys.  Allowed
+// only while maxCover is empty.  Contract from then on: every PC passed in
+// belongs to the universe (KCOV reports only its call sites); a PC outside
+// the universe's key range is rejected, one inside it is trusted.
 extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *pcs, size_t n) {
     CoverState *st = (CoverState *)(uintptr_t)h;
     if (!st || (n && !pcs)) return SYZCOV_EINVAL;
@@ -446,49 +449,64 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
         set_error("set_universe after maxCover was filled");
         return SYZCOV_EINVAL;
     }
-    if (st->utab) hipFree(st->utab);
-    if (st->dmax) hipFree(st->dmax);
-    st->utab = nullptr;
-    st->dmax = nullptr;
-    st->nuniv = 0;
-    st->dwords = 0;
-    if (n == 0) return 0;
-    uint32_t *bm = nullptr, *dn = nullptr;
+    if (st->pc_of_key) hipFree(st->pc_of_key);
+    st->pc_of_key = nullptr;
+    st->X = Index{0, st->pc_lo, 0, 0, st->pc_span};  // back to window mode
+    if (n == 0) return alloc_maps(st);
+    // the sorted unique universe on the device: window bits -> list
+    uint32_t *bm = nullptr, *lst = nullptr, *sc = nullptr;
     void *ws = nullptr;
+    const uint64_t wwords = (st->pc_span + 31) / 32;
     const size_t wsz = syzcov_dev_dict_ws_size(st->pc_span);
-    if (hipMalloc(&st->utab, st->words * 8) != hipSuccess || hipMalloc(&bm, st->words * 4) != hipSuccess ||
-        hipMalloc(&ws, wsz + 256) != hipSuccess) {
-        if (bm) hipFree(bm);
-        if (ws) hipFree(ws);
-        return SYZCOV_ENOMEM;
-    }
-    dn = (uint32_t *)((uint8_t *)ws + wsz);
+    uint64_t *tab = nullptr;
     int rc = 0;
-    uint32_t hn = 0;
     do {
-        if (hipMemsetAsync(bm, 0, st->words * 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
-        if ((rc = set_bits(st, bm, nullptr, pcs, n))) break;
-        if ((rc = syzcov_dev_dict_build_bits(bm, st->pc_span, st->utab, dn, ws, st->s))) break;
-        if (hipMemcpyAsync(&hn, dn, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
-            hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
-        st->nuniv = hn;
-        st->dwords = (hn + 31) / 32 + 1;
-        if (hipMalloc(&st->dmax, (size_t)st->ncalls * st->dwords * 4) != hipSuccess) {
+        if (hipMalloc(&bm, wwords * 4) != hipSuccess || hipMalloc(&tab, wwords * 8) != hipSuccess ||
+            hipMalloc(&ws, wsz + 256) != hipSuccess || hipMalloc(&lst, n * 4 + 4) != hipSuccess ||
+            hipMalloc(&sc, 256) != hipSuccess) {
             rc = SYZCOV_ENOMEM;
             break;
         }
-        if (hipMemsetAsync(st->dmax, 0, (size_t)st->ncalls * st->dwords * 4, st->s) != hipSuccess ||
-            hipStreamSynchronize(st->s) != hipSuccess) rc = SYZCOV_EHIP;
+        if (hipMemsetAsync(bm, 0, wwords * 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if ((rc = set_bits(st, bm, pcs, n))) break;  // window mode: bits over offsets
+        uint32_t *d_n = sc, *d_ks = sc + 1;
+        if ((rc = syzcov_dev_dict_build_bits(bm, st->pc_span, tab, d_n, ws, st->s))) break;
+        if ((rc = syzcov_dev_dict_to_list(tab, st->pc_span, st->pc_lo, lst, d_n, st->s))) break;
+        uint32_t hn = 0;
+        if (hipMemcpyAsync(&hn, d_n, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if (hn == 0) break;  // only sentinels: stay in window mode
+        const uint32_t k31 = 31;
+        if (hipMemcpyAsync(d_ks, &k31, 4, hipMemcpyHostToDevice, st->s) != hipSuccess) {
+            rc = SYZCOV_EHIP;
+            break;
+        }
+        hipLaunchKernelGGL(universe_shift_kernel, dim3(grid_for(hn, 256, 1024)), dim3(256), 0,
+                           st->s, (const uint32_t *)lst, hn, d_ks);
+        uint32_t ks = 0, ends[2] = {0, 0};
+        if (hipMemcpyAsync(&ks, d_ks, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipMemcpyAsync(&ends[0], lst, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipMemcpyAsync(&ends[1], lst + hn - 1, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        const uint32_t kbase = ends[0] >> ks;
+        const uint64_t nkeys = (uint64_t)(ends[1] >> ks) - kbase + 1;
+        if (hipMalloc(&st->pc_of_key, nkeys * 4) != hipSuccess) { rc = SYZCOV_ENOMEM; break; }
+        if (hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if ((rc = syzcov_dev_universe_keymap(lst, hn, ks, kbase, nkeys, st->pc_of_key, d_n, st->s)))
+            break;
+        st->X = Index{1, st->pc_lo, ks, kbase, nkeys};
+        rc = alloc_maps(st);
     } while (0);
-    hipFree(bm);
-    hipFree(ws);
+    if (bm) hipFree(bm);
+    if (tab) hipFree(tab);
+    if (ws) hipFree(ws);
+    if (lst) hipFree(lst);
+    if (sc) hipFree(sc);
     if (rc) {
-        if (st->utab) hipFree(st->utab);
-        if (st->dmax) hipFree(st->dmax);
-        st->utab = nullptr;
-        st->dmax = nullptr;
-        st->nuniv = 0;
-        st->dwords = 0;
+        if (st->pc_of_key) hipFree(st->pc_of_key);
+        st->pc_of_key = nullptr;
+        st->X = Index{0, st->pc_lo, 0, 0, st->pc_span};
+        alloc_maps(st);
     }
     return rc;
 }
@@ -499,7 +517,7 @@ extern "C" int syzcov_state_set_flakes(syzcov_cover_state h, const uint32_t *pcs
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     SYZ_HIP(hipMemsetAsync(st->flakes, 0, st->words * 4, st->s));
-    return set_bits(st, st->flakes, nullptr, pcs, n);
+    return set_bits(st, st->flakes, pcs, n);
 }
 
 extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *out, size_t cap) {
@@ -509,20 +527,9 @@ extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *ou
     hipSetDevice(st->dev);
     int64_t count = 0;
     const uint32_t *bm = st->maxcov + (size_t)call * st->words;
-    uint32_t *tmp = nullptr;
-    if (st->dmax) {  // window bits | dense bits mapped back to their PCs
-        if (hipMalloc(&tmp, st->words * 4) != hipSuccess) return SYZCOV_ENOMEM;
-        SYZ_HIP(hipMemcpyAsync(tmp, bm, st->words * 4, hipMemcpyDeviceToDevice, st->s));
-        hipLaunchKernelGGL(dense_to_window_kernel, dim3(grid_for(st->words, 256, 16384)), dim3(256), 0,
-                           st->s, (const uint64_t *)st->utab, st->words,
-                           (const uint32_t *)(st->dmax + (size_t)call * st->dwords), tmp);
-        bm = tmp;
-    }
-    int rc = bitmap_to_list(bm, st->pc_span, st->pc_lo, out, cap, &count, st->s);
-    if (tmp) {
-        hipStreamSynchronize(st->s);
-        hipFree(tmp);
-    }
+    int rc = st->X.key_mode
+                 ? bitmap_to_list(bm, st->X.span, 0, out, cap, &count, st->s, st->pc_of_key)
+                 : bitmap_to_list(bm, st->pc_span, st->pc_lo, out, cap, &count, st->s, nullptr);
     return rc ? rc : count;
 }
 
@@ -563,9 +570,8 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                        st->ncalls, perm);
     const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
     hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off, pcs,
-                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->pc_lo, st->pc_span,
-                       st->ncalls, (const uint64_t *)st->utab, (const uint32_t *)st->dmax,
-                       st->dwords, (const uint32_t *)perm, is_new, cpc, cnt, stats);
+                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->X, st->ncalls,
+                       (const uint32_t *)perm, is_new, cpc, cnt, stats);
     const unsigned gh = grid_for(std::max<uint64_t>(npc, 512), 256, 8192);
     hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats, hkey,
                        hval);
@@ -575,8 +581,7 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     hipLaunchKernelGGL(newcov_own_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
                        (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
                        (const uint32_t *)stats, (const unsigned long long *)hkey,
-                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->pc_lo,
-                       (const uint64_t *)st->utab, st->dmax, st->dwords);
+                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->X);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

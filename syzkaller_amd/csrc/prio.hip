@@ -42,13 +42,15 @@ __host__ __device__ inline size_t at_off(size_t r, size_t p, size_t rows) {
 }
 
 // ---------------------------------------------------------------- A builders
-// positional: AT[c][p] = (c < len[p]) for c < C, AT[C][p] = (p < nprog).
+// positional: AT[c][p] = (c < len[p]) for c < C, AT[ones][p] = (p < nprog)
+// (ones = C for the full matrix; -1: no ones row, colsum computed apart).
 // One workgroup per K block (64 programs, a contiguous rows x 64 B region):
 // thread t owns program chunk t % 4 (its 16 lengths stay in registers) and
 // rows t / 4 + 64 i, so a wave stores 1 KB contiguous per instruction.
 __global__ __launch_bounds__(256) void prio_build_pos_kernel(const int32_t *__restrict__ lens,
-                                                             size_t nprog, int C, size_t rows,
-                                                             size_t ldp, int8_t *__restrict__ at) {
+                                                             size_t nprog, int C, int ones,
+                                                             size_t rows, size_t ldp,
+                                                             int8_t *__restrict__ at) {
     const size_t nkb = ldp / PK;
     const uint32_t t = threadIdx.x, ch = t & 3u;
     for (size_t kb = blockIdx.x; kb < nkb; kb += gridDim.x) {
@@ -65,7 +67,7 @@ __global__ __launch_bounds__(256) void prio_build_pos_kernel(const int32_t *__re
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const int32_t L = ln[q * 4 + c];
-                    const bool bit = (int)r < C ? (int32_t)r < L : ((int)r == C && L >= 0);
+                    const bool bit = (int)r < C ? (int32_t)r < L : ((int)r == ones && L >= 0);
                     v |= (uint32_t)bit << (8 * c);
                 }
                 w[q] = v;
@@ -132,11 +134,34 @@ __device__ __forceinline__ void mfma_step(const int8_t *Asrc, const int8_t *Bsrc
 // K range, so each operand chunk comes from HBM once per XCD and is re-read
 // by the other tiles from that XCD's L2 (K splits spread over XCDs instead
 // made every XCD fetch every chunk).
+// GEN (positional, active keys): no AT at all -- each thread builds its
+// 16-byte operand chunks in registers from the 16 program lengths of the
+// chunk (byte j of key row r = [r < len(p_j)], the ones row = [p_j exists]),
+// so the only HBM stream is the lengths (4 B per program).
+__device__ __forceinline__ uint4 gen_chunk(const int32_t (&L)[16], int r, int ones) {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const int32_t len = L[q * 4 + c];
+            v |= (uint32_t)(r == ones ? len >= 0 : r < len) << (8 * c);
+        }
+        w[q] = v;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool GEN>
 __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict__ at, size_t ldp,
                                                         size_t kchunk, int ntile_dim,
                                                         int ntiles, int gpx,
                                                         int32_t *__restrict__ counts,
-                                                        size_t rows) {
+                                                        size_t rows, size_t ldc,
+                                                        int32_t *__restrict__ part,
+                                                        const int32_t *__restrict__ lens,
+                                                        size_t nprog, int ones) {
     __shared__ __attribute__((aligned(16))) int8_t As[2][PT * PK];
     __shared__ __attribute__((aligned(16))) int8_t Bs[2][PT * PK];
     const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
@@ -194,15 +219,57 @@ __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict
         if ((KB) + 2 * PK < kb1) PRIO_LOAD(SET, (KB) + 2 * PK);                     \
         mfma_step(As[SET], diag ? As[SET] : Bs[SET], l, wr, wc, acc);               \
     } while (0)
-    if (kb0 < kb1) PRIO_LOAD(0, kb0);
-    if (kb0 + PK < kb1) PRIO_LOAD(1, kb0 + PK);
-    for (size_t kb = kb0; kb < kb1; kb += 2 * PK) {
-        PRIO_STEP(0, kb);
-        if (kb + PK < kb1) PRIO_STEP(1, kb + PK);
+    // GEN: the 16 lengths of this thread's program chunk (-1: no program)
+    int32_t L0[16], L1[16];
+    auto load16 = [&](size_t kb, int32_t (&L)[16]) {
+        const size_t p0 = kb + chq * 16;
+        if (p0 + 16 <= nprog) {
+            const int4 *src = reinterpret_cast<const int4 *>(lens + p0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int4 v = src[q];
+                L[q * 4] = v.x;
+                L[q * 4 + 1] = v.y;
+                L[q * 4 + 2] = v.z;
+                L[q * 4 + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) L[j] = p0 + j < nprog ? lens[p0 + j] : -1;
+        }
+    };
+#define GEN_STEP(SET, KB)                                                           \
+    do {                                                                            \
+        *(uint4 *)(As[SET] + lo0) = gen_chunk(L##SET, (int)(i0 + row0), ones);      \
+        *(uint4 *)(As[SET] + lo1) = gen_chunk(L##SET, (int)(i0 + row1), ones);      \
+        if (!diag) {                                                                \
+            *(uint4 *)(Bs[SET] + lo0) = gen_chunk(L##SET, (int)(j0 + row0), ones);  \
+            *(uint4 *)(Bs[SET] + lo1) = gen_chunk(L##SET, (int)(j0 + row1), ones);  \
+        }                                                                           \
+        __syncthreads();                                                            \
+        if ((KB) + 2 * PK < kb1) load16((KB) + 2 * PK, L##SET);                     \
+        mfma_step(As[SET], diag ? As[SET] : Bs[SET], l, wr, wc, acc);               \
+    } while (0)
+    if (GEN) {
+        if (kb0 < kb1) load16(kb0, L0);
+        if (kb0 + PK < kb1) load16(kb0 + PK, L1);
+        for (size_t kb = kb0; kb < kb1; kb += 2 * PK) {
+            GEN_STEP(0, kb);
+            if (kb + PK < kb1) GEN_STEP(1, kb + PK);
+        }
+    } else {
+        if (kb0 < kb1) PRIO_LOAD(0, kb0);
+        if (kb0 + PK < kb1) PRIO_LOAD(1, kb0 + PK);
+        for (size_t kb = kb0; kb < kb1; kb += 2 * PK) {
+            PRIO_STEP(0, kb);
+            if (kb + PK < kb1) PRIO_STEP(1, kb + PK);
+        }
     }
+#undef GEN_STEP
 #undef PRIO_STEP
 #undef PRIO_LOAD
     // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    int32_t *pt = part ? part + (split * (size_t)ntiles + tile) * (PT * PT) : nullptr;
 #pragma unroll
     for (int mi = 0; mi < 2; mi++)
 #pragma unroll
@@ -210,12 +277,92 @@ __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int32_t v = acc[mi][ni][r];
+                const uint32_t lr = wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+                const uint32_t lc = wc * 64 + ni * 32 + (l & 31);
+                if (pt) {  // few tiles, many K splits: plain partial-tile stores
+                    pt[lr * PT + lc] = v;
+                    continue;
+                }
                 if (!v) continue;
-                const size_t row = i0 + wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-                const size_t col = j0 + wc * 64 + ni * 32 + (l & 31);
-                atomicAdd(&counts[row * rows + col], v);
-                if (!diag) atomicAdd(&counts[col * rows + row], v);
+                const size_t row = i0 + lr, col = j0 + lc;
+                atomicAdd(&counts[row * ldc + col], v);
+                if (!diag) atomicAdd(&counts[col * ldc + row], v);
             }
+}
+
+// counts (ldc stride, zeroed) += the partial tiles of the K splits, mirrored
+// below the diagonal.  blockIdx.y takes every gridDim.y-th split, so each
+// count gets gridDim.y atomic adds (coalesced loads, 8 splits in flight per
+// thread) instead of one thread summing all splits in a latency chain.
+// The ones row (index `ones`, >= every nonzero key) yields colsum in its
+// column: it goes to column C, the slot prio_finish reads it from.
+__global__ __launch_bounds__(256) void prio_reduce_kernel(const int32_t *__restrict__ part,
+                                                          size_t splits, int ntiles, int ntile_dim,
+                                                          int32_t *__restrict__ counts,
+                                                          size_t ldc, int ones, int C) {
+    const size_t per = (size_t)ntiles * PT * PT;
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= per) return;
+    int32_t sum = 0;
+    size_t sp = blockIdx.y;
+    for (; sp + 7 * gridDim.y < splits; sp += 8 * gridDim.y) {
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = part[(sp + u * gridDim.y) * per + e];
+#pragma unroll
+        for (int u = 0; u < 8; u++) sum += v[u];
+    }
+    for (; sp < splits; sp += gridDim.y) sum += part[sp * per + e];
+    if (!sum) return;
+    const int tile = (int)(e / (PT * PT));
+    const uint32_t lr = (uint32_t)(e % (PT * PT)) / PT, lc = (uint32_t)(e % PT);
+    int I = 0, rem = tile;
+    while (rem >= ntile_dim - I) {
+        rem -= ntile_dim - I;
+        I++;
+    }
+    const size_t row = (size_t)I * PT + lr, col = (size_t)(I + rem) * PT + lc;
+    // the ones row lies in the last row block, so every key meets it once as
+    // a COLUMN (tiles (I, last) and the diagonal last tile); its row copy in
+    // the diagonal tile is the same numbers and is skipped
+    if ((int)row == ones) return;
+    if ((int)col == ones) {
+        if ((int)row < C) atomicAdd(&counts[row * ldc + C], sum);
+        return;
+    }
+    atomicAdd(&counts[row * ldc + col], sum);
+    if (rem) atomicAdd(&counts[col * ldc + row], sum);
+}
+
+// Positional colsum: counts[i][C] = #{p : len(p) > i} (the diagonal
+// correction), from a length histogram and a suffix sum.
+__global__ __launch_bounds__(256) void prio_len_hist_kernel(const int32_t *__restrict__ lens,
+                                                            size_t nprog, int C,
+                                                            uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t h[];
+    for (int i = threadIdx.x; i <= C; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < nprog;
+         p += (size_t)gridDim.x * blockDim.x) {
+        const int32_t L = lens[p];
+        atomicAdd(&h[L < 0 ? 0 : (L > C ? C : L)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= C; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__global__ __launch_bounds__(1024) void prio_colsum_kernel(const uint32_t *__restrict__ hist,
+                                                           int C, int32_t *__restrict__ counts,
+                                                           size_t ldc) {
+    // colsum[i] = sum_{L > i} hist[L]: suffix sum in LDS, then parallel stores
+    extern __shared__ int32_t sfx[];
+    for (int i = threadIdx.x; i <= C; i += blockDim.x) sfx[i] = (int32_t)hist[i];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int i = C - 1; i >= 0; i--) sfx[i] += sfx[i + 1];
+    __syncthreads();
+    for (int i = threadIdx.x; i < C; i += blockDim.x) counts[(size_t)i * ldc + C] = sfx[i + 1];
 }
 
 // ---------------------------------------------------- finish: float + normalize
@@ -451,7 +598,7 @@ extern "C" int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens,
     if (key_mode == 0) {
         if (nprog && !lens) return SYZCOV_EINVAL;
         hipLaunchKernelGGL(prio_build_pos_kernel, dim3(grid_for(ldp / PK, 1, 16384)), dim3(256), 0,
-                           s, lens, nprog, C, rows, ldp, at);
+                           s, lens, nprog, C, C, rows, ldp, at);
         SYZ_LAUNCH_CHECK();
         return 0;
     }
@@ -480,8 +627,9 @@ extern "C" int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog
     if (const char *e = getenv("SYZCOV_PRIO_GPX")) gpx = std::max(1, atoi(e));  // tuning sweeps
     const size_t splits = 8 * (size_t)gpx;
     const size_t kchunk = (nk + splits - 1) / splits * PK;
-    hipLaunchKernelGGL(prio_gemm_kernel, dim3((unsigned)(ntiles * splits)), dim3(256), 0,
-                       (hipStream_t)stream, at, ldp, kchunk, nt, ntiles, gpx, counts, rows);
+    hipLaunchKernelGGL(prio_gemm_kernel<false>, dim3((unsigned)(ntiles * splits)), dim3(256), 0,
+                       (hipStream_t)stream, at, ldp, kchunk, nt, ntiles, gpx, counts, rows, rows,
+                       (int32_t *)nullptr, (const int32_t *)nullptr, (size_t)0, -1);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
@@ -519,6 +667,58 @@ extern "C" int syzcov_dev_choose(const int64_t *run, const uint8_t *enabled, int
     if (C <= 0 || !run || !calls || !x || !out || !err_flag) return SYZCOV_EINVAL;
     hipLaunchKernelGGL(choose_kernel, dim3(grid_for(nq, 256, 8192)), dim3(256), 0,
                        (hipStream_t)stream, run, enabled, C, calls, x, (uint64_t)nq, out, err_flag);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------- positional, active rows
+// The reference's positional counts are zero for every key k >= max len
+// (A[p][k] = [k < len(p)]), so the contraction runs over the first
+// rows_act = roundup(max_len + 1, 128) keys only, with the ones row (colsum)
+// at index max_len.  The operands are generated in registers from the
+// program lengths (no AT in HBM); K is split over many workgroups whose
+// partial tiles a reduction sums (a handful of tiles: atomics would put
+// hundreds of adds on every count).  C4 (max len 120): one 128 x 128 tile,
+// 4 MB of lengths read, instead of 55 tiles over a 1.28 GB AT.
+static void pos_plan(size_t nprog, int C, int max_len, size_t *rows_act, size_t *ntiles,
+                     size_t *splits, size_t *kchunk) {
+    const size_t ra = ((size_t)std::min(max_len, C) + 1 + PT - 1) / PT * PT;
+    const size_t nt = ra / PT, tiles = nt * (nt + 1) / 2;
+    const size_t nk = prio_ldp(nprog) / PK;
+    size_t sp = std::max<size_t>(64, 512 / tiles);
+    sp = (sp + 7) / 8 * 8;
+    sp = std::min(sp, std::max<size_t>(8, (nk + 7) / 8 * 8));
+    *rows_act = ra;
+    *ntiles = tiles;
+    *splits = sp;
+    *kchunk = (nk + sp - 1) / sp * PK;
+}
+
+extern "C" size_t syzcov_dev_prio_pos_ws_size(size_t nprog, int C, int max_len) {
+    size_t ra, tiles, sp, kc;
+    pos_plan(nprog, C, max_len, &ra, &tiles, &sp, &kc);
+    return align_up(sp * tiles * PT * PT * 4, 256);
+}
+
+extern "C" int syzcov_dev_prio_counts_pos(const int32_t *lens, size_t nprog, int C, int max_len,
+                                          int32_t *counts, void *ws, size_t ws_size,
+                                          void *stream) {
+    if (C <= 0 || !counts || (nprog && !lens) || max_len < 0 || max_len > C) return SYZCOV_EINVAL;
+    if (nprog == 0) return 0;
+    if (!ws || ws_size < syzcov_dev_prio_pos_ws_size(nprog, C, max_len)) return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    size_t ra, tiles, sp, kc;
+    pos_plan(nprog, C, max_len, &ra, &tiles, &sp, &kc);
+    const size_t ldp = prio_ldp(nprog), ldc = prio_rows(C);
+    int32_t *part = (int32_t *)ws;
+    const int nt = (int)(ra / PT), ones = std::min(max_len, C);
+    hipLaunchKernelGGL(prio_gemm_kernel<true>, dim3((unsigned)(tiles * sp)), dim3(256), 0, s,
+                       (const int8_t *)nullptr, ldp, kc, nt, (int)tiles, (int)(sp / 8), counts, ra,
+                       ldc, part, lens, nprog, ones);
+    hipLaunchKernelGGL(prio_reduce_kernel,
+                       dim3((unsigned)((tiles * PT * PT + 255) / 256), (unsigned)std::min<size_t>(sp, 16)),
+                       dim3(256), 0, s, (const int32_t *)part, sp, (int)tiles, nt, counts, ldc, ones,
+                       C);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -274,7 +274,7 @@ class PrioEngine:
 
     PHASES = ("static", "build", "gemm", "finish")
 
-    def __init__(self, nprog: int, device="cuda", table=None):
+    def __init__(self, nprog: int, device="cuda", table=None, active_rows: bool = True):
         from . import prio as P
         L = lib()
         self.L, self.dev = L, torch.device(device)
@@ -291,15 +291,23 @@ class PrioEngine:
         self.nprog = nprog
         self.rows = L.syzcov_dev_prio_rows(C_)
         self.ldp = L.syzcov_dev_prio_ldp(nprog)
-        self.at = torch.empty(self.rows * self.ldp, dtype=torch.int8, device=self.dev)
+        self.at = (None if active_rows else
+                   torch.empty(self.rows * self.ldp, dtype=torch.int8, device=self.dev))
         self.counts = torch.empty(self.rows * self.rows, dtype=torch.int32, device=self.dev)
         self.static = torch.empty(C_ * C_, dtype=torch.float32, device=self.dev)
         self.out = torch.empty(C_ * C_, dtype=torch.float32, device=self.dev)
         self.err = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        # positional counts over the active keys only (prio.hip): the AT of
+        # roundup(max len, 128) keys lives in the workspace instead of self.at
+        self.active_rows = active_rows
+        self.max_len = None
+        self.pos_ws = None
 
     def gemm_ops(self) -> int:
         """MFMA ops one counts launch executes (upper-triangle 128x128 tiles)."""
         nt = self.rows // 128
+        if self.active_rows and self.max_len is not None:
+            nt = max(1, -(-min(self.max_len, self.C) // 128))
         return nt * (nt + 1) // 2 * 128 * 128 * 2 * self.ldp
 
     def step(self, lens: torch.Tensor, ev=None, reduce=None):
@@ -315,13 +323,28 @@ class PrioEngine:
                                        _p(self.call_off), _p(self.cids), _p(self.cws), self.C,
                                        _p(self.static), s), "dev_static_prio")
         mark_ev(1)
-        check(L.syzcov_dev_prio_build_at(0, _p(lens), None, None, self.nprog, self.C,
-                                         _p(self.at), self.ldp, _p(self.err), s),
-              "dev_prio_build_at")
-        self.counts.zero_()
-        mark_ev(2)
-        check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
-                                       _p(self.counts), s), "dev_prio_counts")
+        if self.active_rows:
+            # max len sizes the active key block (one host read of a device max)
+            ml = int(lens[:self.nprog].max().item()) if self.nprog else 0
+            if ml > self.C:
+                raise ValueError(f"program of {ml} calls > {self.C} (prio.go:148 would panic)")
+            wsz = L.syzcov_dev_prio_pos_ws_size(self.nprog, self.C, ml)
+            if self.pos_ws is None or self.pos_ws.numel() < wsz:
+                self.pos_ws = torch.empty(wsz, dtype=torch.uint8, device=self.dev)
+            self.max_len = ml
+            self.counts.zero_()
+            mark_ev(2)
+            check(L.syzcov_dev_prio_counts_pos(_p(lens), self.nprog, self.C, ml, _p(self.counts),
+                                               _p(self.pos_ws), self.pos_ws.numel(), s),
+                  "dev_prio_counts_pos")
+        else:
+            check(L.syzcov_dev_prio_build_at(0, _p(lens), None, None, self.nprog, self.C,
+                                             _p(self.at), self.ldp, _p(self.err), s),
+                  "dev_prio_build_at")
+            self.counts.zero_()
+            mark_ev(2)
+            check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
+                                           _p(self.counts), s), "dev_prio_counts")
         if reduce is not None:
             reduce(self.counts)
         mark_ev(3)

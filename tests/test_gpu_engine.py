@@ -178,6 +178,23 @@ def test_prio_positional_vs_oracle(torch):
         assert np.array_equal(got, exp)  # and in fact bit-exact
 
 
+@pytest.mark.parametrize("C,nprog,maxlen", [(300, 700, 300), (1170, 300, 1170), (129, 5000, 128),
+                                             (200, 1, 0)])
+def test_prio_positional_active_rows(torch, C, nprog, maxlen):
+    """Positional counts over the active keys only (roundup(max len, 128)
+    rows, partial tiles + reduction, colsum from the length histogram) at
+    the edges: max len = C (active block past C), 128/129, empty programs."""
+    from syzkaller_amd import prio
+    rng = np.random.default_rng(C + nprog)
+    lens = rng.integers(0, maxlen + 1, size=nprog)
+    lens[0] = maxlen
+    corpus = [[0] * int(l) for l in lens]
+    static = rng.uniform(0.1, 1.0, size=(C, C)).astype(np.float32)
+    got, raw = prio.CalculatePriorities(corpus, static, return_raw=True)
+    assert np.array_equal(raw.astype(np.float32), orc.dynamic_raw(lens, C))
+    assert np.array_equal(got, orc.calculate_priorities(lens, static))
+
+
 def test_static_prio_vs_oracle(torch):
     """calcStaticPriorities over all sys/*.txt calls (1170) on the GPU vs the
     float32 restatement (same ascending-id summation order): bit-exact."""

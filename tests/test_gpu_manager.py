@@ -173,33 +173,42 @@ def test_newcov_sentinel_full_window():
     cc.close()
 
 
-@pytest.mark.parametrize("frac", [1.0, 0.7])
-def test_newcov_universe_mode(frac):
-    """Dense-id maxCover (state_set_universe) gives the reference's results,
-    also for PCs outside the universe; maxCover reads back identically."""
+@pytest.mark.parametrize("spacing", ["random", "synthetic"])
+def test_newcov_key_mode(spacing):
+    """Dense-key maxCover (state_set_universe, keys.hip) gives the reference's
+    results for PCs of the universe; maxCover reads back as PCs; a PC outside
+    the universe's key range is rejected; the universe is fixed once
+    maxCover holds data."""
     from syzkaller_amd import SyzcovError
+    from syzkaller_amd.engine import universe_shift
     from syzkaller_amd.fuzzer import CoverState
     rng = np.random.default_rng(36)
     ncalls, lo, span = 23, 0x81000000, 1 << 20
-    univ_all = np.unique(rng.integers(lo, lo + span, size=60000)).astype(np.uint32)
-    univ = univ_all[rng.random(univ_all.size) < frac]
+    if spacing == "random":  # arbitrary PCs: kshift from the closest neighbours
+        univ = np.unique(rng.integers(lo + 7, lo + span, size=60000)).astype(np.uint32)
+    else:  # the bench's universe: 16 offsets per PC, kshift 4
+        univ = np.array([orc.lib().orc_synth_universe(0x5EED0005, k) for k in range(1 << 16)],
+                        np.uint32)
     st = CoverState(ncalls, lo, span)
-    st.set_universe(univ)
-    init = {c: univ_all[rng.random(univ_all.size) < 0.05] for c in range(0, ncalls, 4)}
+    st.set_universe(rng.permutation(np.concatenate([univ, univ[:100]])))  # any order, dups
+    assert universe_shift(univ) == (4 if spacing == "synthetic" else universe_shift(univ))
+    init = {c: univ[rng.random(univ.size) < 0.05] for c in range(0, ncalls, 4)}
     mc = [init.get(c, np.zeros(0, np.uint32)) for c in range(ncalls)]
     for c, v in init.items():
         st.add(c, v)
-    flakes = univ_all[rng.random(univ_all.size) < 0.01]
+    flakes = univ[rng.random(univ.size) < 0.01]
     st.set_flakes(flakes)
     for batch in range(3):
         nrec = 4000
         cids = rng.integers(0, ncalls, size=nrec).astype(np.int32)
-        recs = [np.unique(rng.choice(univ_all, size=int(rng.integers(0, 200)))).astype(np.uint32)
+        recs = [np.unique(rng.choice(univ, size=int(rng.integers(0, 200)))).astype(np.uint32)
                 for _ in range(nrec)]
         exp, mc = orc.newcov_batch(mc, flakes, cids, recs)
         assert np.array_equal(st.new_coverage(cids, recs), exp), batch
         for c in range(ncalls):
             assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
+    with pytest.raises(SyzcovError):  # below the universe: outside the key range
+        st.new_coverage([0], [np.array([univ[0] - 64], np.uint32)])
     with pytest.raises(SyzcovError):  # the universe is fixed once maxCover holds data
         st.set_universe(univ)
     st.close()
