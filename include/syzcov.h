@@ -229,6 +229,41 @@ int syzcov_state_newcov_dev(syzcov_cover_state st, const int32_t *callid, const 
                             const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
                             uint32_t *stats, void *ws, size_t ws_size, void *stream);
 
+/* corpusCover (syz-fuzzer/fuzzer.go:62-89), held by the same handle over the
+ * same index space as maxCover and flakes.  corpus_add: corpusCover[call] =
+ * Union(corpusCover[call], pcs) (fuzzer.go:451, after the caller's
+ * prog.Minimize); corpus_get reads it back like syzcov_state_get. */
+int syzcov_state_corpus_add(syzcov_cover_state st, int call, const uint32_t *pcs, size_t n);
+int64_t syzcov_state_corpus_get(syzcov_cover_state st, int call, uint32_t *out, size_t cap);
+/* Reads the flakes set back (sorted), like syzcov_state_get. */
+int64_t syzcov_state_flakes_get(syzcov_cover_state st, uint32_t *out, size_t cap);
+/* addInput (fuzzer.go:344-375) for a batch of manager-pushed inputs in
+ * order (record k: call id, sorted cover as in syzcov_newcov_batch; the
+ * caller has run Canonicalize, :365, and the corpusHashes check, :361-364):
+ * accepted[k] iff Difference(Difference(cov, maxCover), flakes) != ∅ at its
+ * turn; an accepted input's whole cover joins corpusCover and maxCover
+ * (:372-373).  Returns the number accepted. */
+int64_t syzcov_state_add_inputs(syzcov_cover_state st, const int32_t *callid,
+                                const uint64_t *rec_off, const uint32_t *rec_pcs, size_t nrec,
+                                uint8_t *accepted);
+/* triageInput (fuzzer.go:377-417) for ntri inputs.  Input t: call id
+ * callid[t], sorted cover cov_pcs[cov_off[t] .. cov_off[t+1]); its three
+ * re-executions are runs 3t, 3t+1, 3t+2 of run_off/run_pcs (sorted; an empty
+ * run is a call that did not execute, :401-404).  Schedule: every input's
+ * newCover = Difference(Difference(cov, corpusCover[call]), flakes) (:384-385)
+ * is taken before any flakes update (one interleaving of the reference's
+ * concurrent triage goroutines); then each input with a non-empty newCover
+ * runs its loop: minCover = Intersection(minCover, run), flakes =
+ * Union(flakes, SymmetricDifference(cov, run)) (:405-415).  Outputs
+ * new_cnt[t] = len(newCover) and stableNewCover = Intersection(newCover,
+ * minCover) (:417) at stable_pcs[cov_off[t] ..] (stable_cnt[t] PCs; capacity
+ * = the cover CSR).  flakes is updated in the handle.  Returns the number
+ * of inputs with a non-empty stableNewCover (those go on to prog.Minimize). */
+int64_t syzcov_state_triage(syzcov_cover_state st, size_t ntri, const int32_t *callid,
+                            const uint64_t *cov_off, const uint32_t *cov_pcs,
+                            const uint64_t *run_off, const uint32_t *run_pcs, uint32_t *new_cnt,
+                            uint32_t *stable_cnt, uint32_t *stable_pcs);
+
 /* Executor output of one program (writer executor/executor.cc:455-466,
  * reader ipc/ipc.go:225-291: u32 ncmd, then per completed call u32
  * call_index, call_num, errno, cover_size, pcs[cover_size], little-endian)

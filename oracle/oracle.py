@@ -189,6 +189,56 @@ def newcov_batch(maxcover, flakes, callids, records):
     return is_new[:nrec], mc
 
 
+def add_inputs(maxcover, corpus_cover, flakes, callids, covers):
+    """addInput (syz-fuzzer/fuzzer.go:344-375), sequentially over a batch of
+    canonical covers (Canonicalize :365 is the identity on them; the
+    corpusHashes check :361-364 is the caller's).  maxcover / corpus_cover:
+    lists of per-call sorted arrays, updated in place.  Returns accepted."""
+    acc = []
+    for c, cov in zip(callids, covers):
+        c = int(c)
+        cov = _u32(cov)
+        diff = difference(difference(cov, maxcover[c]), flakes)  # :366-367
+        if len(diff) == 0:
+            acc.append(False)
+            continue
+        corpus_cover[c] = union(corpus_cover[c], cov)  # :372
+        maxcover[c] = union(maxcover[c], cov)  # :373
+        acc.append(True)
+    return acc
+
+
+def triage_batch(corpus_cover, flakes, callids, covers, runs):
+    """triageInput (syz-fuzzer/fuzzer.go:377-417) for a batch, literally, in
+    the schedule of syzcov_state_triage: every input's newCover (:383-386) is
+    taken against the flakes at batch start; then, input by input, the
+    re-execution loop (:398-416) updates minCover and flakes with the
+    updateFlakes predicate as written, and stableNewCover = Intersection(
+    newCover, minCover) (:417).  runs[t]: 3 covers, empty = not executed.
+    Returns (new_counts, stable list, final flakes)."""
+    f0 = _u32(flakes)
+    newc = [difference(difference(_u32(cov), corpus_cover[int(c)]), f0)
+            for c, cov in zip(callids, covers)]
+    fl = f0
+    stable = []
+    for t, cov in enumerate(covers):
+        cov = _u32(cov)
+        if len(newc[t]) == 0:  # :387-389
+            stable.append(np.zeros(0, np.uint32))
+            continue
+        min_cover = cov
+        for run in runs[t]:
+            run = _u32(run)
+            if len(run) == 0:  # :401-404
+                continue
+            diff = symmetric_difference(cov, run)
+            min_cover = intersection(min_cover, run)
+            if len(diff) != 0 and len(difference(diff, fl)) != 0:  # :409
+                fl = union(fl, diff)
+        stable.append(intersection(newc[t], min_cover))
+    return [len(x) for x in newc], stable, fl
+
+
 def dynamic_raw(prog_lens, C_: int) -> np.ndarray:
     pl = np.ascontiguousarray(np.asarray(prog_lens, dtype=np.int32))
     out = np.zeros((C_, C_), dtype=np.float32)

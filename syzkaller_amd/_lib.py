@@ -67,6 +67,11 @@ _SIGS = {
     "syzcov_newcov_batch": (i64, [u64, p_, p_, p_, sz, p_]),
     "syzcov_parse_exec_output": (i64, [p_, sz, sz, p_, p_, sz, p_, p_, p_, p_, p_, sz]),
     "syzcov_state_set_universe": (C.c_int, [u64, p_, sz]),
+    "syzcov_state_corpus_add": (C.c_int, [u64, C.c_int, p_, sz]),
+    "syzcov_state_corpus_get": (i64, [u64, C.c_int, p_, sz]),
+    "syzcov_state_flakes_get": (i64, [u64, p_, sz]),
+    "syzcov_state_add_inputs": (i64, [u64, p_, p_, p_, sz, p_]),
+    "syzcov_state_triage": (i64, [u64, sz, p_, p_, p_, p_, p_, p_, p_, p_]),
     "syzcov_state_newcov_ws_size": (sz, [sz, u64]),
     "syzcov_state_newcov_dev": (C.c_int, [u64, p_, p_, p_, sz, u64, p_, p_, p_, sz, p_]),
     # device tier

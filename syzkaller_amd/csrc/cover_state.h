@@ -1,0 +1,68 @@
+// cover_state.h — the fuzzer's resident coverage state (syz-fuzzer/fuzzer.go:
+// 62-89: maxCover, corpusCover, flakes under coverMu) shared by newcov.hip
+// (execute's new-coverage check, addInput) and triage.hip (triageInput).
+#pragma once
+#include "common.h"
+
+#include <mutex>
+
+namespace syz {
+
+__device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64_t o) {
+    return (bm[o >> 5] >> (o & 31)) & 1u;
+}
+
+// Where a PC lives in the bitmaps: its window offset, or its dense key.
+struct Index {
+    int key_mode;
+    uint32_t pc_lo, kshift, kbase;
+    uint64_t span;  // window span, or nkeys
+};
+
+// Bitmap index of pc; false if pc is outside the window / key range.
+__device__ __forceinline__ bool pc_index(const Index &X, uint32_t pc, uint32_t *idx) {
+    if (X.key_mode) {
+        const uint32_t k = (pc >> X.kshift) - X.kbase;  // wraps past span below kbase
+        *idx = k;
+        return k < X.span;
+    }
+    const uint32_t o = pc - X.pc_lo;
+    *idx = o;
+    return pc >= X.pc_lo && (uint64_t)o < X.span;
+}
+
+struct CoverState {
+    int dev = 0;
+    int ncalls = 0;
+    uint32_t pc_lo = 0;
+    uint64_t pc_span = 0;
+    // bitmap index space: window offsets, or dense keys of the registered
+    // universe (key mode); words = 32-bit words per bitmap
+    Index X{};
+    uint64_t words = 0;
+    uint32_t *maxcov = nullptr;  // ncalls x words
+    uint32_t *corpus = nullptr;  // corpusCover: ncalls x words, allocated on first use
+    uint32_t *flakes = nullptr;  // words
+    uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
+    // LDS-staged candidate pass: per-call record counts | offsets | cursors |
+    // work-item prefix over (call, range) | work-item descriptors; one batch
+    // at a time per state
+    uint32_t *grp = nullptr;
+    bool dirty = false;          // maxCover touched: the universe can no longer change
+    hipStream_t s = nullptr;
+    std::mutex mu;  // the reference's coverMu
+    // grow-only scratch
+    void *scratch = nullptr;
+    size_t scap = 0;
+};
+
+int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
+                   size_t cap, int64_t *count, hipStream_t s, const uint32_t *pc_of_key);
+
+// shared host helpers (newcov.hip)
+int state_grow(CoverState *st, size_t need);
+int state_ensure_corpus(CoverState *st);
+int state_bitmap_get(CoverState *st, const uint32_t *bm, uint32_t *out, size_t cap, int64_t *count);
+int state_set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n);
+
+}  // namespace syz

@@ -21,118 +21,140 @@
 // of nkeys bits (512 KB at the synthetic 2^22-PC universe instead of 8 MB of
 // window bits), so a call's bitmap stays in its XCD's L2 while that XCD
 // walks the call's records.
-#include "common.h"
+#include "cover_state.h"
 
 namespace syz {
-
-__device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64_t o) {
-    return (bm[o >> 5] >> (o & 31)) & 1u;
-}
-
-// Where a PC lives in the bitmaps: its window offset, or its dense key.
-struct Index {
-    int key_mode;
-    uint32_t pc_lo, kshift, kbase;
-    uint64_t span;  // window span, or nkeys
-};
-
-// Bitmap index of pc; false if pc is outside the window / key range.
-__device__ __forceinline__ bool pc_index(const Index &X, uint32_t pc, uint32_t *idx) {
-    if (X.key_mode) {
-        const uint32_t k = (pc >> X.kshift) - X.kbase;  // wraps past span below kbase
-        *idx = k;
-        return k < X.span;
-    }
-    const uint32_t o = pc - X.pc_lo;
-    *idx = o;
-    return pc >= X.pc_lo && (uint64_t)o < X.span;
-}
 
 constexpr int NC_THREADS = 256;
 constexpr int NC_WPB = NC_THREADS / 64;
 constexpr int NC_U = 8;  // rows of 64 PCs in flight per wave
+constexpr uint32_t SENT = 0xFFFFFFFFu;
 
-// Records grouped by CallID (counting sort in one workgroup): the candidate
-// pass walks them in this order so the records of one call run together on
-// one XCD and share its L2 copy of maxCover[call] (the probes of one record
-// touch ~2k random lines of an 8 MB bitmap; a call's records hit mostly the
-// same hot lines).  perm[] is only a visiting order: ownership still uses
-// the batch index k.
-constexpr int GRP_MAX_CALLS = 16384;
+// Candidates: (record k, pc) pairs that pass the maxCover and flakes
+// bitmaps, appended to one list (few once maxCover saturates); stats[1] is
+// the list length.  One atomic per wave-row that has any.
+__device__ __forceinline__ void emit_cands(bool cand, uint32_t k, uint32_t pc,
+                                           uint2 *__restrict__ clist,
+                                           uint32_t *__restrict__ stats) {
+    const uint64_t m = __ballot(cand);
+    if (!m) return;
+    const uint32_t l = __lane_id();
+    uint32_t base = 0;
+    if (l == 0) base = atomicAdd(&stats[1], (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (cand) clist[base + (uint32_t)__popcll(m & ((1ull << l) - 1ull))] = make_uint2(k, pc);
+}
 
-__global__ __launch_bounds__(1024) void newcov_group_kernel(const int32_t *__restrict__ callid,
-                                                             uint32_t nrec, int ncalls,
-                                                             uint32_t *__restrict__ perm) {
-    __shared__ uint32_t h[GRP_MAX_CALLS];
+// ---------------------------------------------------------------------------
+// Records grouped by CallID (counting sort over three kernels): both
+// candidate passes walk a call's records together.
+//   grp_hist: per-call counts   grp_scan: offsets coff   grp_scatter: perm/pos
+constexpr int GRP_MAX_CALLS = 16384;  // LDS counters; above, global atomics
+constexpr int GS_THREADS = 1024, GS_PER = 4;  // scatter: records per thread
+
+__global__ __launch_bounds__(256) void grp_hist_kernel(const int32_t *__restrict__ callid,
+                                                       uint32_t nrec, int ncalls,
+                                                       uint32_t *__restrict__ ccnt,
+                                                       uint32_t *__restrict__ stats) {
+    extern __shared__ uint32_t h[];  // ncalls counters, or none above GRP_MAX_CALLS
+    const bool sh = ncalls <= GRP_MAX_CALLS;
+    if (sh)
+        for (int c = threadIdx.x; c < ncalls; c += blockDim.x) h[c] = 0;
+    __syncthreads();
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrec; k += gridDim.x * blockDim.x) {
+        const int c = callid[k];
+        if (c >= 0 && c < ncalls) atomicAdd(sh ? &h[c] : &ccnt[c], 1u);
+        else stats[0] = 2u;
+    }
+    __syncthreads();
+    if (sh)
+        for (int c = threadIdx.x; c < ncalls; c += blockDim.x)
+            if (h[c]) atomicAdd(&ccnt[c], h[c]);
+}
+
+// call offsets coff[0..ncalls] (exclusive scan); cursors = coff
+__global__ __launch_bounds__(1024) void grp_scan_kernel(const uint32_t *__restrict__ ccnt,
+                                                        int ncalls, uint32_t *__restrict__ coff,
+                                                        uint32_t *__restrict__ cursor) {
     __shared__ uint32_t tmp[1024 / 64 + 1];
-    const uint32_t t = threadIdx.x;
-    if (ncalls > GRP_MAX_CALLS) {
-        for (uint32_t k = t; k < nrec; k += 1024) perm[k] = k;
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < ncalls; c0 += 1024) {
+        const int c = c0 + (int)threadIdx.x;
+        const uint32_t v = c < ncalls ? ccnt[c] : 0u;
+        uint32_t tot;
+        const uint32_t p = block_excl_scan<1024>(v, tmp, &tot);
+        if (c < ncalls) coff[c] = cursor[c] = carry + p;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) coff[ncalls] = carry;
+}
+
+// perm[j] = k with j from the call's cursor (order inside a call
+// is free: perm is only a visiting order, ownership uses the batch index).
+// Each workgroup reserves one range per call it holds (LDS counts, one
+// global atomic per (workgroup, call)) instead of one atomic per record.
+__global__ __launch_bounds__(GS_THREADS) void grp_scatter_kernel(
+    const int32_t *__restrict__ callid, uint32_t nrec, int ncalls, uint32_t *__restrict__ cursor,
+    uint32_t *__restrict__ perm) {
+    extern __shared__ uint32_t h[];  // ncalls local counts, then bases
+    const bool sh = ncalls <= GRP_MAX_CALLS;
+    const uint32_t k0 = blockIdx.x * GS_THREADS * GS_PER;
+    if (!sh) {  // many calls: one global atomic per record
+        for (uint32_t i = threadIdx.x; i < GS_THREADS * GS_PER; i += GS_THREADS) {
+            const uint32_t k = k0 + i;
+            if (k >= nrec) break;
+            const int c = callid[k];
+            if (c >= 0 && c < ncalls) perm[atomicAdd(&cursor[c], 1u)] = k;
+        }
         return;
     }
-    for (int c = t; c < ncalls; c += 1024) h[c] = 0;
+    for (int c = threadIdx.x; c < ncalls; c += GS_THREADS) h[c] = 0;
     __syncthreads();
-    for (uint32_t k = t; k < nrec; k += 1024) {
-        const int c = callid[k];
-        if (c >= 0 && c < ncalls) atomicAdd(&h[c], 1u);
+    uint32_t rank[GS_PER];
+    int cc[GS_PER];
+#pragma unroll
+    for (int u = 0; u < GS_PER; u++) {
+        const uint32_t k = k0 + u * GS_THREADS + threadIdx.x;
+        cc[u] = k < nrec ? callid[k] : -1;
+        if (cc[u] >= ncalls) cc[u] = -1;
+        rank[u] = cc[u] >= 0 ? atomicAdd(&h[cc[u]], 1u) : 0u;
     }
     __syncthreads();
-    uint32_t carry = 0;  // exclusive scan; bad call ids go last
-    for (int c0 = 0; c0 < ncalls; c0 += 1024) {
-        const int c = c0 + (int)t;
-        const uint32_t v = c < ncalls ? h[c] : 0u;
-        uint32_t total;
-        const uint32_t p = block_excl_scan<1024>(v, tmp, &total);
-        __syncthreads();
-        if (c < ncalls) h[c] = carry + p;
-        carry += total;
-        __syncthreads();
-    }
-    __shared__ uint32_t bad_pos;
-    if (t == 0) bad_pos = carry;
+    for (int c = threadIdx.x; c < ncalls; c += GS_THREADS)
+        if (h[c]) h[c] = atomicAdd(&cursor[c], h[c]);
     __syncthreads();
-    for (uint32_t k = t; k < nrec; k += 1024) {
-        const int c = callid[k];
-        const uint32_t pos = (c >= 0 && c < ncalls) ? atomicAdd(&h[c], 1u) : atomicAdd(&bad_pos, 1u);
-        perm[pos] = k;
+#pragma unroll
+    for (int u = 0; u < GS_PER; u++) {
+        const uint32_t k = k0 + u * GS_THREADS + threadIdx.x;
+        if (cc[u] >= 0) perm[h[cc[u]] + rank[u]] = k;
     }
 }
 
-// stats[0] = error (1 window, 2 call id, 3 unsorted), stats[1] = candidates.
-// One WAVEFRONT per record: coalesced 64-PC rows, both bitmap probes per PC,
-// ballot compaction of the survivors into the record's OWN slots of cpc
-// (cpc is indexed like pcs), so no global atomics per row; one atomic per
-// wave for the batch total.  Once maxCover saturates (a fuzzer's steady
-// state) almost every record has zero survivors.
+// ---------------------------------------------------------------------------
+// Probing candidate pass (any index space).  One WAVEFRONT per record in
+// call-grouped order, coalesced 64-PC rows, both bitmap probes per PC.
+// XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so the
+// workgroups of XCD x (blockIdx % 8 == x) take the x-th eighth of the
+// grouped records and a call's records share that XCD's L2 copy of its
+// bitmap.  stats[0] = error (1 outside the index space, 2 call id, 3
+// unsorted).
 __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
     const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
     const uint32_t *__restrict__ pcs, uint32_t nrec, const uint32_t *__restrict__ maxcov,
-    uint64_t words_per_call, const uint32_t *__restrict__ flakes, Index X, int ncalls,
-    const uint32_t *__restrict__ perm, uint8_t *__restrict__ is_new, uint32_t *__restrict__ cpc,
-    uint32_t *__restrict__ rec_cnt, uint32_t *__restrict__ stats) {
+    uint64_t words_per_call, const uint32_t *__restrict__ flakes, Index X,
+    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ coff, int ncalls,
+    uint2 *__restrict__ clist, uint32_t *__restrict__ stats) {
     const uint32_t l = __lane_id();
-    const uint64_t lt = (1ull << l) - 1ull;
-    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
-    // the workgroups of XCD x (blockIdx % 8 == x) take the x-th eighth of
-    // the call-grouped records
+    const uint32_t ng = coff[ncalls];  // grouped (valid) records; the rest: grp_hist flagged
     const uint32_t x = blockIdx.x & 7, nbx = gridDim.x >> 3;
-    const uint32_t j0 = (uint32_t)((uint64_t)nrec * x / 8), j1 = (uint32_t)((uint64_t)nrec * (x + 1) / 8);
+    const uint32_t j0 = (uint32_t)((uint64_t)ng * x / 8), j1 = (uint32_t)((uint64_t)ng * (x + 1) / 8);
     const uint32_t nw = nbx * NC_WPB;
-    uint32_t wave_tot = 0;
     for (uint32_t j = j0 + (blockIdx.x >> 3) * NC_WPB + (threadIdx.x >> 6); j < j1; j += nw) {
         const uint32_t k = perm[j];
-        const int c = callid[k];
-        if (l == 0) is_new[k] = 0;
-        if (c < 0 || c >= ncalls) {
-            if (l == 0) {
-                stats[0] = 2u;
-                rec_cnt[k] = 0;
-            }
-            continue;
-        }
-        const uint32_t *M = maxcov + (uint64_t)c * words_per_call;
+        const uint32_t *M = maxcov + (uint64_t)(uint32_t)callid[k] * words_per_call;
         const uint64_t b = rec_off[k], n = rec_off[k + 1] - b;
-        uint32_t bad = 0, cnt = 0, carry = 0;
+        uint32_t bad = 0, carry = 0;
         // NC_U rows per step: all their loads and maxCover probes in flight together
         for (uint64_t q0 = 0; q0 < n; q0 += 64 * NC_U) {
             uint32_t pc[NC_U], w[NC_U], ix[NC_U];
@@ -148,7 +170,7 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 const bool inw = pc_index(X, pc[u], &ix[u]);
                 // 0xFFFFFFFF is Difference's end sentinel: never part of a
                 // diff (cover.go:43-48,97), so never a candidate, never an error
-                const bool sent = pc[u] == 0xFFFFFFFFu;
+                const bool sent = pc[u] == SENT;
                 ok[u] = q < n && inw && !sent;
                 bad |= (uint32_t)(q < n && !inw && !sent);
                 w[u] = ok[u] ? M[ix[u] >> 5] : 0xFFFFFFFFu;
@@ -165,17 +187,345 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 // maxCover first: once it saturates, flakes are rarely probed
                 const bool cand =
                     ok[u] && !((w[u] >> (ix[u] & 31)) & 1u) && !bit_test(flakes, ix[u]);
-                const uint64_t m = __ballot(cand);
-                if (cand) cpc[b + cnt + (uint32_t)__popcll(m & lt)] = pc[u];
-                cnt += (uint32_t)__popcll(m);
+                emit_cands(cand, k, pc[u], clist, stats);
             }
         }
         if (bad) stats[0] = (bad & 1u) ? 1u : 3u;
-        if (l == 0) rec_cnt[k] = cnt;
-        wave_tot += cnt;
     }
-    if (l == 0 && wave_tot) atomicAdd(&stats[1], wave_tot);
 }
+
+// ---------------------------------------------------------------------------
+// LDS-staged candidate pass.  Probing a per-call bitmap in global memory is
+// one scattered request per PC into a 150 MB set of bitmaps that no L2 holds
+// (C5: 132 M probes per batch).  Instead the index space is cut into ranges
+// of 2^19 keys (64 KB of bitmap): a workgroup stages one range of one call's
+// maxCover in LDS and tests a chunk of that (call, range)'s PCs there.
+//   records grouped by call:   grp_hist -> grp_scan -> grp_scatter (perm, pos)
+//   sub-runs:                  nq[q][j] = grouped record j's PC count in range
+//                              q, Bq[q][j] = where that sub-run starts in pcs
+//   per-range streams:         nq scanned in place: Pq[q][j] = exclusive prefix
+//   work items:                (call, range, chunk of CH PCs of that stream),
+//                              one 16-byte descriptor each (desc_kernel)
+// The synthetic coverage is skewed (40% of PCs in range 0), so chunking by
+// PC count, not by record count, is what balances the workgroups.
+constexpr uint32_t NR_MAX = 32;          // ranges (index space <= 2^24)
+constexpr uint32_t RSH = 19;             // 2^19 indices (64 KB of bitmap) per range:
+                                         // two workgroups per CU
+constexpr uint32_t ITEMS_MAX = 65536;    // chunk-count cap (items_target)
+constexpr int LC_THREADS = 1024;
+constexpr uint32_t LC_WIN = 512;         // records staged per window (LDS: two
+                                         // workgroups per CU = 2 x (64 + 8) KB)
+constexpr uint32_t LC_BATCH = 64 * NC_U; // PCs per wave batch
+constexpr int SQ_G = 8;                  // split queries in flight per wave
+
+// Range boundaries of every grouped record, one wave per record, by 64-way
+// search: 64 evenly spaced samples bracket each query to a bucket of
+// ceil(n / 64) PCs, whose elements are then counted (SQ_G queries' bucket
+// loads in flight together).  Queries: "index < (q+1) << RSH" for q < nr-1
+// and "not the sentinel" (the record's length without its trailing
+// 0xFFFFFFFF, which is never a candidate, cover.go:43-48).  Sorted records
+// only: a record out of order is caught here at the boundaries (stats 3)
+// or inside its sub-runs by the candidate pass; non-monotone boundaries
+// become empty sub-runs.  An end outside the index space: stats 1.
+__global__ __launch_bounds__(256) void newcov_split_kernel(
+    const uint64_t *__restrict__ rec_off, const uint32_t *__restrict__ pcs,
+    const uint32_t *__restrict__ perm, const uint32_t *__restrict__ coff, int ncalls, Index X,
+    uint32_t nr, uint32_t stride, uint32_t *__restrict__ nq, uint64_t *__restrict__ Bq,
+    uint32_t *__restrict__ stats) {
+    const uint32_t l = __lane_id(), ng = coff[ncalls];
+    for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < ng; j += gridDim.x * 4) {
+        const uint32_t k = perm[j];
+        const uint64_t b = rec_off[k];
+        const uint32_t n = (uint32_t)(rec_off[k + 1] - b);
+        const uint32_t *p = pcs + b;
+        // samples: s_l = floor(l n / 64) (every element when n <= 64)
+        const uint32_t ns = min(n, 64u);
+        const uint32_t sl = n <= 64 ? l : (uint32_t)(((uint64_t)l * n) >> 6);
+        const uint32_t x = l < ns ? p[sl] : SENT;
+        uint32_t kx;
+        const bool xin = pc_index(X, x, &kx);
+        uint32_t bad = (uint32_t)(l < ns && x != SENT && !xin);
+        if (x == SENT || !xin) kx = 0xFFFFFFFFu;  // sorts after every query
+        const uint32_t nqry = nr;  // queries 0..nr-2: range bounds; nr-1: the sentinel
+        uint32_t res_mine = 0;     // lane q < nr ends with query q's answer
+        for (uint32_t g0 = 0; g0 < nqry; g0 += SQ_G) {
+            uint32_t lo[SQ_G], hi[SQ_G], cnt[SQ_G], v[SQ_G];
+#pragma unroll
+            for (int g = 0; g < SQ_G; g++) {
+                const uint32_t qy = g0 + g;
+                v[g] = qy + 1 < nqry ? (qy + 1) << RSH : 0xFFFFFFFFu;
+                const uint32_t c = qy < nqry ? (uint32_t)__popcll(__ballot(l < ns && kx < v[g])) : 0u;
+                if (n <= 64) {
+                    lo[g] = c;
+                    hi[g] = c;
+                } else {
+                    lo[g] = c == 0 ? 0u : (uint32_t)(((uint64_t)(c - 1) * n) >> 6) + 1;
+                    hi[g] = c == 64 ? n : (uint32_t)(((uint64_t)c * n) >> 6);
+                    if (qy >= nqry) hi[g] = lo[g];
+                }
+                cnt[g] = 0;
+            }
+            for (uint32_t o = 0;; o += 64) {
+                bool more = false;
+                uint32_t e[SQ_G];
+#pragma unroll
+                for (int g = 0; g < SQ_G; g++) {
+                    const uint32_t i = lo[g] + o + l;
+                    e[g] = i < hi[g] ? p[i] : SENT;
+                    more |= lo[g] + o + 64 < hi[g];
+                }
+#pragma unroll
+                for (int g = 0; g < SQ_G; g++) {
+                    uint32_t ke;
+                    const bool ein = pc_index(X, e[g], &ke);
+                    if (e[g] == SENT || !ein) ke = 0xFFFFFFFFu;
+                    cnt[g] += (uint32_t)__popcll(__ballot(lo[g] + o + l < hi[g] && ke < v[g]));
+                }
+                if (!__ballot(more)) break;
+            }
+#pragma unroll
+            for (int g = 0; g < SQ_G; g++)
+                if (l == g0 + g) res_mine = lo[g] + cnt[g];
+        }
+        // lane q < nr holds boundary q; the last is the length without sentinels
+        const uint32_t neff = __shfl(res_mine, nr - 1, 64);
+        uint32_t prev = __shfl_up(res_mine, 1, 64);
+        if (l == 0) prev = 0;
+        // the record's last PC, and each boundary's neighbours
+        if (l == 0 && neff) {
+            uint32_t kl;
+            bad |= (uint32_t)!pc_index(X, p[neff - 1], &kl);
+        }
+        if (l + 1 < nr && res_mine > 0 && res_mine < neff && p[res_mine - 1] > p[res_mine])
+            bad |= 2u;
+        const bool mono = !__ballot(l < nr && res_mine < prev);
+        const uint64_t eb = __ballot(bad & 1u), eo = __ballot(bad & 2u);
+        if (l == 0 && (eb || eo || !mono)) stats[0] = eb ? 1u : 3u;
+        if (l < nr) {
+            const bool ok = mono && !eb;
+            const uint64_t i = (uint64_t)l * stride + j;
+            nq[i] = ok ? res_mine - prev : 0u;
+            Bq[i] = b + (ok ? prev : 0u);
+        }
+    }
+}
+
+// Exclusive scan of nq[q][0..m) in place for every range q, in chunks of
+// RS_CHUNK: pass 1 sums each chunk, pass 2 scans a chunk from the sum of the
+// chunks before it; nq[q][m] = the total.
+constexpr uint32_t RS_CHUNK = 8192;
+
+__global__ __launch_bounds__(1024) void range_sum_kernel(const uint32_t *__restrict__ nq,
+                                                         uint32_t m, uint32_t stride,
+                                                         uint32_t *__restrict__ csum) {
+    __shared__ uint32_t tmp[1024 / 64 + 1];
+    const uint32_t q = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+    const uint32_t *a = nq + (uint64_t)q * stride + (uint64_t)b * RS_CHUNK;
+    const uint32_t n = min(RS_CHUNK, m - b * RS_CHUNK);
+    uint32_t v = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += a[i];
+    uint32_t tot;
+    block_excl_scan<1024>(v, tmp, &tot);
+    if (threadIdx.x == 0) csum[q * nb + b] = tot;
+}
+
+__global__ __launch_bounds__(1024) void range_scan_kernel(uint32_t *__restrict__ nq, uint32_t m,
+                                                          uint32_t stride,
+                                                          const uint32_t *__restrict__ csum) {
+    __shared__ uint32_t tmp[1024 / 64 + 1];
+    const uint32_t q = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+    uint32_t *a = nq + (uint64_t)q * stride;
+    uint32_t carry = 0;
+    for (uint32_t i = 0; i < b; i++) carry += csum[q * nb + i];
+    constexpr uint32_t PT = RS_CHUNK / 1024;
+    const uint32_t i0 = b * RS_CHUNK + threadIdx.x * PT;
+    uint32_t v[PT], sum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < PT; u++) {
+        v[u] = i0 + u < m ? a[i0 + u] : 0u;
+        sum += v[u];
+    }
+    uint32_t tot;
+    uint32_t run = carry + block_excl_scan<1024>(sum, tmp, &tot);
+#pragma unroll
+    for (uint32_t u = 0; u < PT; u++) {
+        if (i0 + u < m) a[i0 + u] = run;
+        run += v[u];
+    }
+    if (b == nb - 1 && threadIdx.x == 1023) a[m] = run;
+}
+
+// Work-item prefix over (call, range) pairs e = c * nr + q: ceil(T_cq / CH)
+// items each, T_cq = the call's share of range q's stream.
+__global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restrict__ coff,
+                                                         int ncalls, uint32_t nr,
+                                                         const uint32_t *__restrict__ Pq,
+                                                         uint32_t stride, uint32_t CH,
+                                                         uint32_t *__restrict__ ipre) {
+    __shared__ uint32_t tmp[1024 / 64 + 1];
+    const uint32_t ne = (uint32_t)ncalls * nr;
+    uint32_t carry = 0;
+    for (uint32_t e0 = 0; e0 < ne; e0 += 1024) {
+        const uint32_t e = e0 + threadIdx.x;
+        uint32_t v = 0;
+        if (e < ne) {
+            const uint32_t c = e / nr, q = e - c * nr;
+            const uint32_t *P = Pq + (uint64_t)q * stride;
+            v = (P[coff[c + 1]] - P[coff[c]] + CH - 1) / CH;
+        }
+        uint32_t tot;
+        const uint32_t p = block_excl_scan<1024>(v, tmp, &tot);
+        if (e < ne) ipre[e] = carry + p;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ipre[ne] = carry;
+}
+
+// Work-item descriptors {e = c * nr + q, F0, F1, first record}: chunk i of
+// pair e is stream positions [P0 + i CH, min(P0 + (i+1) CH, P1)) of range q,
+// and starts in the record j with P[j] <= F0 < P[j+1].  One wave per pair;
+// lane j finds the chunk starts inside its record.
+__global__ __launch_bounds__(256) void desc_kernel(const uint32_t *__restrict__ coff, int ncalls,
+                                                   uint32_t nr, const uint32_t *__restrict__ Pq,
+                                                   uint32_t stride, uint32_t CH,
+                                                   const uint32_t *__restrict__ ipre,
+                                                   uint4 *__restrict__ desc) {
+    const uint32_t l = __lane_id(), ne = (uint32_t)ncalls * nr;
+    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < ne; e += gridDim.x * 4) {
+        const uint32_t c = e / nr, q = e - c * nr;
+        const uint32_t *P = Pq + (uint64_t)q * stride;
+        const uint32_t j0 = coff[c], j1 = coff[c + 1];
+        const uint32_t P0 = P[j0], P1 = P[j1], base = ipre[e];
+        if (P1 == P0) continue;
+        for (uint32_t j = j0 + l; j < j1; j += 64) {
+            const uint32_t a = P[j] - P0, b = P[j + 1] - P0;
+            if (b <= a) continue;
+            for (uint32_t i = (a + CH - 1) / CH; (uint64_t)i * CH < b; i++) {
+                const uint32_t F0 = P0 + i * CH;
+                desc[base + i] = make_uint4(e, F0, min(F0 + CH, P1), j);
+            }
+        }
+    }
+}
+
+// The candidate pass.  Work item w -> (call c, range q, stream positions
+// [F0, F1), first record) from its descriptor.  The chunk's records are
+// staged in windows of up to LC_WIN (stream start and PC base in LDS); the
+// 16 waves take 512-PC batches of the window round-robin, a lane finds its
+// record by walking the window's starts from the batch's first record.
+__global__ __launch_bounds__(LC_THREADS) void newcov_cand_lds_kernel(
+    const uint32_t *__restrict__ pcs, const uint32_t *__restrict__ maxcov, uint64_t words_per_call,
+    const uint32_t *__restrict__ flakes, Index X, uint32_t nr, const uint32_t *__restrict__ perm,
+    const uint32_t *__restrict__ coff, const uint32_t *__restrict__ ipre, uint32_t ne,
+    const uint4 *__restrict__ desc, const uint32_t *__restrict__ Pq,
+    const uint64_t *__restrict__ Bq, uint32_t stride, uint2 *__restrict__ clist,
+    uint32_t *__restrict__ stats) {
+    extern __shared__ uint4 s_m4[];  // (1 << RSH) / 128 uint4 of maxCover[call]
+    __shared__ uint32_t s_P[LC_WIN + 1], s_k[LC_WIN];
+    __shared__ uint64_t s_b[LC_WIN];  // pcs index of stream position 0 of record j
+    const uint32_t t = threadIdx.x, w = blockIdx.x, l = __lane_id(), wv = t >> 6;
+    if (w >= ipre[ne]) return;  // grid is an upper bound
+    const uint4 d = desc[w];
+    const uint32_t e = d.x, c = e / nr, q = e - c * nr, F0 = d.y, F1 = d.z;
+    uint32_t jr = d.w;
+    const uint32_t j1 = coff[c + 1];
+    const uint32_t *P = Pq + (uint64_t)q * stride;
+    const uint64_t *B = Bq + (uint64_t)q * stride;
+    // stage maxCover[c] | flakes over indices [q << RSH, (q + 1) << RSH)
+    // (words_per_call is a multiple of 4), all loads issued before the LDS
+    // stores: one LDS test per PC decides "in neither" (the flakes range is
+    // read by every workgroup of range q and stays in L2)
+    const uint64_t wbase = (uint64_t)q << (RSH - 5);
+    const uint32_t nv = (uint32_t)(min<uint64_t>((uint64_t)1 << (RSH - 5), words_per_call - wbase) >> 2);
+    const uint4 *M4 = (const uint4 *)(maxcov + (uint64_t)c * words_per_call + wbase);
+    const uint4 *F4 = (const uint4 *)(flakes + wbase);
+    constexpr int SV = (1 << (RSH - 7)) / LC_THREADS;  // uint4 per thread
+    {
+        uint4 v[SV], f[SV];
+#pragma unroll
+        for (int i = 0; i < SV; i++) {
+            const uint32_t j = t + i * LC_THREADS;
+            v[i] = j < nv ? M4[j] : make_uint4(0, 0, 0, 0);
+            f[i] = j < nv ? F4[j] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < SV; i++) {
+            const uint32_t j = t + i * LC_THREADS;
+            if (j < nv)
+                s_m4[j] = make_uint4(v[i].x | f[i].x, v[i].y | f[i].y, v[i].z | f[i].z, v[i].w | f[i].w);
+        }
+    }
+    const uint32_t *s_m = (const uint32_t *)s_m4;
+    const uint32_t kbase_r = q << RSH;
+    uint32_t bad = 0;
+    for (;;) {
+        // window: records [jr, jr + nwin), stream starts s_P[0..nwin]
+        const uint32_t nwin = min(LC_WIN, j1 - jr);
+        if (t == 0) s_P[nwin] = P[jr + nwin];
+        if (t < nwin) {
+            const uint32_t p0 = P[jr + t];
+            s_P[t] = p0;
+            s_k[t] = perm[jr + t];
+            s_b[t] = B[jr + t] - p0;
+        }
+        __syncthreads();
+        const uint32_t W0 = max(F0, s_P[0]), W1 = min(F1, s_P[nwin]);
+        for (uint32_t f0 = W0 + wv * LC_BATCH; f0 < W1; f0 += LC_THREADS / 64 * LC_BATCH) {
+            uint32_t lo = 0, hi = nwin;  // largest r with s_P[r] <= f0
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_P[mid] <= f0) lo = mid; else hi = mid;
+            }
+            uint32_t r = lo;
+            uint32_t pc[NC_U], rr[NC_U];
+#pragma unroll
+            for (int u = 0; u < NC_U; u++) {
+                const uint32_t f = f0 + u * 64 + l;
+                if (f < W1) {
+                    while (s_P[r + 1] <= f) r++;
+                    rr[u] = r;
+                    pc[u] = pcs[s_b[r] + f];
+                } else {
+                    rr[u] = 0xFFFFFFFFu;
+                    pc[u] = 0;
+                }
+            }
+            // the PC before the batch, for the sortedness check of its first PC
+            uint32_t carry = 0;
+            if (f0 > s_P[lo]) carry = pcs[s_b[lo] + f0 - 1];
+#pragma unroll
+            for (int u = 0; u < NC_U; u++) {
+                const uint32_t f = f0 + u * 64 + l;
+                const bool live = rr[u] != 0xFFFFFFFFu;
+                uint32_t prev = __shfl_up(pc[u], 1, 64);
+                if (l == 0) prev = carry;
+                carry = __builtin_amdgcn_readlane(pc[u], 63);
+                uint32_t key = 0;
+                const bool inw = pc_index(X, pc[u], &key);
+                const uint32_t o = key - kbase_r;
+                const bool ok = live && inw && o < (1u << RSH) && pc[u] != SENT;
+                // outside the index space: 1; a sentinel or a PC of another
+                // range inside a sub-run (only an unsorted record puts them
+                // there) or out of order: 3
+                bad |= (uint32_t)(live && !inw && pc[u] != SENT) | ((uint32_t)(live && !ok) << 1);
+                if (live && f > s_P[rr[u]] && prev > pc[u]) bad |= 2u;
+                const bool cand = ok && !((s_m[o >> 5] >> (o & 31)) & 1u);
+                emit_cands(cand, live ? s_k[rr[u]] : 0u, pc[u], clist, stats);
+            }
+        }
+        jr += nwin;
+        const bool more = jr < j1 && s_P[nwin] < F1;
+        __syncthreads();  // window arrays are rewritten next
+        if (!more) break;
+    }
+    if (bad) stats[0] = (bad & 1u) ? 1u : 3u;
+}
+
+// ---------------------------------------------------------------------------
+// First cover over the candidate list: hval[(call, pc)] = min record index,
+// then a record is new iff it owns one of its candidates, and each owned
+// candidate is OR-ed into maxCover once.
 
 // table capacity for ncand candidates (power of two, load <= 1/2)
 __device__ __forceinline__ uint64_t hash_cap(uint32_t ncand) {
@@ -207,65 +557,48 @@ __device__ __forceinline__ uint64_t hash64(uint64_t k) {
 
 constexpr uint64_t EMPTY_KEY = ~0ull;
 
-// first-cover of every candidate key (CallID, pc): hval = min record index
-__global__ __launch_bounds__(NC_THREADS) void newcov_insert_kernel(
-    const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
-    const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
+__global__ __launch_bounds__(256) void newcov_insert_kernel(
+    const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
     const uint32_t *__restrict__ stats, unsigned long long *__restrict__ hkey,
     uint32_t *__restrict__ hval) {
     if (stats[0] || !stats[1]) return;
-    const uint64_t mask = hash_cap(stats[1]) - 1;
-    const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
-    for (uint32_t k = blockIdx.x * NC_WPB + (threadIdx.x >> 6); k < nrec; k += nw) {
-        const uint32_t cnt = rec_cnt[k];
-        if (!cnt) continue;
-        const uint64_t hi = (uint64_t)(uint32_t)callid[k] << 32, b = rec_off[k];
-        for (uint32_t i = l; i < cnt; i += 64) {
-            const uint64_t key = hi | cpc[b + i];
-            uint64_t h = hash64(key) & mask;
-            for (;;) {
-                const unsigned long long prev = atomicCAS(&hkey[h], EMPTY_KEY, key);
-                if (prev == EMPTY_KEY || prev == key) {
-                    atomicMin(&hval[h], k);
-                    break;
-                }
-                h = (h + 1) & mask;
+    const uint32_t n = stats[1];
+    const uint64_t mask = hash_cap(n) - 1;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 kp = clist[i];
+        const uint64_t key = (uint64_t)(uint32_t)callid[kp.x] << 32 | kp.y;
+        uint64_t h = hash64(key) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&hkey[h], EMPTY_KEY, key);
+            if (prev == EMPTY_KEY || prev == key) {
+                atomicMin(&hval[h], kp.x);
+                break;
             }
+            h = (h + 1) & mask;
         }
     }
 }
 
-// record k is new iff it owns (first-covers) one of its keys; each owned key
-// is OR-ed into maxCover once
-__global__ __launch_bounds__(NC_THREADS) void newcov_own_kernel(
-    const int32_t *__restrict__ callid, const uint64_t *__restrict__ rec_off,
-    const uint32_t *__restrict__ cpc, const uint32_t *__restrict__ rec_cnt, uint32_t nrec,
+__global__ __launch_bounds__(256) void newcov_own_kernel(
+    const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
     const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
     uint32_t *__restrict__ maxcov, uint64_t words_per_call, Index X) {
     if (stats[0] || !stats[1]) return;
-    const uint64_t mask = hash_cap(stats[1]) - 1;
-    const uint32_t l = __lane_id(), nw = gridDim.x * NC_WPB;
-    for (uint32_t k = blockIdx.x * NC_WPB + (threadIdx.x >> 6); k < nrec; k += nw) {
-        const uint32_t cnt = rec_cnt[k];
-        if (!cnt) continue;
-        const uint32_t c = (uint32_t)callid[k];
-        const uint64_t hi = (uint64_t)c << 32, b = rec_off[k];
-        uint32_t *M = maxcov + (uint64_t)c * words_per_call;
-        bool own = false;
-        for (uint32_t i = l; i < cnt; i += 64) {
-            const uint32_t pc = cpc[b + i];
-            const uint64_t key = hi | pc;
-            uint64_t h = hash64(key) & mask;
-            while (hkey[h] != key) h = (h + 1) & mask;
-            if (hval[h] == k) {
-                own = true;
-                uint32_t ix;
-                pc_index(X, pc, &ix);  // candidates are inside (checked by the cand pass)
-                atomicOr(&M[ix >> 5], 1u << (ix & 31));
-            }
+    const uint32_t n = stats[1];
+    const uint64_t mask = hash_cap(n) - 1;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 kp = clist[i];
+        const uint32_t c = (uint32_t)callid[kp.x];
+        const uint64_t key = (uint64_t)c << 32 | kp.y;
+        uint64_t h = hash64(key) & mask;
+        while (hkey[h] != key) h = (h + 1) & mask;
+        if (hval[h] == kp.x) {
+            is_new[kp.x] = 1;
+            uint32_t ix;
+            pc_index(X, kp.y, &ix);  // candidates are inside (checked by the cand pass)
+            atomicOr(&maxcov[(uint64_t)c * words_per_call + (ix >> 5)], 1u << (ix & 31));
         }
-        if (__ballot(own) && l == 0) is_new[k] = 1;
     }
 }
 
@@ -296,40 +629,45 @@ __global__ void universe_shift_kernel(const uint32_t *__restrict__ u, uint32_t n
     if (__lane_id() == 0) atomicMin(out, m);
 }
 
+// addInput (fuzzer.go:372-373): an accepted input's whole cover (flakes
+// included, the sentinel excluded) joins corpusCover and maxCover.  One wave
+// per record; nothing on a rejected batch.
+__global__ __launch_bounds__(256) void accept_or_kernel(const int32_t *__restrict__ callid,
+                                                        const uint64_t *__restrict__ rec_off,
+                                                        const uint32_t *__restrict__ pcs,
+                                                        uint32_t nrec,
+                                                        const uint8_t *__restrict__ is_new,
+                                                        const uint32_t *__restrict__ stats,
+                                                        uint32_t *__restrict__ maxcov,
+                                                        uint32_t *__restrict__ corpus,
+                                                        uint64_t words, Index X) {
+    if (stats[0]) return;
+    const uint32_t l = __lane_id();
+    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < nrec; k += gridDim.x * 4) {
+        if (!is_new[k]) continue;
+        const uint64_t c = (uint32_t)callid[k], b = rec_off[k], n = rec_off[k + 1] - b;
+        for (uint64_t i = l; i < n; i += 64) {
+            const uint32_t pc = pcs[b + i];
+            uint32_t ix;
+            if (pc == 0xFFFFFFFFu || !pc_index(X, pc, &ix)) continue;
+            atomicOr(&maxcov[c * words + (ix >> 5)], 1u << (ix & 31));
+            atomicOr(&corpus[c * words + (ix >> 5)], 1u << (ix & 31));
+        }
+    }
+}
+
 }  // namespace syz
 
 // ------------------------------------------------ host-side orchestration
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <new>
 #include <vector>
 
 using namespace syz;
 
-namespace syz {
-struct CoverState {
-    int dev = 0;
-    int ncalls = 0;
-    uint32_t pc_lo = 0;
-    uint64_t pc_span = 0;
-    // bitmap index space: window offsets, or dense keys of the registered
-    // universe (key mode); words = 32-bit words per bitmap
-    Index X{};
-    uint64_t words = 0;
-    uint32_t *maxcov = nullptr;  // ncalls x words
-    uint32_t *flakes = nullptr;  // words
-    uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
-    bool dirty = false;          // maxCover touched: the universe can no longer change
-    hipStream_t s = nullptr;
-    std::mutex mu;  // the reference's coverMu
-    // grow-only scratch
-    void *scratch = nullptr;
-    size_t scap = 0;
-};
-
-int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_t *out,
-                   size_t cap, int64_t *count, hipStream_t s, const uint32_t *pc_of_key);
-}  // namespace syz
 
 static int grow(CoverState *st, size_t need) {
     if (need <= st->scap) return 0;
@@ -345,12 +683,24 @@ static int grow(CoverState *st, size_t need) {
     return 0;
 }
 
+// CoverState::grp: 3 x (ncalls + 1) + ncalls * NR_MAX + 1 u32, then the
+// descriptors (<= ITEMS_MAX + ncalls * NR_MAX + 1 uint4, 16-byte aligned)
+static size_t grp_desc_off(int ncalls) {
+    return align_up(4 * (3 * ((size_t)ncalls + 1) + (size_t)ncalls * NR_MAX + 1), 256);
+}
+static size_t grp_bytes(int ncalls) {
+    return grp_desc_off(ncalls) + 16 * ((size_t)ITEMS_MAX + (size_t)ncalls * NR_MAX + 1);
+}
+
 // (re)allocate the bitmaps for the current index space, zeroed
 static int alloc_maps(CoverState *st) {
     if (st->maxcov) hipFree(st->maxcov);
     if (st->flakes) hipFree(st->flakes);
-    st->maxcov = st->flakes = nullptr;
-    st->words = (st->X.span + 31) / 32;
+    if (st->corpus) hipFree(st->corpus);
+    st->maxcov = st->flakes = st->corpus = nullptr;
+    st->words = ((st->X.span + 127) / 128) * 4;  // 16-byte rows (LDS staging)
+    if (!st->grp && hipMalloc(&st->grp, grp_bytes(st->ncalls)) != hipSuccess)
+        return SYZCOV_ENOMEM;
     if (hipMalloc(&st->maxcov, (size_t)st->ncalls * st->words * 4) != hipSuccess ||
         hipMalloc(&st->flakes, st->words * 4) != hipSuccess)
         return SYZCOV_ENOMEM;
@@ -381,6 +731,7 @@ extern "C" int syzcov_state_create(int ncalls, uint32_t pc_lo, uint64_t pc_span,
     if (rc) {
         if (st->maxcov) hipFree(st->maxcov);
         if (st->flakes) hipFree(st->flakes);
+        if (st->grp) hipFree(st->grp);
         if (st->s) hipStreamDestroy(st->s);
         delete st;
         return rc;
@@ -395,7 +746,9 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     hipStreamSynchronize(st->s);
     hipFree(st->maxcov);
     hipFree(st->flakes);
+    if (st->corpus) hipFree(st->corpus);
     if (st->pc_of_key) hipFree(st->pc_of_key);
+    if (st->grp) hipFree(st->grp);
     if (st->scratch) hipFree(st->scratch);
     hipStreamDestroy(st->s);
     delete st;
@@ -424,6 +777,31 @@ static int set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n)
     }
     return 0;
 }
+
+namespace syz {
+int state_grow(CoverState *st, size_t need) { return grow(st, need); }
+int state_set_bits(CoverState *st, uint32_t *bm, const uint32_t *pcs, size_t n) {
+    return set_bits(st, bm, pcs, n);
+}
+// corpusCover bitmaps, zeroed, on first use (fuzzer.go:372, 451)
+int state_ensure_corpus(CoverState *st) {
+    if (st->corpus) return 0;
+    const size_t bytes = (size_t)st->ncalls * st->words * 4;
+    if (hipMalloc(&st->corpus, bytes) != hipSuccess) {
+        st->corpus = nullptr;
+        return SYZCOV_ENOMEM;
+    }
+    SYZ_HIP(hipMemsetAsync(st->corpus, 0, bytes, st->s));
+    return 0;
+}
+// one per-call bitmap back as a sorted PC list (keys mapped to PCs)
+int state_bitmap_get(CoverState *st, const uint32_t *bm, uint32_t *out, size_t cap,
+                     int64_t *count) {
+    return st->X.key_mode
+               ? bitmap_to_list(bm, st->X.span, 0, out, cap, count, st->s, st->pc_of_key)
+               : bitmap_to_list(bm, st->pc_span, st->pc_lo, out, cap, count, st->s, nullptr);
+}
+}  // namespace syz
 
 extern "C" int syzcov_state_add(syzcov_cover_state h, int call, const uint32_t *pcs, size_t n) {
     CoverState *st = (CoverState *)(uintptr_t)h;
@@ -526,60 +904,132 @@ extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *ou
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     int64_t count = 0;
-    const uint32_t *bm = st->maxcov + (size_t)call * st->words;
-    int rc = st->X.key_mode
-                 ? bitmap_to_list(bm, st->X.span, 0, out, cap, &count, st->s, st->pc_of_key)
-                 : bitmap_to_list(bm, st->pc_span, st->pc_lo, out, cap, &count, st->s, nullptr);
+    int rc = state_bitmap_get(st, st->maxcov + (size_t)call * st->words, out, cap, &count);
     return rc ? rc : count;
 }
 
-// device workspace: cpc u32[npc] | rec_cnt u32[nrec] | perm u32[nrec] | hkey u64[cap] |
-//                   hval u32[cap] | stats
-static void nc_layout(size_t nrec, uint64_t npc, size_t *o_cnt, size_t *o_hkey, size_t *o_hval,
-                      size_t *o_stats, size_t *end) {
+// device workspace: clist uint2[npc] | perm u32[nrec] | nq u32[NR_MAX x (nrec + 1)] |
+//   Bq u64[NR_MAX x (nrec + 1)] | csum u32[chunks x NR_MAX] | hkey u64[cap] |
+//   hval u32[cap] | stats
+struct NcLayout {
+    size_t perm, nq, bq, csum, hkey, hval, stats, end;
+};
+static NcLayout nc_layout(size_t nrec, uint64_t npc) {
     uint64_t cap = 1024;
     while (cap < 2ull * npc) cap <<= 1;
-    *o_cnt = align_up(npc * 4 + 4, 256);
-    *o_hkey = align_up(*o_cnt + 2 * align_up(nrec * 4 + 4, 256), 256);
-    *o_hval = align_up(*o_hkey + cap * 8, 256);
-    *o_stats = align_up(*o_hval + cap * 4, 256);
-    *end = *o_stats + 256;
+    NcLayout L;
+    L.perm = align_up(npc * 8 + 8, 256);
+    L.nq = align_up(L.perm + nrec * 4 + 4, 256);
+    L.bq = align_up(L.nq + (nrec + 1) * NR_MAX * 4, 256);
+    L.csum = align_up(L.bq + (nrec + 1) * NR_MAX * 8, 256);
+    L.hkey = align_up(L.csum + ((nrec + RS_CHUNK - 1) / RS_CHUNK) * NR_MAX * 4 + 4, 256);
+    L.hval = align_up(L.hkey + cap * 8, 256);
+    L.stats = align_up(L.hval + cap * 4, 256);
+    L.end = L.stats + 256;
+    return L;
 }
 
 extern "C" size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc) {
-    size_t a, b, c, d, e;
-    nc_layout(nrec, npc, &a, &b, &c, &d, &e);
-    return e;
+    return nc_layout(nrec, npc).end;
+}
+
+// Candidate pass choice.  LDS staging (ranges of 2^19 indices, nr <= 32)
+// pays when the bitmap bytes staged (about nr x calls x 64 KB) stay well
+// under the PCs streamed; otherwise (sparse calls, huge windows) every PC
+// probes the bitmap in global memory.  SYZCOV_NEWCOV_PATH=lds|probe forces one.
+static int env_path() {  // read per batch (tests switch it)
+    const char *e = getenv("SYZCOV_NEWCOV_PATH");
+    return e ? (!strcmp(e, "lds") ? 1 : !strcmp(e, "probe") ? 2 : 0) : 0;
+}
+static uint32_t env_items() {
+    static const uint32_t v = [] {
+        const char *e = getenv("SYZCOV_NEWCOV_ITEMS");
+        return e ? (uint32_t)atoi(e) : 1024u;
+    }();
+    return v ? std::min(v, ITEMS_MAX) : 1024u;
 }
 
 static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
                          const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
                          uint8_t *ws, uint32_t **stats_out, hipStream_t s) {
-    size_t o_cnt, o_hkey, o_hval, o_stats, end;
-    nc_layout(nrec, npc, &o_cnt, &o_hkey, &o_hval, &o_stats, &end);
-    uint32_t *cpc = (uint32_t *)ws;
-    uint32_t *cnt = (uint32_t *)(ws + o_cnt);
-    uint32_t *perm = (uint32_t *)(ws + o_cnt + align_up(nrec * 4 + 4, 256));
-    unsigned long long *hkey = (unsigned long long *)(ws + o_hkey);
-    uint32_t *hval = (uint32_t *)(ws + o_hval);
-    uint32_t *stats = (uint32_t *)(ws + o_stats);
+    const NcLayout Lw = nc_layout(nrec, npc);
+    uint2 *clist = (uint2 *)ws;
+    uint32_t *perm = (uint32_t *)(ws + Lw.perm);
+    unsigned long long *hkey = (unsigned long long *)(ws + Lw.hkey);
+    uint32_t *hval = (uint32_t *)(ws + Lw.hval);
+    uint32_t *stats = (uint32_t *)(ws + Lw.stats);
     *stats_out = stats;
     SYZ_HIP(hipMemsetAsync(stats, 0, 16, s));
-    const unsigned gr = grid_for(nrec, NC_WPB, 4096);
-    hipLaunchKernelGGL(newcov_group_kernel, dim3(1), dim3(1024), 0, s, callid, (uint32_t)nrec,
-                       st->ncalls, perm);
-    const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
-    hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off, pcs,
-                       (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->X, st->ncalls,
-                       (const uint32_t *)perm, is_new, cpc, cnt, stats);
+    SYZ_HIP(hipMemsetAsync(is_new, 0, nrec, s));
+    const uint32_t nc = (uint32_t)st->ncalls;
+    uint32_t *ccnt = st->grp, *coff = ccnt + nc + 1, *cur = coff + nc + 1, *ipre = cur + nc + 1;
+    // records grouped by call (both passes)
+    static std::atomic<uint32_t> gs_done{0};
+    if (nc <= GRP_MAX_CALLS) {
+        int rc = set_dyn_lds_once((const void *)grp_scatter_kernel, GRP_MAX_CALLS * 4, gs_done);
+        if (rc) return rc;
+    }
+    SYZ_HIP(hipMemsetAsync(ccnt, 0, 4 * (size_t)nc, s));
+    hipLaunchKernelGGL(grp_hist_kernel, dim3(grid_for(nrec, 256, 1024)), dim3(256),
+                       nc <= GRP_MAX_CALLS ? (size_t)nc * 4 : 0, s, callid, (uint32_t)nrec,
+                       st->ncalls, ccnt, stats);
+    hipLaunchKernelGGL(grp_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)ccnt,
+                       st->ncalls, coff, cur);
+    hipLaunchKernelGGL(grp_scatter_kernel,
+                       dim3((unsigned)((nrec + GS_THREADS * GS_PER - 1) / (GS_THREADS * GS_PER))),
+                       dim3(GS_THREADS), nc <= GRP_MAX_CALLS ? (size_t)nc * 4 : 0, s, callid,
+                       (uint32_t)nrec, st->ncalls, cur, perm);
+    const uint64_t nr64 = (st->X.span + (1ull << RSH) - 1) >> RSH;
+    const int forced = env_path();
+    const uint64_t range_bytes = std::min<uint64_t>(st->words * 4, 1u << (RSH - 3));
+    const bool lds = nr64 <= NR_MAX &&
+                     (forced == 1 ||
+                      (forced == 0 && 2 * nr64 * (uint64_t)nc * range_bytes <= npc * 4));
+    if (lds) {
+        static std::atomic<uint32_t> lds_done{0};
+        int rc = set_dyn_lds_once((const void *)newcov_cand_lds_kernel, 1 << (RSH - 3), lds_done);
+        if (rc) return rc;
+        const uint32_t nr = (uint32_t)nr64, stride = (uint32_t)nrec + 1;
+        uint4 *desc = (uint4 *)((uint8_t *)st->grp + grp_desc_off(st->ncalls));
+        uint32_t *nq = (uint32_t *)(ws + Lw.nq), *csum = (uint32_t *)(ws + Lw.csum);
+        uint64_t *bq = (uint64_t *)(ws + Lw.bq);
+        // chunk: about env_items() work items over the batch, >= 16 K PCs
+        const uint32_t CH = (uint32_t)std::max<uint64_t>(16384, (npc + env_items() - 1) / env_items());
+        // sub-runs of the grouped records; the grid covers every record
+        // (records with a bad call id are not grouped: coff[nc] <= nrec)
+        hipLaunchKernelGGL(newcov_split_kernel, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0, s,
+                           rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls,
+                           st->X, nr, stride, nq, bq, stats);
+        const uint32_t nb = (uint32_t)((nrec + RS_CHUNK - 1) / RS_CHUNK);
+        hipLaunchKernelGGL(range_sum_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
+                           (uint32_t)nrec, stride, csum);
+        hipLaunchKernelGGL(range_scan_kernel, dim3(nb, nr), dim3(1024), 0, s, nq, (uint32_t)nrec,
+                           stride, (const uint32_t *)csum);
+        hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
+                           st->ncalls, nr, (const uint32_t *)nq, stride, CH, ipre);
+        const uint32_t ne = nc * nr;
+        hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 4, 4096)), dim3(256), 0, s,
+                           (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)nq, stride, CH,
+                           (const uint32_t *)ipre, desc);
+        // items <= npc / CH + non-empty (call, range) pairs; the excess exits
+        const uint64_t items = npc / CH + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
+        hipLaunchKernelGGL(newcov_cand_lds_kernel, dim3((unsigned)items), dim3(LC_THREADS),
+                           (size_t)range_bytes, s, pcs, (const uint32_t *)st->maxcov, st->words,
+                           (const uint32_t *)st->flakes, st->X, nr, (const uint32_t *)perm,
+                           (const uint32_t *)coff, (const uint32_t *)ipre, ne, (const uint4 *)desc,
+                           (const uint32_t *)nq, (const uint64_t *)bq, stride, clist, stats);
+    } else {
+        const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
+        hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off,
+                           pcs, (uint32_t)nrec, st->maxcov, st->words, st->flakes, st->X,
+                           (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls, clist, stats);
+    }
     const unsigned gh = grid_for(std::max<uint64_t>(npc, 512), 256, 8192);
     hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats, hkey,
                        hval);
-    hipLaunchKernelGGL(newcov_insert_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
-                       (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
-                       (const uint32_t *)stats, hkey, hval);
-    hipLaunchKernelGGL(newcov_own_kernel, dim3(gr), dim3(NC_THREADS), 0, s, callid, rec_off,
-                       (const uint32_t *)cpc, (const uint32_t *)cnt, (uint32_t)nrec,
+    hipLaunchKernelGGL(newcov_insert_kernel, dim3(gh), dim3(256), 0, s, callid,
+                       (const uint2 *)clist, (const uint32_t *)stats, hkey, hval);
+    hipLaunchKernelGGL(newcov_own_kernel, dim3(gh), dim3(256), 0, s, callid, (const uint2 *)clist,
                        (const uint32_t *)stats, (const unsigned long long *)hkey,
                        (const uint32_t *)hval, is_new, st->maxcov, st->words, st->X);
     SYZ_LAUNCH_CHECK();
@@ -610,10 +1060,11 @@ extern "C" int syzcov_state_newcov_dev(syzcov_cover_state h, const int32_t *call
     return 0;
 }
 
-extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *callid,
-                                       const uint64_t *rec_off, const uint32_t *rec_pcs,
-                                       size_t nrec, uint8_t *is_new) {
-    CoverState *st = (CoverState *)(uintptr_t)h;
+// The host-buffer batch of execute() (add_input false) or addInput
+// (add_input true: accepted inputs then OR their whole cover into maxCover
+// and corpusCover).
+static int64_t newcov_host(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
+                           const uint32_t *rec_pcs, size_t nrec, uint8_t *is_new, bool add_input) {
     if (!st || (nrec && (!callid || !rec_off || !is_new))) return SYZCOV_EINVAL;
     if (nrec == 0) return 0;
     if (nrec > 0x7FFFFFFF) return SYZCOV_EINVAL;
@@ -623,11 +1074,13 @@ extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *call
     const uint64_t npc = rec_off[nrec] - base0;
     if (npc && !rec_pcs) return SYZCOV_EINVAL;
     if (npc > 0xFFFFFFFFull) return SYZCOV_EINVAL;
+    int rc = add_input ? state_ensure_corpus(st) : 0;
+    if (rc) return rc;
     // staging: callid | off | pcs | is_new | newcov workspace
     const size_t o_off = align_up(nrec * 4, 256), o_pcs = align_up(o_off + (nrec + 1) * 8, 256),
                  o_new = align_up(o_pcs + npc * 4 + 4, 256), o_ws = align_up(o_new + nrec, 256),
                  o_end = o_ws + syzcov_state_newcov_ws_size(nrec, npc);
-    int rc = grow(st, o_end);
+    rc = grow(st, o_end);
     if (rc) return rc;
     uint8_t *S = (uint8_t *)st->scratch;
     hipStream_t s = st->s;
@@ -641,6 +1094,14 @@ extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *call
     rc = newcov_launch(st, (const int32_t *)S, (const uint64_t *)(S + o_off),
                        (const uint32_t *)(S + o_pcs), nrec, npc, S + o_new, S + o_ws, &dstats, s);
     if (rc) return rc;
+    if (add_input) {
+        hipLaunchKernelGGL(accept_or_kernel, dim3(grid_for(nrec, 4, 8192)), dim3(256), 0, s,
+                           (const int32_t *)S, (const uint64_t *)(S + o_off),
+                           (const uint32_t *)(S + o_pcs), (uint32_t)nrec,
+                           (const uint8_t *)(S + o_new), (const uint32_t *)dstats, st->maxcov,
+                           st->corpus, st->words, st->X);
+        SYZ_LAUNCH_CHECK();
+    }
     uint32_t hs[2];
     SYZ_HIP(hipMemcpyAsync(hs, dstats, 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(is_new, S + o_new, nrec, hipMemcpyDeviceToHost, s));
@@ -654,4 +1115,16 @@ extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *call
     int64_t nnew = 0;
     for (size_t k = 0; k < nrec; k++) nnew += is_new[k];
     return nnew;
+}
+
+extern "C" int64_t syzcov_newcov_batch(syzcov_cover_state h, const int32_t *callid,
+                                       const uint64_t *rec_off, const uint32_t *rec_pcs,
+                                       size_t nrec, uint8_t *is_new) {
+    return newcov_host((CoverState *)(uintptr_t)h, callid, rec_off, rec_pcs, nrec, is_new, false);
+}
+
+extern "C" int64_t syzcov_state_add_inputs(syzcov_cover_state h, const int32_t *callid,
+                                           const uint64_t *rec_off, const uint32_t *rec_pcs,
+                                           size_t nrec, uint8_t *accepted) {
+    return newcov_host((CoverState *)(uintptr_t)h, callid, rec_off, rec_pcs, nrec, accepted, true);
 }

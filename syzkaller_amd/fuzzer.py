@@ -1,6 +1,7 @@
-"""Resident fuzzer-side coverage state: per-CallID maxCover + flakes on the
-GPU, and the batched new-coverage check of syz-fuzzer execute()
-(syz-fuzzer/fuzzer.go:456-480)."""
+"""Resident fuzzer-side coverage state: per-CallID maxCover, corpusCover and
+flakes on the GPU; the batched new-coverage check of syz-fuzzer execute()
+(syz-fuzzer/fuzzer.go:456-480), addInput (:344-375) and triageInput's
+coverage steps (:377-417)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -12,6 +13,16 @@ from ._lib import check, lib
 
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def _csr(lists):
+    """list of PC lists -> (off u64[n+1], pcs u32[max(total, 1)])."""
+    lens = np.fromiter((len(r) for r in lists), dtype=np.uint64, count=len(lists))
+    off = np.zeros(len(lists) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    pcs = (np.concatenate([np.asarray(r, dtype=np.uint32) for r in lists])
+           if len(lists) and off[-1] else np.zeros(1, dtype=np.uint32))
+    return off, np.ascontiguousarray(pcs, dtype=np.uint32)
 
 
 class CoverState:
@@ -51,6 +62,55 @@ class CoverState:
         out = np.empty(max(n, 1), dtype=np.uint32)
         n = check(lib().syzcov_state_get(self.h, call, _ptr(out), out.size), "state_get")
         return out[:n]
+
+    def corpus_add(self, call: int, pcs):
+        """corpusCover[call] = Union(corpusCover[call], pcs) (fuzzer.go:451)."""
+        a = np.ascontiguousarray(pcs, dtype=np.uint32)
+        check(lib().syzcov_state_corpus_add(self.h, call, _ptr(a), a.size), "state_corpus_add")
+
+    def corpus_cover(self, call: int) -> np.ndarray:
+        n = check(lib().syzcov_state_corpus_get(self.h, call, None, 0), "state_corpus_get")
+        out = np.empty(max(n, 1), dtype=np.uint32)
+        n = check(lib().syzcov_state_corpus_get(self.h, call, _ptr(out), out.size),
+                  "state_corpus_get")
+        return out[:n]
+
+    def flakes(self) -> np.ndarray:
+        n = check(lib().syzcov_state_flakes_get(self.h, None, 0), "state_flakes_get")
+        out = np.empty(max(n, 1), dtype=np.uint32)
+        n = check(lib().syzcov_state_flakes_get(self.h, _ptr(out), out.size), "state_flakes_get")
+        return out[:n]
+
+    def add_inputs(self, callids, covers) -> np.ndarray:
+        """addInput (fuzzer.go:344-375) for manager-pushed inputs in order
+        (covers already canonical): accepted[k]; accepted covers join
+        corpusCover and maxCover."""
+        cid = np.ascontiguousarray(callids, dtype=np.int32)
+        off, pcs = _csr(covers)
+        acc = np.zeros(max(len(covers), 1), dtype=np.uint8)
+        check(lib().syzcov_state_add_inputs(self.h, _ptr(cid), _ptr(off), _ptr(pcs), len(covers),
+                                            _ptr(acc)), "state_add_inputs")
+        return acc[:len(covers)]
+
+    def triage(self, callids, covers, runs):
+        """triageInput's coverage steps (fuzzer.go:377-417) for a batch:
+        covers[t] the input's cover, runs[t] its three re-execution covers
+        (empty = not executed).  Returns (len(newCover) per input,
+        stableNewCover per input); flakes grows by the runs' symmetric
+        differences (see syzcov_state_triage for the schedule)."""
+        n = len(covers)
+        assert len(runs) == n and all(len(r) == 3 for r in runs)
+        cid = np.ascontiguousarray(callids, dtype=np.int32)
+        coff, cpcs = _csr(covers)
+        roff, rpcs = _csr([r for rr in runs for r in rr])
+        new_cnt = np.zeros(max(n, 1), dtype=np.uint32)
+        st_cnt = np.zeros(max(n, 1), dtype=np.uint32)
+        st_pcs = np.zeros(max(cpcs.size, 1), dtype=np.uint32)
+        check(lib().syzcov_state_triage(self.h, n, _ptr(cid), _ptr(coff), _ptr(cpcs), _ptr(roff),
+                                        _ptr(rpcs), _ptr(new_cnt), _ptr(st_cnt), _ptr(st_pcs)),
+              "state_triage")
+        stable = [st_pcs[int(coff[t]):int(coff[t]) + int(st_cnt[t])].copy() for t in range(n)]
+        return new_cnt[:n], stable
 
     def new_coverage(self, callids, records) -> np.ndarray:
         """is_new[k] for a batch of executed call records, in batch order,

@@ -93,7 +93,15 @@ def test_new_inputs_vs_sequential():
     cc.close()
 
 
-def test_newcov_device_api_vs_oracle():
+@pytest.fixture(params=["lds", "probe"])
+def newcov_path(request, monkeypatch):
+    """Both candidate passes of newcov.hip: LDS-staged key ranges and global
+    bitmap probes (the library picks one per batch from its shape)."""
+    monkeypatch.setenv("SYZCOV_NEWCOV_PATH", request.param)
+    return request.param
+
+
+def test_newcov_device_api_vs_oracle(newcov_path):
     """syzcov_state_newcov_dev (batch already in HBM, async on torch's stream)
     == the sequential reference loop, incl. flakes and a rejected batch."""
     import ctypes as C
@@ -139,8 +147,43 @@ def test_newcov_device_api_vs_oracle():
     with pytest.raises(SyzcovError):
         st.new_coverage([1, 2], [np.array([lo + 5, lo + 9], np.uint32),
                                  np.array([lo + 9, lo + 5], np.uint32)])
+    # unsorted across a key-range boundary / non-monotone split points
+    with pytest.raises(SyzcovError):
+        st.new_coverage([3], [np.array([lo + span - 3, lo + 7, lo + span - 2], np.uint32)])
+    with pytest.raises(SyzcovError):  # below the window
+        st.new_coverage([3], [np.array([lo - 1, lo + 7], np.uint32)])
+    with pytest.raises(SyzcovError):  # call id out of range
+        st.new_coverage([ncalls], [np.array([lo + 7], np.uint32)])
     for c in range(ncalls):
         assert np.array_equal(st.max_cover(c), before[c])
+    st.close()
+
+
+def test_newcov_multi_range(newcov_path):
+    """A window of 2^22 PCs: the LDS pass cuts it into 4 key ranges, so records
+    cross range boundaries (sub-runs, pieces in the hash passes); trailing
+    sentinels; records of one call spread over several slices."""
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(38)
+    ncalls, lo, span = 5, 0x81000000, 1 << 22
+    st = CoverState(ncalls, lo, span)
+    flakes = np.unique(rng.integers(lo, lo + span, size=5000)).astype(np.uint32)
+    st.set_flakes(flakes)
+    mc = [[] for _ in range(ncalls)]
+    for batch in range(3):
+        nrec = 3000
+        cids = rng.integers(0, ncalls, size=nrec).astype(np.int32)
+        recs = []
+        for _ in range(nrec):
+            r = np.unique(rng.integers(lo, lo + span, size=int(rng.integers(0, 400))))
+            r = r.astype(np.uint32)
+            if rng.random() < 0.1:
+                r = np.append(r, np.uint32(0xFFFFFFFF))
+            recs.append(r)
+        exp, mc = orc.newcov_batch(mc, flakes, cids, recs)
+        assert np.array_equal(st.new_coverage(cids, recs), exp), batch
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
     st.close()
 
 
@@ -173,8 +216,31 @@ def test_newcov_sentinel_full_window():
     cc.close()
 
 
+def test_newcov_tiny_records(newcov_path):
+    """Many records of 0-3 PCs in few calls: one LDS work item's chunk covers
+    thousands of records (several 1024-record windows), and records straddle
+    chunk edges."""
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(39)
+    ncalls, lo, span = 2, 0x81000000, 1 << 21
+    st = CoverState(ncalls, lo, span)
+    mc = [[] for _ in range(ncalls)]
+    for batch in range(2):
+        nrec = 40000
+        cids = rng.integers(0, ncalls, size=nrec).astype(np.int32)
+        recs = [np.unique(rng.integers(lo, lo + int(rng.choice([64, span])),
+                                       size=int(rng.integers(0, 4)))).astype(np.uint32)
+                for _ in range(nrec)]
+        recs[7] = np.arange(lo, lo + 40000, dtype=np.uint32)  # one long record
+        exp, mc = orc.newcov_batch(mc, [], cids, recs)
+        assert np.array_equal(st.new_coverage(cids, recs), exp), batch
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
+    st.close()
+
+
 @pytest.mark.parametrize("spacing", ["random", "synthetic"])
-def test_newcov_key_mode(spacing):
+def test_newcov_key_mode(spacing, newcov_path):
     """Dense-key maxCover (state_set_universe, keys.hip) gives the reference's
     results for PCs of the universe; maxCover reads back as PCs; a PC outside
     the universe's key range is rejected; the universe is fixed once

@@ -226,3 +226,18 @@ def test_ui_stats_restatement():
     # per input: PCs held by exactly one input (3 and 4 are held twice)
     assert pyref.corpus_stats(calls, covs, "a") == [(0, 3, 2), (1, 2, 0)]
     assert pyref.corpus_stats(calls, covs, "c") == [(3, 2, 1)]
+
+
+def test_triage_oracle_kat():
+    """triageInput (fuzzer.go:377-417) worked by hand: newCover [2,3,4];
+    run 1 drops 4 and adds 5, run 2 drops 1, run 3 did not execute."""
+    from oracle import oracle as o
+    corpus = [np.zeros(0, np.uint32), np.array([1], np.uint32)]
+    new, stable, fl = o.triage_batch(corpus, [9], [1], [[1, 2, 3, 4]],
+                                     [[[1, 2, 3, 5], [2, 3, 4], []]])
+    assert new == [3] and stable[0].tolist() == [2, 3] and fl.tolist() == [1, 4, 5, 9]
+    # addInput: accepted iff something outside maxCover and flakes
+    mc = [np.zeros(0, np.uint32)]
+    cc = [np.zeros(0, np.uint32)]
+    assert o.add_inputs(mc, cc, [5], [0, 0, 0], [[5], [1, 5], [1]]) == [False, True, False]
+    assert mc[0].tolist() == [1, 5] and cc[0].tolist() == [1, 5]

@@ -3,7 +3,8 @@
 WRITE_SIZE in separate runs, MI355X_MICROARCH.md 'HBM'):
   bytes_read  = 2 * FETCH_SIZE[KB] * 1024   (gfx950 tallies 128-B requests at 64 B)
   bytes_write = WRITE_SIZE[KB] * 1024
-per step of each phase = sum over the phase's kernels of their per-step totals.  Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json]"""
+per step of each phase = sum over the phase's kernels of their per-step totals.
+Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json] [kernel run once per step]"""
 import collections
 import csv
 import glob
@@ -13,14 +14,19 @@ import sys
 
 PHASES = {
     "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
-              "large_"),
-    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel",
+              "keyify_list_kernel", "large_"),
+    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel", "first_to_bits_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
+    "newcov": ("newcov_", "hash_clear_kernel"),
+    "prio": ("prio_",),
     "order": ("gsort::",),
     "compact": ("compact_", "scan_blocks"),
     "union": ("dict_",),
     "merge": ("bitmap_op_kernel",),
 }
+
+
+STEP_KERNEL = "bin_kernel"
 
 
 def per_step(d, counter):
@@ -37,7 +43,7 @@ def per_step(d, counter):
             k = r["Kernel_Name"]
             tot[k] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
-    steps = max([len(v) for k, v in disp.items() if "bin_kernel" in k] or [1])
+    steps = max([len(v) for k, v in disp.items() if STEP_KERNEL in k] or [1])
     return {k: tot[k] / steps for k in tot}
 
 
@@ -48,7 +54,10 @@ def phase_of(name):
     return None
 
 
-def main(fd, wd, out=None):
+def main(fd, wd, out=None, step_kernel=None):
+    global STEP_KERNEL
+    if step_kernel:  # the kernel that runs once per step (default: canon's bin_kernel)
+        STEP_KERNEL = step_kernel
     fetch = per_step(fd, "FETCH_SIZE")
     write = per_step(wd, "WRITE_SIZE")
     res = {}
