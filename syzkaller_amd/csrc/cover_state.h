@@ -43,6 +43,11 @@ struct CoverState {
     uint32_t *maxcov = nullptr;  // ncalls x words
     uint32_t *corpus = nullptr;  // corpusCover: ncalls x words, allocated on first use
     uint32_t *flakes = nullptr;  // words
+    // maxCover[c] | flakes per call, the LDS-staged candidate pass's one test
+    // per PC; allocated on first use, rebuilt when marked stale (flakes or
+    // maxCover changed outside the newcov kernels, which keep it in step)
+    uint32_t *mfl = nullptr;
+    bool mfl_stale = true;
     uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
     // LDS-staged candidate pass: per-call record counts | offsets | cursors |
     // work-item prefix over (call, range) | work-item descriptors; one batch

@@ -199,23 +199,25 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
 // one scattered request per PC into a 150 MB set of bitmaps that no L2 holds
 // (C5: 132 M probes per batch).  Instead the index space is cut into ranges
 // of 2^19 keys (64 KB of bitmap): a workgroup stages one range of one call's
-// maxCover in LDS and tests a chunk of that (call, range)'s PCs there.
-//   records grouped by call:   grp_hist -> grp_scan -> grp_scatter (perm, pos)
+// maxCover (| flakes) in LDS and tests a chunk of that (call, range)'s PCs
+// there.
+//   records grouped by call:   grp_hist -> grp_scan -> grp_scatter (perm)
 //   sub-runs:                  nq[q][j] = grouped record j's PC count in range
 //                              q, Bq[q][j] = where that sub-run starts in pcs
-//   per-range streams:         nq scanned in place: Pq[q][j] = exclusive prefix
-//   work items:                (call, range, chunk of CH PCs of that stream),
-//                              one 16-byte descriptor each (desc_kernel)
+//   row streams:               each sub-run cut into rows of <= 256 PCs (16-byte
+//                              aligned: one dwordx4 per lane); Rq[q][j]
+//                              = exclusive prefix of row counts (range_scan),
+//                              one 16-byte row descriptor each (row_fill)
+//   work items:                (call, range, chunk of CHR rows of its stream)
 // The synthetic coverage is skewed (40% of PCs in range 0), so chunking by
-// PC count, not by record count, is what balances the workgroups.
+// rows, not by records, is what balances the workgroups.
 constexpr uint32_t NR_MAX = 32;          // ranges (index space <= 2^24)
 constexpr uint32_t RSH = 19;             // 2^19 indices (64 KB of bitmap) per range:
                                          // two workgroups per CU
 constexpr uint32_t ITEMS_MAX = 65536;    // chunk-count cap (items_target)
-constexpr int LC_THREADS = 1024;
-constexpr uint32_t LC_WIN = 512;         // records staged per window (LDS: two
-                                         // workgroups per CU = 2 x (64 + 8) KB)
-constexpr uint32_t LC_BATCH = 64 * NC_U; // PCs per wave batch
+constexpr int LC_THREADS = 1024;         // LDS: two workgroups per CU
+constexpr uint32_t LC_CBW = 16;          // candidates buffered per wave
+constexpr int LC_U = 4;                  // 256-PC rows per step (two steps in flight)
 constexpr int SQ_G = 8;                  // split queries in flight per wave
 
 // Range boundaries of every grouped record, one wave per record, by 64-way
@@ -310,31 +312,42 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
     }
 }
 
-// Exclusive scan of nq[q][0..m) in place for every range q, in chunks of
-// RS_CHUNK: pass 1 sums each chunk, pass 2 scans a chunk from the sum of the
-// chunks before it; nq[q][m] = the total.
+// rows of a sub-run of n PCs starting at pcs index b: 256-PC rows aligned to 4
+__device__ __forceinline__ uint32_t sub_rows(uint32_t n, uint64_t b) {
+    return n ? (uint32_t)(((b & 3) + n + 255) >> 8) : 0u;
+}
+
+// Row counts scanned exclusively into Rq[q][0..m) for every
+// range q, in chunks of RS_CHUNK: pass 1 sums each chunk, pass 2 scans a
+// chunk from the sum of the chunks before it; Rq[q][m] = the range's rows.
 constexpr uint32_t RS_CHUNK = 8192;
 
 __global__ __launch_bounds__(1024) void range_sum_kernel(const uint32_t *__restrict__ nq,
+                                                         const uint64_t *__restrict__ Bq,
                                                          uint32_t m, uint32_t stride,
                                                          uint32_t *__restrict__ csum) {
     __shared__ uint32_t tmp[1024 / 64 + 1];
     const uint32_t q = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
     const uint32_t *a = nq + (uint64_t)q * stride + (uint64_t)b * RS_CHUNK;
+    const uint64_t *bb = Bq + (uint64_t)q * stride + (uint64_t)b * RS_CHUNK;
     const uint32_t n = min(RS_CHUNK, m - b * RS_CHUNK);
     uint32_t v = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += a[i];
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) v += sub_rows(a[i], bb[i]);
     uint32_t tot;
     block_excl_scan<1024>(v, tmp, &tot);
     if (threadIdx.x == 0) csum[q * nb + b] = tot;
 }
 
-__global__ __launch_bounds__(1024) void range_scan_kernel(uint32_t *__restrict__ nq, uint32_t m,
-                                                          uint32_t stride,
-                                                          const uint32_t *__restrict__ csum) {
+__global__ __launch_bounds__(1024) void range_scan_kernel(const uint32_t *__restrict__ nq,
+                                                          const uint64_t *__restrict__ Bq,
+                                                          uint32_t m, uint32_t stride,
+                                                          const uint32_t *__restrict__ csum,
+                                                          uint32_t *__restrict__ Rq) {
     __shared__ uint32_t tmp[1024 / 64 + 1];
     const uint32_t q = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
-    uint32_t *a = nq + (uint64_t)q * stride;
+    const uint32_t *a = nq + (uint64_t)q * stride;
+    const uint64_t *bb = Bq + (uint64_t)q * stride;
+    uint32_t *R = Rq + (uint64_t)q * stride;
     uint32_t carry = 0;
     for (uint32_t i = 0; i < b; i++) carry += csum[q * nb + i];
     constexpr uint32_t PT = RS_CHUNK / 1024;
@@ -342,25 +355,25 @@ __global__ __launch_bounds__(1024) void range_scan_kernel(uint32_t *__restrict__
     uint32_t v[PT], sum = 0;
 #pragma unroll
     for (uint32_t u = 0; u < PT; u++) {
-        v[u] = i0 + u < m ? a[i0 + u] : 0u;
+        v[u] = i0 + u < m ? sub_rows(a[i0 + u], bb[i0 + u]) : 0u;
         sum += v[u];
     }
     uint32_t tot;
     uint32_t run = carry + block_excl_scan<1024>(sum, tmp, &tot);
 #pragma unroll
     for (uint32_t u = 0; u < PT; u++) {
-        if (i0 + u < m) a[i0 + u] = run;
+        if (i0 + u < m) R[i0 + u] = run;
         run += v[u];
     }
-    if (b == nb - 1 && threadIdx.x == 1023) a[m] = run;
+    if (b == nb - 1 && threadIdx.x == 1023) R[m] = run;
 }
 
-// Work-item prefix over (call, range) pairs e = c * nr + q: ceil(T_cq / CH)
-// items each, T_cq = the call's share of range q's stream.
+// Work-item prefix over (call, range) pairs e = c * nr + q: ceil(rows / CHR)
+// items each.
 __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restrict__ coff,
                                                          int ncalls, uint32_t nr,
-                                                         const uint32_t *__restrict__ Pq,
-                                                         uint32_t stride, uint32_t CH,
+                                                         const uint32_t *__restrict__ Rq,
+                                                         uint32_t stride, uint32_t CHR,
                                                          uint32_t *__restrict__ ipre) {
     __shared__ uint32_t tmp[1024 / 64 + 1];
     const uint32_t ne = (uint32_t)ncalls * nr;
@@ -370,8 +383,8 @@ __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restr
         uint32_t v = 0;
         if (e < ne) {
             const uint32_t c = e / nr, q = e - c * nr;
-            const uint32_t *P = Pq + (uint64_t)q * stride;
-            v = (P[coff[c + 1]] - P[coff[c]] + CH - 1) / CH;
+            const uint32_t *R = Rq + (uint64_t)q * stride;
+            v = (R[coff[c + 1]] - R[coff[c]] + CHR - 1) / CHR;
         }
         uint32_t tot;
         const uint32_t p = block_excl_scan<1024>(v, tmp, &tot);
@@ -382,144 +395,267 @@ __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restr
     if (threadIdx.x == 0) ipre[ne] = carry;
 }
 
-// Work-item descriptors {e = c * nr + q, F0, F1, first record}: chunk i of
-// pair e is stream positions [P0 + i CH, min(P0 + (i+1) CH, P1)) of range q,
-// and starts in the record j with P[j] <= F0 < P[j+1].  One wave per pair;
-// lane j finds the chunk starts inside its record.
+// Where each range's rows start in the row array: qoff[q] = sum of the
+// earlier ranges' row counts.
+__global__ void row_offsets_kernel(const uint32_t *__restrict__ Rq, uint32_t m, uint32_t stride,
+                                   uint32_t nr, uint32_t *__restrict__ qoff) {
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (uint32_t q = 0; q < nr; q++) {
+            qoff[q] = o;
+            o += Rq[(uint64_t)q * stride + m];
+        }
+        qoff[nr] = o;
+    }
+}
+
+// Work-item descriptors {e, first row, end row}: thread per pair e.
 __global__ __launch_bounds__(256) void desc_kernel(const uint32_t *__restrict__ coff, int ncalls,
-                                                   uint32_t nr, const uint32_t *__restrict__ Pq,
-                                                   uint32_t stride, uint32_t CH,
+                                                   uint32_t nr, const uint32_t *__restrict__ Rq,
+                                                   uint32_t stride, uint32_t CHR,
                                                    const uint32_t *__restrict__ ipre,
                                                    uint4 *__restrict__ desc) {
-    const uint32_t l = __lane_id(), ne = (uint32_t)ncalls * nr;
-    for (uint32_t e = blockIdx.x * 4 + (threadIdx.x >> 6); e < ne; e += gridDim.x * 4) {
+    const uint32_t ne = (uint32_t)ncalls * nr;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
         const uint32_t c = e / nr, q = e - c * nr;
-        const uint32_t *P = Pq + (uint64_t)q * stride;
-        const uint32_t j0 = coff[c], j1 = coff[c + 1];
-        const uint32_t P0 = P[j0], P1 = P[j1], base = ipre[e];
-        if (P1 == P0) continue;
-        for (uint32_t j = j0 + l; j < j1; j += 64) {
-            const uint32_t a = P[j] - P0, b = P[j + 1] - P0;
-            if (b <= a) continue;
-            for (uint32_t i = (a + CH - 1) / CH; (uint64_t)i * CH < b; i++) {
-                const uint32_t F0 = P0 + i * CH;
-                desc[base + i] = make_uint4(e, F0, min(F0 + CH, P1), j);
-            }
+        const uint32_t *R = Rq + (uint64_t)q * stride;
+        const uint32_t r0 = R[coff[c]], r1 = R[coff[c + 1]], base = ipre[e];
+        for (uint32_t i = 0; r0 + i * CHR < r1; i++)
+            desc[base + i] = make_uint4(e, r0 + i * CHR, min(r0 + (i + 1) * CHR, r1), 0u);
+    }
+}
+
+// Row descriptors of range q's stream, one thread per (grouped record, q):
+// {pcs index of the row's first element (a multiple of 4), record k, first
+// valid element | end element << 9 | "the row starts the sub-run" << 18
+// (its first valid PC has no predecessor to compare with), 0}.
+__global__ __launch_bounds__(256) void row_fill_kernel(const uint32_t *__restrict__ nq,
+                                                       const uint64_t *__restrict__ Bq,
+                                                       const uint32_t *__restrict__ Rq,
+                                                       const uint32_t *__restrict__ perm,
+                                                       const uint32_t *__restrict__ coff,
+                                                       int ncalls, uint32_t nr, uint32_t stride,
+                                                       const uint32_t *__restrict__ qoff,
+                                                       uint4 *__restrict__ rows) {
+    const uint32_t ng = coff[ncalls];
+    const uint64_t total = (uint64_t)ng * nr;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = (uint32_t)(i / ng), j = (uint32_t)(i - (uint64_t)q * ng);
+        const uint64_t x = (uint64_t)q * stride + j;
+        const uint32_t n = nq[x], r = Rq[x];
+        if (!n) continue;
+        const uint32_t b = (uint32_t)Bq[x], k = perm[j], a0 = b & ~3u, end = b + n;
+        uint4 *out = rows + qoff[q] + r;
+        for (uint32_t st = a0, i = 0; st < end; st += 256, i++) {
+            const uint32_t lo = st == a0 ? b - a0 : 0u, hi = min(256u, end - st);
+            out[i] = make_uint4(st, k, lo | hi << 9 | (st == a0 ? 1u << 18 : 0u), 0u);
         }
     }
 }
 
-// The candidate pass.  Work item w -> (call c, range q, stream positions
-// [F0, F1), first record) from its descriptor.  The chunk's records are
-// staged in windows of up to LC_WIN (stream start and PC base in LDS); the
-// 16 waves take 512-PC batches of the window round-robin, a lane finds its
-// record by walking the window's starts from the batch's first record.
-__global__ __launch_bounds__(LC_THREADS) void newcov_cand_lds_kernel(
-    const uint32_t *__restrict__ pcs, const uint32_t *__restrict__ maxcov, uint64_t words_per_call,
-    const uint32_t *__restrict__ flakes, Index X, uint32_t nr, const uint32_t *__restrict__ perm,
-    const uint32_t *__restrict__ coff, const uint32_t *__restrict__ ipre, uint32_t ne,
-    const uint4 *__restrict__ desc, const uint32_t *__restrict__ Pq,
-    const uint64_t *__restrict__ Bq, uint32_t stride, uint2 *__restrict__ clist,
-    uint32_t *__restrict__ stats) {
-    extern __shared__ uint4 s_m4[];  // (1 << RSH) / 128 uint4 of maxCover[call]
-    __shared__ uint32_t s_P[LC_WIN + 1], s_k[LC_WIN];
-    __shared__ uint64_t s_b[LC_WIN];  // pcs index of stream position 0 of record j
+// The candidate pass.  Work item w -> (call c, range q, rows [r0, r1) of
+// range q's row stream).  The workgroup stages (maxCover[c] | flakes) over
+// range q in LDS; each wave takes 64 consecutive rows at a time (one
+// descriptor per lane, read back wave-uniform with readlane) and streams
+// them NC_U rows per step through buffer loads (row base in an SGPR, lane
+// offset constant), the next step's loads in flight while the current step
+// is tested.  The staging loads and each wave's first step are in flight
+// together.  Per PC: one subtract (index relative to the range), one LDS
+// bit test, one compare with its predecessor (DPP wave shift).
+// Validity: the split pass checks each record's ends against the index
+// space and its range boundaries; a sorted record then has every PC of
+// sub-run q inside range q, so the only per-PC check is sortedness (stats
+// 3), which every unsorted record fails somewhere (the LDS index is masked,
+// so a stray PC of an unsorted record stays in bounds until the batch is
+// rejected).  KEY: dense keys (pc >> kshift) - kbase, else pc - pc_lo.
+// lanes [a, b) of a wave as a mask (a <= b <= 64)
+__device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {
+    const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+    const uint64_t lo = a >= 64 ? ~0ull : ((1ull << a) - 1ull);
+    return hi & ~lo;
+}
+
+// SGPRs capped: above 80 the hardware admits one 1024-thread workgroup per
+// CU instead of two (MI355X_MICROARCH.md, residency), whatever the
+// occupancy API reports.
+template <bool KEY>
+__global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72))) void newcov_cand_lds_kernel(
+    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
+    uint64_t words_per_call, Index X, uint32_t nr, const uint32_t *__restrict__ ipre, uint32_t ne,
+    const uint4 *__restrict__ desc, const uint4 *__restrict__ rows,
+    const uint32_t *__restrict__ qoff, uint2 *__restrict__ clist, uint32_t *__restrict__ stats,
+    uint32_t dbg, uint64_t *__restrict__ stamp) {
+    extern __shared__ uint4 s_m4[];  // (1 << RSH) / 128 uint4
+    __shared__ uint2 s_cb[LC_THREADS / 64 * LC_CBW];  // per wave: pending candidates
     const uint32_t t = threadIdx.x, w = blockIdx.x, l = __lane_id(), wv = t >> 6;
     if (w >= ipre[ne]) return;  // grid is an upper bound
+    const uint64_t ts0 = (dbg & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint4 d = desc[w];
-    const uint32_t e = d.x, c = e / nr, q = e - c * nr, F0 = d.y, F1 = d.z;
-    uint32_t jr = d.w;
-    const uint32_t j1 = coff[c + 1];
-    const uint32_t *P = Pq + (uint64_t)q * stride;
-    const uint64_t *B = Bq + (uint64_t)q * stride;
-    // stage maxCover[c] | flakes over indices [q << RSH, (q + 1) << RSH)
-    // (words_per_call is a multiple of 4), all loads issued before the LDS
-    // stores: one LDS test per PC decides "in neither" (the flakes range is
-    // read by every workgroup of range q and stays in L2)
+    const uint32_t e = d.x, c = e / nr, q = e - c * nr, r0 = d.y, r1 = d.z;
+    const uint4 *R = rows + qoff[q];
+    const __amdgpu_buffer_rsrc_t pr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)pcs, 0, npc * 4u, 0x00020000);
+    // staging loads of (maxCover[c] | flakes) over indices [q << RSH, (q+1) << RSH)
+    // (words_per_call is a multiple of 4)
     const uint64_t wbase = (uint64_t)q << (RSH - 5);
     const uint32_t nv = (uint32_t)(min<uint64_t>((uint64_t)1 << (RSH - 5), words_per_call - wbase) >> 2);
-    const uint4 *M4 = (const uint4 *)(maxcov + (uint64_t)c * words_per_call + wbase);
-    const uint4 *F4 = (const uint4 *)(flakes + wbase);
+    const uint4 *M4 = (const uint4 *)(mfl + (uint64_t)c * words_per_call + wbase);
     constexpr int SV = (1 << (RSH - 7)) / LC_THREADS;  // uint4 per thread
-    {
-        uint4 v[SV], f[SV];
+    uint4 sv[SV];
 #pragma unroll
-        for (int i = 0; i < SV; i++) {
-            const uint32_t j = t + i * LC_THREADS;
-            v[i] = j < nv ? M4[j] : make_uint4(0, 0, 0, 0);
-            f[i] = j < nv ? F4[j] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < SV; i++) {
-            const uint32_t j = t + i * LC_THREADS;
-            if (j < nv)
-                s_m4[j] = make_uint4(v[i].x | f[i].x, v[i].y | f[i].y, v[i].z | f[i].z, v[i].w | f[i].w);
-        }
+    for (int i = 0; i < SV; i++) {
+        const uint32_t j = t + i * LC_THREADS;
+        sv[i] = M4[j < nv ? j : 0u];  // (selected at the LDS store)
     }
     const uint32_t *s_m = (const uint32_t *)s_m4;
-    const uint32_t kbase_r = q << RSH;
-    uint32_t bad = 0;
-    for (;;) {
-        // window: records [jr, jr + nwin), stream starts s_P[0..nwin]
-        const uint32_t nwin = min(LC_WIN, j1 - jr);
-        if (t == 0) s_P[nwin] = P[jr + nwin];
-        if (t < nwin) {
-            const uint32_t p0 = P[jr + t];
-            s_P[t] = p0;
-            s_k[t] = perm[jr + t];
-            s_b[t] = B[jr + t] - p0;
-        }
-        __syncthreads();
-        const uint32_t W0 = max(F0, s_P[0]), W1 = min(F1, s_P[nwin]);
-        for (uint32_t f0 = W0 + wv * LC_BATCH; f0 < W1; f0 += LC_THREADS / 64 * LC_BATCH) {
-            uint32_t lo = 0, hi = nwin;  // largest r with s_P[r] <= f0
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_P[mid] <= f0) lo = mid; else hi = mid;
-            }
-            uint32_t r = lo;
-            uint32_t pc[NC_U], rr[NC_U];
-#pragma unroll
-            for (int u = 0; u < NC_U; u++) {
-                const uint32_t f = f0 + u * 64 + l;
-                if (f < W1) {
-                    while (s_P[r + 1] <= f) r++;
-                    rr[u] = r;
-                    pc[u] = pcs[s_b[r] + f];
-                } else {
-                    rr[u] = 0xFFFFFFFFu;
-                    pc[u] = 0;
-                }
-            }
-            // the PC before the batch, for the sortedness check of its first PC
-            uint32_t carry = 0;
-            if (f0 > s_P[lo]) carry = pcs[s_b[lo] + f0 - 1];
-#pragma unroll
-            for (int u = 0; u < NC_U; u++) {
-                const uint32_t f = f0 + u * 64 + l;
-                const bool live = rr[u] != 0xFFFFFFFFu;
-                uint32_t prev = __shfl_up(pc[u], 1, 64);
-                if (l == 0) prev = carry;
-                carry = __builtin_amdgcn_readlane(pc[u], 63);
-                uint32_t key = 0;
-                const bool inw = pc_index(X, pc[u], &key);
-                const uint32_t o = key - kbase_r;
-                const bool ok = live && inw && o < (1u << RSH) && pc[u] != SENT;
-                // outside the index space: 1; a sentinel or a PC of another
-                // range inside a sub-run (only an unsorted record puts them
-                // there) or out of order: 3
-                bad |= (uint32_t)(live && !inw && pc[u] != SENT) | ((uint32_t)(live && !ok) << 1);
-                if (live && f > s_P[rr[u]] && prev > pc[u]) bad |= 2u;
-                const bool cand = ok && !((s_m[o >> 5] >> (o & 31)) & 1u);
-                emit_cands(cand, live ? s_k[rr[u]] : 0u, pc[u], clist, stats);
+    const uint32_t obase = (KEY ? X.kbase : X.pc_lo) + (q << RSH);
+    const uint32_t ks = KEY ? X.kshift : 0u;
+    uint64_t bad = 0;  // lanes that saw a PC below its predecessor
+    uint4 my = make_uint4(0, 0, 0, 0);
+    uint32_t nrow = 0, p0v = 0;
+    uint2 *cb = s_cb + wv * LC_CBW;
+    uint32_t nc = 0;  // candidates in cb (wave-uniform)
+    auto flush = [&]() {
+        uint32_t base = 0;
+        if (l == 0) base = atomicAdd(&stats[1], nc);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (l < nc) clist[base + l] = cb[l];
+        nc = 0;
+    };
+    auto emit = [&](bool cand, uint32_t k, uint32_t pc) {
+        // candidates collect in the wave's LDS buffer (no global atomic round
+        // trip in the loop)
+        const uint64_t m = __ballot(cand);
+        if (m) {
+            const uint32_t n = (uint32_t)__popcll(m);
+            const uint32_t rank = (uint32_t)__popcll(m & ((1ull << l) - 1ull));
+            if (nc + n > LC_CBW) flush();
+            if (n > LC_CBW) {  // a row with many: straight to the list
+                uint32_t base = 0;
+                if (l == 0) base = atomicAdd(&stats[1], n);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (cand) clist[base + rank] = make_uint2(k, pc);
+            } else {
+                if (cand) cb[nc + rank] = make_uint2(k, pc);
+                nc += n;
             }
         }
-        jr += nwin;
-        const bool more = jr < j1 && s_P[nwin] < F1;
-        __syncthreads();  // window arrays are rewritten next
-        if (!more) break;
+    };
+    // the 64 rows' descriptors (lane i: row rb + i) and the PC before each
+    // row (0 when the row starts its sub-run: nothing to compare against)
+    // this wave's rows: an even share of the item's, contiguous
+    const uint32_t per = (r1 - r0 + LC_THREADS / 64 - 1) / (LC_THREADS / 64);
+    const uint32_t w0 = min(r1, r0 + wv * per), w1 = min(r1, w0 + per);
+    auto rows64 = [&](uint32_t rb_) {
+        nrow = min(64u, w1 - rb_);
+        const uint4 dsc = R[rb_ + min(l, nrow - 1)];
+        my = l < nrow ? dsc : make_uint4(dsc.x, 0, 0, 0);  // past the end: no valid element
+        const bool need = l < nrow && !(my.z >> 18 & 1u);
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(pr, need ? (my.x - 1) * 4u : 0xFFFFFFF0u, 0, 0);
+        p0v = need ? v : 0u;
+    };
+    // loads of rows [s0, s0 + NC_U) of the current 64: lane l holds elements
+    // 4l .. 4l+3 of a row; a lane with none valid reads past the buffer's end
+    // (returns 0, fetches nothing)
+    auto issue = [&](uint32_t s0, uint4 *pc) {
+#pragma unroll
+        for (int u = 0; u < LC_U; u++) {
+            const uint32_t i = (s0 + u) & 63;
+            const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
+            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
+            const bool any = s0 + u < nrow && 4 * l + 3 >= lo && 4 * l < hi;
+            pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  pr, any ? l * 16u : 0xFFFFFFF0u, any ? ra * 4u : 0u, 0));
+        }
+    };
+    uint32_t sink = 0;
+    auto test = [&](uint32_t s0, const uint4 *pc) {
+        if (dbg & 32) {  // timing probe: loads only
+#pragma unroll
+            for (int u = 0; u < LC_U; u++) sink += pc[u].x ^ pc[u].w;
+            return;
+        }
+#pragma unroll
+        for (int u = 0; u < LC_U; u++) {
+            if (s0 + u >= nrow) break;  // wave-uniform
+            const uint32_t i = (s0 + u) & 63;
+            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
+            const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
+            // bitmap words of the four components (the word index is masked
+            // into the staged range, so reads are unconditional and in flight
+            // together)
+            uint32_t o[4], wd[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                o[c] = (KEY ? v[c] >> ks : v[c]) - obase;
+                wd[c] = s_m[(o[c] >> 5) & ((1u << (RSH - 5)) - 1)];
+            }
+            // element 4l's predecessor: lane l-1's last element (DPP wave shift),
+            // for lane 0 the PC before the row
+            const uint32_t p0 =
+                __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                // lanes whose element 4l + c is valid / has a predecessor in the
+                // sub-run to compare with (scalar masks)
+                const uint64_t vm = lane_range(lo > (uint32_t)c ? (lo - c + 3) >> 2 : 0u,
+                                               hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
+                const uint32_t lo1 = first ? lo + 1 : lo;
+                const uint64_t pm = lane_range(lo1 > (uint32_t)c ? (lo1 - c + 3) >> 2 : 0u,
+                                               hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
+                bad |= __ballot((c ? v[c - 1] : p0) > v[c]) & pm;
+                const uint64_t cm = __ballot(!((wd[c] >> (o[c] & 31)) & 1u)) & vm;
+                if (cm) emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);  // rare
+            }
+        }
+    };
+    uint4 pcA[LC_U], pcB[LC_U];
+    uint32_t rb = w0;
+    if (rb < w1) {  // this wave's first step, in flight with the staging loads
+        rows64(rb);
+        issue(0, pcA);
     }
-    if (bad) stats[0] = (bad & 1u) ? 1u : 3u;
+#pragma unroll
+    for (int i = 0; i < SV; i++) {
+        const uint32_t j = t + i * LC_THREADS;
+        s_m4[j] = j < nv && !(dbg & 1) ? sv[i] : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    __syncthreads();
+    const uint64_t ts1 = (dbg & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (dbg & 2) return;  // timing probe: staging and first loads only
+    for (; rb < w1; rb += 64) {
+        if (rb != w0) {
+            rows64(rb);
+            issue(0, pcA);
+        }
+        // unconditional issues: a load under a branch makes the compiler drain
+        // every load at the loop head, which would serialise the two buffers
+        for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * LC_U) {
+            issue(s0 + LC_U, pcB);
+            test(s0, pcA);
+            issue(s0 + 2 * LC_U, pcA);
+            test(s0 + LC_U, pcB);
+        }
+    }
+    if (nc) flush();
+    if (sink == 0x9E3779B9u) stats[2] = sink;
+    if (bad && l == 0) stats[0] = 3u;
+    if (dbg & 8) {  // timing probe: per-workgroup stamps (100 MHz clock)
+        __syncthreads();
+        if (t == 0) {
+            stamp[4 * w] = ts0;
+            stamp[4 * w + 1] = ts1;
+            stamp[4 * w + 2] = __builtin_amdgcn_s_memrealtime();
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
+            stamp[4 * w + 3] = (uint64_t)(r1 - r0) | (uint64_t)q << 24 |
+                               (uint64_t)((hw >> 8) & 0xFF) << 32 | (uint64_t)(hw >> 13 & 7) << 40 |
+                               (uint64_t)(xcc & 15) << 48;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -583,7 +719,7 @@ __global__ __launch_bounds__(256) void newcov_own_kernel(
     const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
     const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
-    uint32_t *__restrict__ maxcov, uint64_t words_per_call, Index X) {
+    uint32_t *__restrict__ maxcov, uint32_t *__restrict__ mfl, uint64_t words_per_call, Index X) {
     if (stats[0] || !stats[1]) return;
     const uint32_t n = stats[1];
     const uint64_t mask = hash_cap(n) - 1;
@@ -598,7 +734,18 @@ __global__ __launch_bounds__(256) void newcov_own_kernel(
             uint32_t ix;
             pc_index(X, kp.y, &ix);  // candidates are inside (checked by the cand pass)
             atomicOr(&maxcov[(uint64_t)c * words_per_call + (ix >> 5)], 1u << (ix & 31));
+            if (mfl) atomicOr(&mfl[(uint64_t)c * words_per_call + (ix >> 5)], 1u << (ix & 31));
         }
+    }
+}
+
+// mfl[c] = maxcov[c] | flakes for every call
+__global__ void mfl_build_kernel(const uint4 *__restrict__ maxcov, const uint4 *__restrict__ flakes,
+                                 uint64_t vec_per_call, uint64_t n, uint4 *__restrict__ mfl) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 m = maxcov[i], f = flakes[i % vec_per_call];
+        mfl[i] = make_uint4(m.x | f.x, m.y | f.y, m.z | f.z, m.w | f.w);
     }
 }
 
@@ -697,7 +844,9 @@ static int alloc_maps(CoverState *st) {
     if (st->maxcov) hipFree(st->maxcov);
     if (st->flakes) hipFree(st->flakes);
     if (st->corpus) hipFree(st->corpus);
-    st->maxcov = st->flakes = st->corpus = nullptr;
+    if (st->mfl) hipFree(st->mfl);
+    st->maxcov = st->flakes = st->corpus = st->mfl = nullptr;
+    st->mfl_stale = true;
     st->words = ((st->X.span + 127) / 128) * 4;  // 16-byte rows (LDS staging)
     if (!st->grp && hipMalloc(&st->grp, grp_bytes(st->ncalls)) != hipSuccess)
         return SYZCOV_ENOMEM;
@@ -747,6 +896,7 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     hipFree(st->maxcov);
     hipFree(st->flakes);
     if (st->corpus) hipFree(st->corpus);
+    if (st->mfl) hipFree(st->mfl);
     if (st->pc_of_key) hipFree(st->pc_of_key);
     if (st->grp) hipFree(st->grp);
     if (st->scratch) hipFree(st->scratch);
@@ -809,6 +959,7 @@ extern "C" int syzcov_state_add(syzcov_cover_state h, int call, const uint32_t *
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     st->dirty = true;
+    st->mfl_stale = true;
     return set_bits(st, st->maxcov + (size_t)call * st->words, pcs, n);
 }
 
@@ -895,6 +1046,7 @@ extern "C" int syzcov_state_set_flakes(syzcov_cover_state h, const uint32_t *pcs
     std::lock_guard<std::mutex> g(st->mu);
     hipSetDevice(st->dev);
     SYZ_HIP(hipMemsetAsync(st->flakes, 0, st->words * 4, st->s));
+    st->mfl_stale = true;
     return set_bits(st, st->flakes, pcs, n);
 }
 
@@ -909,10 +1061,11 @@ extern "C" int64_t syzcov_state_get(syzcov_cover_state h, int call, uint32_t *ou
 }
 
 // device workspace: clist uint2[npc] | perm u32[nrec] | nq u32[NR_MAX x (nrec + 1)] |
-//   Bq u64[NR_MAX x (nrec + 1)] | csum u32[chunks x NR_MAX] | hkey u64[cap] |
+//   Bq u64[NR_MAX x (nrec + 1)] | Rq u32[NR_MAX x (nrec + 1)] | csum u32[chunks x NR_MAX] |
+//   qoff u32[NR_MAX + 1] | rows uint4[npc / 64 + min(npc, nrec x NR_MAX)] | hkey u64[cap] |
 //   hval u32[cap] | stats
 struct NcLayout {
-    size_t perm, nq, bq, csum, hkey, hval, stats, end;
+    size_t perm, nq, bq, rq, csum, qoff, rows, hkey, hval, stats, end;
 };
 static NcLayout nc_layout(size_t nrec, uint64_t npc) {
     uint64_t cap = 1024;
@@ -921,8 +1074,12 @@ static NcLayout nc_layout(size_t nrec, uint64_t npc) {
     L.perm = align_up(npc * 8 + 8, 256);
     L.nq = align_up(L.perm + nrec * 4 + 4, 256);
     L.bq = align_up(L.nq + (nrec + 1) * NR_MAX * 4, 256);
-    L.csum = align_up(L.bq + (nrec + 1) * NR_MAX * 8, 256);
-    L.hkey = align_up(L.csum + ((nrec + RS_CHUNK - 1) / RS_CHUNK) * NR_MAX * 4 + 4, 256);
+    L.rq = align_up(L.bq + (nrec + 1) * NR_MAX * 8, 256);
+    L.csum = align_up(L.rq + (nrec + 1) * NR_MAX * 4, 256);
+    L.qoff = align_up(L.csum + ((nrec + RS_CHUNK - 1) / RS_CHUNK) * NR_MAX * 4 + 4, 256);
+    L.rows = align_up(L.qoff + (NR_MAX + 1) * 4, 256);
+    const uint64_t nrows = npc / 256 + 2 * std::min<uint64_t>(npc, (uint64_t)nrec * NR_MAX) + 1;
+    L.hkey = align_up(L.rows + nrows * 16, 256);
     L.hval = align_up(L.hkey + cap * 8, 256);
     L.stats = align_up(L.hval + cap * 4, 256);
     L.end = L.stats + 256;
@@ -940,6 +1097,41 @@ extern "C" size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc) {
 static int env_path() {  // read per batch (tests switch it)
     const char *e = getenv("SYZCOV_NEWCOV_PATH");
     return e ? (!strcmp(e, "lds") ? 1 : !strcmp(e, "probe") ? 2 : 0) : 0;
+}
+static uint32_t env_dbg() {  // timing probes of the LDS pass (results invalid)
+    const char *e = getenv("SYZCOV_NC_DBG");
+    return e ? (uint32_t)atoi(e) : 0u;
+}
+// timing probe (SYZCOV_NC_DBG & 8): per-workgroup stamps of the LDS pass,
+// summarised to SYZCOV_NC_STAMP_FILE after each launch
+static uint64_t *g_stamp = nullptr;
+static size_t g_stamp_n = 0;
+static uint64_t *stamp_buf(uint64_t items) {
+    if (!(env_dbg() & 8)) return nullptr;
+    if (g_stamp_n < items) {
+        if (g_stamp) hipFree(g_stamp);
+        g_stamp = nullptr;
+        if (hipMalloc(&g_stamp, items * 32) != hipSuccess) return nullptr;
+        g_stamp_n = items;
+    }
+    hipMemset(g_stamp, 0, items * 32);
+    return g_stamp;
+}
+static void stamp_dump(hipStream_t s, uint64_t items) {
+    const char *fn = getenv("SYZCOV_NC_STAMP_FILE");
+    if (!g_stamp || !fn) return;
+    std::vector<uint64_t> h(items * 4);
+    hipStreamSynchronize(s);
+    hipMemcpy(h.data(), g_stamp, items * 32, hipMemcpyDeviceToHost);
+    FILE *f = fopen(fn, "a");
+    if (!f) return;
+    for (uint64_t w = 0; w < items; w++)
+        if (h[4 * w + 2])
+            fprintf(f, "%llu %llu %llu %llu %llu\n", (unsigned long long)w,
+                    (unsigned long long)h[4 * w], (unsigned long long)h[4 * w + 1],
+                    (unsigned long long)h[4 * w + 2], (unsigned long long)h[4 * w + 3]);
+    fprintf(f, "--\n");
+    fclose(f);
 }
 static uint32_t env_items() {
     static const uint32_t v = [] {
@@ -982,42 +1174,78 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     const uint64_t nr64 = (st->X.span + (1ull << RSH) - 1) >> RSH;
     const int forced = env_path();
     const uint64_t range_bytes = std::min<uint64_t>(st->words * 4, 1u << (RSH - 3));
-    const bool lds = nr64 <= NR_MAX &&
+    const bool lds = nr64 <= NR_MAX && npc < (1ull << 30) &&  // buffer offsets: 4 GB of PCs
                      (forced == 1 ||
                       (forced == 0 && 2 * nr64 * (uint64_t)nc * range_bytes <= npc * 4));
     if (lds) {
-        static std::atomic<uint32_t> lds_done{0};
-        int rc = set_dyn_lds_once((const void *)newcov_cand_lds_kernel, 1 << (RSH - 3), lds_done);
+        if (!st->mfl) {
+            if (hipMalloc(&st->mfl, (size_t)st->ncalls * st->words * 4) != hipSuccess) {
+                st->mfl = nullptr;
+                return SYZCOV_ENOMEM;
+            }
+            st->mfl_stale = true;
+        }
+        if (st->mfl_stale) {
+            const uint64_t vpc = st->words / 4, nv = vpc * st->ncalls;
+            hipLaunchKernelGGL(mfl_build_kernel, dim3(grid_for(nv, 256, 16384)), dim3(256), 0, s,
+                               (const uint4 *)st->maxcov, (const uint4 *)st->flakes, vpc, nv,
+                               (uint4 *)st->mfl);
+            st->mfl_stale = false;
+        }
+        static std::atomic<uint32_t> lds_done[2];
+        auto kfn = st->X.key_mode ? newcov_cand_lds_kernel<true> : newcov_cand_lds_kernel<false>;
+        int rc = set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[st->X.key_mode ? 1 : 0]);
         if (rc) return rc;
         const uint32_t nr = (uint32_t)nr64, stride = (uint32_t)nrec + 1;
         uint4 *desc = (uint4 *)((uint8_t *)st->grp + grp_desc_off(st->ncalls));
         uint32_t *nq = (uint32_t *)(ws + Lw.nq), *csum = (uint32_t *)(ws + Lw.csum);
+        uint32_t *rq = (uint32_t *)(ws + Lw.rq), *qoff = (uint32_t *)(ws + Lw.qoff);
         uint64_t *bq = (uint64_t *)(ws + Lw.bq);
-        // chunk: about env_items() work items over the batch, >= 16 K PCs
-        const uint32_t CH = (uint32_t)std::max<uint64_t>(16384, (npc + env_items() - 1) / env_items());
-        // sub-runs of the grouped records; the grid covers every record
-        // (records with a bad call id are not grouped: coff[nc] <= nrec)
+        uint4 *rows = (uint4 *)(ws + Lw.rows);
+        // chunk: about env_items() work items over the batch, >= 64 rows, and
+        // rows <= nrows / CHR <= ITEMS_MAX, so the descriptors fit ITEMS_MAX +
+        // the pairs
+        const uint64_t nrows = npc / 256 + 2 * std::min<uint64_t>(npc, (uint64_t)nrec * nr) + 1;
+        const uint64_t est = npc / 256 + (uint64_t)nrec * nr / 2;  // ~half a row of slack per sub-run
+        const uint32_t CHR = (uint32_t)std::max<uint64_t>(
+            std::max<uint64_t>(64, (est + env_items() - 1) / env_items()),
+            (nrows + ITEMS_MAX - 1) / ITEMS_MAX);
+        // sub-runs of the grouped records (records with a bad call id are not
+        // grouped: coff[nc] <= nrec)
         hipLaunchKernelGGL(newcov_split_kernel, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0, s,
                            rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls,
                            st->X, nr, stride, nq, bq, stats);
         const uint32_t nb = (uint32_t)((nrec + RS_CHUNK - 1) / RS_CHUNK);
         hipLaunchKernelGGL(range_sum_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
-                           (uint32_t)nrec, stride, csum);
-        hipLaunchKernelGGL(range_scan_kernel, dim3(nb, nr), dim3(1024), 0, s, nq, (uint32_t)nrec,
-                           stride, (const uint32_t *)csum);
+                           (const uint64_t *)bq, (uint32_t)nrec, stride, csum);
+        hipLaunchKernelGGL(range_scan_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
+                           (const uint64_t *)bq, (uint32_t)nrec, stride, (const uint32_t *)csum, rq);
         hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
-                           st->ncalls, nr, (const uint32_t *)nq, stride, CH, ipre);
+                           st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre);
+        hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(64), 0, s, (const uint32_t *)rq,
+                           (uint32_t)nrec, stride, nr, qoff);
         const uint32_t ne = nc * nr;
-        hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 4, 4096)), dim3(256), 0, s,
-                           (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)nq, stride, CH,
+        hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, s,
+                           (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)rq, stride, CHR,
                            (const uint32_t *)ipre, desc);
-        // items <= npc / CH + non-empty (call, range) pairs; the excess exits
-        const uint64_t items = npc / CH + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
-        hipLaunchKernelGGL(newcov_cand_lds_kernel, dim3((unsigned)items), dim3(LC_THREADS),
-                           (size_t)range_bytes, s, pcs, (const uint32_t *)st->maxcov, st->words,
-                           (const uint32_t *)st->flakes, st->X, nr, (const uint32_t *)perm,
-                           (const uint32_t *)coff, (const uint32_t *)ipre, ne, (const uint4 *)desc,
-                           (const uint32_t *)nq, (const uint64_t *)bq, stride, clist, stats);
+        hipLaunchKernelGGL(row_fill_kernel, dim3(grid_for((uint64_t)nrec * nr, 256, 16384)),
+                           dim3(256), 0, s, (const uint32_t *)nq, (const uint64_t *)bq,
+                           (const uint32_t *)rq, (const uint32_t *)perm, (const uint32_t *)coff,
+                           st->ncalls, nr, stride, (const uint32_t *)qoff, rows);
+        // items <= rows / CHR + non-empty (call, range) pairs; the excess exits
+        const uint64_t items = nrows / CHR + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
+        hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS), (size_t)(1u << (RSH - 3)), s, pcs,
+                           (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
+                           st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
+                           (const uint4 *)rows, (const uint32_t *)qoff, clist, stats, env_dbg(),
+                           stamp_buf(items));
+        if (env_dbg() & 8) stamp_dump(s, items);
+        if (env_dbg() & 16) {  // timing probe: occupancy of the LDS pass
+            int nb = 0;
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, LC_THREADS, 1u << (RSH - 3));
+            fprintf(stderr, "newcov LDS pass: %d workgroups/CU, %llu launched\n", nb,
+                    (unsigned long long)items);
+        }
     } else {
         const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
         hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off,
@@ -1031,7 +1259,7 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                        (const uint2 *)clist, (const uint32_t *)stats, hkey, hval);
     hipLaunchKernelGGL(newcov_own_kernel, dim3(gh), dim3(256), 0, s, callid, (const uint2 *)clist,
                        (const uint32_t *)stats, (const unsigned long long *)hkey,
-                       (const uint32_t *)hval, is_new, st->maxcov, st->words, st->X);
+                       (const uint32_t *)hval, is_new, st->maxcov, st->mfl, st->words, st->X);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
@@ -1101,6 +1329,7 @@ static int64_t newcov_host(CoverState *st, const int32_t *callid, const uint64_t
                            (const uint8_t *)(S + o_new), (const uint32_t *)dstats, st->maxcov,
                            st->corpus, st->words, st->X);
         SYZ_LAUNCH_CHECK();
+        st->mfl_stale = true;
     }
     uint32_t hs[2];
     SYZ_HIP(hipMemcpyAsync(hs, dstats, 8, hipMemcpyDeviceToHost, s));

@@ -282,6 +282,7 @@ extern "C" int64_t syzcov_state_triage(syzcov_cover_state h, size_t ntri, const 
                        (uint32_t)ntri, d_coff, d_cpcs, d_roff, d_rpcs, st->flakes, st->X, d_mark,
                        (const uint32_t *)d_new, d_scnt, d_spcs, (const uint32_t *)d_err);
     SYZ_LAUNCH_CHECK();
+    st->mfl_stale = true;  // flakes may have grown
     uint32_t herr = 0;
     SYZ_HIP(hipMemcpyAsync(&herr, d_err, 4, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(new_cnt, d_new, ntri * 4, hipMemcpyDeviceToHost, s));

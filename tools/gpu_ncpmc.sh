@@ -4,9 +4,9 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ncp
 i=0
-for ctr in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU" "FETCH_SIZE" "SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD"; do
+for ctr in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU" "FETCH_SIZE" "SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  SYZCOV_NEWCOV_PATH=${NCPATH:-lds} timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "newcov_cand|synth_pcs" --output-format csv -d gpurun_out/ncp/p$i -o run -- python3 bench.py --workload newcov --steps 5 --warmup 2 --no-cpu > gpurun_out/ncp/p$i.log 2>&1 || { tail -5 gpurun_out/ncp/p$i.log; exit 1; }
+  SYZCOV_NEWCOV_PATH=${NCPATH:-lds} timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "newcov_cand|newcov_split" --output-format csv -d gpurun_out/ncp/p$i -o run -- python3 bench.py --workload newcov --steps 5 --warmup 2 --no-cpu > gpurun_out/ncp/p$i.log 2>&1 || { tail -5 gpurun_out/ncp/p$i.log; exit 1; }
 done
 python3 - <<'PY'
 import csv, glob, collections
