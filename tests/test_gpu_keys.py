@@ -75,3 +75,29 @@ def test_engine_key_mode_window_error(torch):
                        universe=synth_universe(log2, 0x5EED0002))
     with pytest.raises(RuntimeError):
         eng.step(off, raw, n)
+
+
+@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
+def test_engine_offsets_past_2_32(torch, keys):
+    """Inputs stored past element 2^32 + 2^31 of the PC array (as in C3's
+    82 GB corpus): 64-bit CSR offsets whose low halves are >= 2^31 reach every
+    kernel (the whole-wave minimize path once read them sign-extended).  Long
+    inputs take the whole-wave path; canonicalized in place."""
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, seed, log2, base = 3000, 0x5EED0002, 20, (1 << 32) + (1 << 31) + 3
+    off, raw, lens, total = synth_corpus(n, seed, mean=2048, sigma=512, log2_space=log2)
+    big = torch.empty(base + total + 1, dtype=torch.int32, device="cuda")
+    big[base:base + total + 1].copy_(raw)
+    offb = off + base
+    del raw
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, base + total, int(lens.max().item()), lo, span, canon_in_place=True,
+                       universe=synth_universe(log2, seed) if keys else None)
+    res = eng.step(offb, big, n)
+    o_off, o_pcs = orc.synth_corpus(seed, n, mean=2048, sigma=512, log2_space=log2)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
+    del big
+    torch.cuda.empty_cache()
