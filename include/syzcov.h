@@ -57,12 +57,13 @@ extern "C" {
 const char *syzcov_version(void);
 /* Human-readable text for the last error on this thread. */
 const char *syzcov_last_error(void);
-/* Device contexts (stream + arenas) the pool has created on `device`: calls
- * lease one for their duration, so this is the peak number of concurrent
- * callers, independent of how many OS threads ever called in. */
+/* Device contexts (stream + arenas) the pool holds on `device`: calls lease
+ * one for their duration, so this is the peak number of concurrent callers
+ * since the last trim, independent of how many OS threads ever called in. */
 int64_t syzcov_pool_contexts(int device);
-/* Free the arenas of every idle pooled context (a call keeps up to 3 x 32 MB
- * of arena per context between calls; larger ones are freed as it returns). */
+/* Destroy every idle pooled context: its arenas (a call keeps up to 3 x 32 MB
+ * between calls; larger ones are freed as it returns) and its stream.  Later
+ * calls create contexts again as needed. */
 int syzcov_pool_trim(void);
 
 /* ======================= 1. drop-in host API ========================= */

@@ -39,6 +39,7 @@ constexpr int SMALL = 4096;  // segment finished in one workgroup's LDS
 #define SYZ_GSORT_TINY 32
 #endif
 constexpr int TINY = SYZ_GSORT_TINY;  // leaf finished by one lane
+static_assert(TINY <= 64, "leaf pdqsort: BitStack holds 3 parked tasks of a <= 64-element leaf");
 constexpr int CH = 4096;     // elements per block in the global rounds
 constexpr int WG = 256;
 
@@ -736,7 +737,7 @@ __global__ __launch_bounds__(WG) void small_kernel(const Seg *__restrict__ small
         const int nt = sh[1];
         for (int q = threadIdx.x; q < nt; q += WG) {
             const LTask lt = tiny[q];
-            gocore::pdq_loop<LAcc, 12>(d, gocore::Task{a + lt.a, a + lt.b, lt.limit,
+            gocore::pdq_loop<LAcc, 3, gocore::BitStack>(d, gocore::Task{a + lt.a, a + lt.b, lt.limit,
                                                        (bool)(lt.flags & 1),
                                                        (bool)(lt.flags & 2)});
         }

@@ -173,13 +173,52 @@ struct Task {
     bool wb, wp;
 };
 
-template <class D, int STACK = 40>
-__host__ __device__ inline void pdq_loop(D &d, Task t0) {
-    Task st[STACK];
+// Task stacks: an array (host), or registers (device leaves: an array indexed
+// by the stack pointer would live in scratch memory, which the HIP runtime
+// then keeps allocated per queue, ~100 MB each).  The parked side is the
+// larger one and the loop continues on the smaller (<= half), so the depth is
+// at most log2(n) (<= 5 for the 32-element leaves).
+template <int N>
+struct ArrayStack {
+    Task e[N];
     int sp = 0;
-    st[sp++] = t0;
-    while (sp) {
-        Task t = st[--sp];
+    __host__ __device__ void push(const Task &t) { e[sp++] = t; }
+    __host__ __device__ Task pop() { return e[--sp]; }
+};
+// Leaf stack in ONE 64-bit register: up to 3 parked tasks of 21 bits each
+// (a and b relative to the leaf start, 7 bits each; limit 5 bits; the two
+// flags).  A leaf of n <= 64 parks at most 3 (64 -> 31 -> 15 -> 7).  An
+// array (even of named members) indexed by the stack pointer is compiled to
+// scratch memory, which the HIP runtime then keeps allocated per queue.
+struct BitStack {
+    uint64_t bits = 0;
+    int sp = 0, base = 0;
+    __host__ __device__ explicit BitStack(int leaf_start) : base(leaf_start) {}
+    __host__ __device__ void push(const Task &t) {
+        const uint64_t e = (uint64_t)(t.a - base) | (uint64_t)(t.b - base) << 7 |
+                           (uint64_t)t.limit << 14 | (uint64_t)t.wb << 19 | (uint64_t)t.wp << 20;
+        bits = bits << 21 | e;
+        sp++;
+    }
+    __host__ __device__ Task pop() {
+        const uint64_t e = bits & 0x1FFFFFull;
+        bits >>= 21;
+        sp--;
+        return Task{base + (int)(e & 127), base + (int)((e >> 7) & 127), (int)((e >> 14) & 31),
+                    (bool)((e >> 19) & 1), (bool)((e >> 20) & 1)};
+    }
+};
+template <int N>
+struct ArrayStackAt : ArrayStack<N> {
+    __host__ __device__ explicit ArrayStackAt(int) {}
+};
+
+template <class D, int STACK = 40, class Stack = ArrayStackAt<STACK>>
+__host__ __device__ inline void pdq_loop(D &d, Task t0) {
+    Stack st(t0.a);
+    st.push(t0);
+    while (st.sp) {
+        Task t = st.pop();
         int a = t.a, b = t.b, limit = t.limit;
         bool wb = t.wb, wp = t.wp;
         for (;;) {
@@ -215,10 +254,10 @@ __host__ __device__ inline void pdq_loop(D &d, Task t0) {
             // on the larger one.  The larger side's loop state is parked on
             // the stack while the smaller side runs (depth <= log2 n).
             if (ln < rn) {
-                st[sp++] = Task{mid + 1, b, limit, ln >= thr, already};
+                st.push(Task{mid + 1, b, limit, ln >= thr, already});
                 b = mid;
             } else {
-                st[sp++] = Task{a, mid, limit, rn >= thr, already};
+                st.push(Task{a, mid, limit, rn >= thr, already});
                 a = mid + 1;
             }
             wb = true;

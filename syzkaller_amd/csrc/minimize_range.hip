@@ -222,7 +222,8 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint
 // SMALL_M: sub-runs up to this length take the lane-per-item path.
 // TEST = false is a tuning variant that streams the data without the
 // covered tests (not exact; selected only through SYZCOV_MR_CFG).
-template <uint32_t SMALL_M, bool TEST, bool WHOLE = false, int GS = 8, int UG = 4>
+template <uint32_t SMALL_M, bool TEST, bool WHOLE = false, int GS = 8, int UG = 4,
+          bool DEFER = false>
 __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b, uint32_t P,
                                                         int load_cov) {
     extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
                     }
                 }
-                if (__ballot(um != 0)) um = prune_ranked<UG>(um, v, rki, A);
+                if (!DEFER && __ballot(um != 0)) um = prune_ranked<UG>(um, v, rki, A);
                 if (__ballot(um != 0)) {
                     // reserve this lane's records, then write them
                     const uint32_t cnt = (uint32_t)__popc(um);
@@ -347,9 +348,11 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             for (int k = 0; k < 4; k++)
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
-                                    atomicMin(&A.first_w[wo], rki);
+                                    if (!DEFER) atomicMin(&A.first_w[wo], rki);
                                     if (slot < A.cap_k)
                                         rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    else if (DEFER)  // no room: its min cannot wait
+                                        atomicMin(&A.first_w[wo], rki);
                                     slot++;
                                 }
                         }
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
                     }
                 }
-                if (__ballot(um != 0)) um = prune_ranked<UB>(um, v, rki, A);
+                if (!DEFER && __ballot(um != 0)) um = prune_ranked<UB>(um, v, rki, A);
                 if (__ballot(um != 0)) {
                     const uint32_t cnt = (uint32_t)__popc(um);
                     const uint32_t incl = wave_incl_scan(cnt);
@@ -423,9 +426,11 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             for (int k = 0; k < 4; k++)
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
-                                    atomicMin(&A.first_w[wo], rki);
+                                    if (!DEFER) atomicMin(&A.first_w[wo], rki);
                                     if (slot < A.cap_k)
                                         rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    else if (DEFER)  // no room: its min cannot wait
+                                        atomicMin(&A.first_w[wo], rki);
                                     slot++;
                                 }
                         }
@@ -442,6 +447,210 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
         st[1] = ts1;
         st[2] = __builtin_amdgcn_s_memrealtime();
         st[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
+    }
+#endif
+}
+
+// Pass 1 as a CHUNK STREAM (first covers deferred to min_records_kernel).
+// A wave takes 64 items at a time and concatenates their sub-runs into one
+// list of 16-byte chunks (an exclusive scan of the per-item chunk counts;
+// lane j holds item j's start); lane l then loads chunks l, l + 64, l + 128,
+// ... of that list.  Every load instruction is a full wave of useful 16-byte
+// pieces whatever the sub-run lengths (the lane-group and whole-wave paths
+// above idle the lanes of short or ragged sub-runs), and consecutive lanes
+// read consecutive chunks of one sub-run.  The item of a chunk comes from a
+// WAVE-UNIFORM walk over the item starts (readlane, no LDS round trips): the
+// 64 chunks of one load instruction are contiguous, so only the items that
+// start inside them are visited.  Loads and the covered tests are branch-free
+// straight-line code, so the next UG x 64 chunks stay in flight while the
+// current ones are tested (a conditional load or test made the compiler wait
+// for every outstanding load, vmcnt(0), and for each LDS read in turn).
+template <int UG, bool TEST = true>
+__global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t a, uint32_t b,
+                                                               uint32_t P, int load_cov) {
+    extern __shared__ uint32_t s_cov[];
+    __shared__ uint32_t s_plan[MAX_R + 1];
+    __shared__ uint64_t s_a0[NWAVE][64];   // 16-byte aligned base of the sub-run
+    __shared__ uint32_t s_he[NWAVE][64];   // (end << 2) | head, in PCs from s_a0
+    __shared__ uint32_t s_ex[NWAVE][64];   // first chunk of the item in the stream
+    __shared__ int32_t s_rk[NWAVE][64];
+#ifdef SYZ_MR_DEBUG
+    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    uint32_t rho, i0, i1;
+    if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
+    const uint32_t region = blockIdx.x % NCTR;
+    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
+    unsigned long long *const rrec = A.rec + region * A.cap_k;
+    const uint32_t nwords = (1u << A.rshift) >> 5;
+    {
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
+        uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
+        if (load_cov) {
+            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
+        } else {
+            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
+                s4[q] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    __syncthreads();
+#ifdef SYZ_MR_DEBUG
+    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint32_t l = __lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t rbase = rho << A.rshift;
+    const uint32_t bmask = nwords * 32 - 1;
+    const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+    const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+    for (uint32_t ib = w0; ib < w1; ib += 64) {
+        const uint32_t item = ib + l;
+        uint32_t m = 0, nch = 0, he = 0;
+        uint64_t a0 = 0;
+        int32_t rk = 0;
+        if (item < w1) {
+            rk = A.ranks ? A.ranks[item] : (int32_t)item;
+            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            const uint64_t st = A.base_r[item] + s0;
+            m = s1 - s0;
+#ifdef SYZ_MR_DEBUG
+            if (s1 < s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
+#endif
+            a0 = st & ~3ull;
+            const uint32_t head = (uint32_t)(st - a0);
+            he = ((head + m) << 2) | head;
+            nch = m ? (head + m + 3) >> 2 : 0u;
+        }
+        const uint32_t incl = wave_incl_scan(nch);
+        const uint32_t ex_l = incl - nch;  // lane j: item j's first chunk
+        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        s_a0[w][l] = a0;
+        s_he[w][l] = he;
+        s_ex[w][l] = ex_l;
+        s_rk[w][l] = rk;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // start of item t (t <= 64; item 64 = the end of the stream)
+        auto ex_at = [&](uint32_t t) -> uint32_t {
+            return t < 64 ? (uint32_t)__builtin_amdgcn_readlane(ex_l, t) : tot;
+        };
+        uint32_t sj = 0;  // uniform: the item of the first chunk of the window
+        uint4 v[UG];
+        uint32_t cj[UG], co[UG], hv[UG];  // item (64: past the end), chunk in it, its (end, head)
+        auto issue = [&](uint32_t c0, uint4 (&dst)[UG], uint32_t (&dj)[UG], uint32_t (&dc)[UG],
+                         uint32_t (&dh)[UG]) {
+            uint32_t jj[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t cb = c0 + u * 64;  // uniform
+                while (sj < 63 && ex_at(sj + 1) <= cb) sj++;
+                uint32_t j = sj;
+                const uint32_t c = cb + l;
+                for (uint32_t t = sj + 1; t < 64 && ex_at(t) < cb + 64; t++)
+                    j = c >= ex_at(t) ? t : j;
+                jj[u] = j;
+                dj[u] = c < tot ? j : 64u;
+            }
+            uint64_t ba[UG];
+            uint32_t bx[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                ba[u] = s_a0[w][jj[u]];
+                bx[u] = s_ex[w][jj[u]];
+                dh[u] = s_he[w][jj[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t c = c0 + u * 64 + l;
+                dc[u] = dj[u] < 64 ? c - bx[u] : 0u;  // past the end: chunk 0, never tested
+                dst[u] = reinterpret_cast<const uint4 *>(A.pcs + ba[u])[dc[u]];
+            }
+        };
+        // unconditional: chunks past the end load a valid line and are never
+        // tested, and straight-line loads keep the compiler's vmcnt exact
+        issue(0, v, cj, co, hv);
+        for (uint32_t c0 = 0; c0 < tot; c0 += 64 * UG) {
+            uint4 vn[UG];
+            uint32_t nj[UG], nc[UG], nh[UG];
+            issue(c0 + 64 * UG, vn, nj, nc, nh);
+            uint32_t um = 0;
+            uint32_t wv[UG * 4], bit[UG * 4];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    bit[u * 4 + k] = (vv[k] - A.pc_lo - rbase) & bmask;
+                    if (TEST) wv[u * 4 + k] = s_cov[bit[u * 4 + k] >> 5];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t head = hv[u] & 3u, end = hv[u] >> 2;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t idx = co[u] * 4 + k;
+                    const uint32_t valid =
+                        (uint32_t)(cj[u] < 64) & (uint32_t)(idx >= head) & (uint32_t)(idx < end);
+#ifdef SYZ_MR_DEBUG
+                    {
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                        if (valid) MR_CHK(A, 8, vv[k] - A.pc_lo - rbase, nwords * 32);
+                    }
+#endif
+                    // TEST = false: tuning probe, the stream alone (not exact)
+                    const uint32_t unc = TEST ? ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u : 0u;
+                    um |= (valid & unc) << (u * 4 + k);
+                }
+            }
+            if (__ballot(um != 0)) {
+                const uint32_t cnt = (uint32_t)__popc(um);
+                const uint32_t inc2 = wave_incl_scan(cnt);
+                const uint32_t t2 = __shfl(inc2, 63, 64);
+                unsigned long long basei = 0;
+                if (l == 0) basei = atomicAdd(rctr, (unsigned long long)t2);
+                uint64_t slot = __shfl(basei, 0, 64) + (inc2 - cnt);
+                if (um) {
+#pragma unroll
+                    for (int u = 0; u < UG; u++) {
+                        if (!((um >> (u * 4)) & 15u)) continue;
+                        const int32_t rki = s_rk[w][cj[u]];
+                        A.cand[ib + cj[u]] = 1;
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            if ((um >> (u * 4 + k)) & 1u) {
+                                const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
+                                if (slot < A.cap_k)
+                                    rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                else  // no room: its min cannot wait
+                                    atomicMin(&A.first_w[wo], rki);
+                                slot++;
+                            }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                v[u] = vn[u];
+                cj[u] = nj[u];
+                co[u] = nc[u];
+                hv[u] = nh[u];
+            }
+        }
+        // the next batch rewrites this wave's descriptors
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+#ifdef SYZ_MR_DEBUG
+    __syncthreads();
+    if (threadIdx.x == 0 && A.stamp) {
+        uint64_t *stp = A.stamp + 4 * (uint64_t)blockIdx.x;
+        stp[0] = ts0;
+        stp[1] = ts1;
+        stp[2] = __builtin_amdgcn_s_memrealtime();
+        stp[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
     }
 #endif
 }
@@ -469,6 +678,29 @@ __global__ void cover_records_kernel(Args A, int par) {
         const uint32_t wo = (uint32_t)r;
         const uint32_t mbit = 1u << (wo & 31);
         if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
+    }
+}
+
+// Deferred first covers (pass1 DEFER): first_w[pc] = min over the records
+// appended since the last chunk, and covered |= them unless the caller
+// rebuilds covered from first_w.  Pass 1 then never waits on an atomic: on
+// gfx950 one counter (vmcnt) tracks loads, stores and atomics together, so an
+// atomicMin in the streaming loop made the NEXT iteration's loads wait for it,
+// and the early chunks' contended first-cover atomics (every item of the
+// chunk holds the hot PCs) set their time (~100 us each at C2).
+__global__ void min_records_kernel(Args A, int par, int or_cover) {
+    const unsigned long long *done_in = A.done + (par ? 1 : 0) * NCTR * CTR_STRIDE;
+    unsigned long long *done_out = A.done + (par ? 0 : 1) * NCTR * CTR_STRIDE;
+    if (blockIdx.x < NCTR && threadIdx.x == 0)
+        done_out[blockIdx.x * CTR_STRIDE] =
+            std::min<uint64_t>(A.ctr[blockIdx.x * CTR_STRIDE], A.cap_k);
+    SYZ_FOR_RECORDS(A, done_in[(blockIdx.x % NCTR) * CTR_STRIDE], i, r) {
+        const uint32_t wo = (uint32_t)r;
+        atomicMin(&A.first_w[wo], (int32_t)(r >> 32));
+        if (or_cover) {
+            const uint32_t mbit = 1u << (wo & 31);
+            if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
+        }
     }
 }
 
@@ -699,13 +931,17 @@ extern "C" int syzcov_dev_minimize_range(
     // few long sub-runs per item (dense keys: 4 ranges at C2) take the whole
     // wave above 512 PCs (variant 14: minimize 3.07 vs 3.57 ms, C2 key mode);
     // many short ones (64 window ranges) the 4-lane groups throughout
-    int variant = nrange <= 16 ? 14 : 0, pmode = 0;
+    // 15/16 = 14/0 with the first-cover atomics deferred to min_records_kernel;
+    // 17 = the chunk stream (default for few ranges, with P = 16R pieces per
+    // slice).  C2 key mode, minimize ms: 14 3.07, 15 3.00, 17 2.75 at P = 2R,
+    // 2.35 at 8R, 2.26-2.30 at 12R..32R (tools/gpu_mrvar.sh)
+    int variant = nrange <= 16 ? 17 : 16, pmode = nrange <= 16 ? 16 : 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
     // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
     // minimize ms: (4,4) 4.6, (2,8) 4.9, (4,8) 5.0, (4,2) 5.05, (2,4) 5.05,
     // (8,2) 5.7, (8,4) 5.9, (16,2) 8.4, one lane per item (old) 7.0
-    constexpr int NVAR = 15;
+    constexpr int NVAR = 21;
     const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>, mr::pass1_kernel<0, true>,
                           mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
                           mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
@@ -717,9 +953,16 @@ extern "C" int syzcov_dev_minimize_range(
                           // 12..14: lane groups up to 256 / 128 / 512 PCs, whole wave above
                           mr::pass1_kernel<256, true, false, 4, 4>,
                           mr::pass1_kernel<128, true, false, 4, 4>,
-                          mr::pass1_kernel<512, true, false, 4, 4>};
+                          mr::pass1_kernel<512, true, false, 4, 4>,
+                          mr::pass1_kernel<512, true, false, 4, 4, true>,
+                          mr::pass1_kernel<0x40000000, true, false, 4, 4, true>,
+                          // 17, 18: the chunk stream, 4 / 2 x 64 chunks per step
+                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<2>,
+                          // 19: probe, stream without tests; 20: 8 x 64 chunks per step
+                          mr::pass1_stream_kernel<4, false>, mr::pass1_stream_kernel<8>};
     const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
+    const bool defer = vi >= 15;
     static std::atomic<uint32_t> attr_set[NVAR];
     if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[vi]))) return rc;
     if (const char *e = getenv("SYZCOV_MR_CHUNK")) {  // tuning: "first,growth"
@@ -749,7 +992,7 @@ extern "C" int syzcov_dev_minimize_range(
         G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
         uint64_t P = 2 * nrange;
         if (pmode == 1) P = G;
-        else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // tuning: wider slices
+        else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // more pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
@@ -817,12 +1060,15 @@ extern "C" int syzcov_dev_minimize_range(
             if (b >= strtoull(e, nullptr, 0)) return SYZCOV_EINVAL;  // debug: stop before the fault
         }
 #endif
+        if (defer)  // the chunk's first covers (+ covered, unless rebuilt below)
+            hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
+                               (int)!cover_from_first);
         if (cover_from_first) {
             // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
             // first_w (16 MB at 2^22 keys) instead of an atomicOr per record
             // (C2 key mode: 5 vs 74-274 us per early chunk)
             if (b < n_items) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
-        } else {
+        } else if (!defer) {
             hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A, par);
         }
         par ^= 1;

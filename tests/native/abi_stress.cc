@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/syzcov.h"
@@ -132,7 +133,7 @@ int main(int argc, char **argv) {
         std::vector<std::thread> th;
         for (int t = 0; t < nt; t++) th.emplace_back(hip_probe ? hip_only : worker, t + round * nt, iters);
         for (auto &x : th) x.join();
-        if (failures) return 1;
+        if (failures) { fflush(stdout); _exit(1); }
         hipDeviceSynchronize();
         size_t free1 = 0;
         hipMemGetInfo(&free1, &total);
@@ -147,12 +148,12 @@ int main(int argc, char **argv) {
         if (hip_probe) continue;
         if (nctx > nt) {
             fprintf(stderr, "%lld contexts for %d concurrent callers\n", (long long)nctx, nt);
-            return 1;
+            { fflush(stdout); _exit(1); }
         }
         // idle contexts keep at most 3 arenas of 32 MB (+ 25% growth slack) each
         if (lost > nctx * 3 * (40ll << 20) + (512ll << 20)) {
             fprintf(stderr, "%lld MB held by %lld idle contexts\n", lost >> 20, (long long)nctx);
-            return 1;
+            { fflush(stdout); _exit(1); }
         }
         if (round == 0) {
             ctx_r0 = nctx;
@@ -160,7 +161,7 @@ int main(int argc, char **argv) {
             // a new set of OS threads reuses the pooled contexts
             fprintf(stderr, "contexts grew across thread churn: %lld -> %lld\n",
                     (long long)ctx_r0, (long long)nctx);
-            return 1;
+            { fflush(stdout); _exit(1); }
         }
     }
     if (!hip_probe) {  // trimming gives the arenas back
@@ -168,9 +169,18 @@ int main(int argc, char **argv) {
         size_t free2 = 0;
         hipMemGetInfo(&free2, &total);
         const long long held = (long long)free0 - (long long)free2;
-        printf("after syzcov_pool_trim: %lld MB held\n", held >> 20);
-        if (held > (512ll << 20)) return 1;
+        printf("after syzcov_pool_trim: %lld MB held, pooled contexts %lld\n", held >> 20,
+               (long long)syzcov_pool_contexts(0));
+        fflush(stdout);
+        // what the HIP runtime alone keeps after as many threads (the "hip"
+        // probe mode, passed in by the test) plus 256 MB
+        long long base = 256;
+        if (const char *e = getenv("SYZCOV_STRESS_RUNTIME_MB")) base = atoll(e);
+        if (held > ((base + 256) << 20)) { fflush(stdout); _exit(1); }
     }
     printf("OK\n");
-    return 0;
+    // no static teardown: the HIP runtime's exit-time frees trip the ASan
+    // device allocator's own check (its runtime is marked unloaded by then)
+    fflush(stdout);
+    _exit(0);
 }

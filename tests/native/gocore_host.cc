@@ -19,5 +19,9 @@ extern "C" void gocore_sort(const long long *len, int n, int *idx) {
     for (int i = 0; i < n; i++) idx[i] = i;
     if (n <= 1) return;
     Acc d{idx, len};
-    syz::gocore::pdq_loop<Acc, 64>(d, syz::gocore::Task{0, n, syz::gocore::bits_len(n), true, true});
+    const syz::gocore::Task t{0, n, syz::gocore::bits_len(n), true, true};
+    if (n <= 64)  // the device leaves' register stack
+        syz::gocore::pdq_loop<Acc, 3, syz::gocore::BitStack>(d, t);
+    else
+        syz::gocore::pdq_loop<Acc, 64>(d, t);
 }

@@ -24,8 +24,9 @@ def core(tmp_path_factory):
 
 def test_core_matches_go_sort(core):
     rng = np.random.default_rng(21)
-    for trial in range(300):
-        n = int(rng.integers(0, 5000))
+    for trial in range(600):
+        # every other trial a leaf-sized input (<= 64: the register BitStack)
+        n = int(rng.integers(0, 5000)) if trial % 2 else int(rng.integers(0, 65))
         kind = trial % 5
         lens = (rng.integers(0, 6, size=n) if kind == 0 else
                 rng.integers(0, 1 << 20, size=n) if kind == 1 else

@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r2a
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r2a/pytest.log 2>&1 || { tail -30 gpurun_out/r2a/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r2a/pytest.log 2>&1 || { tail -30 gpurun_out/r2a/pytest.log; exit 1; }
 tail -2 gpurun_out/r2a/pytest.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r2a/smoke.log 2>&1 || { cat gpurun_out/r2a/smoke.log; exit 1; }
 cat gpurun_out/r2a/smoke.log

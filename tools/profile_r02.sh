@@ -18,7 +18,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/new
 python3 tools/trace_summary.py $o/newcov_trace > $o/newcov_summary.txt && head -10 $o/newcov_summary.txt
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/newcov_fetch -o run -- $N --steps 2 --warmup 0 --history 4 > $o/nf.log 2>&1 || { tail -5 $o/nf.log; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/newcov_write -o run -- $N --steps 2 --warmup 0 --history 4 > $o/nw.log 2>&1 || { tail -5 $o/nw.log; exit 1; }
-python3 tools/traffic.py $o/newcov_fetch $o/newcov_write $o/newcov_traffic.json newcov_cand_kernel > /dev/null && cat $o/newcov_traffic.json
+python3 tools/traffic.py $o/newcov_fetch $o/newcov_write $o/newcov_traffic.json newcov_own_kernel > /dev/null && cat $o/newcov_traffic.json
 P="$B --workload prio"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prio_trace -o run -- $P --steps 10 --warmup 3 > $o/prio_trace.log 2>&1 || { tail -20 $o/prio_trace.log; exit 1; }
 python3 tools/trace_summary.py $o/prio_trace > $o/prio_summary.txt && head -8 $o/prio_summary.txt
