@@ -15,7 +15,8 @@ import sys
 PHASES = {
     "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
               "keyify_list_kernel", "large_"),
-    "minimize": ("prep_kernel", "pass1_kernel", "cover_records_kernel", "first_to_bits_kernel",
+    "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "min_records_kernel",
+                 "cover_records_kernel", "first_to_bits_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
     "newcov": ("newcov_", "hash_clear_kernel"),
     "prio": ("prio_",),
