@@ -467,6 +467,286 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     }
 }
 
+// ---------------------------------------------------------------------------
+// Key mode, <= 2^22 keys: the wave sorts the dense KEYS themselves in 2 LSD
+// passes of 11-bit digits (the window offsets take 3 passes of 9 bits).
+// The 2048-bin histogram is held as u16 PAIRS, bin d in half (d & 1) of word
+// d >> 1 (4 KB; a segment holds < 2^16 keys, so a half never carries into the
+// other), and the next pass's digit is counted after the scatter instead of
+// during it, so one 4 KB array serves both passes: 12.3 KB of LDS per wave
+// against 10.5 KB for the 3-pass sort, within the 3 waves per SIMD the
+// registers allow anyway (the packed u32 format needed 8 KB of histogram and
+// halved the resident waves, 9.45 vs 7.9 ms).  Random-address LDS operations
+// per key: 6 (2 x count, rank, scatter) instead of 9.
+// A PC outside the window is flagged (SYZCOV_ERR_WINDOW: the step's results
+// are invalid and the engine raises) and sorts as the last key, so nothing
+// downstream indexes past the key range.
+constexpr int KB = 11;
+constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
+
+__device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
+
+// exclusive scan of the 2048 u16 counts in bin order, in place
+__device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
+    uint4 *h4 = reinterpret_cast<uint4 *>(h);
+    uint4 v[4];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        v[q] = h4[4 * l + q];
+        const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) sum += (w4[i] & 0xFFFFu) + (w4[i] >> 16);
+    }
+    uint32_t p = wave_incl_scan(sum) - sum;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t lo = w4[i] & 0xFFFFu, hi = w4[i] >> 16;
+            w4[i] = p | ((p + lo) << 16);
+            p += lo + hi;
+        }
+        h4[4 * l + q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
+    uint4 *h4 = reinterpret_cast<uint4 *>(h);
+#pragma unroll
+    for (int q = 0; q < 4; q++) h4[4 * l + q] = make_uint4(0, 0, 0, 0);
+}
+
+// count the digit (k >> sh) & 2047 of the real slots (pads: the lane's dummy word)
+template <bool RAW, int NK>
+__device__ __forceinline__ void count16(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
+                                       uint32_t lo, uint32_t hi, uint32_t *h, uint32_t sh) {
+    constexpr int NQ = NK / 4;
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+        if ((uint32_t)q < nq) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const bool ok = real_slot<RAW, NK>(q * 4 + c, l, lo, hi);
+                const uint32_t d = (k[q * 4 + c] >> sh) & 2047u;
+                atomicAdd(&h[ok ? d >> 1 : KWORDS + l], ok ? hinc(d) : 1u);
+            }
+        }
+}
+
+// rank (ds_add_rtn on the u16 half) and scatter; atomics of BQ row quads
+// issued before their stores, as scatter_rows
+template <bool RAW, int NK, int BQ = SYZ_CANON_BQ>
+__device__ __forceinline__ void scatter16(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
+                                          uint32_t lo, uint32_t hi, uint32_t *buf, uint32_t *h,
+                                          uint32_t sh) {
+    constexpr int NQ = NK / 4;
+    constexpr uint32_t CAP = 64 * NK;
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += BQ) {
+        if ((uint32_t)q0 >= nq) continue;
+        uint32_t pos[4 * BQ];
+        bool ok[4 * BQ];
+#pragma unroll
+        for (int j = 0; j < 4 * BQ; j++) {
+            ok[j] = real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
+            const uint32_t d = (k[q0 * 4 + j] >> sh) & 2047u;
+            if ((uint32_t)(q0 + j / 4) < nq)
+                pos[j] = atomicAdd(&h[ok[j] ? d >> 1 : KWORDS + l], ok[j] ? hinc(d) : 1u) >>
+                         ((d & 1u) << 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4 * BQ; j++)
+            if ((uint32_t)(q0 + j / 4) < nq) buf[ok[j] ? pos[j] & 0xFFFFu : CAP + l] = k[q0 * 4 + j];
+    }
+}
+
+template <int NK, int MINW, int BQK = SYZ_CANON_BQ>
+__global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, const uint32_t *list,
+                                                                   const uint32_t *count) {
+    constexpr int CAP = 64 * NK;
+    constexpr int NQ = NK / 4;
+    __shared__ uint32_t s_buf[WPB][CAP + 64];
+    __shared__ __attribute__((aligned(16))) uint32_t s_h[WPB][KWORDS + 64];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t l = __lane_id();
+    uint32_t *buf = s_buf[w];
+    uint32_t *h = s_h[w];
+    const uint64_t lt = (1ull << l) - 1ull;
+    const uint32_t span_m1 = (uint32_t)(P.span - 1);
+    const uint32_t kmax = (uint32_t)(P.nkeys - 1);
+    const bool inplace = P.out == P.raw;
+    uint32_t racc[MAX_RPL];
+#pragma unroll
+    for (int q = 0; q < MAX_RPL; q++) racc[q] = 0;
+    const uint32_t nl = *count;
+    const uint32_t nw = gridDim.x * WPB;
+    uint4 vn[NQ];
+    uint32_t seg_n = 0, n_n = 0;
+    uint64_t base_n = 0;
+    auto issue = [&](uint32_t li_) {
+        seg_n = list[li_];
+        base_n = P.off[seg_n];
+        n_n = (uint32_t)(P.off[seg_n + 1] - base_n);
+        const uint64_t a0 = base_n & ~3ull;
+        const uint32_t end = (uint32_t)(base_n - a0) + n_n;
+        const uint32_t nq = (end + 255) >> 8;
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.raw + a0);
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+                const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+                vn[q] = src[e4 < end ? q * 64 + l : 0];
+            }
+    };
+    uint32_t li = blockIdx.x * WPB + w;
+    if (li < nl) issue(li);
+    for (; li < nl; li += nw) {
+        const uint32_t seg = seg_n;
+        const uint64_t base = base_n;
+        const uint32_t n = n_n;
+        const uint64_t a0 = base & ~3ull;
+        const uint32_t head = (uint32_t)(base - a0), end = head + n;
+        const uint32_t nq = (end + 255) >> 8;
+        uint32_t k[NK];
+        bool oob = false;
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            if ((uint32_t)q < nq) {
+                const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+                const uint32_t vv[4] = {vn[q].x, vn[q].y, vn[q].z, vn[q].w};
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t idx = e4 + c;
+                    const bool valid = idx >= head && idx < end;
+                    const bool out = vv[c] - P.pc_lo > span_m1;
+                    oob |= valid && out;
+                    k[q * 4 + c] = out ? kmax : (vv[c] >> P.kshift) - P.kbase;
+                }
+            }
+        }
+        if (li + nw < nl) issue(li + nw);
+        if (__ballot(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
+        // ---------------------------------------- pass 0: low 11 bits
+        hist16_zero<NQ>(h, l);
+        wave_sync();
+        count16<true, NK>(k, nq, l, head, end, h, 0);
+        wave_sync();
+        hist16_scan(h, l);
+        wave_sync();
+        scatter16<true, NK, BQK>(k, nq, l, head, end, buf, h, 0);
+        wave_sync();
+        // ---------------------------- pass 1: high 11 bits, stable (row-major)
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
+            }
+        hist16_zero<NQ>(h, l);
+        wave_sync();
+        count16<false, NK>(k, nq, l, 0, n, h, KB);
+        wave_sync();
+        hist16_scan(h, l);
+        wave_sync();
+        scatter16<false, NK, BQK>(k, nq, l, 0, n, buf, h, KB);
+        wave_sync();
+        // --------------------------------- order check + unique + write
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
+            }
+        uint32_t bad = 0;
+        if (inplace) {  // nothing may be written before the order is known
+            uint32_t carry = P.sent_key;
+#pragma unroll
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                        const uint32_t v = k[q * 4 + c];
+                        const uint32_t prev = shift_up(v, carry);
+                        carry = __builtin_amdgcn_readlane(v, 63);
+                        bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                    }
+                }
+            if (__ballot(bad)) {
+                if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = seg;
+                continue;
+            }
+        }
+        uint32_t cnt = 0, carry = P.sent_key;
+        uint32_t *outp = P.out + base;
+#pragma unroll
+        for (int q = 0; q < NQ; q++)
+            if ((uint32_t)q < nq) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                    const uint32_t v = k[q * 4 + c];
+                    const uint32_t prev = shift_up(v, carry);
+                    carry = __builtin_amdgcn_readlane(v, 63);
+                    bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                    const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
+                    const uint64_t m = __ballot(keep);
+                    const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                    if (keep) {
+                        outp[pos] = v;
+                        buf[pos] = v;
+                    }
+                    cnt += (uint32_t)__popcll(m);
+                }
+            }
+        if (__ballot(bad)) {
+            if (l == 0) P.redo_list[atomicAdd(P.redo_cnt, 1u)] = seg;
+            continue;
+        }
+        if (l == 0) P.new_len[seg] = cnt;
+        if (!P.split) {
+            if (l == 0) racc[0] += cnt;
+        } else {
+            wave_sync();
+            uint32_t carry2 = 0;
+            uint32_t *sp = P.split + (uint64_t)seg * P.nrange;
+#pragma unroll
+            for (int q = 0; q < MAX_RPL; q++) {
+                const uint32_t j = q * 64 + l;
+                if (q * 64 < (int)P.nrange) {
+                    uint32_t s2 = cnt;
+                    if (j + 1 < P.nrange) {
+                        const uint32_t b = (j + 1) << P.rshift;  // keys below range j + 1
+                        uint32_t lo2 = 0, hi2 = cnt;
+                        while (lo2 < hi2) {
+                            const uint32_t mid = (lo2 + hi2) >> 1;
+                            if (buf[mid] < b) lo2 = mid + 1; else hi2 = mid;
+                        }
+                        s2 = lo2;
+                    }
+                    const uint32_t prev_s = __shfl_up(s2, 1, 64);
+                    const uint32_t c2 = s2 - (l == 0 ? carry2 : prev_s);
+                    carry2 = __shfl(s2, 63, 64);
+                    if (j < P.nrange) {
+                        sp[j] = s2;
+                        racc[q] += c2;
+                    }
+                }
+            }
+        }
+    }
+    if (P.range_tot) {
+#pragma unroll
+        for (int q = 0; q < MAX_RPL; q++) {
+            const uint32_t j = q * 64 + l;
+            if (j < P.nrange && racc[q]) atomicAdd(&P.range_tot[j], (unsigned long long)racc[q]);
+        }
+    }
+}
+
 // Splits + range totals of listed segments (fallback / long paths), from the
 // canonical lists already in `out`.  One wave per listed segment.
 __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t *list,
@@ -556,6 +836,31 @@ static unsigned resident_grid(uint64_t nseg) {
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, cap));
 }
 
+template <int NK, int MW>
+static unsigned resident_grid_key(uint64_t nseg) {
+    static unsigned cap = 0;
+    if (!cap) {
+        int dev = 0, ncu = 256, nb = 0;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            hipDeviceProp_t pr;
+            if (hipGetDeviceProperties(&pr, dev) == hipSuccess) ncu = pr.multiProcessorCount;
+        }
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &nb, reinterpret_cast<const void *>(cw::canon_key_kernel<NK, MW>), 64 * cw::WPB,
+                0) != hipSuccess || nb < 1)
+            nb = 1;
+        cap = (unsigned)(nb * ncu);
+    }
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, cap));
+}
+
+template <int NK, int MW>
+static void launch_key_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
+                             uint64_t nseg, hipStream_t s) {
+    hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW>), dim3(resident_grid_key<NK, MW>(nseg)),
+                       dim3(64 * cw::WPB), 0, s, P, lc, cnt);
+}
+
 extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
     // counters | redo list | big list | class lists
     return 256 + (2 + cw::NCLS) * align_up(nseg * sizeof(uint32_t), 256);
@@ -636,6 +941,18 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     bool hb11 = false;
     if (const char *e = getenv("SYZCOV_CANON_HB"))
         hb11 = atoi(e) == 11 && P.nbits >= 19 && P.nbits <= 22;
+    // key mode over <= 2^22 keys: sort the keys themselves, 2 passes of 11
+    // bits with u16-pair histograms (canon_key_kernel); SYZCOV_CANON_KEY2=0
+    // keeps the 3-pass window-offset sort (tuning / comparison)
+    // Measured per class at C2 (us, 2-pass / 3-pass): 2048 keys 2908 / 3153,
+    // 2560: 2908 / 2873, 3072: 2391 / 1601 (the compiler cannot fit 48 keys per
+    // lane in 168 VGPRs and falls to one wave per SIMD), 4096: 371 / 341,
+    // 8192: 41 / 50; so only the 2048-key class takes it (SYZCOV_CANON_KEY2:
+    // 0 = none, 1 = that class, 2 = every class).
+    int key2 = (key_out && nkeys <= (1ull << 22)) ? 1 : 0;
+    if (const char *e = getenv("SYZCOV_CANON_KEY2")) key2 = key2 ? atoi(e) : 0;
+    cw::Params PK = P;  // the key kernel's unique loop compares KEYS
+    PK.sent_key = so < pc_span ? (0xFFFFFFFFu >> kshift) - kbase : 0xFFFFFFFFu;
     // bin by capacity class (wave-aggregated atomics), one launch per class
     // (a register bitonic network measured 20.3 ms at C2 against the LDS
     // radix's 7.8: 147 VALU ops per key)
@@ -657,12 +974,22 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     for (int c = 0; c < cw::NCLS; c++) {
         if (max_seg_len < C.lo[c]) break;
         const uint32_t *lc = clists + (size_t)c * nseg;
-        switch (c) {
-        case 0: launch_class<32, SYZ_CANON_W32>(hb11, P, lc, ccnt + c, nseg, s); break;
-        case 1: launch_class<40, SYZ_CANON_W40>(hb11, P, lc, ccnt + c, nseg, s); break;
-        case 2: launch_class<48, SYZ_CANON_W48>(hb11, P, lc, ccnt + c, nseg, s); break;
-        case 3: launch_class<64, 2>(hb11, P, lc, ccnt + c, nseg, s); break;
-        case 4: launch_class<128, 1>(hb11, P, lc, ccnt + c, nseg, s); break;
+        if (key2 == 2 || (key2 == 1 && c == 0)) {
+            switch (c) {
+            case 0: launch_key_class<32, SYZ_CANON_W32>(PK, lc, ccnt + c, nseg, s); break;
+            case 1: launch_key_class<40, SYZ_CANON_W40>(PK, lc, ccnt + c, nseg, s); break;
+            case 2: launch_key_class<48, SYZ_CANON_W48>(PK, lc, ccnt + c, nseg, s); break;
+            case 3: launch_key_class<64, 2>(PK, lc, ccnt + c, nseg, s); break;
+            case 4: launch_key_class<128, 1>(PK, lc, ccnt + c, nseg, s); break;
+            }
+        } else {
+            switch (c) {
+            case 0: launch_class<32, SYZ_CANON_W32>(hb11, P, lc, ccnt + c, nseg, s); break;
+            case 1: launch_class<40, SYZ_CANON_W40>(hb11, P, lc, ccnt + c, nseg, s); break;
+            case 2: launch_class<48, SYZ_CANON_W48>(hb11, P, lc, ccnt + c, nseg, s); break;
+            case 3: launch_class<64, 2>(hb11, P, lc, ccnt + c, nseg, s); break;
+            case 4: launch_class<128, 1>(hb11, P, lc, ccnt + c, nseg, s); break;
+            }
         }
         SYZ_LAUNCH_CHECK();
     }

@@ -29,6 +29,10 @@
 #include <vector>
 
 #include "common.h"
+
+#include <cstring>
+#include <mutex>
+#include <vector>
 #include "gosort_core.h"
 
 namespace syz {
@@ -811,13 +815,54 @@ extern "C" size_t syzcov_dev_sort_seg_ws_size(size_t n, size_t ngroups) {
 // seeded >= 0: the host already knows the seed (one segment of `seeded`
 // elements), so the first read-back is skipped; an input error flagged by the
 // init kernel is then reported by the final read-back.
+// Pinned host words for the round read-backs: a copy into pageable memory
+// (a stack array) is staged by the runtime and left the GPU idle ~35 us per
+// read-back.  Leased from a process-wide pool for the call's duration.
+class PinnedCtl {
+  public:
+    PinnedCtl() {
+        std::lock_guard<std::mutex> g(mu());
+        if (!free_list().empty()) {
+            p_ = free_list().back();
+            free_list().pop_back();
+        } else if (hipHostMalloc((void **)&p_, 64, hipHostMallocDefault) != hipSuccess) {
+            p_ = nullptr;
+        }
+    }
+    ~PinnedCtl() {
+        if (!p_) return;
+        std::lock_guard<std::mutex> g(mu());
+        free_list().push_back(p_);
+    }
+    uint32_t *get() const { return p_; }
+
+  private:
+    static std::mutex &mu() {
+        static std::mutex *m = new std::mutex();
+        return *m;
+    }
+    static std::vector<uint32_t *> &free_list() {
+        static std::vector<uint32_t *> *v = new std::vector<uint32_t *>();
+        return *v;
+    }
+    uint32_t *p_ = nullptr;
+};
+
+// ctl[0..n) -> h through the pinned words (or directly, if none could be had)
+static int read_ctl(uint32_t *h, const uint32_t *ctl, size_t n, uint32_t *pin, hipStream_t s) {
+    SYZ_HIP(hipMemcpyAsync(pin ? pin : h, ctl, n * 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (pin) memcpy(h, pin, n * 4);
+    return 0;
+}
+
 static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
+    PinnedCtl pin;
     Seg *cur = w.segA, *nxt = w.segB;
     uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
     uint32_t h[6] = {0, 0, 0, 0, 0, 0};
     if (seeded < 0) {
-        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
     } else if (seeded > SMALL) {
         h[1] = 1;
         h[4] = (uint32_t)seeded;
@@ -858,8 +903,7 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
         ncur = std::min(2 * ncur, cap_seg);
         maxlen = maxlen > 1 ? maxlen - 1 : 0;
         if ((round + 1) % SYNC_EVERY == 0 || maxlen <= SMALL) {
-            SYZ_HIP(hipMemcpyAsync(h, w.ctl, 24, hipMemcpyDeviceToHost, s));
-            SYZ_HIP(hipStreamSynchronize(s));
+            if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
             ncur = h[ccount - w.ctl];
             maxlen = h[cmax - w.ctl];
         }
@@ -870,8 +914,7 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
         SYZ_LAUNCH_CHECK();
     }
     if (!h[0] && (h[3] || seeded >= 0)) {
-        SYZ_HIP(hipMemcpyAsync(h, w.ctl, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        if (int rc = read_ctl(h, w.ctl, 1, pin.get(), s)) return rc;
     }
     if (h[0]) {
         set_error("device sort: internal error %u", h[0]);
