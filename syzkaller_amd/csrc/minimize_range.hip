@@ -91,6 +91,8 @@ struct Args {
     uint32_t *dbg;             // [0] first failing check id, [1..2] its value
     uint64_t dbg_npcs, dbg_nseg, dbg_span;
     uint64_t *stamp;           // [G][4] per-workgroup timing stamps (debug builds)
+    uint32_t *pctr;            // dynamic pieces: this chunk's next-piece counter
+    uint32_t npieces;          // dynamic pieces: pieces of this chunk (G)
 };
 
 #ifdef SYZ_MR_DEBUG
@@ -172,16 +174,9 @@ __device__ __forceinline__ uint32_t prune_ranked(uint32_t um, const uint4 (&v)[N
     return um;
 }
 
-// Workgroup -> (range, item slice [i0, i1)).  The chunk's items are cut into
-// S slices; each slice is covered by P = G / S consecutive workgroups, range j
-// getting p_j = 1 + floor(w_j * (P - R) / W) of them (w_j: its PC count), so
-// a hot range's part of a slice is split further.  Consecutive workgroups
-// thus read different ranges of the SAME segments at the same time: the
-// sub-runs of one segment are neighbours in HBM (DRAM row locality) and a
-// line shared by two ranges is still in L2 when the second one asks for it.
-__device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint32_t b,
-                         uint32_t *rho, uint32_t *i0, uint32_t *i1, uint32_t *sh) {
-    // sh: LDS scratch of MAX_R + 1 entries; computed by wave 0
+// The range plan of a chunk: sh[j] = first piece position of range j (wave 0
+// computes it into LDS; every thread waits).
+__device__ void plan_pieces(const Args &A, uint32_t G, uint32_t P, uint32_t *sh) {
     const uint32_t l = __lane_id();
     if (threadIdx.x < 64) {
         unsigned long long wsum = 0;
@@ -201,8 +196,17 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint
         if (l == 0) sh[0] = 0;
     }
     __syncthreads();
+}
+
+// Piece g (slice-major: slice g / P, position g % P) -> (range, item slice
+// [i0, i1)).  The chunk's items are cut into S = G / P slices; each slice is
+// covered by P consecutive pieces, range j getting p_j = 1 + floor(w_j * (P -
+// R) / W) of them (w_j: its key count), so a hot range's part of a slice is
+// split further.
+__device__ bool map_piece(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint32_t b, uint32_t g,
+                          uint32_t *rho, uint32_t *i0, uint32_t *i1, const uint32_t *sh) {
     const uint32_t S = G / P;  // slices
-    const uint32_t g = blockIdx.x, sl = g / P, r = g % P;
+    const uint32_t sl = g / P, r = g % P;
     if (sl >= S || r >= sh[A.nrange]) return false;
     uint32_t lo = 0, hi = A.nrange;  // largest j with sh[j] <= r
     while (hi - lo > 1) {
@@ -216,6 +220,16 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint
     *i0 = a + (uint32_t)(s0 + (s1 - s0) * q / p);
     *i1 = a + (uint32_t)(s0 + (s1 - s0) * (q + 1) / p);
     return true;
+}
+
+// Workgroup -> piece for the fixed-grid kernels.  Consecutive workgroups read
+// different ranges of the SAME segments at the same time: the sub-runs of one
+// segment are neighbours in HBM and a line shared by two ranges is still in
+// L2 when the second one asks for it.
+__device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint32_t b,
+                         uint32_t *rho, uint32_t *i0, uint32_t *i1, uint32_t *sh) {
+    plan_pieces(A, G, P, sh);
+    return map_piece(A, G, P, a, b, blockIdx.x, rho, i0, i1, sh);
 }
 
 // Pass 1 over items [a, b) (one chunk).
@@ -465,7 +479,10 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
 // straight-line code, so the next UG x 64 chunks stay in flight while the
 // current ones are tested (a conditional load or test made the compiler wait
 // for every outstanding load, vmcnt(0), and for each LDS read in turn).
-template <int UG, bool TEST = true>
+// DYN: a grid of one workgroup per CU takes pieces from a counter in
+// range-major order (a piece of the same range keeps the LDS bitmap), so the
+// chunk has no tail of late, unevenly sized workgroups.
+template <int UG, bool TEST = true, bool DYN = false>
 __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t a, uint32_t b,
                                                                uint32_t P, int load_cov) {
     extern __shared__ uint32_t s_cov[];
@@ -474,16 +491,34 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     __shared__ uint32_t s_he[NWAVE][64];   // (end << 2) | head, in PCs from s_a0
     __shared__ uint32_t s_ex[NWAVE][64];   // first chunk of the item in the stream
     __shared__ int32_t s_rk[NWAVE][64];
+    __shared__ uint32_t s_next;
 #ifdef SYZ_MR_DEBUG
     const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    uint32_t rho, i0, i1;
-    if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
+    const uint32_t G = DYN ? A.npieces : gridDim.x;
+    plan_pieces(A, G, P, s_plan);
     const uint32_t region = blockIdx.x % NCTR;
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
     unsigned long long *const rrec = A.rec + region * A.cap_k;
     const uint32_t nwords = (1u << A.rshift) >> 5;
-    {
+    uint32_t cur_rho = 0xFFFFFFFFu;
+    for (;;) {
+    uint32_t g = blockIdx.x;
+    if (DYN) {
+        if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+        __syncthreads();
+        g = s_next;
+        __syncthreads();
+        if (g >= G) break;
+        const uint32_t S = G / P;  // range-major: g = position * S + slice
+        g = (g % S) * P + g / S;
+    }
+    uint32_t rho, i0, i1;
+    if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) {
+        if (DYN) continue;
+        return;
+    }
+    if (rho != cur_rho) {
         const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
         if (load_cov) {
@@ -492,8 +527,9 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
             for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
                 s4[q] = make_uint4(0, 0, 0, 0);
         }
+        cur_rho = rho;
+        __syncthreads();
     }
-    __syncthreads();
 #ifdef SYZ_MR_DEBUG
     const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -644,15 +680,20 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         __builtin_amdgcn_wave_barrier();
     }
 #ifdef SYZ_MR_DEBUG
-    __syncthreads();
-    if (threadIdx.x == 0 && A.stamp) {
-        uint64_t *stp = A.stamp + 4 * (uint64_t)blockIdx.x;
-        stp[0] = ts0;
-        stp[1] = ts1;
-        stp[2] = __builtin_amdgcn_s_memrealtime();
-        stp[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
+    if (!DYN) {
+        __syncthreads();
+        if (threadIdx.x == 0 && A.stamp) {
+            uint64_t *stp = A.stamp + 4 * (uint64_t)blockIdx.x;
+            stp[0] = ts0;
+            stp[1] = ts1;
+            stp[2] = __builtin_amdgcn_s_memrealtime();
+            stp[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
+        }
     }
 #endif
+    if (!DYN) break;
+    __syncthreads();  // every wave is done before the LDS bitmap is replaced
+    }
 }
 
 // Region loops: block b serves region b % NCTR (the grid is a multiple of
@@ -805,7 +846,10 @@ using namespace syz;
 
 /* ws: region counters ctr | done marks x 2 (NCTR * 256 B each) | base_r [n_items] u64 |
  *     split_t [nrange][n_items] u32 */
-static constexpr size_t MR_HDR = 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t);
+// region counters | done marks x 2 | per-chunk piece counters (dynamic pieces)
+static constexpr int MR_MAX_CHUNKS = 64;
+static constexpr size_t MR_HDR = 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
+                                 MR_MAX_CHUNKS * 256;
 static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
     return (span + (1ull << rshift) - 1) >> rshift;
 }
@@ -815,6 +859,14 @@ extern "C" size_t syzcov_dev_minimize_range_ws_size(size_t n_items, uint64_t pc_
     if (range_shift > 20) range_shift = 20;
     return MR_HDR + align_up(n_items * 8, 256) +
            align_up(mr_nrange(pc_span, range_shift) * n_items * 4, 256);
+}
+
+static int dev_cus() {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+    return n > 0 ? n : 256;
 }
 
 static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
@@ -855,6 +907,8 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.split_t = (uint32_t *)((uint8_t *)A.base_r + align_up(n_items * 8, 256));
     A.dbg = nullptr;
     A.stamp = nullptr;
+    A.pctr = nullptr;
+    A.npieces = 0;
     A.dbg_npcs = A.dbg_nseg = ~0ull;
     A.dbg_span = pc_span;
 #ifdef SYZ_MR_DEBUG
@@ -932,16 +986,17 @@ extern "C" int syzcov_dev_minimize_range(
     // wave above 512 PCs (variant 14: minimize 3.07 vs 3.57 ms, C2 key mode);
     // many short ones (64 window ranges) the 4-lane groups throughout
     // 15/16 = 14/0 with the first-cover atomics deferred to min_records_kernel;
-    // 17 = the chunk stream (default for few ranges, with P = 16R pieces per
-    // slice).  C2 key mode, minimize ms: 14 3.07, 15 3.00, 17 2.75 at P = 2R,
-    // 2.35 at 8R, 2.26-2.30 at 12R..32R (tools/gpu_mrvar.sh)
-    int variant = nrange <= 16 ? 17 : 16, pmode = nrange <= 16 ? 16 : 0;
+    // 17 = the chunk stream, 21 = the chunk stream over dynamic pieces (the
+    // default for few ranges, with P = 16R pieces per slice).  C2 key mode,
+    // minimize ms: 14 3.07, 15 3.00, 17 2.75 at P = 2R, 2.35 at 8R, 2.26-2.30
+    // at 12R..32R; 21 2.13-2.15 at 8R..32R (tools/gpu_mrvar.sh)
+    int variant = nrange <= 16 ? 21 : 16, pmode = nrange <= 16 ? 16 : 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
     // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
     // minimize ms: (4,4) 4.6, (2,8) 4.9, (4,8) 5.0, (4,2) 5.05, (2,4) 5.05,
     // (8,2) 5.7, (8,4) 5.9, (16,2) 8.4, one lane per item (old) 7.0
-    constexpr int NVAR = 21;
+    constexpr int NVAR = 22;
     const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>, mr::pass1_kernel<0, true>,
                           mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
                           mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
@@ -959,7 +1014,9 @@ extern "C" int syzcov_dev_minimize_range(
                           // 17, 18: the chunk stream, 4 / 2 x 64 chunks per step
                           mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<2>,
                           // 19: probe, stream without tests; 20: 8 x 64 chunks per step
-                          mr::pass1_stream_kernel<4, false>, mr::pass1_stream_kernel<8>};
+                          mr::pass1_stream_kernel<4, false>, mr::pass1_stream_kernel<8>,
+                          // 21: the chunk stream over dynamic pieces
+                          mr::pass1_stream_kernel<4, true, true>};
     const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
     const bool defer = vi >= 15;
@@ -984,6 +1041,7 @@ extern "C" int syzcov_dev_minimize_range(
     if (const char *e = getenv("SYZCOV_MR_COVER")) cover_from_first = atoi(e) == 1;  // tuning
     uint64_t a = 0, step = first_chunk;
     int par = 0;  // done-mark set of this chunk
+    uint32_t nchunk = 0;
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
         // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
@@ -994,7 +1052,16 @@ extern "C" int syzcov_dev_minimize_range(
         if (pmode == 1) P = G;
         else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // more pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
-        hipLaunchKernelGGL(k1, dim3((unsigned)G), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
+        unsigned grid = (unsigned)G;
+        if (vi == 21) {  // dynamic pieces: one workgroup per CU draws them
+            if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
+            A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
+                                  (size_t)nchunk * 256);
+            A.npieces = (uint32_t)G;
+            grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
+        }
+        nchunk++;
+        hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
 #ifdef SYZ_MR_DEBUG
         {

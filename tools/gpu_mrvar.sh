@@ -12,7 +12,8 @@ for v in $PAR; do
 done
 for v in $BENCH; do
   wg=${v#*:}; [ "$wg" = "$v" ] && wg=""
-  SYZCOV_MR_WG=$wg SYZCOV_MR_CFG=${v%%:*} timeout -k 10 200 python -u bench.py --no-cpu --steps 10 --warmup 3 > $o/b_$v.json 2> $o/b_$v.err || { tail -5 $o/b_$v.err; exit 1; }
+  ch=${v#*@}; [ "$ch" = "$v" ] && ch=""; v0=${v%%@*}
+  SYZCOV_MR_CHUNK=$ch SYZCOV_MR_WG=$wg SYZCOV_MR_CFG=${v0%%:*} timeout -k 10 200 python -u bench.py --no-cpu --steps 10 --warmup 3 > $o/b_$v.json 2> $o/b_$v.err || { tail -5 $o/b_$v.err; exit 1; }
   python3 -c "import json; d=json.load(open('$o/b_$v.json')); print('variant $v', round(d['ms_per_step'],3), d['phases_ms'], d['results']['kept'])"
 done
 for v in $STAMP; do
