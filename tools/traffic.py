@@ -13,7 +13,8 @@ import os
 import sys
 
 PHASES = {
-    "canon": ("bin_kernel", "canon_wave_kernel", "canon_class_kernel", "split_list_kernel",
+    "canon": ("bin_kernel", "canon_wave_kernel", "canon_key_kernel", "canon_class_kernel",
+              "split_list_kernel",
               "keyify_list_kernel", "large_"),
     "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "min_records_kernel",
                  "cover_records_kernel", "first_to_bits_kernel",
