@@ -90,7 +90,9 @@ def gather_lens(local_lens: torch.Tensor, world: int) -> torch.Tensor:
 
 def local_items(order: torch.Tensor, rank: int, n_local: int):
     """Work items of this shard in global processing order: (local input
-    index, global rank) for every global rank whose input lives here."""
+    index, global rank) for every global rank whose input lives here.  (Host
+    reference form; the device engine uses ShardedEngine._local_items, which
+    has no host sync.)"""
     base = rank * n_local
     sel = (order >= base) & (order < base + n_local)
     ranks = torch.nonzero(sel, as_tuple=False).flatten().to(torch.int32)
@@ -118,10 +120,33 @@ class ShardedEngine(CorpusEngine):
         self.ws2 = torch.empty(max(self.L.syzcov_dev_dict_ws_size(pc_span),
                                    self.L.syzcov_dev_compact_ws_size(n * world)),
                                dtype=torch.uint8, device=self.dev)
+        # local work items: global ranks of this shard's inputs and the inputs
+        # themselves, by two ordered compactions (exactly n of them: the order
+        # is a permutation of the N global inputs)
+        self.iota = torch.arange(n * world, dtype=torch.int32, device=self.dev)
+        self.sel = torch.empty(n * world, dtype=torch.uint8, device=self.dev)
+        self.ranks_l = torch.empty(n + 1, dtype=torch.int32, device=self.dev)
+        self.items_l = torch.empty(n + 1, dtype=torch.int32, device=self.dev)
+        self.cnt_l = torch.zeros(2, dtype=torch.int32, device=self.dev)
 
     # "exchange": the covered OR, the dictionary, the first-rank MIN merge,
     # pass 2 and the kept merge (the only phase with collectives besides order)
     PHASES = ("canon", "order", "minimize", "exchange", "compact", "union", "merge")
+
+    def _local_items(self, N: int):
+        """(local input index, global rank) of this shard's items in global
+        processing order, on the device with no host sync."""
+        n, base, s = self.n_local, self.rank * self.n_local, _stream()
+        order = self.order[:N]
+        torch.logical_and(order >= base, order < base + n, out=self.sel.view(torch.bool))
+        check(self.L.syzcov_dev_compact_kept(_p(self.sel), _p(self.iota), N, _p(self.ranks_l),
+                                             _p(self.cnt_l[0:1]), _p(self.ws2), s),
+              "dev_compact_kept")
+        check(self.L.syzcov_dev_compact_kept(_p(self.sel), _p(order), N, _p(self.items_l),
+                                             _p(self.cnt_l[1:2]), _p(self.ws2), s),
+              "dev_compact_kept")
+        self.items_l[:n].sub_(base)
+        return self.items_l[:n], self.ranks_l[:n]
 
     def _or_into(self, dst, src):
         check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
@@ -146,8 +171,8 @@ class ShardedEngine(CorpusEngine):
         self.glens = gather_lens(self.new_len[:n], self.world)   # RCCL all-gather
         self.sort_order(self.glens, N)                          # identical on every rank
         mark_ev()
-        items, ranks = local_items(self.order[:N], self.rank, n)
-        m = items.numel()
+        items, ranks = self._local_items(N)
+        m = n
         self.minimize(off, items, ranks, m, do_pass2=False)
         mark_ev()
         if self.key_mode:
