@@ -320,6 +320,10 @@ int syzcov_dev_dict_build(const uint8_t *pres, uint64_t pc_span, uint64_t *tab, 
  * (Union drops the sentinel).  *n_out (device u32) receives the count. */
 int syzcov_dev_dict_to_list(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo,
                             uint32_t *out, uint32_t *n_out, void *stream);
+/* The same with the dropped value given: in key mode the KEY of 0xFFFFFFFF
+ * (the largest key, the key map being monotone); 0xFFFFFFFF otherwise. */
+int syzcov_dev_dict_to_list_drop(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo,
+                                 uint32_t drop, uint32_t *out, uint32_t *n_out, void *stream);
 
 /* Minimize pass 1 over n work items in rank order: item j is input
  * order[j] with rank ranks[j] (ranks == NULL: rank j).  first[id] (pre-set to

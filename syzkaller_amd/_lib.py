@@ -83,6 +83,7 @@ _SIGS = {
     "syzcov_dev_dict_ws_size": (sz, [u64]),
     "syzcov_dev_dict_build": (C.c_int, [p_, u64, p_, p_, p_, p_]),
     "syzcov_dev_dict_to_list": (C.c_int, [p_, u64, u32, p_, p_, p_]),
+    "syzcov_dev_dict_to_list_drop": (C.c_int, [p_, u64, u32, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass1": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_]),
     "syzcov_dev_minimize_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, p_, u32, p_, p_, p_, p_]),
     "syzcov_dev_canon_split_ws_size": (sz, [sz]),

@@ -978,7 +978,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
             switch (c) {
             case 0: launch_key_class<32, SYZ_CANON_W32>(PK, lc, ccnt + c, nseg, s); break;
             case 1: launch_key_class<40, SYZ_CANON_W40>(PK, lc, ccnt + c, nseg, s); break;
-            case 2: launch_key_class<48, SYZ_CANON_W48>(PK, lc, ccnt + c, nseg, s); break;
+            case 2: launch_key_class<48, 2>(PK, lc, ccnt + c, nseg, s); break;  // 168 VGPRs do not fit
             case 3: launch_key_class<64, 2>(PK, lc, ccnt + c, nseg, s); break;
             case 4: launch_key_class<128, 1>(PK, lc, ccnt + c, nseg, s); break;
             }

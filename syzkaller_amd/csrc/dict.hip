@@ -228,8 +228,11 @@ __global__ void dict_pass_c(uint64_t *__restrict__ tab, uint64_t nwords,
     }
 }
 
+// `drop`: the value Union drops (cover.go:97): PC 0xFFFFFFFF, or its KEY in
+// key mode.  It is the largest value of the list either way (the key map is
+// monotone), so leaving it out never leaves a hole.
 __global__ void dict_to_list_kernel(const uint64_t *__restrict__ tab, uint64_t nwords,
-                                    uint32_t pc_lo, uint32_t *__restrict__ out,
+                                    uint32_t pc_lo, uint32_t drop, uint32_t *__restrict__ out,
                                     uint32_t *__restrict__ n_out) {
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
          w += (uint64_t)gridDim.x * blockDim.x) {
@@ -240,13 +243,13 @@ __global__ void dict_to_list_kernel(const uint64_t *__restrict__ tab, uint64_t n
             const int b = __ffs(bits) - 1;
             bits &= bits - 1;
             const uint32_t pc = pc_lo + (uint32_t)(w * 32 + b);
-            if (out && pc != SYZ_SENT) out[pos] = pc;  // Union drops the sentinel (cover.go:97)
+            if (out && pc != drop) out[pos] = pc;  // Union drops the sentinel (cover.go:97)
             pos++;
         }
         if (w == nwords - 1) {
             // total = prefix of the last word + its popcount; minus sentinel
             uint32_t total = (uint32_t)e + __popc((uint32_t)(e >> 32));
-            const uint64_t last_off = (uint64_t)(uint32_t)(SYZ_SENT - pc_lo);
+            const uint64_t last_off = (uint64_t)(uint32_t)(drop - pc_lo);
             if (last_off / 32 == w && ((e >> 32) >> (last_off & 31)) & 1u) total -= 1;
             *n_out = total;
         }
@@ -394,14 +397,20 @@ extern "C" int syzcov_dev_dict_build(const uint8_t *pres, uint64_t pc_span, uint
     return 0;
 }
 
-extern "C" int syzcov_dev_dict_to_list(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo,
-                                       uint32_t *out, uint32_t *n_out, void *stream) {
+extern "C" int syzcov_dev_dict_to_list_drop(const uint64_t *tab, uint64_t pc_span,
+                                            uint32_t pc_lo, uint32_t drop, uint32_t *out,
+                                            uint32_t *n_out, void *stream) {
     if (!tab || !out || !n_out || pc_span == 0) return SYZCOV_EINVAL;
     const uint64_t nwords = (pc_span + 31) / 32;
     hipLaunchKernelGGL(dict_to_list_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
-                       (hipStream_t)stream, tab, nwords, pc_lo, out, n_out);
+                       (hipStream_t)stream, tab, nwords, pc_lo, drop, out, n_out);
     SYZ_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int syzcov_dev_dict_to_list(const uint64_t *tab, uint64_t pc_span, uint32_t pc_lo,
+                                       uint32_t *out, uint32_t *n_out, void *stream) {
+    return syzcov_dev_dict_to_list_drop(tab, pc_span, pc_lo, SYZ_SENT, out, n_out, stream);
 }
 
 extern "C" int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, uint64_t nbytes,
@@ -457,14 +466,14 @@ int bitmap_to_list(const uint32_t *bm, uint64_t pc_span, uint32_t pc_lo, uint32_
         if (!out) {
             // count minus a present sentinel
             hipLaunchKernelGGL(dict_to_list_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
-                               s, tab, nwords, pc_lo, (uint32_t *)nullptr, dn);
+                               s, tab, nwords, pc_lo, SYZ_SENT, (uint32_t *)nullptr, dn);
         } else {
             if (hipMalloc(&dout, (size_t)hn * 4 + 4) != hipSuccess) {
                 rc = SYZCOV_ENOMEM;
                 break;
             }
             hipLaunchKernelGGL(dict_to_list_kernel, dim3(grid_for(nwords, 256, 16384)), dim3(256), 0,
-                               s, tab, nwords, pc_lo, dout, dn);
+                               s, tab, nwords, pc_lo, SYZ_SENT, dout, dn);
         }
         if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&hn, dn, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {

@@ -199,8 +199,13 @@ class CorpusEngine:
               "dev_dict_build_bits")
 
     def union_list(self):
-        check(self.L.syzcov_dev_dict_to_list(_p(self.tab), self.span, self.pc_lo, _p(self.union),
-                                             _p(self.scal[3:4]), _stream()), "dev_dict_to_list")
+        # Union drops 0xFFFFFFFF (cover.go:97): in key mode, its key
+        drop = 0xFFFFFFFF
+        if self.key_mode:
+            drop = self.sent_key if self.sent_key is not None else 0xFFFFFFFF
+        check(self.L.syzcov_dev_dict_to_list_drop(_p(self.tab), self.span, self.pc_lo, drop,
+                                                  _p(self.union), _p(self.scal[3:4]), _stream()),
+              "dev_dict_to_list_drop")
         if self.key_mode:  # sorted keys -> sorted PCs (the key map is monotone)
             check(self.L.syzcov_dev_keys_to_pcs(_p(self.pc_of_key), self.span, _p(self.union),
                                                 _p(self.union),

@@ -101,3 +101,43 @@ def test_engine_offsets_past_2_32(torch, keys):
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
     del big
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("key2", ["1", "0", "2"])
+def test_engine_key_mode_sentinel(torch, key2, monkeypatch):
+    """Key mode with a universe whose last PC is 0xFFFFFFFF: inputs made only of
+    the sentinel canonicalize to empty, otherwise it is an ordinary key
+    (cover.go:28-40, 104-131).  key2 selects the canonicalization: the 2-pass
+    key sort for the 2048-key class (default), none, or every class."""
+    monkeypatch.setenv("SYZCOV_CANON_KEY2", key2)
+    from syzkaller_amd.engine import CorpusEngine
+    rng = np.random.default_rng(33)
+    univ = (np.uint64(0xFFFF0000) + 4 * np.arange(1 << 14, dtype=np.uint64) + 3).astype(np.uint32)
+    covers = []
+    for i in range(900):
+        ln = int(rng.integers(0, 3000)) if i % 3 else int(rng.integers(0, 300))
+        c = univ[rng.integers(0, univ.size, size=ln)]
+        if i % 7 == 0:
+            c = np.full(int(rng.integers(1, 5)), 0xFFFFFFFF, np.uint32)
+        elif i % 5 == 0:
+            c = np.concatenate([c, np.full(3, 0xFFFFFFFF, np.uint32)])
+        covers.append(c.astype(np.uint32))
+    lens = np.array([len(c) for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers + [np.zeros(1, np.uint32)])
+    n = len(covers)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
+    eng = CorpusEngine(n, int(lens.sum()), int(lens.max()), 0xFFFF0000, 1 << 16,
+                       universe=univ)
+    assert eng.key_mode and eng.kshift == 2 and eng.span == 1 << 14
+    res = eng.step(off, raw, n)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs[:int(lens.sum())])
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    canon = eng.canonical_pcs(off, n).cpu().numpy().view(np.uint32)
+    for i in range(n):
+        a, b = int(o_off[i]), int(o_off[i]) + int(c_off[i + 1] - c_off[i])
+        assert np.array_equal(canon[a:b], c_pcs[c_off[i]:c_off[i + 1]]), i
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
