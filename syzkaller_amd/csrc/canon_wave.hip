@@ -550,16 +550,14 @@ __device__ __forceinline__ void scatter16(const uint32_t (&k)[NK], uint32_t nq, 
         uint32_t pos[4 * BQ];
         bool ok[4 * BQ];
 #pragma unroll
-        for (int j = 0; j < 4 * BQ; j++) {
-            ok[j] = real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
+        for (int j = 0; j < 4 * BQ; j++) {  // branch-free, as scatter_rows
+            ok[j] = (uint32_t)(q0 + j / 4) < nq && real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
             const uint32_t d = (k[q0 * 4 + j] >> sh) & 2047u;
-            if ((uint32_t)(q0 + j / 4) < nq)
-                pos[j] = atomicAdd(&h[ok[j] ? d >> 1 : KWORDS + l], ok[j] ? hinc(d) : 1u) >>
-                         ((d & 1u) << 4);
+            pos[j] = atomicAdd(&h[ok[j] ? d >> 1 : KWORDS + l], ok[j] ? hinc(d) : 1u) >>
+                     ((d & 1u) << 4);
         }
 #pragma unroll
-        for (int j = 0; j < 4 * BQ; j++)
-            if ((uint32_t)(q0 + j / 4) < nq) buf[ok[j] ? pos[j] & 0xFFFFu : CAP + l] = k[q0 * 4 + j];
+        for (int j = 0; j < 4 * BQ; j++) buf[ok[j] ? pos[j] & 0xFFFFu : CAP + l] = k[q0 * 4 + j];
     }
 }
 
@@ -610,7 +608,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
         const uint32_t nq = (end + 255) >> 8;
-        uint32_t k[NK];
+        uint32_t k[NK] = {};  // slots of inactive row quads rank on dummies
         bool oob = false;
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
@@ -944,12 +942,12 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     // key mode over <= 2^22 keys: sort the keys themselves, 2 passes of 11
     // bits with u16-pair histograms (canon_key_kernel); SYZCOV_CANON_KEY2=0
     // keeps the 3-pass window-offset sort (tuning / comparison)
-    // Measured per class at C2 (us, 2-pass / 3-pass): 2048 keys 2908 / 3153,
-    // 2560: 2908 / 2873, 3072: 2391 / 1601 (the compiler cannot fit 48 keys per
-    // lane in 168 VGPRs and falls to one wave per SIMD), 4096: 371 / 341,
-    // 8192: 41 / 50; so only the 2048-key class takes it (SYZCOV_CANON_KEY2:
-    // 0 = none, 1 = that class, 2 = every class).
-    int key2 = (key_out && nkeys <= (1ull << 22)) ? 1 : 0;
+    // Every class takes it (SYZCOV_CANON_KEY2: 0 = none, 1 = the 2048-key
+    // class only, 2 = every class).  C2 canon ms: 8.03 / 7.66 / 7.23 once the
+    // scatter batches were branch-free (with a conditional last row quad the
+    // larger classes were slower than the 3-pass sort; 3072 keys run at 2
+    // waves per SIMD: 48 keys per lane do not fit 168 VGPRs).
+    int key2 = (key_out && nkeys <= (1ull << 22)) ? 2 : 0;
     if (const char *e = getenv("SYZCOV_CANON_KEY2")) key2 = key2 ? atoi(e) : 0;
     cw::Params PK = P;  // the key kernel's unique loop compares KEYS
     PK.sent_key = so < pc_span ? (0xFFFFFFFFu >> kshift) - kbase : 0xFFFFFFFFu;

@@ -928,15 +928,25 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
 }
 
 // pass 2 + resets (first_w back to INT32_MAX)
+// first_w back to INT32_MAX by a fill below this many PCs/keys
+static constexpr uint64_t kFillSpan = 1ull << 24;
+
 static int mr_pass2(const mr::Args &A, uint64_t pc_span, const uint64_t *tab,
                     const int32_t *first_d, uint8_t *kept, hipStream_t s) {
     const unsigned long long *cnt = A.rec_cnt;
     hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, A, tab, first_d, kept);
     hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, A.n_items,
                        (const int32_t *)A.first_w, tab, first_d, kept);
-    hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s, cnt, A.rec_cap, A.first_w,
-                       pc_span);
+    if (pc_span <= kFillSpan) {
+        // a small key space: one coalesced fill (16 MB at 2^22 keys, ~5 us)
+        // instead of a scattered reset per record (~40 us at C2) + the
+        // overflow reset
+        SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)A.first_w, INT32_MAX, pc_span, s));
+    } else {
+        hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s, cnt, A.rec_cap,
+                           A.first_w, pc_span);
+    }
     SYZ_LAUNCH_CHECK();
     return 0;
 }
@@ -1144,10 +1154,12 @@ extern "C" int syzcov_dev_minimize_range(
     }
     hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
     if (cover_from_first) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
-    // record overflow: the union comes from first_w instead
-    hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
-                       (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
-                       pc_span, covered);
+    // record overflow: the union comes from first_w instead (cover_from_first
+    // already rebuilt covered from first_w)
+    if (!cover_from_first)
+        hipLaunchKernelGGL(mr::ovf_union_kernel, dim3(2048), dim3(256), 0, s,
+                           (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
+                           pc_span, covered);
     SYZ_LAUNCH_CHECK();
 #ifdef SYZ_MR_DEBUG
     {
