@@ -60,14 +60,18 @@ static inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 1
 // ---------------------------------------------------------------- device side
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-// Wave-wide inclusive scan of a u32 (64 lanes) via DPP-lowered shuffles.
+// Wave-wide inclusive scan of a u32 (64 lanes) in DPP, no LDS: row_shr 1, 2,
+// 4, 8 scan each row of 16 lanes (lanes shifted in from outside the row read
+// the identity 0), then row_bcast:15 adds row r-1's total to rows 1 and 3 and
+// row_bcast:31 adds rows 0-1's total to rows 2 and 3 (gfx9 DPP broadcasts).
+// The __shfl_up form compiled to a ds_bpermute round trip per step.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t l = __lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (l >= (uint32_t)d) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
 

@@ -8,6 +8,7 @@ export TMPDIR=/tmp
 o=${1:-gpurun_out/round}
 mkdir -p $o
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit 1;; esac; }
+[ -x tools/probe/scan_dpp ] && { timeout -k 10 60 tools/probe/scan_dpp || exit 1; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     ${2:+-k "$2"} > $o/pytest.log 2>&1
 rc=$?; tail -3 $o/pytest.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error" $o/pytest.log | head -20; }
