@@ -864,21 +864,15 @@ extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
     return 256 + (2 + cw::NCLS) * align_up(nseg * sizeof(uint32_t), 256);
 }
 
-// One class launch: HB = 11 (2048-entry histograms) when 19..22-bit keys
-// then take 2 passes instead of 3, else HB = 9.
+// One class launch of the 3-pass sort (9-bit digits; window mode, or key
+// spaces above 2^22).  (2 passes of 11-bit digits with packed u32 histograms
+// measured 9.45 vs 7.9 ms at C2: 8 KB histograms halve the resident waves; the
+// key mode's 2-pass sort holds them as u16 pairs instead, canon_key_kernel.)
 template <int NK, int MW>
-static void launch_class(bool hb11, const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
+static void launch_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
                          uint64_t nseg, hipStream_t s) {
-    // 8 KB histograms: LDS allows 2 waves per SIMD at most
-    constexpr int MW11 = MW > 2 ? 2 : MW;
-    if (hb11)
-        hipLaunchKernelGGL((cw::canon_wave_kernel<NK, MW11, 11>),
-                           dim3(resident_grid<NK, MW11, 11>(nseg)), dim3(64 * cw::WPB), 0, s, P,
-                           lc, cnt);
-    else
-        hipLaunchKernelGGL((cw::canon_wave_kernel<NK, MW, 9>),
-                           dim3(resident_grid<NK, MW, 9>(nseg)), dim3(64 * cw::WPB), 0, s, P, lc,
-                           cnt);
+    hipLaunchKernelGGL((cw::canon_wave_kernel<NK, MW, 9>), dim3(resident_grid<NK, MW, 9>(nseg)),
+                       dim3(64 * cw::WPB), 0, s, P, lc, cnt);
 }
 
 static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *out,
@@ -933,12 +927,6 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.big_list = big;
     P.big_cnt = cnts + 1;
     P.err = err_flag;
-    // 2 passes of 11-bit digits (2048-entry histograms) for 19..22-bit keys
-    // measured slower than 3 passes of <= 9 bits (C2 key mode 9.45 vs 7.9 ms:
-    // 8 KB histograms halve the resident waves), so it is a tuning option only
-    bool hb11 = false;
-    if (const char *e = getenv("SYZCOV_CANON_HB"))
-        hb11 = atoi(e) == 11 && P.nbits >= 19 && P.nbits <= 22;
     // key mode over <= 2^22 keys: sort the keys themselves, 2 passes of 11
     // bits with u16-pair histograms (canon_key_kernel); SYZCOV_CANON_KEY2=0
     // keeps the 3-pass window-offset sort (tuning / comparison)
@@ -982,11 +970,11 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
             }
         } else {
             switch (c) {
-            case 0: launch_class<32, SYZ_CANON_W32>(hb11, P, lc, ccnt + c, nseg, s); break;
-            case 1: launch_class<40, SYZ_CANON_W40>(hb11, P, lc, ccnt + c, nseg, s); break;
-            case 2: launch_class<48, SYZ_CANON_W48>(hb11, P, lc, ccnt + c, nseg, s); break;
-            case 3: launch_class<64, 2>(hb11, P, lc, ccnt + c, nseg, s); break;
-            case 4: launch_class<128, 1>(hb11, P, lc, ccnt + c, nseg, s); break;
+            case 0: launch_class<32, SYZ_CANON_W32>(P, lc, ccnt + c, nseg, s); break;
+            case 1: launch_class<40, SYZ_CANON_W40>(P, lc, ccnt + c, nseg, s); break;
+            case 2: launch_class<48, SYZ_CANON_W48>(P, lc, ccnt + c, nseg, s); break;
+            case 3: launch_class<64, 2>(P, lc, ccnt + c, nseg, s); break;
+            case 4: launch_class<128, 1>(P, lc, ccnt + c, nseg, s); break;
             }
         }
         SYZ_LAUNCH_CHECK();

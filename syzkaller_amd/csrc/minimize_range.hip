@@ -987,49 +987,25 @@ extern "C" int syzcov_dev_minimize_range(
     }
 #endif
     const size_t lds = ((size_t)1 << range_shift) / 8;
-    // tuning knobs (SYZCOV_MR_CFG="variant,pmode"): variant 0 = default (32-lane groups),
-    // 1 = lane-per-item never, 2 = always, 3..5 = the same without tests;
-    // pmode 0 = slice-major (P = 2R; default: 4.47 vs 4.60 ms at C2 with the
-    // 4-lane-group kernel), 1 = range-major (one slice; it was faster with the
-    // lane-per-item kernel, 7.1 vs 8.0 ms), k >= 3 = P = kR (4.6 ms)
-    // few long sub-runs per item (dense keys: 4 ranges at C2) take the whole
-    // wave above 512 PCs (variant 14: minimize 3.07 vs 3.57 ms, C2 key mode);
-    // many short ones (64 window ranges) the 4-lane groups throughout
-    // 15/16 = 14/0 with the first-cover atomics deferred to min_records_kernel;
-    // 17 = the chunk stream, 21 = the chunk stream over dynamic pieces (the
-    // default for few ranges, with P = 16R pieces per slice).  C2 key mode,
-    // minimize ms: 14 3.07, 15 3.00, 17 2.75 at P = 2R, 2.35 at 8R, 2.26-2.30
-    // at 12R..32R; 21 2.13-2.15 at 8R..32R (tools/gpu_mrvar.sh)
-    int variant = nrange <= 16 ? 21 : 16, pmode = nrange <= 16 ? 16 : 0;
+    // SYZCOV_MR_CFG="variant,pmode" (tuning): variant 0 = lane groups with the
+    // first-cover atomics in the streaming loop (round 1), 1 = lane groups with
+    // deferred first covers, 2 = the same with whole-wave sub-runs above 512
+    // PCs, 3 = the chunk stream over a fixed grid, 4 = the chunk stream over
+    // dynamic pieces; pmode 0 = P = 2R pieces per slice, 1 = one slice,
+    // k >= 3 = P = kR.  C2 key mode, minimize ms (tools/gpu_mrvar.sh): lane
+    // groups + whole wave 3.07 (deferred 3.00), stream 2.75 at P = 2R, 2.35 at
+    // 8R, 2.26-2.30 at 12R..32R, dynamic pieces 2.13-2.15 at 8R..32R.
+    int variant = nrange <= 16 ? 4 : 1, pmode = nrange <= 16 ? 16 : 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    // 8..11: (group lanes, chunks per lane) = (2,8) (4,2) (4,8) (2,4).  C2 sweep,
-    // minimize ms: (4,4) 4.6, (2,8) 4.9, (4,8) 5.0, (4,2) 5.05, (2,4) 5.05,
-    // (8,2) 5.7, (8,4) 5.9, (16,2) 8.4, one lane per item (old) 7.0
-    constexpr int NVAR = 22;
-    const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>, mr::pass1_kernel<0, true>,
-                          mr::pass1_kernel<0x40000000, true>, mr::pass1_kernel<96, false>,
-                          mr::pass1_kernel<0, false>, mr::pass1_kernel<0x40000000, false>,
-                          mr::pass1_kernel<96, false, true>, mr::pass1_kernel<96, true, true>,
-                          mr::pass1_kernel<0x40000000, true, false, 2, 8>,
-                          mr::pass1_kernel<0x40000000, true, false, 4, 2>,
-                          mr::pass1_kernel<0x40000000, true, false, 4, 8>,
-                          mr::pass1_kernel<0x40000000, true, false, 2, 4>,
-                          // 12..14: lane groups up to 256 / 128 / 512 PCs, whole wave above
-                          mr::pass1_kernel<256, true, false, 4, 4>,
-                          mr::pass1_kernel<128, true, false, 4, 4>,
-                          mr::pass1_kernel<512, true, false, 4, 4>,
-                          mr::pass1_kernel<512, true, false, 4, 4, true>,
+    constexpr int NVAR = 5;
+    const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>,
                           mr::pass1_kernel<0x40000000, true, false, 4, 4, true>,
-                          // 17, 18: the chunk stream, 4 / 2 x 64 chunks per step
-                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<2>,
-                          // 19: probe, stream without tests; 20: 8 x 64 chunks per step
-                          mr::pass1_stream_kernel<4, false>, mr::pass1_stream_kernel<8>,
-                          // 21: the chunk stream over dynamic pieces
-                          mr::pass1_stream_kernel<4, true, true>};
+                          mr::pass1_kernel<512, true, false, 4, 4, true>,
+                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<4, true, true>};
     const int vi = variant >= 0 && variant < NVAR ? variant : 0;
     const K k1 = kern[vi];
-    const bool defer = vi >= 15;
+    const bool defer = vi >= 1;
     static std::atomic<uint32_t> attr_set[NVAR];
     if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[vi]))) return rc;
     if (const char *e = getenv("SYZCOV_MR_CHUNK")) {  // tuning: "first,growth"
@@ -1063,7 +1039,7 @@ extern "C" int syzcov_dev_minimize_range(
         else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // more pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         unsigned grid = (unsigned)G;
-        if (vi == 21) {  // dynamic pieces: one workgroup per CU draws them
+        if (vi == 4) {  // dynamic pieces: one workgroup per CU draws them
             if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
             A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
                                   (size_t)nchunk * 256);
