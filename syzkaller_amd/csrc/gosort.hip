@@ -38,7 +38,10 @@
 namespace syz {
 namespace gsort {
 
-constexpr int SMALL = 4096;  // segment finished in one workgroup's LDS
+#ifndef SYZ_GSORT_SMALL
+#define SYZ_GSORT_SMALL 4096
+#endif
+constexpr int SMALL = SYZ_GSORT_SMALL;  // segment finished in one workgroup's LDS
 #ifndef SYZ_GSORT_TINY
 #define SYZ_GSORT_TINY 32
 #endif
@@ -182,65 +185,8 @@ __global__ void seg_gather_kernel(const int32_t *__restrict__ I, const uint64_t 
     }
 }
 
-// one lane per segment: control steps of one pdqsort loop iteration
-__global__ void plan_kernel(Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p, Plan *__restrict__ plan,
-                            uint32_t *__restrict__ K, int32_t *__restrict__ I, Ctl c) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s == 0) {  // the children of this round are pushed by swap_kernel (after this grid)
-        *c.next_count = 0u;
-        *c.next_maxlen = 0u;
-    }
-    if (s >= *ncur_p) return;
-    Seg g = cur[s];
-    Plan p{};
-    const int n = g.b - g.a;
-    GAcc d{K, I};
-    if (n <= SMALL) {  // (only the seed can be small here)
-        push_seg(c, g);
-        p.mode = M_DONE;
-    } else if (g.limit == 0) {  // `if limit == 0 { heapSort(data, a, b); return }`
-        gocore::heap_sort(d, g.a, g.b);
-        p.mode = M_DONE;
-    } else {
-        const bool wb = g.flags & 1, wp = g.flags & 2;
-        if (!wb) {
-            gocore::break_patterns(d, g.a, g.b);
-            g.limit--;
-            cur[s].limit = g.limit;
-        }
-        int hint;
-        int pivot = gocore::choose_pivot(d, g.a, g.b, &hint);
-        if (hint == gocore::kDecreasing) {
-            p.rev = 1;
-            pivot = (g.b - 1) - (pivot - g.a);
-            hint = gocore::kIncreasing;
-        }
-        p.pis = wb && wp && hint == gocore::kIncreasing;
-        p.pivot = pivot;
-        p.mode = M_ACTIVE;
-    }
-    plan[s] = p;
-}
-
-__global__ void reverse_kernel(const Seg *__restrict__ cur, const uint32_t *__restrict__ ncur_p,
-                               const Plan *__restrict__ plan, uint32_t *__restrict__ K,
-                               int32_t *__restrict__ I) {
-    const uint32_t s = blockIdx.y;
-    if (s >= *ncur_p) return;
-    const Plan p = plan[s];
-    if (p.mode != M_ACTIVE || !p.rev) return;
-    const Seg g = cur[s];
-    const int half = (g.b - g.a) / 2;
-    GAcc d{K, I};
-    for (int i = blockIdx.x * CH + threadIdx.x; i < min(half, (int)(blockIdx.x + 1) * CH);
-         i += blockDim.x)
-        d.swap(g.a + i, g.b - 1 - i);
-}
-
-// WG-cooperative partialInsertionSort (cover: gosort_core.h's sequential form),
-// then on lane 0 the partitionEqual test and the partition's Swap(a, pivot)
+// WG-cooperative first index i in [from, b) with K[i] > K[i-1], or b
 __device__ int wg_find_first_descent(const uint32_t *K, int from, int b, int *sh) {
-    // first i in [from, b) with K[i] > K[i-1], or b
     for (int c0 = from; c0 < b; c0 += WG) {
         const int i = c0 + threadIdx.x;
         const bool hit = i < b && K[i] > K[i - 1];
@@ -256,28 +202,76 @@ __device__ int wg_find_first_descent(const uint32_t *K, int from, int b, int *sh
     return b;
 }
 
-__global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
-                                                  const uint32_t *__restrict__ ncur_p,
-                                                  Plan *__restrict__ plan,
-                                                  uint32_t *__restrict__ K,
-                                                  int32_t *__restrict__ I) {
+// The control steps of one pdqsort loop iteration for each segment of the
+// round, one workgroup per segment (gocore's sequential form, pdqsort in
+// sort/zsortinterface.go): lane 0 runs the O(1) steps (breakPatterns,
+// choosePivot; heapSort at limit 0), the workgroup reverses a decreasing
+// segment and runs partialInsertionSort's scans, then lane 0 takes the
+// partitionEqual test and the Swap(a, pivot) both partition forms start with.
+// (Was three launches per round: plan, reverse, partial insertion sort.)
+__global__ __launch_bounds__(WG) void lead_kernel(Seg *__restrict__ cur,
+                                                   const uint32_t *__restrict__ ncur_p,
+                                                   Plan *__restrict__ plan,
+                                                   uint32_t *__restrict__ K,
+                                                   int32_t *__restrict__ I, Ctl c) {
     __shared__ int sh[WG / 64 + 2];
+    __shared__ Plan sp;
     const uint32_t s = blockIdx.x;
-    if (s >= *ncur_p || plan[s].mode != M_ACTIVE) return;
-    const Seg g = cur[s];
-    const int a = g.a, b = g.b;
-    int i = a + 1;
+    if (s == 0 && threadIdx.x == 0) {  // the children of this round are pushed by swap_kernel
+        *c.next_count = 0u;
+        *c.next_maxlen = 0u;
+    }
+    if (s >= *ncur_p) return;
+    Seg g = cur[s];
+    const int a = g.a, b = g.b, n = b - a;
+    GAcc d{K, I};
+    if (threadIdx.x == 0) {
+        Plan p{};
+        if (n <= SMALL) {  // (only the seed can be small here)
+            push_seg(c, g);
+            p.mode = M_DONE;
+        } else if (g.limit == 0) {  // `if limit == 0 { heapSort(data, a, b); return }`
+            gocore::heap_sort(d, a, b);
+            p.mode = M_DONE;
+        } else {
+            const bool wb = g.flags & 1, wp = g.flags & 2;
+            if (!wb) {
+                gocore::break_patterns(d, a, b);
+                g.limit--;
+                cur[s].limit = g.limit;
+            }
+            int hint;
+            int pivot = gocore::choose_pivot(d, a, b, &hint);
+            if (hint == gocore::kDecreasing) {
+                p.rev = 1;
+                pivot = (b - 1) - (pivot - a);
+                hint = gocore::kIncreasing;
+            }
+            p.pis = wb && wp && hint == gocore::kIncreasing;
+            p.pivot = pivot;
+            p.mode = M_ACTIVE;
+        }
+        sp = p;
+    }
+    __threadfence_block();
+    __syncthreads();
+    Plan p = sp;
+    if (p.mode == M_ACTIVE && p.rev) {  // reverseRange
+        for (int i = threadIdx.x; i < n / 2; i += WG) d.swap(a + i, b - 1 - i);
+        __threadfence_block();
+        __syncthreads();
+    }
     bool sorted = false;
-    for (int step = 0; plan[s].pis && step < 5; step++) {
+    int i = a + 1;
+    for (int step = 0; p.mode == M_ACTIVE && p.pis && step < 5; step++) {
         i = wg_find_first_descent(K, i, b, sh);
         if (i == b) {
             sorted = true;
             break;
         }
-        if (b - a < 50) break;
+        if (n < 50) break;
         // the three moves of one step run on lane 0 (bounded by the segment)
         if (threadIdx.x == 0) {
-            GAcc d{K, I};
             d.swap(i, i - 1);
             if (i - a >= 2)
                 for (int j = i - 1; j >= 1 && d.less(j, j - 1); j--) d.swap(j, j - 1);
@@ -288,17 +282,18 @@ __global__ __launch_bounds__(WG) void pis_kernel(const Seg *__restrict__ cur,
         __syncthreads();
     }
     if (threadIdx.x != 0) return;
-    if (sorted) {
-        plan[s].mode = M_DONE;
-        return;
+    if (p.mode == M_ACTIVE) {
+        if (sorted) {
+            p.mode = M_DONE;
+        } else {
+            // the partitionEqual test, then Swap(a, pivot) (lane 0 made the
+            // moves above: no fence needed)
+            p.eq = a > 0 && !d.less(a - 1, p.pivot);
+            d.swap(a, p.pivot);
+            p.kp = K[a];
+        }
     }
-    // the partitionEqual test, then Swap(a, pivot) that both partition forms
-    // start with (same lane as the moves above: no fence needed)
-    const int pivot = plan[s].pivot;
-    GAcc d{K, I};
-    plan[s].eq = a > 0 && !d.less(a - 1, pivot);
-    d.swap(a, pivot);
-    plan[s].kp = K[a];
+    plan[s] = p;
 }
 
 // f(x): x belongs to the left group (partition: Less(x, a) = K[x] > kp;
@@ -883,12 +878,8 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
         // the children of this round go to nxt
         // (plan_kernel zeroes ncount / nmax)
         Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
-        const unsigned gs = (ncur + 63) / 64;
         const unsigned nch = (unsigned)((maxlen + CH - 1) / CH);
-        hipLaunchKernelGGL(plan_kernel, dim3(gs), dim3(64), 0, s, cur, ccount, w.plan, w.K, w.I, cn);
-        hipLaunchKernelGGL(reverse_kernel, dim3((nch + 1) / 2 + 1, ncur), dim3(WG), 0, s, cur,
-                           ccount, w.plan, w.K, w.I);
-        hipLaunchKernelGGL(pis_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I);
+        hipLaunchKernelGGL(lead_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I, cn);
         hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
                            w.cc, w.cc_stride);
         hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
