@@ -47,7 +47,8 @@ constexpr int SMALL = SYZ_GSORT_SMALL;  // segment finished in one workgroup's L
 #endif
 constexpr int TINY = SYZ_GSORT_TINY;  // leaf finished by one lane
 static_assert(TINY <= 64, "leaf pdqsort: BitStack holds 3 parked tasks of a <= 64-element leaf");
-constexpr int CH = 4096;     // elements per block in the global rounds
+constexpr int CH = 4096;     // elements per work item in the global rounds
+constexpr unsigned ITEM_GRID = 1024;  // workgroups looping over a round's work items
 constexpr int WG = 256;
 
 struct Seg {
@@ -213,13 +214,18 @@ __global__ __launch_bounds__(WG) void lead_kernel(Seg *__restrict__ cur,
                                                    const uint32_t *__restrict__ ncur_p,
                                                    Plan *__restrict__ plan,
                                                    uint32_t *__restrict__ K,
-                                                   int32_t *__restrict__ I, Ctl c) {
+                                                   int32_t *__restrict__ I, Ctl c,
+                                                   uint32_t *__restrict__ items_cur,
+                                                   uint32_t *__restrict__ items_next,
+                                                   uint2 *__restrict__ items, uint32_t item_cap) {
     __shared__ int sh[WG / 64 + 2];
     __shared__ Plan sp;
+    __shared__ uint32_t ibase;
     const uint32_t s = blockIdx.x;
     if (s == 0 && threadIdx.x == 0) {  // the children of this round are pushed by swap_kernel
         *c.next_count = 0u;
         *c.next_maxlen = 0u;
+        *items_next = 0u;  // the next round's work items (this round's were zeroed before it)
     }
     if (s >= *ncur_p) return;
     Seg g = cur[s];
@@ -281,19 +287,32 @@ __global__ __launch_bounds__(WG) void lead_kernel(Seg *__restrict__ cur,
         __threadfence_block();
         __syncthreads();
     }
-    if (threadIdx.x != 0) return;
-    if (p.mode == M_ACTIVE) {
-        if (sorted) {
-            p.mode = M_DONE;
-        } else {
-            // the partitionEqual test, then Swap(a, pivot) (lane 0 made the
-            // moves above: no fence needed)
-            p.eq = a > 0 && !d.less(a - 1, p.pivot);
-            d.swap(a, p.pivot);
-            p.kp = K[a];
+    // the partition's work items: (segment, chunk of CH elements of (a, b))
+    const uint32_t nch = (uint32_t)((n - 1 + CH - 1) / CH);
+    if (threadIdx.x == 0) {
+        if (p.mode == M_ACTIVE) {
+            if (sorted) {
+                p.mode = M_DONE;
+            } else {
+                // the partitionEqual test, then Swap(a, pivot) (lane 0 made the
+                // moves above: no fence needed)
+                p.eq = a > 0 && !d.less(a - 1, p.pivot);
+                d.swap(a, p.pivot);
+                p.kp = K[a];
+            }
         }
+        plan[s] = p;
+        uint32_t b0 = item_cap;
+        if (p.mode == M_ACTIVE) {
+            b0 = atomicAdd(items_cur, nch);
+            if (b0 + nch > item_cap) *c.err = 6u;
+        }
+        ibase = b0;
     }
-    plan[s] = p;
+    __syncthreads();
+    const uint32_t b0 = ibase;
+    if (b0 + nch <= item_cap)
+        for (uint32_t j = threadIdx.x; j < nch; j += WG) items[b0 + j] = make_uint2(s, j);
 }
 
 // f(x): x belongs to the left group (partition: Less(x, a) = K[x] > kp;
@@ -302,25 +321,30 @@ __device__ __forceinline__ bool left_group(uint32_t k, uint32_t kp, int eq) {
     return eq ? k >= kp : k > kp;
 }
 
+// count, rank and swap loop over the round's work items (lead_kernel's
+// (segment, chunk) list) with a grid of at most ITEM_GRID workgroups, so the
+// host's loose bounds on the segment count and length never size a grid.
 __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
-                                                    const uint32_t *__restrict__ ncur_p,
+                                                    const uint32_t *__restrict__ nitems_p,
+                                                    const uint2 *__restrict__ items,
                                                     const Plan *__restrict__ plan,
                                                     const uint32_t *__restrict__ K,
                                                     uint32_t *__restrict__ cc, uint32_t stride) {
     __shared__ uint32_t tmp[WG / 64 + 1];
-    const uint32_t s = blockIdx.y;
-    if (s >= *ncur_p) return;
-    const Plan p = plan[s];
-    if (p.mode != M_ACTIVE) return;
-    const Seg g = cur[s];
-    const int x0 = g.a + 1 + (int)blockIdx.x * CH;
-    if (x0 >= g.b) return;
-    const int x1 = min(g.b, x0 + CH);
-    uint32_t c = 0;
-    for (int x = x0 + threadIdx.x; x < x1; x += WG) c += left_group(K[x], p.kp, p.eq);
-    uint32_t total;
-    block_excl_scan<WG>(c, tmp, &total);
-    if (threadIdx.x == 0) cc[(size_t)s * stride + blockIdx.x] = total;
+    const uint32_t nitems = *nitems_p;
+    for (uint32_t t = blockIdx.x; t < nitems; t += gridDim.x) {
+        const uint2 it = items[t];
+        const uint32_t s = it.x, j = it.y;
+        const Plan p = plan[s];
+        const Seg g = cur[s];
+        const int x0 = g.a + 1 + (int)j * CH;
+        const int x1 = min(g.b, x0 + CH);
+        uint32_t c = 0;
+        for (int x = x0 + threadIdx.x; x < x1; x += WG) c += left_group(K[x], p.kp, p.eq);
+        uint32_t total;
+        block_excl_scan<WG>(c, tmp, &total);
+        if (threadIdx.x == 0) cc[(size_t)s * stride + j] = total;
+    }
 }
 
 // ranks of the misplaced elements: PL[a + k] / PR[a + k] = position of the
@@ -331,7 +355,8 @@ __global__ __launch_bounds__(WG) void count_kernel(const Seg *__restrict__ cur,
 // barrier gives the waves' offsets, and it then ranks its rows with ballots
 // (no block scans inside the loop).
 __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
-                                                   const uint32_t *__restrict__ ncur_p,
+                                                   const uint32_t *__restrict__ nitems_p,
+                                                   const uint2 *__restrict__ items,
                                                    Plan *__restrict__ plan,
                                                    const uint32_t *__restrict__ K,
                                                    const uint32_t *__restrict__ cc,
@@ -339,92 +364,66 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
                                                    int32_t *__restrict__ PR) {
     constexpr int NW = WG / 64, WCH = CH / NW;  // elements per wave
     __shared__ uint32_t wcnt[NW], wpre[NW], wtot[NW];
-    const uint32_t s = blockIdx.y;
-    if (s >= *ncur_p) return;
-    const Plan p = plan[s];
-    if (p.mode != M_ACTIVE) return;
-    const Seg g = cur[s];
-    const int x0 = g.a + 1 + (int)blockIdx.x * CH;
-    if (x0 >= g.b) return;
-    const int x1 = min(g.b, x0 + CH);
-    const uint32_t w = threadIdx.x >> 6, l = __lane_id();
-    const uint64_t lt = (1ull << l) - 1ull;
-    const int w0 = x0 + (int)w * WCH, w1 = min(x1, w0 + WCH);
-    uint32_t c = 0;
-    for (int x = w0 + (int)l; x < w1; x += 64) c += left_group(K[x], p.kp, p.eq);
-    c = wave_sum(c);
-    const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
-    uint32_t pre = 0, tot = 0;
-    for (uint32_t q = threadIdx.x; q < nch; q += WG) {
-        const uint32_t v = cc[(size_t)s * stride + q];
-        tot += v;
-        pre += q < blockIdx.x ? v : 0u;
-    }
-    pre = wave_sum(pre);
-    tot = wave_sum(tot);
-    if (l == 0) {
-        wcnt[w] = c;
-        wpre[w] = pre;
-        wtot[w] = tot;
-    }
-    __syncthreads();
-    uint32_t base = 0, cnt = 0;
-    for (uint32_t v = 0; v < (uint32_t)NW; v++) {
-        base += wpre[v] + (v < w ? wcnt[v] : 0u);
-        cnt += wtot[v];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) plan[s].cnt = (int)cnt;
-    const int L = g.a + (int)cnt;  // left region [a+1, L]
-    uint32_t mloc = 0;
-    for (int c0 = w0; c0 < w1; c0 += 64) {
-        const int x = c0 + (int)l;
-        const bool in = x < w1;
-        const bool f = in && left_group(K[x], p.kp, p.eq);
-        const uint64_t m = __ballot(f);
-        const uint32_t pf = base + (uint32_t)__popcll(m & lt);
-        if (in) {
-            if (x > L && f) PR[g.a + ((int)cnt - (int)pf - 1)] = x;
-            if (x <= L && !f) {
-                PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
-                mloc++;
-            }
+    const uint32_t nitems = *nitems_p;
+    for (uint32_t t = blockIdx.x; t < nitems; t += gridDim.x) {
+        const uint2 it = items[t];
+        const uint32_t s = it.x, j = it.y;
+        const Plan p = plan[s];
+        const Seg g = cur[s];
+        const int x0 = g.a + 1 + (int)j * CH;
+        const int x1 = min(g.b, x0 + CH);
+        const uint32_t w = threadIdx.x >> 6, l = __lane_id();
+        const uint64_t lt = (1ull << l) - 1ull;
+        const int w0 = x0 + (int)w * WCH, w1 = min(x1, w0 + WCH);
+        uint32_t c = 0;
+        for (int x = w0 + (int)l; x < w1; x += 64) c += left_group(K[x], p.kp, p.eq);
+        c = wave_sum(c);
+        const uint32_t nch = (uint32_t)((g.b - g.a - 1 + CH - 1) / CH);
+        uint32_t pre = 0, tot = 0;
+        for (uint32_t q = threadIdx.x; q < nch; q += WG) {
+            const uint32_t v = cc[(size_t)s * stride + q];
+            tot += v;
+            pre += q < j ? v : 0u;
         }
-        base += (uint32_t)__popcll(m);
+        pre = wave_sum(pre);
+        tot = wave_sum(tot);
+        if (l == 0) {
+            wcnt[w] = c;
+            wpre[w] = pre;
+            wtot[w] = tot;
+        }
+        __syncthreads();
+        uint32_t base = 0, cnt = 0;
+        for (uint32_t v = 0; v < (uint32_t)NW; v++) {
+            base += wpre[v] + (v < w ? wcnt[v] : 0u);
+            cnt += wtot[v];
+        }
+        __syncthreads();  // wcnt / wpre / wtot are rewritten by the next item
+        if (j == 0 && threadIdx.x == 0) plan[s].cnt = (int)cnt;
+        const int L = g.a + (int)cnt;  // left region [a+1, L]
+        uint32_t mloc = 0;
+        for (int c0 = w0; c0 < w1; c0 += 64) {
+            const int x = c0 + (int)l;
+            const bool in = x < w1;
+            const bool f = in && left_group(K[x], p.kp, p.eq);
+            const uint64_t m = __ballot(f);
+            const uint32_t pf = base + (uint32_t)__popcll(m & lt);
+            if (in) {
+                if (x > L && f) PR[g.a + ((int)cnt - (int)pf - 1)] = x;
+                if (x <= L && !f) {
+                    PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
+                    mloc++;
+                }
+            }
+            base += (uint32_t)__popcll(m);
+        }
+        mloc = wave_sum(mloc);
+        if (l == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
     }
-    mloc = wave_sum(mloc);
-    if (l == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
 }
 
-// The m swaps of the partition, then the tail of the loop iteration:
-// partitionEqual's `a = mid` continue, or the pivot swap and the two
-// recursions (smaller side first, as Go recurses on it).  The tail touches
-// only positions a (never swapped: PL, PR lie in (a, b)) and mid = a + cnt,
-// which a swap moves only if it is the last left-misplaced element
-// (PL[m - 1] == mid).  So the block that owns swap m - 1 runs the tail after
-// its own swaps (block 0 if mid does not move): no cross-block hand-off.
-__global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
-                                                   const uint32_t *__restrict__ ncur_p,
-                                                   Plan *__restrict__ plan, uint32_t *__restrict__ K,
-                                                   int32_t *__restrict__ I,
-                                                   const int32_t *__restrict__ PL,
-                                                   const int32_t *__restrict__ PR, Ctl c) {
-    const uint32_t s = blockIdx.y;
-    if (s >= *ncur_p) return;
-    const Plan p = plan[s];
-    if (p.mode != M_ACTIVE) return;
-    const uint32_t nparts = p.m > 0 ? (uint32_t)((p.m + CH - 1) / CH) : 1u;
-    if (blockIdx.x >= nparts) return;
-    const Seg g = cur[s];
-    GAcc d{K, I};
-    for (int k = blockIdx.x * CH + threadIdx.x; k < min(p.m, (int)(blockIdx.x + 1) * CH);
-         k += blockDim.x)
-        d.swap(PL[g.a + k], PR[g.a + k]);
-    const int mid = g.a + p.cnt;
-    const bool moved = !p.eq && p.m > 0 && PL[g.a + p.m - 1] == mid;
-    const uint32_t owner = moved ? (uint32_t)((p.m - 1) / CH) : 0u;
-    if (blockIdx.x != owner) return;
-    __syncthreads();  // this block's swaps (incl. the one moving mid) before the tail
-    if (threadIdx.x != 0) return;
+// lane 0 of the owner block
+__device__ void swap_tail(const Ctl &c, const Plan &p, const Seg &g, const GAcc &d, int mid) {
     if (p.eq) {  // partitionEqual returns a + 1 + cnt; the loop continues
         push_seg(c, Seg{g.a + 1 + p.cnt, g.b, g.limit, g.flags});
         return;
@@ -438,6 +437,40 @@ __global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
     } else {
         push_seg(c, Seg{mid + 1, g.b, g.limit, 3});
         push_seg(c, Seg{g.a, mid, g.limit, (rn >= thr) | (already << 1)});
+    }
+}
+
+// The m swaps of the partition, then the tail of the loop iteration:
+// partitionEqual's `a = mid` continue, or the pivot swap and the two
+// recursions (smaller side first, as Go recurses on it).  The tail touches
+// only positions a (never swapped: PL, PR lie in (a, b)) and mid = a + cnt,
+// which a swap moves only if it is the last left-misplaced element
+// (PL[m - 1] == mid).  So the block that owns swap m - 1 runs the tail after
+// its own swaps (block 0 if mid does not move): no cross-block hand-off.
+__global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
+                                                   const uint32_t *__restrict__ nitems_p,
+                                                   const uint2 *__restrict__ items,
+                                                   Plan *__restrict__ plan, uint32_t *__restrict__ K,
+                                                   int32_t *__restrict__ I,
+                                                   const int32_t *__restrict__ PL,
+                                                   const int32_t *__restrict__ PR, Ctl c) {
+    const uint32_t nitems = *nitems_p;
+    for (uint32_t t = blockIdx.x; t < nitems; t += gridDim.x) {
+        const uint2 it = items[t];
+        const uint32_t s = it.x, j = it.y;
+        const Plan p = plan[s];
+        const uint32_t nparts = p.m > 0 ? (uint32_t)((p.m + CH - 1) / CH) : 1u;
+        if (j >= nparts) continue;  // (m <= (n - 1) / 2: never more parts than chunks)
+        const Seg g = cur[s];
+        GAcc d{K, I};
+        for (int k = (int)j * CH + threadIdx.x; k < min(p.m, (int)(j + 1) * CH); k += blockDim.x)
+            d.swap(PL[g.a + k], PR[g.a + k]);
+        const int mid = g.a + p.cnt;
+        const bool moved = !p.eq && p.m > 0 && PL[g.a + p.m - 1] == mid;
+        const uint32_t owner = moved ? (uint32_t)((p.m - 1) / CH) : 0u;
+        if (j != owner) continue;
+        __syncthreads();  // this block's swaps (incl. the one moving mid) before the tail
+        if (threadIdx.x == 0) swap_tail(c, p, g, d, mid);
     }
 }
 
@@ -759,8 +792,10 @@ struct SortWs {
     Seg *segA, *segB, *small;
     Plan *plan;
     uint32_t *cc;
+    uint2 *items;   // the round's (segment, chunk) work items
     uint32_t *ctl;  // [0] err [1] countA [2] countB [3] small count [4] maxA [5] maxB
-    uint32_t seg_cap, small_cap, cc_stride;
+                    // [6] itemsA [7] itemsB
+    uint32_t seg_cap, small_cap, cc_stride, item_cap;
     size_t n;  // positions
 };
 
@@ -768,6 +803,7 @@ static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
     const uint32_t seg_cap = (uint32_t)(2 * (n / SMALL) + 16);
     const uint32_t small_cap = (uint32_t)(2 * (n / SMALL + 1) * 64 + 64 + ngroups);
     const uint32_t cc_stride = (uint32_t)(n / CH + 2);
+    const uint32_t item_cap = (uint32_t)(n / CH + seg_cap + 16);
     size_t o = 0;
     auto take = [&](size_t bytes) {
         size_t r = o;
@@ -777,7 +813,8 @@ static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
     size_t oK = take(n * 4), oI = take(n * 4), oPL = take(n * 4), oPR = take(n * 4),
            oA = take(seg_cap * sizeof(Seg)), oB = take(seg_cap * sizeof(Seg)),
            oS = take(small_cap * sizeof(Seg)), oP = take(seg_cap * sizeof(Plan)),
-           oC = take((size_t)seg_cap * cc_stride * 4), oT = take(64);
+           oC = take((size_t)seg_cap * cc_stride * 4), oIt = take((size_t)item_cap * 8),
+           oT = take(64);
     if (w) {
         w->K = (uint32_t *)(base + oK);
         w->I = (int32_t *)(base + oI);
@@ -788,7 +825,9 @@ static size_t ws_layout(size_t n, size_t ngroups, SortWs *w, uint8_t *base) {
         w->small = (Seg *)(base + oS);
         w->plan = (Plan *)(base + oP);
         w->cc = (uint32_t *)(base + oC);
+        w->items = (uint2 *)(base + oIt);
         w->ctl = (uint32_t *)(base + oT);
+        w->item_cap = item_cap;
         w->seg_cap = seg_cap;
         w->small_cap = small_cap;
         w->cc_stride = cc_stride;
@@ -855,6 +894,7 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     PinnedCtl pin;
     Seg *cur = w.segA, *nxt = w.segB;
     uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
+    uint32_t *citems = w.ctl + 6, *nitems = w.ctl + 7;
     uint32_t h[6] = {0, 0, 0, 0, 0, 0};
     if (seeded < 0) {
         if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
@@ -868,28 +908,37 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     // rounds are queued without a host round trip: the host keeps only UPPER
     // BOUNDS for the grids (a segment has at most two large children, each
     // shorter than it, and at most total/(SMALL+1) large segments exist) and
-    // reads the true count back every SYNC_EVERY rounds.
-    int SYNC_EVERY = 4;
+    // reads the true count back every SYNC_EVERY rounds.  Rounds queued after
+    // the last large segment finished find no work items and return at once
+    // (≈5 µs a round against ≈50 µs of host turnaround per read-back; a
+    // pipelined read-back, the next rounds queued behind an event before the
+    // host waits, measured slower: its bounds are a batch older).
+    int SYNC_EVERY = 8;
     if (const char *e = getenv("SYZCOV_SORT_SYNC")) SYNC_EVERY = std::max(1, atoi(e));  // tuning
     const uint32_t cap_seg = std::min<uint32_t>(w.seg_cap, w.n / (SMALL + 1) + 1);
     uint32_t ncur = h[1], maxlen = h[4];
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
         // the children of this round go to nxt
-        // (plan_kernel zeroes ncount / nmax)
+        // (lead_kernel zeroes ncount / nmax)
         Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
-        const unsigned nch = (unsigned)((maxlen + CH - 1) / CH);
-        hipLaunchKernelGGL(lead_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I, cn);
-        hipLaunchKernelGGL(count_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+        const uint64_t nch = (maxlen + CH - 1) / CH;
+        // work items: at most ncur * nch, and sum ceil((n_s - 1) / CH) <= n / CH + ncur
+        const unsigned gi = (unsigned)std::min<uint64_t>(
+            std::min<uint64_t>(nch * ncur, w.n / CH + ncur), ITEM_GRID);
+        hipLaunchKernelGGL(lead_kernel, dim3(ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K, w.I, cn,
+                           citems, nitems, w.items, w.item_cap);
+        hipLaunchKernelGGL(count_kernel, dim3(gi), dim3(WG), 0, s, cur, citems, w.items, w.plan, w.K,
                            w.cc, w.cc_stride);
-        hipLaunchKernelGGL(rank_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+        hipLaunchKernelGGL(rank_kernel, dim3(gi), dim3(WG), 0, s, cur, citems, w.items, w.plan, w.K,
                            w.cc, w.cc_stride, w.PL, w.PR);
-        hipLaunchKernelGGL(swap_kernel, dim3(nch, ncur), dim3(WG), 0, s, cur, ccount, w.plan, w.K,
+        hipLaunchKernelGGL(swap_kernel, dim3(gi), dim3(WG), 0, s, cur, citems, w.items, w.plan, w.K,
                            w.I, w.PL, w.PR, cn);
         SYZ_LAUNCH_CHECK();
         std::swap(cur, nxt);
         std::swap(ccount, ncount);
         std::swap(cmax, nmax);
+        std::swap(citems, nitems);
         // bounds for the next round (exact after a read-back)
         ncur = std::min(2 * ncur, cap_seg);
         maxlen = maxlen > 1 ? maxlen - 1 : 0;
