@@ -715,11 +715,25 @@ __global__ __launch_bounds__(256) void newcov_insert_kernel(
     }
 }
 
+// The batch's zero fills in one launch: stats, the per-call counters, is_new
+__global__ __launch_bounds__(256) void nc_zero_kernel(uint32_t *__restrict__ stats,
+                                                      uint32_t *__restrict__ ccnt, uint32_t nc,
+                                                      uint8_t *__restrict__ is_new, uint32_t nrec) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    if (t < 4) stats[t] = 0u;
+    for (uint32_t c = t; c < nc; c += nt) ccnt[c] = 0u;
+    for (uint32_t k = t; k < nrec; k += nt) is_new[k] = 0;
+}
+
+// stats_out (nullable): the caller's copy of stats[0..2), taken here (the
+// last kernel of the batch) instead of by a separate device copy
 __global__ __launch_bounds__(256) void newcov_own_kernel(
     const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ hkey,
     const uint32_t *__restrict__ hval, uint8_t *__restrict__ is_new,
-    uint32_t *__restrict__ maxcov, uint32_t *__restrict__ mfl, uint64_t words_per_call, Index X) {
+    uint32_t *__restrict__ maxcov, uint32_t *__restrict__ mfl, uint64_t words_per_call, Index X,
+    uint32_t *__restrict__ stats_out) {
+    if (stats_out && blockIdx.x == 0 && threadIdx.x < 2) stats_out[threadIdx.x] = stats[threadIdx.x];
     if (stats[0] || !stats[1]) return;
     const uint32_t n = stats[1];
     const uint64_t mask = hash_cap(n) - 1;
@@ -1143,7 +1157,7 @@ static uint32_t env_items() {
 
 static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
                          const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
-                         uint8_t *ws, uint32_t **stats_out, hipStream_t s) {
+                         uint8_t *ws, uint32_t **stats_out, uint32_t *stats_user, hipStream_t s) {
     const NcLayout Lw = nc_layout(nrec, npc);
     uint2 *clist = (uint2 *)ws;
     uint32_t *perm = (uint32_t *)(ws + Lw.perm);
@@ -1151,17 +1165,16 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     uint32_t *hval = (uint32_t *)(ws + Lw.hval);
     uint32_t *stats = (uint32_t *)(ws + Lw.stats);
     *stats_out = stats;
-    SYZ_HIP(hipMemsetAsync(stats, 0, 16, s));
-    SYZ_HIP(hipMemsetAsync(is_new, 0, nrec, s));
     const uint32_t nc = (uint32_t)st->ncalls;
     uint32_t *ccnt = st->grp, *coff = ccnt + nc + 1, *cur = coff + nc + 1, *ipre = cur + nc + 1;
+    hipLaunchKernelGGL(nc_zero_kernel, dim3(grid_for(std::max<uint64_t>(nrec, nc), 256, 256)),
+                       dim3(256), 0, s, stats, ccnt, nc, is_new, (uint32_t)nrec);
     // records grouped by call (both passes)
     static std::atomic<uint32_t> gs_done{0};
     if (nc <= GRP_MAX_CALLS) {
         int rc = set_dyn_lds_once((const void *)grp_scatter_kernel, GRP_MAX_CALLS * 4, gs_done);
         if (rc) return rc;
     }
-    SYZ_HIP(hipMemsetAsync(ccnt, 0, 4 * (size_t)nc, s));
     hipLaunchKernelGGL(grp_hist_kernel, dim3(grid_for(nrec, 256, 1024)), dim3(256),
                        nc <= GRP_MAX_CALLS ? (size_t)nc * 4 : 0, s, callid, (uint32_t)nrec,
                        st->ncalls, ccnt, stats);
@@ -1259,7 +1272,8 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                        (const uint2 *)clist, (const uint32_t *)stats, hkey, hval);
     hipLaunchKernelGGL(newcov_own_kernel, dim3(gh), dim3(256), 0, s, callid, (const uint2 *)clist,
                        (const uint32_t *)stats, (const unsigned long long *)hkey,
-                       (const uint32_t *)hval, is_new, st->maxcov, st->mfl, st->words, st->X);
+                       (const uint32_t *)hval, is_new, st->maxcov, st->mfl, st->words, st->X,
+                       stats_user);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
@@ -1282,10 +1296,8 @@ extern "C" int syzcov_state_newcov_dev(syzcov_cover_state h, const int32_t *call
     hipStream_t s = (hipStream_t)stream;
     st->dirty = true;
     uint32_t *dstats = nullptr;
-    int rc = newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws, &dstats, s);
-    if (rc) return rc;
-    if (stats) SYZ_HIP(hipMemcpyAsync(stats, dstats, 8, hipMemcpyDeviceToDevice, s));
-    return 0;
+    return newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws, &dstats, stats,
+                         s);
 }
 
 // The host-buffer batch of execute() (add_input false) or addInput
@@ -1320,7 +1332,8 @@ static int64_t newcov_host(CoverState *st, const int32_t *callid, const uint64_t
     if (npc) SYZ_HIP(hipMemcpyAsync(S + o_pcs, rec_pcs + base0, npc * 4, hipMemcpyHostToDevice, s));
     uint32_t *dstats = nullptr;
     rc = newcov_launch(st, (const int32_t *)S, (const uint64_t *)(S + o_off),
-                       (const uint32_t *)(S + o_pcs), nrec, npc, S + o_new, S + o_ws, &dstats, s);
+                       (const uint32_t *)(S + o_pcs), nrec, npc, S + o_new, S + o_ws, &dstats, nullptr,
+                       s);
     if (rc) return rc;
     if (add_input) {
         hipLaunchKernelGGL(accept_or_kernel, dim3(grid_for(nrec, 4, 8192)), dim3(256), 0, s,
