@@ -219,11 +219,18 @@ constexpr int LC_THREADS = 1024;         // LDS: two workgroups per CU
 constexpr uint32_t LC_CBW = 16;          // candidates buffered per wave
 constexpr int LC_U = 4;                  // 256-PC rows per step (two steps in flight)
 constexpr int SQ_G = 8;                  // split queries in flight per wave
+#ifndef SYZ_NC_SPLIT_LNS
+#define SYZ_NC_SPLIT_LNS 5
+#endif
+constexpr uint32_t SPLIT_LNS = SYZ_NC_SPLIT_LNS;  // log2 of the samples per record
+constexpr uint32_t SPLIT_NS = 1u << SPLIT_LNS;    // (each sample fetches its own line)
+static_assert(SPLIT_NS <= 64, "one sample per lane");
 
-// Range boundaries of every grouped record, one wave per record, by 64-way
-// search: 64 evenly spaced samples bracket each query to a bucket of
-// ceil(n / 64) PCs, whose elements are then counted (SQ_G queries' bucket
-// loads in flight together).  Queries: "index < (q+1) << RSH" for q < nr-1
+// Range boundaries of every grouped record, one wave per record, by
+// SPLIT_NS-way search: SPLIT_NS evenly spaced samples bracket each query to a
+// bucket of ceil(n / SPLIT_NS) PCs, whose elements are then counted (SQ_G
+// queries' bucket loads in flight together).  32 samples: 32 sample lines +
+// ~2 lines per query's bucket, against 64 + ~1 at 64 samples.  Queries: "index < (q+1) << RSH" for q < nr-1
 // and "not the sentinel" (the record's length without its trailing
 // 0xFFFFFFFF, which is never a candidate, cover.go:43-48).  Sorted records
 // only: a record out of order is caught here at the boundaries (stats 3)
@@ -240,9 +247,9 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
         const uint64_t b = rec_off[k];
         const uint32_t n = (uint32_t)(rec_off[k + 1] - b);
         const uint32_t *p = pcs + b;
-        // samples: s_l = floor(l n / 64) (every element when n <= 64)
-        const uint32_t ns = min(n, 64u);
-        const uint32_t sl = n <= 64 ? l : (uint32_t)(((uint64_t)l * n) >> 6);
+        // samples: s_l = floor(l n / NS) (every element when n <= NS)
+        const uint32_t ns = min(n, SPLIT_NS);
+        const uint32_t sl = n <= SPLIT_NS ? l : (uint32_t)(((uint64_t)l * n) >> SPLIT_LNS);
         const uint32_t x = l < ns ? p[sl] : SENT;
         uint32_t kx;
         const bool xin = pc_index(X, x, &kx);
@@ -257,12 +264,12 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
                 const uint32_t qy = g0 + g;
                 v[g] = qy + 1 < nqry ? (qy + 1) << RSH : 0xFFFFFFFFu;
                 const uint32_t c = qy < nqry ? (uint32_t)__popcll(__ballot(l < ns && kx < v[g])) : 0u;
-                if (n <= 64) {
+                if (n <= SPLIT_NS) {
                     lo[g] = c;
                     hi[g] = c;
                 } else {
-                    lo[g] = c == 0 ? 0u : (uint32_t)(((uint64_t)(c - 1) * n) >> 6) + 1;
-                    hi[g] = c == 64 ? n : (uint32_t)(((uint64_t)c * n) >> 6);
+                    lo[g] = c == 0 ? 0u : (uint32_t)(((uint64_t)(c - 1) * n) >> SPLIT_LNS) + 1;
+                    hi[g] = c == SPLIT_NS ? n : (uint32_t)(((uint64_t)c * n) >> SPLIT_LNS);
                     if (qy >= nqry) hi[g] = lo[g];
                 }
                 cnt[g] = 0;
