@@ -358,8 +358,7 @@ def cpu_baseline_newcov(args, nrec: int, nhist: int = 16384):
                                 args.log2_space)
     c_off, c_pcs = orc.canonicalize_csr(off, pcs)
     recs = [c_pcs[c_off[i]:c_off[i + 1]] for i in range(nhist + nrec)]
-    rng = np.random.default_rng(SEED_NEWCOV)
-    cids = rng.integers(0, args.ncalls, size=nhist + nrec)
+    cids = orc.synth_callids(SEED_NEWCOV, nhist + nrec, args.ncalls)  # the GPU stream's first records
     fo, fp = orc.synth_corpus(SEED_NEWCOV, 1, 1 << (args.log2_space - 7), 1, args.log2_space,
                               first=FLAKE_INPUT)
     flakes = orc.canonicalize(fp[:int(fo[1])])
@@ -385,37 +384,20 @@ def bench_newcov(args):
     import torch
     world, rank, dev = init_dist()
     from syzkaller_amd import _lib
-    from syzkaller_amd.engine import synth_corpus, synth_window
+    from syzkaller_amd.engine import synth_corpus, synth_records, synth_window
     from syzkaller_amd.fuzzer import CoverState
     L = _lib.lib()
     s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
     P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
     lo, span = synth_window(args.log2_space)
     nrec, nb = args.records, args.warmup + args.steps
-    gen = torch.Generator(device="cpu").manual_seed(SEED_NEWCOV + rank)
 
     def make_batch(b):
-        first = (rank * (nb + args.history) + b) * nrec
-        off, raw, lens, total = synth_corpus(nrec, SEED_NEWCOV, first=first, mean=args.mean,
-                                             sigma=args.sigma, log2_space=args.log2_space,
-                                             device=dev)
-        new_len = torch.empty(nrec + 1, dtype=torch.int32, device=dev)
-        err = torch.zeros(4, dtype=torch.int32, device=dev)
-        wsz = L.syzcov_dev_canon_split_ws_size(nrec)
-        ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
-        _lib.check(L.syzcov_dev_canon_split(P(off), P(raw), P(raw), P(new_len), nrec,
-                                            int(lens.max().item()), lo, span, 20, None, None,
-                                            P(err), P(ws), wsz, s()), "canon_split")
-        # compact the canonical prefixes into a record CSR (setup, untimed)
-        nl = new_len[:nrec].to(torch.int64)
-        roff = torch.zeros(nrec + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(nl, 0, out=roff[1:])
-        npc = int(roff[-1].item())
-        seg = torch.repeat_interleave(torch.arange(nrec, device=dev), nl)
-        src = off[:-1][seg] + (torch.arange(npc, device=dev) - roff[:-1][seg])
-        pcs = raw[src].contiguous()
-        cid = torch.randint(0, args.ncalls, (nrec,), generator=gen, dtype=torch.int32).to(dev)
-        return cid, roff, pcs, npc
+        # batch b of rank r's stream: records (r * (history + nb) + b) * nrec + k
+        # (history batches first): the stream oracle/newcov_full.c restates
+        first = (rank * (args.history + nb) + b) * nrec
+        return synth_records(nrec, SEED_NEWCOV, first, args.ncalls, mean=args.mean,
+                             sigma=args.sigma, log2_space=args.log2_space, device=dev)
 
     import numpy as np
     st = CoverState(args.ncalls, lo, span)
@@ -433,7 +415,7 @@ def bench_newcov(args):
     # same check before the bench (maxCover near saturation, as in steady state)
     hist_new = 0
     for h in range(args.history):
-        cid, roff, pcs, npc = make_batch(nb + h)
+        cid, roff, pcs, npc = make_batch(h)
         wsz = L.syzcov_state_newcov_ws_size(nrec, npc)
         ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
         flags = torch.zeros(nrec, dtype=torch.uint8, device=dev)
@@ -441,7 +423,7 @@ def bench_newcov(args):
                                              None, P(ws), wsz, s()), "state_newcov_dev")
         hist_new += int(flags.sum().item())
         del ws, pcs
-    batches = [make_batch(b) for b in range(nb)]
+    batches = [make_batch(args.history + b) for b in range(nb)]
     max_npc = max(b[3] for b in batches)
     wsz = L.syzcov_state_newcov_ws_size(nrec, max_npc)
     ws = torch.empty(wsz, dtype=torch.uint8, device=dev)

@@ -52,6 +52,10 @@ extern "C" {
 /* bits of a device err_flag word (engine kernels) */
 #define SYZCOV_ERR_WINDOW 1u  /* a PC outside the configured PC window */
 #define SYZCOV_ERR_SEGLEN 2u  /* a segment longer than the declared max_seg_len */
+#define SYZCOV_ERR_UNIVERSE 4u /* key mode: a PC that is not in the registered universe */
+/* Key mode: the key shift is capped so a universe PC's low kshift bits fit one
+ * byte of the membership table with 0xFF left for "no universe PC". */
+#define SYZCOV_KSHIFT_MAX 7u
 
 /* Version / build identification: "syzcov <ver> gfx950". */
 const char *syzcov_version(void);
@@ -202,11 +206,16 @@ int syzcov_state_destroy(syzcov_cover_state st);
 /* maxCover[call] = Union(maxCover[call], pcs) (sorted list). */
 int syzcov_state_add(syzcov_cover_state st, int call, const uint32_t *pcs, size_t n);
 int syzcov_state_set_flakes(syzcov_cover_state st, const uint32_t *pcs, size_t n);
-/* Optional, before the first add/newcov: the PC universe (the reference's
- * allCoverPCs, syz-manager/cover.go:57-69 — the __sanitizer_cov_trace_pc call
- * sites).  maxCover of universe PCs is then kept over dense universe ids
- * (1 bit per known PC instead of per window offset); other PCs still work
- * through the window bitmaps.  Results are identical either way. */
+/* Optional, before the first add/newcov: the PC universe = every PC KCOV can
+ * report, i.e. the RETURN address of each `call __sanitizer_cov_trace_pc`
+ * (the call sites of allCoverPCs, syz-manager/cover.go:274-306, plus the
+ * call's length: KCOV records return addresses, which is why cover.go:82
+ * subtracts 1), truncated to u32.  maxCover, corpusCover and flakes are then
+ * kept over the universe's dense keys (keys.hip).  Every PC passed in from
+ * then on is checked against the universe: one that is not in it fails the
+ * call (SYZCOV_ERANGE; a newcov/triage batch is rejected whole) instead of
+ * sharing a key with a universe PC, so results are the reference's or an
+ * error, never different ones. */
 int syzcov_state_set_universe(syzcov_cover_state st, const uint32_t *pcs, size_t n);
 /* Reads maxCover[call] back as a sorted list (out capacity: pc_span or the
  * count from a NULL-out call); returns its length. */
@@ -365,23 +374,28 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
                            uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
                            void *stream);
 /* Key mode (keys.hip): key(pc) = (pc >> kshift) - kbase over a registered PC
- * universe (allCoverPCs) with kshift = the largest collision-free shift.
- * The sort runs on window offsets of [pc_lo, pc_lo + pc_span) as in
- * syzcov_dev_canon_split; every canonical PC is written as its KEY, and
- * split[] / range_tot[] count ranges of 2^range_shift keys.  The window must
- * map into [0, nkeys).  Contract: every PC belongs to the universe (KCOV only
- * reports call sites of the kernel the universe was taken from); distinct
- * non-universe PCs may share a key. */
+ * universe (the PCs KCOV reports: return addresses of the
+ * __sanitizer_cov_trace_pc calls) with kshift = the largest collision-free
+ * shift, at most SYZCOV_KSHIFT_MAX.  Canonicalize runs on the PCs of
+ * [pc_lo, pc_lo + pc_span) exactly as syzcov_dev_canon_split; every canonical
+ * PC is written as its KEY, and split[] / range_tot[] count ranges of
+ * 2^range_shift keys.  The window must map into [0, nkeys).  Every canonical
+ * PC is checked against the universe (low_of_key, from
+ * syzcov_dev_universe_keymap): a PC outside it sets SYZCOV_ERR_UNIVERSE, and
+ * the keys of that step must not be used (two PCs may share a key). */
 int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                                 uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
                                 uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
-                                uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
-                                uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
-/* pc_of_key[key(univ[i])] = univ[i] (univ sorted, collision-free under
- * kshift, else *err_flag |= 1). */
+                                const uint8_t *low_of_key, uint32_t range_shift, uint32_t *split,
+                                uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
+                                void *stream);
+/* Key tables of a universe (univ sorted, collision-free under kshift <=
+ * SYZCOV_KSHIFT_MAX, else *err_flag |= 1): pc_of_key[key(univ[i])] = univ[i]
+ * (0 for keys without a universe PC) and low_of_key[key(univ[i])] =
+ * univ[i] & (2^kshift - 1) (0xFF without one).  Either table may be NULL. */
 int syzcov_dev_universe_keymap(const uint32_t *univ, size_t n, uint32_t kshift, uint32_t kbase,
-                               uint64_t nkeys, uint32_t *pc_of_key, uint32_t *err_flag,
-                               void *stream);
+                               uint64_t nkeys, uint32_t *pc_of_key, uint8_t *low_of_key,
+                               uint32_t *err_flag, void *stream);
 /* out[i] = pc_of_key[keys[i]] for i < min(*n_dev, n_max) (n_dev: device count,
  * nullable); keys >= nkeys give 0xFFFFFFFF; in place allowed. */
 int syzcov_dev_keys_to_pcs(const uint32_t *pc_of_key, uint64_t nkeys, const uint32_t *keys,
@@ -459,6 +473,10 @@ int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean
                           uint32_t *lens, void *stream);
 int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
                          uint32_t log2_space, int uniform, uint32_t *pcs, void *stream);
+/* C5's synthetic call records: out[i] = CallID of record first + i, uniform
+ * over [0, ncalls) (counter-based: oracle/synth_oracle.c regenerates it). */
+int syzcov_dev_synth_callids(uint64_t seed, uint64_t first, size_t n, uint32_t ncalls,
+                             int32_t *out, void *stream);
 /* The synthetic PC universe U[k], k < 2^log2_space (sorted). */
 int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out, void *stream);
 /* dst <- src, 16-byte aligned, nbytes % 16 == 0: the streaming-copy kernel

@@ -85,6 +85,7 @@ uint32_t orc_synth_len(uint64_t seed, uint64_t input, uint32_t mean, uint32_t si
 void orc_synth_input(uint64_t seed, uint64_t input, uint32_t len, uint32_t log2_space,
                      int uniform, uint32_t *out);
 uint32_t orc_synth_universe(uint64_t seed, uint32_t k);
+int32_t orc_synth_callid(uint64_t seed, uint64_t input, uint32_t ncalls);
 
 #ifdef __cplusplus
 }

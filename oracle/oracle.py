@@ -58,6 +58,8 @@ def lib():
                                          C.c_int, p]
         _lib.orc_synth_universe.argtypes = [C.c_uint64, C.c_uint32]
         _lib.orc_synth_universe.restype = C.c_uint32
+        _lib.orc_synth_callid.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+        _lib.orc_synth_callid.restype = C.c_int32
     return _lib
 
 
@@ -281,6 +283,12 @@ def synth_input(seed: int, i: int, length: int, log2_space: int = 22, uniform: b
     out = np.empty(max(int(length), 1), dtype=np.uint32)
     lib().orc_synth_input(seed, i, int(length), log2_space, int(uniform), _ptr(out))
     return out[:length]
+
+
+def synth_callids(seed: int, n: int, ncalls: int, first: int = 0) -> np.ndarray:
+    """CallIDs of the synthetic call records first .. first + n - 1 (C5)."""
+    f = lib().orc_synth_callid
+    return np.array([f(seed, first + i, ncalls) for i in range(n)], dtype=np.int32)
 
 
 def synth_corpus(seed: int, n: int, mean: int = 2048, sigma: int = 512, log2_space: int = 22,

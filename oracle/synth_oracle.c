@@ -5,7 +5,8 @@
  *   universe  U[k] = 0x81000000 + 16k + (h(k) & 15), k < 2^S  (S = log2_space)
  *   length    L_i  = clamp(round(mean + sigma * z_i), 1, 65535), z_i = Irwin-Hall(12) - 6
  *                    (integer stand-in for the Box-Muller normal of §8d)
- *   draw      k    = floor(2^S * u^3), u = x / 2^21, x = 21 hash bits  -> (x^3) >> (63 - S)
+ *   draw      k    = floor(2^S * u^3), u = x / 2^32, x = 32 hash bits  -> (x^3) >> (96 - S)
+ *                    (every key < 2^S is reachable; S <= 32)
  *             (uniform variant: k = top S hash bits)
  * TEST INFRASTRUCTURE ONLY.
  */
@@ -48,9 +49,16 @@ void orc_synth_input(uint64_t seed, uint64_t input, uint32_t len, uint32_t log2_
         if (uniform) {
             k = (uint32_t)(h >> (64 - log2_space));
         } else {
-            uint64_t x = h >> 43; /* 21 bits */
-            k = (uint32_t)((x * x * x) >> (63 - log2_space));
+            uint64_t x = h >> 32; /* 32 bits; x^3 < 2^96 */
+            k = (uint32_t)((uint64_t)(((unsigned __int128)(x * x) * x) >> 64) >> (32 - log2_space));
         }
         out[j] = orc_synth_universe(seed, k);
     }
+}
+
+/* C5 (syz-fuzzer execute): the CallID of synthetic call record `input`,
+ * uniform over [0, ncalls) (the multiply-high of a 32-bit hash: no modulo). */
+int32_t orc_synth_callid(uint64_t seed, uint64_t input, uint32_t ncalls) {
+    uint64_t h = splitmix64(seed ^ splitmix64(input ^ 0xC2B2AE3D27D4EB4Full));
+    return (int32_t)(((h >> 32) * (uint64_t)ncalls) >> 32);
 }

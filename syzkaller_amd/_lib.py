@@ -90,8 +90,8 @@ _SIGS = {
     "syzcov_dev_canon_split": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, p_, p_, p_, p_, sz,
                                          p_]),
     "syzcov_dev_canon_split_keys": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, u32, u64,
-                                              u32, p_, p_, p_, p_, sz, p_]),
-    "syzcov_dev_universe_keymap": (C.c_int, [p_, sz, u32, u32, u64, p_, p_, p_]),
+                                              p_, u32, p_, p_, p_, p_, sz, p_]),
+    "syzcov_dev_universe_keymap": (C.c_int, [p_, sz, u32, u32, u64, p_, p_, p_, p_]),
     "syzcov_dev_keys_to_pcs": (C.c_int, [p_, u64, p_, p_, p_, sz, p_]),
     "syzcov_dev_first_to_bits": (C.c_int, [p_, u64, p_, p_]),
     "syzcov_dev_minimize_range_ws_size": (sz, [sz, u64, u32]),
@@ -110,6 +110,7 @@ _SIGS = {
     "syzcov_dev_synth_lens": (C.c_int, [u64, u64, sz, u32, u32, p_, p_]),
     "syzcov_dev_synth_pcs": (C.c_int, [u64, u64, sz, p_, u32, C.c_int, p_, p_]),
     "syzcov_dev_synth_universe": (C.c_int, [u64, u32, p_, p_]),
+    "syzcov_dev_synth_callids": (C.c_int, [u64, u64, sz, u32, p_, p_]),
     "syzcov_dev_stream_copy": (C.c_int, [p_, p_, sz, p_]),
     "syzcov_dev_prio_rows": (sz, [C.c_int]),
     "syzcov_dev_prio_ldp": (sz, [sz]),

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/syzcov.h"
+#include "force.h"
 
 namespace syz {
 
@@ -28,6 +29,21 @@ void set_error(const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
+}
+
+// The library's one run-time override (tests of the exact fallbacks; every
+// tuning choice is a compile-time default): SYZCOV_FORCE, a comma-separated
+// list of "canon3" (key mode canonicalizes with the 3-pass window-offset sort
+// instead of the 2-pass key sort) and "redo" (every wave-canonicalized segment
+// takes the order-check-failure path, the workgroup sort of canon.hip).  Read
+// at every call, so a test can set and clear it.
+uint32_t force_flags() {
+    const char *e = getenv("SYZCOV_FORCE");
+    if (!e || !*e) return 0;
+    uint32_t f = 0;
+    if (strstr(e, "canon3")) f |= FORCE_CANON3;
+    if (strstr(e, "redo")) f |= FORCE_REDO;
+    return f;
 }
 
 size_t setop_ws_size(size_t ntot);

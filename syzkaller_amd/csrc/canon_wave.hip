@@ -169,6 +169,8 @@ struct Params {
     uint32_t nbits;
     uint32_t kshift, kbase;   // output key = (pc >> kshift) - kbase (key mode)
     uint64_t nkeys;
+    const uint8_t *low_of_key;  // key mode: universe membership (keys.hip)
+    uint32_t lowmask;           // 2^kshift - 1
     int key_out;              // write keys (key mode) instead of PCs
     uint32_t sent_key;        // key of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
     uint32_t *split;          // nullable: [nseg][nrange]
@@ -177,6 +179,7 @@ struct Params {
     uint32_t *redo_list, *redo_cnt;  // wave sort failed its order check
     uint32_t *big_list, *big_cnt;    // n > WAVE_MAX (listed by bin_kernel)
     uint32_t *err;
+    uint32_t force_redo;             // SYZCOV_FORCE=redo: every segment takes the redo path
 };
 
 // Wave-aggregated binning of segments into capacity classes (one atomic per
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 #pragma unroll
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
-        uint32_t bad = 0;
+        uint32_t bad = P.force_redo;
         if (inplace) {  // nothing may be written before the order is known
             uint32_t carry = P.sent_key;
 #pragma unroll
@@ -426,6 +429,23 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
             continue;
         }
         if (l == 0) P.new_len[seg] = cnt;
+        if (P.key_out) {  // every canonical PC must be a universe PC (keys.hip)
+            uint32_t nm = 0;
+#pragma unroll
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                        const uint32_t pc = k[q * 4 + c] + P.pc_lo;
+                        const uint32_t key = (pc >> P.kshift) - P.kbase;
+                        const bool in = e < n && k[q * 4 + c] <= span_m1;
+                        const uint32_t t = P.low_of_key[in ? key : 0u];
+                        nm |= (uint32_t)in & (uint32_t)(t != (pc & P.lowmask));
+                    }
+                }
+            if (__ballot(nm) && l == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
+        }
         // ------------------------------------------- range splits
         if (!P.split) {
             if (l == 0) racc[0] += cnt;  // one range: its total is the PC count
@@ -481,7 +501,18 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 // A PC outside the window is flagged (SYZCOV_ERR_WINDOW: the step's results
 // are invalid and the engine raises) and sorts as the last key, so nothing
 // downstream indexes past the key range.
+// Exactness on any input: the sorted word is key | (pc & lowmask) << 22, the
+// PC's low kshift bits riding above the 22 key bits as payload (the digits
+// never read them).  Unique compares whole words, i.e. PCs, and every
+// canonical word is checked against the universe's membership table
+// (low_of_key, keys.hip): two PCs share a key only if one of them is not in
+// the universe, and then SYZCOV_ERR_UNIVERSE is set instead of aliasing them.
+// The byte gathers of a segment are all issued before the first test (other
+// waves' LDS work hides their latency; holding them across the split searches
+// instead spilled 32 more VGPRs).
 constexpr int KB = 11;
+constexpr uint32_t KEY_BITS = 2 * KB;              // keys < 2^22 in the low bits
+constexpr uint32_t KEY_MASK = (1u << KEY_BITS) - 1u;
 constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
@@ -621,7 +652,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const bool valid = idx >= head && idx < end;
                     const bool out = vv[c] - P.pc_lo > span_m1;
                     oob |= valid && out;
-                    k[q * 4 + c] = out ? kmax : (vv[c] >> P.kshift) - P.kbase;
+                    k[q * 4 + c] = out ? kmax
+                                       : ((vv[c] >> P.kshift) - P.kbase) |
+                                             ((vv[c] & P.lowmask) << KEY_BITS);
                 }
             }
         }
@@ -658,7 +691,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
 #pragma unroll
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
-        uint32_t bad = 0;
+        uint32_t bad = P.force_redo;
         if (inplace) {  // nothing may be written before the order is known
             uint32_t carry = P.sent_key;
 #pragma unroll
@@ -670,7 +703,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
-                        bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                        bad |= (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                               (uint32_t)(e - 1u < n - 1u);
                     }
                 }
             if (__ballot(bad)) {
@@ -689,13 +723,15 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
+                    bad |= (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                           (uint32_t)(e - 1u < n - 1u);
+                    // whole words: distinct PCs stay distinct even if they share a key
                     const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        outp[pos] = v;
-                        buf[pos] = v;
+                        outp[pos] = v & KEY_MASK;
+                        buf[pos] = v & KEY_MASK;
                     }
                     cnt += (uint32_t)__popcll(m);
                 }
@@ -705,6 +741,29 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
             continue;
         }
         if (l == 0) P.new_len[seg] = cnt;
+        {  // membership: one byte gather per sorted slot, 32-bit offsets from a
+           // buffer resource (64-bit addresses for 32+ gathers spilled VGPRs)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(P.low_of_key), (short)0, (int)(kmax + 1), 0x00020000);
+            uint32_t nm = 0;
+#pragma unroll
+            for (int q = 0; q < NQ; q++)
+                if ((uint32_t)q < nq) {
+                    uint32_t mt[4];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                        mt[c] = __builtin_amdgcn_raw_buffer_load_b8(
+                            rs, e < n ? (int)(k[q * 4 + c] & KEY_MASK) : 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
+                        nm |= (uint32_t)(e < n) & (uint32_t)(mt[c] != k[q * 4 + c] >> KEY_BITS);
+                    }
+                }
+            if (__ballot(nm) && l == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
+        }
         if (!P.split) {
             if (l == 0) racc[0] += cnt;
         } else {
@@ -793,12 +852,18 @@ __global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_
         if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
         uint32_t *c = P.out + P.off[seg];
         const uint32_t cnt = P.new_len[seg];
-        bool bad = false;
+        bool bad = false, nm = false;
         for (uint32_t i = __lane_id(); i < cnt; i += 64) {
             const uint32_t pc = c[i];
-            bad |= pc - P.pc_lo > (uint32_t)(P.span - 1);
-            if (P.key_out) c[i] = (pc >> P.kshift) - P.kbase;
+            const bool out = pc - P.pc_lo > (uint32_t)(P.span - 1);
+            bad |= out;
+            if (P.key_out && !out) {
+                const uint32_t key = (pc >> P.kshift) - P.kbase;
+                nm |= P.low_of_key[key] != (pc & P.lowmask);
+                c[i] = key;
+            }
         }
+        if (__ballot(nm) && __lane_id() == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
         if (__ballot(bad)) {  // flagged; the segment is dropped (memory-safe downstream)
             if (__lane_id() == 0) {
                 atomicOr(P.err, SYZCOV_ERR_WINDOW);
@@ -878,7 +943,8 @@ static void launch_class(const cw::Params &P, const uint32_t *lc, const uint32_t
 static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                             uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
                             uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
-                            int key_out, uint32_t range_shift, uint32_t *split,
+                            const uint8_t *low_of_key, int key_out, uint32_t range_shift,
+                            uint32_t *split,
                             uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
                             void *stream) {
     if (nseg == 0) return 0;
@@ -886,8 +952,9 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
         return SYZCOV_ERANGE;
     if (key_out) {  // every window PC must map into [0, nkeys)
+        if (!low_of_key || kshift > SYZCOV_KSHIFT_MAX) return SYZCOV_EINVAL;
         const uint64_t k0 = pc_lo >> kshift, k1 = (pc_lo + pc_span - 1) >> kshift;
-        if (kshift > 31 || nkeys == 0 || k0 < kbase || k1 - kbase >= nkeys) return SYZCOV_ERANGE;
+        if (nkeys == 0 || k0 < kbase || k1 - kbase >= nkeys) return SYZCOV_ERANGE;
     } else {
         nkeys = pc_span;
     }
@@ -915,6 +982,8 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.kbase = kbase;
     P.nkeys = nkeys;
     P.key_out = key_out;
+    P.low_of_key = low_of_key;
+    P.lowmask = (1u << kshift) - 1u;
     P.nbits = pc_span <= 1 ? 1 : 64 - __builtin_clzll(pc_span - 1);
     const uint64_t so = (uint64_t)(uint32_t)(0xFFFFFFFFu - pc_lo);
     P.sent_key = so < pc_span ? (uint32_t)so : 0xFFFFFFFFu;
@@ -928,17 +997,21 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.big_cnt = cnts + 1;
     P.err = err_flag;
     // key mode over <= 2^22 keys: sort the keys themselves, 2 passes of 11
-    // bits with u16-pair histograms (canon_key_kernel); SYZCOV_CANON_KEY2=0
-    // keeps the 3-pass window-offset sort (tuning / comparison)
-    // Every class takes it (SYZCOV_CANON_KEY2: 0 = none, 1 = the 2048-key
-    // class only, 2 = every class).  C2 canon ms: 8.03 / 7.66 / 7.23 once the
-    // scatter batches were branch-free (with a conditional last row quad the
-    // larger classes were slower than the 3-pass sort; 3072 keys run at 2
-    // waves per SIMD: 48 keys per lane do not fit 168 VGPRs).
-    int key2 = (key_out && nkeys <= (1ull << 22)) ? 2 : 0;
-    if (const char *e = getenv("SYZCOV_CANON_KEY2")) key2 = key2 ? atoi(e) : 0;
-    cw::Params PK = P;  // the key kernel's unique loop compares KEYS
-    PK.sent_key = so < pc_span ? (0xFFFFFFFFu >> kshift) - kbase : 0xFFFFFFFFu;
+    // bits with u16-pair histograms (canon_key_kernel).  C2 canon ms: 8.03 with
+    // the 3-pass window-offset sort in every class, 7.66 with the key sort in
+    // the 2048-key class only, 7.23 in every class once the scatter batches
+    // were branch-free (3072 keys run at 2 waves per SIMD: 48 keys per lane do
+    // not fit 168 VGPRs).  SYZ_CANON_KEY2=0 builds keep the 3-pass sort.
+#ifndef SYZ_CANON_KEY2
+#define SYZ_CANON_KEY2 2
+#endif
+    const uint32_t force = force_flags();
+    const int key2 =
+        (key_out && nkeys <= (1ull << 22) && !(force & FORCE_CANON3)) ? SYZ_CANON_KEY2 : 0;
+    P.force_redo = (force & FORCE_REDO) ? 1u : 0u;
+    cw::Params PK = P;  // the key kernel's unique loop compares (key | low bits) words
+    PK.sent_key = so < pc_span ? ((0xFFFFFFFFu >> kshift) - kbase) | (P.lowmask << cw::KEY_BITS)
+                               : 0xFFFFFFFFu;  // words are < 2^29: never equal
     // bin by capacity class (wave-aggregated atomics), one launch per class
     // (a register bitonic network measured 20.3 ms at C2 against the LDS
     // radix's 7.8: 147 VALU ops per key)
@@ -1019,18 +1092,19 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
                                       uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
                                       void *ws, size_t ws_size, void *stream) {
     return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, 0, pc_lo,
-                            pc_span, 0, range_shift, split, range_tot, err_flag, ws, ws_size,
-                            stream);
+                            pc_span, nullptr, 0, range_shift, split, range_tot, err_flag, ws,
+                            ws_size, stream);
 }
 
 extern "C" int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                                            uint32_t *new_len, size_t nseg, size_t max_seg_len,
                                            uint32_t pc_lo, uint64_t pc_span, uint32_t kshift,
-                                           uint32_t kbase, uint64_t nkeys, uint32_t range_shift,
+                                           uint32_t kbase, uint64_t nkeys,
+                                           const uint8_t *low_of_key, uint32_t range_shift,
                                            uint32_t *split, uint64_t *range_tot,
                                            uint32_t *err_flag, void *ws, size_t ws_size,
                                            void *stream) {
     return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, kshift,
-                            kbase, nkeys, 1, range_shift, split, range_tot, err_flag, ws, ws_size,
-                            stream);
+                            kbase, nkeys, low_of_key, 1, range_shift, split, range_tot, err_flag,
+                            ws, ws_size, stream);
 }

@@ -8,6 +8,7 @@
 #include <atomic>
 
 #include "../../include/syzcov.h"
+#include "force.h"
 
 #define SYZ_SENT 0xFFFFFFFFu
 #define SYZ_WAVE 64

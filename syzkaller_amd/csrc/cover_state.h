@@ -16,15 +16,18 @@ __device__ __forceinline__ bool bit_test(const uint32_t *__restrict__ bm, uint64
 struct Index {
     int key_mode;
     uint32_t pc_lo, kshift, kbase;
-    uint64_t span;  // window span, or nkeys
+    uint64_t span;                 // window span, or nkeys
+    const uint8_t *low_of_key;     // key mode: universe membership (keys.hip)
 };
 
-// Bitmap index of pc; false if pc is outside the window / key range.
+// Bitmap index of pc; false if pc is outside the window / key range, or, in
+// key mode, not a universe PC (its key belongs to another PC or to none: the
+// caller rejects it instead of aliasing it, keys.hip).
 __device__ __forceinline__ bool pc_index(const Index &X, uint32_t pc, uint32_t *idx) {
     if (X.key_mode) {
         const uint32_t k = (pc >> X.kshift) - X.kbase;  // wraps past span below kbase
         *idx = k;
-        return k < X.span;
+        return k < X.span && X.low_of_key[k] == (pc & ((1u << X.kshift) - 1u));
     }
     const uint32_t o = pc - X.pc_lo;
     *idx = o;
@@ -49,6 +52,7 @@ struct CoverState {
     uint32_t *mfl = nullptr;
     bool mfl_stale = true;
     uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
+    uint8_t *low_of_key = nullptr;  // key mode: membership table (pc_index)
     // LDS-staged candidate pass: per-call record counts | offsets | cursors |
     // work-item prefix over (call, range) | work-item descriptors; one batch
     // at a time per state

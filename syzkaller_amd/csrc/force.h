@@ -1,0 +1,9 @@
+// force.h — SYZCOV_FORCE, the library's one run-time override (api.cc), for
+// tests of the exact fallback paths.
+#pragma once
+#include <stdint.h>
+
+namespace syz {
+enum : uint32_t { FORCE_CANON3 = 1u, FORCE_REDO = 2u };
+uint32_t force_flags();
+}  // namespace syz

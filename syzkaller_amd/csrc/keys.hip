@@ -1,25 +1,35 @@
 // keys.hip — the engine's dense key space over a registered PC universe.
 //
-// The manager knows every PC the kernel can report: the call sites of
-// __sanitizer_cov_trace_pc (allCoverPCs, syz-manager/cover.go:57-69).  With
-// kshift = the largest shift that keeps that universe collision-free
-// (no two universe PCs share pc >> kshift) and kbase = U[0] >> kshift,
+// The universe is the set of PCs KCOV can REPORT: the return address of every
+// `call __sanitizer_cov_trace_pc` (the call sites objdump lists for
+// allCoverPCs, syz-manager/cover.go:274-306, plus the call's length — KCOV
+// records the return address, which is why cover.go:82 subtracts 1 again),
+// truncated to u32 as the executor does (executor.cc:455-466).  With
+// kshift = the largest shift (capped at KSHIFT_MAX) that keeps that universe
+// collision-free (no two universe PCs share pc >> kshift) and
+// kbase = U[0] >> kshift,
 //     key(pc) = (pc >> kshift) - kbase
 // is injective on the universe and maps it onto [0, nkeys): a dense key space
-// computed with a shift and a subtract, no dictionary lookup (a per-PC
-// lookup is a random access, which a 2 G-PC corpus cannot afford).  The
-// synthetic universe gives kshift = 4 and nkeys = 2^22 instead
-// of 2^26 window offsets; an x86 kernel's call sites are >= 5 bytes apart, so
-// kshift >= 2 there.  Canonicalize emits keys (canon_wave.hip, key mode),
-// Minimize's LDS ranges, the union bitmap and the first-cover array are over
-// keys, and the union list maps back through pc_of_key.
+// computed with a shift and a subtract.  The synthetic universe
+// gives kshift = 4 and nkeys = 2^22 instead of 2^26 window offsets; an x86
+// kernel's return addresses are >= 5 bytes apart, so kshift >= 2 there.
+//
+// EXACT ON ANY INPUT.  Two PCs can share a key only if one of them is not in
+// the universe, so every place that forms a key also checks membership:
+//     low_of_key[key] == (pc & lowmask),  lowmask = 2^kshift - 1
+// (one byte per key: the universe PC's low kshift bits, 0xFF for a key with no
+// universe PC; kshift <= 7 keeps 0xFF out of reach).  A PC that fails it sets
+// SYZCOV_ERR_UNIVERSE and the step / batch raises instead of aliasing it with
+// its neighbour: canon_wave.hip carries the low bits through the key sort as
+// payload and checks every canonical PC; the fuzzer state's pc_index checks
+// every PC it indexes (cover_state.h).
 #include "common.h"
 
 namespace syz {
 
 __global__ void keymap_kernel(const uint32_t *__restrict__ univ, uint64_t n, uint32_t kshift,
                               uint32_t kbase, uint64_t nkeys, uint32_t *__restrict__ pc_of_key,
-                              uint32_t *__restrict__ err) {
+                              uint8_t *__restrict__ low_of_key, uint32_t *__restrict__ err) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t pc = univ[i];
@@ -28,7 +38,8 @@ __global__ void keymap_kernel(const uint32_t *__restrict__ univ, uint64_t n, uin
             atomicOr(err, 1u);  // not sorted / not collision-free / outside the key range
             continue;
         }
-        pc_of_key[key] = pc;
+        if (pc_of_key) pc_of_key[key] = pc;
+        if (low_of_key) low_of_key[key] = (uint8_t)(pc & ((1u << kshift) - 1u));
     }
 }
 
@@ -75,12 +86,18 @@ extern "C" int syzcov_dev_first_to_bits(const int32_t *first, uint64_t span, uin
 
 extern "C" int syzcov_dev_universe_keymap(const uint32_t *univ, size_t n, uint32_t kshift,
                                           uint32_t kbase, uint64_t nkeys, uint32_t *pc_of_key,
-                                          uint32_t *err_flag, void *stream) {
+                                          uint8_t *low_of_key, uint32_t *err_flag, void *stream) {
+    if (!univ || (!pc_of_key && !low_of_key) || !err_flag || kshift > SYZCOV_KSHIFT_MAX ||
+        nkeys == 0)
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    // keys without a universe PC: pc_of_key 0 (never read for a valid key),
+    // low_of_key 0xFF (no PC's low kshift <= 7 bits equal it)
+    if (pc_of_key) SYZ_HIP(hipMemsetAsync(pc_of_key, 0, nkeys * 4, s));
+    if (low_of_key) SYZ_HIP(hipMemsetAsync(low_of_key, 0xFF, nkeys, s));
     if (n == 0) return 0;
-    if (!univ || !pc_of_key || !err_flag || kshift > 31 || nkeys == 0) return SYZCOV_EINVAL;
-    hipLaunchKernelGGL(keymap_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
-                       (hipStream_t)stream, univ, (uint64_t)n, kshift, kbase, nkeys, pc_of_key,
-                       err_flag);
+    hipLaunchKernelGGL(keymap_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, univ,
+                       (uint64_t)n, kshift, kbase, nkeys, pc_of_key, low_of_key, err_flag);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -518,7 +518,14 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
     const uint32_t *s_m = (const uint32_t *)s_m4;
     const uint32_t obase = (KEY ? X.kbase : X.pc_lo) + (q << RSH);
     const uint32_t ks = KEY ? X.kshift : 0u;
+    // key mode: every PC is checked against the universe (keys.hip), one byte
+    // gather per PC with a 32-bit offset (a lane past the sub-run reads past
+    // the table's end: 0, no fetch)
+    const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)X.low_of_key, 0, KEY ? (int)X.span : 0, 0x00020000);
+    const uint32_t lowmask = (1u << ks) - 1u;
     uint64_t bad = 0;  // lanes that saw a PC below its predecessor
+    uint64_t nonmem = 0;  // lanes that saw a PC outside the universe
     uint4 my = make_uint4(0, 0, 0, 0);
     uint32_t nrow = 0, p0v = 0;
     uint2 *cb = s_cb + wv * LC_CBW;
@@ -594,11 +601,16 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
             // bitmap words of the four components (the word index is masked
             // into the staged range, so reads are unconditional and in flight
             // together)
-            uint32_t o[4], wd[4];
+            uint32_t o[4], wd[4], mb[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 o[c] = (KEY ? v[c] >> ks : v[c]) - obase;
                 wd[c] = s_m[(o[c] >> 5) & ((1u << (RSH - 5)) - 1)];
+                if (KEY) {
+                    const bool in = 4 * l + c >= lo && 4 * l + c < hi;
+                    mb[c] = __builtin_amdgcn_raw_buffer_load_b8(
+                        lr, in ? o[c] + (q << RSH) : 0xFFFFFFF0u, 0, 0);
+                }
             }
             // element 4l's predecessor: lane l-1's last element (DPP wave shift),
             // for lane 0 the PC before the row
@@ -614,6 +626,7 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
                 const uint64_t pm = lane_range(lo1 > (uint32_t)c ? (lo1 - c + 3) >> 2 : 0u,
                                                hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
                 bad |= __ballot((c ? v[c - 1] : p0) > v[c]) & pm;
+                if (KEY) nonmem |= __ballot(mb[c] != (v[c] & lowmask)) & vm;
                 const uint64_t cm = __ballot(!((wd[c] >> (o[c] & 31)) & 1u)) & vm;
                 if (cm) emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);  // rare
             }
@@ -650,6 +663,7 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
     if (nc) flush();
     if (sink == 0x9E3779B9u) stats[2] = sink;
     if (bad && l == 0) stats[0] = 3u;
+    if (nonmem && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
     if (dbg & 8) {  // timing probe: per-workgroup stamps (100 MHz clock)
         __syncthreads();
         if (t == 0) {
@@ -895,7 +909,7 @@ extern "C" int syzcov_state_create(int ncalls, uint32_t pc_lo, uint64_t pc_span,
     st->ncalls = ncalls;
     st->pc_lo = pc_lo;
     st->pc_span = pc_span;
-    st->X = Index{0, pc_lo, 0, 0, pc_span};
+    st->X = Index{0, pc_lo, 0, 0, pc_span, nullptr};
     int rc = hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking) == hipSuccess
                  ? alloc_maps(st) : SYZCOV_EHIP;
     if (rc) {
@@ -919,6 +933,7 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     if (st->corpus) hipFree(st->corpus);
     if (st->mfl) hipFree(st->mfl);
     if (st->pc_of_key) hipFree(st->pc_of_key);
+    if (st->low_of_key) hipFree(st->low_of_key);
     if (st->grp) hipFree(st->grp);
     if (st->scratch) hipFree(st->scratch);
     hipStreamDestroy(st->s);
@@ -984,12 +999,14 @@ extern "C" int syzcov_state_add(syzcov_cover_state h, int call, const uint32_t *
     return set_bits(st, st->maxcov + (size_t)call * st->words, pcs, n);
 }
 
-// Key mode (keys.hip): the PC universe (allCoverPCs, syz-manager/cover.go:57-69;
-// inside the window, any order, duplicates allowed) fixes kshift / kbase /
-// nkeys; maxCover and flakes become bitmaps over its dense keys.  Allowed
-// only while maxCover is empty.  Contract from then on: every PC passed in
-// belongs to the universe (KCOV reports only its call sites); a PC outside
-// the universe's key range is rejected, one inside it is trusted.
+// Key mode (keys.hip): the PC universe (every PC KCOV can report: the return
+// addresses of the __sanitizer_cov_trace_pc calls, syz-manager/cover.go:
+// 274-306 and :82; inside the window, any order, duplicates allowed) fixes
+// kshift / kbase / nkeys; maxCover and flakes become bitmaps over its dense
+// keys.  Allowed only while maxCover is empty.  From then on every PC passed
+// in is checked against the universe (pc_index): one outside it is rejected
+// (the whole batch, or the call), never aliased with the universe PC that
+// owns its key.
 extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *pcs, size_t n) {
     CoverState *st = (CoverState *)(uintptr_t)h;
     if (!st || (n && !pcs)) return SYZCOV_EINVAL;
@@ -1000,8 +1017,10 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
         return SYZCOV_EINVAL;
     }
     if (st->pc_of_key) hipFree(st->pc_of_key);
+    if (st->low_of_key) hipFree(st->low_of_key);
     st->pc_of_key = nullptr;
-    st->X = Index{0, st->pc_lo, 0, 0, st->pc_span};  // back to window mode
+    st->low_of_key = nullptr;
+    st->X = Index{0, st->pc_lo, 0, 0, st->pc_span, nullptr};  // back to window mode
     if (n == 0) return alloc_maps(st);
     // the sorted unique universe on the device: window bits -> list
     uint32_t *bm = nullptr, *lst = nullptr, *sc = nullptr;
@@ -1026,8 +1045,8 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
         if (hipMemcpyAsync(&hn, d_n, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
             hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
         if (hn == 0) break;  // only sentinels: stay in window mode
-        const uint32_t k31 = 31;
-        if (hipMemcpyAsync(d_ks, &k31, 4, hipMemcpyHostToDevice, st->s) != hipSuccess) {
+        const uint32_t kmax = SYZCOV_KSHIFT_MAX;  // the shift is capped (keys.hip)
+        if (hipMemcpyAsync(d_ks, &kmax, 4, hipMemcpyHostToDevice, st->s) != hipSuccess) {
             rc = SYZCOV_EHIP;
             break;
         }
@@ -1040,11 +1059,25 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
             hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
         const uint32_t kbase = ends[0] >> ks;
         const uint64_t nkeys = (uint64_t)(ends[1] >> ks) - kbase + 1;
-        if (hipMalloc(&st->pc_of_key, nkeys * 4) != hipSuccess) { rc = SYZCOV_ENOMEM; break; }
-        if (hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
-        if ((rc = syzcov_dev_universe_keymap(lst, hn, ks, kbase, nkeys, st->pc_of_key, d_n, st->s)))
+        if (hipMalloc(&st->pc_of_key, nkeys * 4) != hipSuccess ||
+            hipMalloc(&st->low_of_key, nkeys) != hipSuccess) {
+            rc = SYZCOV_ENOMEM;
             break;
-        st->X = Index{1, st->pc_lo, ks, kbase, nkeys};
+        }
+        if (hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        // (the keymap zero-fills pc_of_key and 0xFF-fills low_of_key first)
+        if ((rc = syzcov_dev_universe_keymap(lst, hn, ks, kbase, nkeys, st->pc_of_key,
+                                             st->low_of_key, d_n, st->s)))
+            break;
+        uint32_t kerr = 0;
+        if (hipMemcpyAsync(&kerr, d_n, 4, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+            hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if (kerr) {  // cannot happen for a sorted unique list under its own shift
+            set_error("universe keymap failed");
+            rc = SYZCOV_EINVAL;
+            break;
+        }
+        st->X = Index{1, st->pc_lo, ks, kbase, nkeys, st->low_of_key};
         rc = alloc_maps(st);
     } while (0);
     if (bm) hipFree(bm);
@@ -1054,8 +1087,10 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
     if (sc) hipFree(sc);
     if (rc) {
         if (st->pc_of_key) hipFree(st->pc_of_key);
+        if (st->low_of_key) hipFree(st->low_of_key);
         st->pc_of_key = nullptr;
-        st->X = Index{0, st->pc_lo, 0, 0, st->pc_span};
+        st->low_of_key = nullptr;
+        st->X = Index{0, st->pc_lo, 0, 0, st->pc_span, nullptr};
         alloc_maps(st);
     }
     return rc;

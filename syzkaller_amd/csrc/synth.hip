@@ -43,11 +43,24 @@ __global__ void synth_pcs_kernel(uint64_t seed, uint64_t first, uint64_t n,
             if (uniform) {
                 k = (uint32_t)(h >> (64 - log2_space));
             } else {
-                const uint64_t x = h >> 43;
-                k = (uint32_t)((x * x * x) >> (63 - log2_space));
+                // u = x / 2^32 (32 hash bits: every one of the 2^S keys is
+                // reachable); k = floor(2^S u^3) = x^3 >> (96 - S), and
+                // x^3 < 2^96 so that is the high 64 bits of x^2 * x >> (32 - S)
+                const uint64_t x = h >> 32;
+                k = (uint32_t)(__umul64hi(x * x, x) >> (32 - log2_space));
             }
             pcs[b + j] = synth_universe(seed, k);
         }
+    }
+}
+
+// C5 call records: CallID of record `first + i`, uniform over [0, ncalls)
+__global__ void synth_callids_kernel(uint64_t seed, uint64_t first, uint64_t n, uint32_t ncalls,
+                                     int32_t *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = splitmix64(seed ^ splitmix64((first + i) ^ 0xC2B2AE3D27D4EB4Full));
+        out[i] = (int32_t)(((h >> 32) * (uint64_t)ncalls) >> 32);
     }
 }
 
@@ -114,6 +127,16 @@ extern "C" int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, con
     hipLaunchKernelGGL(synth_pcs_kernel, dim3(grid_for(n, 1, 16384)), dim3(256), 0,
                        (hipStream_t)stream, seed, first, (uint64_t)n, off, log2_space, uniform,
                        pcs);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_synth_callids(uint64_t seed, uint64_t first, size_t n, uint32_t ncalls,
+                                        int32_t *out, void *stream) {
+    if (n == 0) return 0;
+    if (!out || ncalls == 0) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(synth_callids_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, seed, first, (uint64_t)n, ncalls, out);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -29,7 +29,8 @@ import torch
 from ._lib import check, lib
 
 INT32_MAX = 0x7FFFFFFF
-SYZCOV_ERR_WINDOW, SYZCOV_ERR_SEGLEN = 1, 2  # err_flag bits (include/syzcov.h)
+SYZCOV_ERR_WINDOW, SYZCOV_ERR_SEGLEN, SYZCOV_ERR_UNIVERSE = 1, 2, 4  # err_flag bits (syzcov.h)
+KSHIFT_MAX = 7  # SYZCOV_KSHIFT_MAX: a universe PC's low bits fit the membership byte
 RANGE_SHIFT = 20  # 2^20 PCs per LDS-resident range (128 KB covered bitmap)
 
 
@@ -76,8 +77,8 @@ class CorpusEngine:
         self.kshift, self.kbase = 0, pc_lo
         self.win_lo, self.win_span = pc_lo, pc_span  # Canonicalize's sort window
         if self.key_mode:
-            self.kshift, self.kbase, nkeys, self.pc_of_key, ulo, uhi = universe_keymap(universe,
-                                                                                      dev)
+            (self.kshift, self.kbase, nkeys, self.pc_of_key, self.low_of_key, ulo,
+             uhi) = universe_keymap(universe, dev)
             self.win_lo, self.win_span = ulo, uhi - ulo + 1  # the universe's extent
             pc_lo, pc_span = 0, nkeys  # minimize / union / maxCover window = the key range
         self.pc_lo, self.span = pc_lo, pc_span
@@ -144,7 +145,8 @@ class CorpusEngine:
         if self.key_mode:
             check(self.L.syzcov_dev_canon_split_keys(
                 _p(off), _p(raw), _p(self.canon), _p(self.new_len), n, self.max_seg, self.win_lo,
-                self.win_span, self.kshift, self.kbase, self.span, self.rshift, _p(self.split),
+                self.win_span, self.kshift, self.kbase, self.span, _p(self.low_of_key),
+                self.rshift, _p(self.split),
                 _p(self.range_tot), _p(self.scal), _p(self.ws), self.ws_size, _stream()),
                 "dev_canon_split_keys")
             return
@@ -254,6 +256,9 @@ class CorpusEngine:
             raise RuntimeError("a PC fell outside the engine's PC window")
         if sc[0] & SYZCOV_ERR_SEGLEN:
             raise RuntimeError(f"an input is longer than max_seg_len={self.max_seg}")
+        if sc[0] & SYZCOV_ERR_UNIVERSE:
+            raise RuntimeError("a PC is not in the registered PC universe (key mode would alias "
+                               "it with a universe PC; keys.hip)")
         if sc[0] & 0xFFFFFFFF:
             raise RuntimeError(f"engine error flags {sc[0] & 0xFFFFFFFF:#x}")
         n_ids, n_kept, n_union = (int(x) & 0xFFFFFFFF for x in sc[1:4])
@@ -377,24 +382,63 @@ def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int
     return off, pcs, lens, total
 
 
+def synth_records(nrec: int, seed: int, first: int, ncalls: int, mean: int = 2048,
+                  sigma: int = 512, log2_space: int = 22, device="cuda"):
+    """Config C5's call records first .. first + nrec - 1 in HBM: the
+    canonical cover of synthetic input `first + k` (Canonicalize on the GPU,
+    then compacted into a record CSR) and its CallID.  Returns (callid i32,
+    rec_off i64[nrec + 1], pcs i32-viewed u32, number of PCs); the CPU twin is
+    oracle/newcov_full.c."""
+    L = lib()
+    dev = torch.device(device)
+    off, raw, lens, total = synth_corpus(nrec, seed, first=first, mean=mean, sigma=sigma,
+                                         log2_space=log2_space, device=dev)
+    lo, span = synth_window(log2_space)
+    new_len = torch.empty(nrec + 1, dtype=torch.int32, device=dev)
+    err = torch.zeros(4, dtype=torch.int32, device=dev)
+    wsz = L.syzcov_dev_canon_split_ws_size(nrec)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    s = _stream()
+    check(L.syzcov_dev_canon_split(_p(off), _p(raw), _p(raw), _p(new_len), nrec,
+                                   int(lens.max().item()), lo, span, 20, None, None, _p(err),
+                                   _p(ws), wsz, s), "canon_split")
+    if int(err[0].item()):
+        raise RuntimeError(f"canonicalize flags {int(err[0].item()):#x}")
+    nl = new_len[:nrec].to(torch.int64)
+    roff = torch.zeros(nrec + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nl, 0, out=roff[1:])
+    npc = int(roff[-1].item())
+    seg = torch.repeat_interleave(torch.arange(nrec, device=dev), nl)
+    src = off[:-1][seg] + (torch.arange(npc, device=dev) - roff[:-1][seg])
+    pcs = raw[src].contiguous()
+    cid = torch.empty(nrec, dtype=torch.int32, device=dev)
+    check(L.syzcov_dev_synth_callids(seed, first, nrec, ncalls, _p(cid), s), "synth_callids")
+    return cid, roff, pcs, npc
+
+
 SYNTH_PC_LO = 0x81000000
 
 
 def universe_shift(u: np.ndarray) -> int:
-    """Largest kshift with no two neighbouring (sorted, unique) universe PCs
-    sharing pc >> kshift: (a >> s) != (b >> s) iff a ^ b has a bit >= s, so
-    kshift = min over neighbours of the highest differing bit."""
+    """Largest kshift <= KSHIFT_MAX with no two neighbouring (sorted, unique)
+    universe PCs sharing pc >> kshift: (a >> s) != (b >> s) iff a ^ b has a
+    bit >= s, so the bound is the min over neighbours of the highest differing
+    bit."""
     u = np.asarray(u, dtype=np.uint32)
     if u.size < 2:
         return 0
     if not np.all(u[1:] > u[:-1]):
         raise ValueError("the PC universe must be sorted and unique")
-    return int((u[1:] ^ u[:-1]).min()).bit_length() - 1
+    return min(KSHIFT_MAX, int((u[1:] ^ u[:-1]).min()).bit_length() - 1)
 
 
 def universe_keymap(universe, dev):
-    """(kshift, kbase, nkeys, pc_of_key, lowest PC, highest PC) of a registered PC universe
-    (sorted unique uint32 PCs: allCoverPCs, syz-manager/cover.go:57-69)."""
+    """(kshift, kbase, nkeys, pc_of_key, low_of_key, lowest PC, highest PC) of a
+    registered PC universe: the sorted unique u32 PCs KCOV can report, i.e. the
+    return addresses of the __sanitizer_cov_trace_pc calls (the call sites
+    syz-manager/cover.go:274-306 lists, plus the call's length; cover.go:82
+    subtracts the 1 back).  low_of_key is the membership table every key-mode
+    kernel checks (keys.hip)."""
     if isinstance(universe, torch.Tensor):
         uh = universe.cpu().numpy().view(np.uint32)
         ud = universe.to(dev)
@@ -404,14 +448,15 @@ def universe_keymap(universe, dev):
     ks = universe_shift(uh)
     kbase = int(uh[0]) >> ks
     nkeys = (int(uh[-1]) >> ks) - kbase + 1
-    pc_of_key = torch.zeros(nkeys, dtype=torch.int32, device=dev)
+    pc_of_key = torch.empty(nkeys, dtype=torch.int32, device=dev)
+    low_of_key = torch.empty(nkeys, dtype=torch.uint8, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     L = lib()
-    check(L.syzcov_dev_universe_keymap(_p(ud), uh.size, ks, kbase, nkeys, _p(pc_of_key), _p(err),
-                                       _stream()), "dev_universe_keymap")
+    check(L.syzcov_dev_universe_keymap(_p(ud), uh.size, ks, kbase, nkeys, _p(pc_of_key),
+                                       _p(low_of_key), _p(err), _stream()), "dev_universe_keymap")
     if int(err.item()):
         raise ValueError("universe keymap failed (unsorted or colliding universe)")
-    return ks, kbase, nkeys, pc_of_key, int(uh[0]), int(uh[-1])
+    return ks, kbase, nkeys, pc_of_key, low_of_key, int(uh[0]), int(uh[-1])
 
 
 def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda") -> torch.Tensor:

@@ -8,6 +8,9 @@ tools/gen_golden_fullsize.py from oracle/fullsize.c).
   C2  world-8 sharded rehearsal on one GPU    kept / union / order digests
   C4  1M programs: raw co-occurrence counts against the closed form
       D[i][j] = #{p : len(p) > max(i, j)}, D[i][i] = 0 (prio.go:137-154)
+  C5  the bench's new-coverage stream: 32 history batches + 2 more of 65,536
+      call records over 293 calls (key and window mode), per-batch is_new
+      and the final per-call maxCover against oracle/newcov_full.c
 """
 import hashlib
 import json
@@ -156,3 +159,54 @@ def test_c4_closed_form_1m(torch):
     exp = orc.normalize_prio(D.astype(np.float32))
     assert np.array_equal(eng.out.cpu().numpy().reshape(Cn, Cn), exp)
     assert out is eng.out
+
+
+@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
+def test_c5_newcov_stream_fullsize(torch, keys):
+    """Config C5 at its own size (syz-fuzzer/fuzzer.go:456-480): the stream
+    bench.py --workload newcov times (seed 0x5EED0005, batch b = records
+    b * 65536 ..), every batch through syzcov_state_newcov_dev, is_new of each
+    batch and every call's maxCover at the end bit-identical to the oracle."""
+    import ctypes as C
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import synth_corpus, synth_records, synth_universe, synth_window
+    from syzkaller_amd.fuzzer import CoverState
+    g = golden("C5")
+    L = _lib.lib()
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+    lo, span = synth_window(g["log2_space"])
+    st = CoverState(g["ncalls"], lo, span)
+    if keys:
+        u = synth_universe(g["log2_space"], g["seed"])
+        st.set_universe(u.cpu().numpy().view(np.uint32))
+        del u
+    fo, fp, _, _ = synth_corpus(1, g["seed"], first=1 << 40, mean=1 << (g["log2_space"] - 7),
+                                sigma=1, log2_space=g["log2_space"])
+    st.set_flakes(np.unique(fp[:int(fo[1].item())].cpu().numpy().view(np.uint32)))
+    nrec = g["records"]
+    is_new = torch.empty(nrec, dtype=torch.uint8, device="cuda")
+    stats = torch.zeros(2, dtype=torch.int32, device="cuda")
+    total = 0
+    for b in range(g["batches"]):
+        cid, roff, pcs, npc = synth_records(nrec, g["seed"], b * nrec, g["ncalls"],
+                                            mean=g["mean"], sigma=g["sigma"],
+                                            log2_space=g["log2_space"])
+        total += npc
+        wsz = L.syzcov_state_newcov_ws_size(nrec, npc)
+        ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+        _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc, P(is_new),
+                                             P(stats), P(ws), wsz, s()), "state_newcov_dev")
+        assert int(stats[0].item()) == 0, b
+        h = hashlib.sha256(is_new.cpu().numpy().tobytes()).hexdigest()
+        assert (int(is_new.sum().item()), h) == (g["new_per_batch"][b], g["is_new_sha256"][b]), b
+        del ws, pcs
+    assert total == g["record_pcs"]
+    mn = np.array([st.max_cover(c).size for c in range(g["ncalls"])], np.uint32)
+    assert int(mn.sum()) == g["max_cover_total"]
+    assert hashlib.sha256(mn.tobytes()).hexdigest() == g["max_cover_n_sha256"]
+    hh = hashlib.sha256()
+    for c in range(g["ncalls"]):
+        hh.update(st.max_cover(c).astype("<u4").tobytes())
+    assert hh.hexdigest() == g["max_cover_sha256"]
+    st.close()

@@ -21,9 +21,17 @@ def test_keymap_roundtrip(torch):
     u = synth_universe(16, 0x5EED0002)
     uh = u.cpu().numpy().view(np.uint32)
     assert np.array_equal(uh, [orc.lib().orc_synth_universe(0x5EED0002, k) for k in range(1 << 16)])
-    ks, kbase, nkeys, pok, ulo, uhi = universe_keymap(u, "cuda")
+    ks, kbase, nkeys, pok, lok, ulo, uhi = universe_keymap(u, "cuda")
     assert (ulo, uhi) == (int(uh[0]), int(uh[-1]))
     assert ks == 4 and nkeys == 1 << 16
+    # membership table: the low kshift bits of each key's universe PC
+    assert np.array_equal(lok.cpu().numpy(), (uh & 15).astype(np.uint8))
+    keep = np.arange(uh.size) % 3 != 2  # every third key without a universe PC
+    ks2, _, n2, _, lok2, _, _ = universe_keymap(uh[keep].copy(), "cuda")
+    assert ks2 == 4 and n2 == (1 << 16) - 1
+    l2 = lok2.cpu().numpy()
+    assert np.array_equal(l2[keep[:n2]], (uh[keep] & 15).astype(np.uint8)[:int(keep[:n2].sum())])
+    assert np.all(l2[~keep[:n2]] == 0xFF)
     keys = torch.from_numpy(((uh >> ks) - kbase).astype(np.int32)).cuda()
     out = torch.empty_like(keys)
     L = _lib.lib()
@@ -103,13 +111,15 @@ def test_engine_offsets_past_2_32(torch, keys):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("key2", ["1", "0", "2"])
-def test_engine_key_mode_sentinel(torch, key2, monkeypatch):
+@pytest.mark.parametrize("force", ["", "canon3", "redo"])
+def test_engine_key_mode_sentinel(torch, force, monkeypatch):
     """Key mode with a universe whose last PC is 0xFFFFFFFF: inputs made only of
     the sentinel canonicalize to empty, otherwise it is an ordinary key
-    (cover.go:28-40, 104-131).  key2 selects the canonicalization: the 2-pass
-    key sort for the 2048-key class (default), none, or every class."""
-    monkeypatch.setenv("SYZCOV_CANON_KEY2", key2)
+    (cover.go:28-40, 104-131).  force (SYZCOV_FORCE) selects the
+    canonicalization: the 2-pass key sort (default), the 3-pass window-offset
+    sort, or the workgroup sort every segment whose wave order check fails
+    takes."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
     from syzkaller_amd.engine import CorpusEngine
     rng = np.random.default_rng(33)
     univ = (np.uint64(0xFFFF0000) + 4 * np.arange(1 << 14, dtype=np.uint64) + 3).astype(np.uint32)
@@ -141,3 +151,99 @@ def test_engine_key_mode_sentinel(torch, key2, monkeypatch):
         assert np.array_equal(canon[a:b], c_pcs[c_off[i]:c_off[i + 1]]), i
     assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
+
+
+def _stray(u: np.ndarray, i: int) -> int:
+    """A PC next to universe PC u[i] that is not in the universe."""
+    us = set(u.tolist())
+    return next(int(u[j]) + d for j in range(i, u.size) for d in (1, 2, 3, 5)
+                if int(u[j]) + d not in us and int(u[j]) + d <= int(u[-1]))
+
+
+@pytest.mark.parametrize("force", ["", "canon3", "redo"])
+@pytest.mark.parametrize("in_place", [False, True], ids=["out-of-place", "in-place"])
+def test_engine_key_mode_nonuniverse(torch, force, in_place, monkeypatch):
+    """A PC inside the universe's key range that is not a universe PC (it
+    shares its key with a universe PC, cover.go would treat them as two PCs):
+    the step raises, never returns an aliased result.  Every canonicalization
+    path checks membership (keys.hip)."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 2000, 16, 0x5EED0002
+    u = synth_universe(log2, seed)
+    uh = u.cpu().numpy().view(np.uint32)
+    lo, span = synth_window(log2)
+    for where in (0, 777, 1999):
+        off, raw, lens, total = synth_corpus(n, seed, mean=1500, sigma=600, log2_space=log2)
+        eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u,
+                           canon_in_place=in_place)
+        res = eng.step(off, raw, n)  # clean corpus: fine
+        assert res.n_kept > 0
+        off, raw, lens, total = synth_corpus(n, seed, mean=1500, sigma=600, log2_space=log2)
+        j = int(off[where].item()) + int(lens[where].item()) // 2
+        k = int(raw[j].item()) & 0xFFFFFFFF
+        raw[j] = np.int32(np.uint32(_stray(uh, int(np.searchsorted(uh, k)))))
+        with pytest.raises(RuntimeError, match="universe"):
+            eng.step(off, raw, n)
+
+
+def test_engine_key_mode_gap_key(torch):
+    """A universe with keys that hold no PC (every other synthetic PC): a PC
+    on such a key is rejected; the universe's own PCs give the oracle's
+    results."""
+    from syzkaller_amd.engine import CorpusEngine
+    rng = np.random.default_rng(7)
+    full = np.array([orc.lib().orc_synth_universe(0x5EED0002, k) for k in range(1 << 14)],
+                    np.uint32)
+    univ = full[::2].copy()
+    covers = [np.sort(rng.choice(univ, size=int(rng.integers(1, 900)))) for _ in range(600)]
+    lens = np.array([c.size for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers).astype(np.uint32)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
+    eng = CorpusEngine(len(covers), int(lens.sum()), int(lens.max()), int(univ[0]),
+                       int(univ[-1]) - int(univ[0]) + 1, universe=univ)
+    res = eng.step(off, raw, len(covers))
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
+    raw[int(o_off[300]) + 0] = np.int32(full[101].view(np.int32))  # a removed PC: a gap key
+    with pytest.raises(RuntimeError, match="universe"):
+        eng.step(off, raw, len(covers))
+
+
+@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
+def test_engine_forced_redo_vs_oracle(torch, keys, monkeypatch):
+    """The canon wave sort checks its own order and sends a failing segment to
+    the workgroup sort (canon.hip).  Forcing every segment down that path
+    (SYZCOV_FORCE=redo) must give the oracle's results."""
+    monkeypatch.setenv("SYZCOV_FORCE", "redo")
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 3000, 18, 0x5EED0002
+    off, raw, lens, total = synth_corpus(n, seed, mean=2048, sigma=900, log2_space=log2)
+    lo, span = synth_window(log2)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span,
+                       universe=synth_universe(log2, seed) if keys else None)
+    res = eng.step(off, raw, n)
+    o_off, o_pcs = orc.synth_corpus(seed, n, mean=2048, sigma=900, log2_space=log2)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
+
+
+@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
+def test_engine_segment_longer_than_declared(torch, keys):
+    """An input longer than the engine's declared max_seg_len is not
+    canonicalized silently: SYZCOV_ERR_SEGLEN, and the step raises."""
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 500, 16, 0x5EED0002
+    off, raw, lens, total = synth_corpus(n, seed, mean=2048, sigma=512, log2_space=log2)
+    lo, span = synth_window(log2)
+    ml = int(lens.max().item())
+    eng = CorpusEngine(n, total, ml - 1, lo, span,
+                       universe=synth_universe(log2, seed) if keys else None)
+    with pytest.raises(RuntimeError, match="max_seg_len"):
+        eng.step(off, raw, n)

@@ -275,9 +275,47 @@ def test_newcov_key_mode(spacing, newcov_path):
             assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
     with pytest.raises(SyzcovError):  # below the universe: outside the key range
         st.new_coverage([0], [np.array([univ[0] - 64], np.uint32)])
+    # inside the key range but not a universe PC: it would share a key with a
+    # universe PC (or take a key of none); rejected whole, nothing changes
+    uset = set(univ.tolist())
+    stray = next(int(p) + d for p in univ[100:] for d in (1, 2, 3) if int(p) + d not in uset)
+    before = [st.max_cover(c) for c in range(ncalls)]
+    for rec in (np.array([stray], np.uint32), np.sort(np.array([univ[5], stray], np.uint32)),
+                np.sort(np.concatenate([univ[:300], [stray]])).astype(np.uint32)):
+        with pytest.raises(SyzcovError):
+            st.new_coverage([1, 2], [univ[:50], rec])
+    for c in range(ncalls):
+        assert np.array_equal(st.max_cover(c), before[c])
+    with pytest.raises(SyzcovError):
+        st.add(3, np.array([stray], np.uint32))
     with pytest.raises(SyzcovError):  # the universe is fixed once maxCover holds data
         st.set_universe(univ)
     st.close()
+
+
+def test_newcov_universe_of_call_sites(newcov_path):
+    """A universe registered as the call SITES of __sanitizer_cov_trace_pc
+    (objdump's addresses) while KCOV reports return addresses (site + 5 on
+    x86, syz-manager/cover.go:82 subtracts the 1 back): every reported PC is
+    outside the universe, so every batch is rejected, never misread."""
+    from syzkaller_amd import SyzcovError
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(41)
+    lo, span = 0x81000000, 1 << 20
+    sites = np.unique(rng.integers(lo, lo + span - 16, size=20000) // 8 * 8).astype(np.uint32)
+    st = CoverState(4, lo, span)
+    st.set_universe(sites)
+    recs = [np.unique(rng.choice(sites, size=50)) + np.uint32(5) for _ in range(8)]
+    with pytest.raises(SyzcovError):
+        st.new_coverage(list(range(4)) * 2, recs)
+    assert all(st.max_cover(c).size == 0 for c in range(4))
+    # the same PCs are fine once the universe is the return addresses
+    st2 = CoverState(4, lo, span)
+    st2.set_universe(sites + np.uint32(5))
+    exp, _ = orc.newcov_batch([[] for _ in range(4)], [], list(range(4)) * 2, recs)
+    assert np.array_equal(st2.new_coverage(list(range(4)) * 2, recs), exp)
+    st.close()
+    st2.close()
 
 
 @pytest.mark.parametrize("per_call", [False, True])

@@ -241,3 +241,33 @@ def test_triage_oracle_kat():
     cc = [np.zeros(0, np.uint32)]
     assert o.add_inputs(mc, cc, [5], [0, 0, 0], [[5], [1, 5], [1]]) == [False, True, False]
     assert mc[0].tolist() == [1, 5] and cc[0].tolist() == [1, 5]
+
+
+def test_newcov_full_vs_list_oracle(tmp_path):
+    """oracle/newcov_full.c (the bitmap restatement of fuzzer.go:456-480 that
+    pins config C5 at full size) == the sorted-list restatement
+    (orc_newcov_batch) on a small stream: 3 batches, flakes, 17 calls."""
+    import subprocess
+    import os
+    seed, nrec, nb, ncalls, mean, sigma, log2 = 0x5EED0005, 1500, 3, 17, 300, 200, 12
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle")], check=True)
+    subprocess.run([os.path.join(root, "oracle", "build", "newcov_full"), hex(seed), str(nrec),
+                    str(nb), str(ncalls), str(mean), str(sigma), str(log2), "3", str(tmp_path)],
+                   check=True, capture_output=True)
+    is_new = np.fromfile(tmp_path / "is_new.u8", dtype=np.uint8)
+    mn = np.fromfile(tmp_path / "maxcover_n.u32", dtype=np.uint32)
+    mcp = np.fromfile(tmp_path / "maxcover.u32", dtype=np.uint32)
+    fo, fp = orc.synth_corpus(seed, 1, 1 << (log2 - 7), 1, log2, first=1 << 40)
+    flakes = orc.canonicalize(fp[:int(fo[1])])
+    mc = [[] for _ in range(ncalls)]
+    for b in range(nb):
+        off, pcs = orc.synth_corpus(seed, nrec, mean, sigma, log2, first=b * nrec)
+        c_off, c_pcs = orc.canonicalize_csr(off, pcs)
+        recs = [c_pcs[c_off[i]:c_off[i + 1]] for i in range(nrec)]
+        cids = orc.synth_callids(seed, nrec, ncalls, first=b * nrec)
+        exp, mc = orc.newcov_batch(mc, flakes, cids, recs)
+        assert np.array_equal(is_new[b * nrec:(b + 1) * nrec], exp), b
+        assert 0 < exp.sum() < nrec
+    assert mn.tolist() == [len(m) for m in mc]
+    assert np.array_equal(mcp, np.concatenate([np.asarray(m, np.uint32) for m in mc]))

@@ -6,6 +6,10 @@ digests the GPU tests compare the engine against.
   C1  10k inputs   seed 0x5EED0001   (CPU-only config)
   C2  1M inputs    seed 0x5EED0002   (one MI355X; also the world-8 rehearsal)
   C3  10M inputs   seed 0x5EED0003   (the 8-GPU config; 82 GB of raw PCs)
+  C5  34 batches of 65,536 call records, seed 0x5EED0005, 293 calls: the
+      fuzzer's new-coverage check (oracle/newcov_full.c), per-batch is_new
+      flags and the final per-call maxCover (the bench's stream: 32 history
+      batches, then the batches it times)
 
 Each run is oracle/build/fullsize (oracle/fullsize.c): the reference's
 Canonicalize + sort.Sort + Minimize loop + Union fold, restated so the corpus
@@ -34,6 +38,7 @@ CONFIGS = {
     "C3": dict(seed=0x5EED0003, n=10_000_000),
 }
 MEAN, SIGMA, LOG2 = 2048, 512, 22
+C5 = dict(seed=0x5EED0005, records=65536, batches=34, ncalls=293)
 
 
 def sha(path: str) -> str:
@@ -68,6 +73,30 @@ def run(name: str, threads: int) -> dict:
     return out
 
 
+def run_c5(threads: int) -> dict:
+    c = C5
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    exe = os.path.join(ROOT, "oracle", "build", "newcov_full")
+    with tempfile.TemporaryDirectory() as d:
+        t0 = time.time()
+        r = subprocess.run([exe, hex(c["seed"]), str(c["records"]), str(c["batches"]),
+                            str(c["ncalls"]), str(MEAN), str(SIGMA), str(LOG2), str(threads), d],
+                           check=True, capture_output=True, text=True)
+        summary = json.loads(r.stdout)
+        is_new = np.fromfile(os.path.join(d, "is_new.u8"), dtype=np.uint8)
+        is_new = is_new.reshape(c["batches"], c["records"])
+        return dict(seed=c["seed"], records=c["records"], batches=c["batches"],
+                    ncalls=c["ncalls"], mean=MEAN, sigma=SIGMA, log2_space=LOG2,
+                    record_pcs=summary["record_pcs"],
+                    new_per_batch=[int(x) for x in is_new.sum(axis=1)],
+                    is_new_sha256=[hashlib.sha256(row.tobytes()).hexdigest() for row in is_new],
+                    max_cover_total=summary["max_cover_total"],
+                    max_cover_n_sha256=sha(os.path.join(d, "maxcover_n.u32")),
+                    max_cover_sha256=sha(os.path.join(d, "maxcover.u32")),
+                    flakes="unique PCs of synthetic input 2^40, length 2^(log2-7)",
+                    oracle_seconds=round(time.time() - t0, 1), oracle_threads=threads)
+
+
 def main():
     names = sys.argv[1:] or list(CONFIGS)
     data = {}
@@ -81,7 +110,8 @@ def main():
                       "lengths, lens = canonical lengths (uint32 LE)")
     for name in names:
         print(f"{name} ...", flush=True)
-        data[name] = run(name, os.cpu_count() or 8)
+        nt = os.cpu_count() or 8
+        data[name] = run_c5(nt) if name == "C5" else run(name, nt)
         print(json.dumps(data[name]), flush=True)
         with open(OUT, "w") as f:
             json.dump(data, f, indent=1)
