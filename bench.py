@@ -281,8 +281,8 @@ def bench_corpus(args):
             "unit": "GB/s", "frac": alg["minimize"] / (ph["minimize"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "traffic": tj.get("minimize", {}).get("bytes"),
             "alg_bytes_per_launch": alg["minimize"]},
-        "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph["compact"]
-                                                          + ph["union"] + ph["merge"]) * 1e-3),
+        "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph.get("exchange", 0.0)
+                                                          + ph["finish"]) * 1e-3),
     }
     if world == 1:
         pk = stream_peak(dev)

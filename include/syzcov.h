@@ -53,9 +53,10 @@ extern "C" {
 #define SYZCOV_ERR_WINDOW 1u  /* a PC outside the configured PC window */
 #define SYZCOV_ERR_SEGLEN 2u  /* a segment longer than the declared max_seg_len */
 #define SYZCOV_ERR_UNIVERSE 4u /* key mode: a PC that is not in the registered universe */
-/* Key mode: the key shift is capped so a universe PC's low kshift bits fit one
- * byte of the membership table with 0xFF left for "no universe PC". */
-#define SYZCOV_KSHIFT_MAX 7u
+/* Key mode: the key shift is capped so a universe PC's low kshift bits fit
+ * one byte of the membership table with bit 7 free and 0x7F left for "no
+ * universe PC", and a canonical key word (key | low << 26) fits 32 bits. */
+#define SYZCOV_KSHIFT_MAX 6u
 
 /* Version / build identification: "syzcov <ver> gfx950". */
 const char *syzcov_version(void);
@@ -290,6 +291,130 @@ int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncal
                                  uint32_t *rec_call_index, uint64_t *rec_off, uint32_t *rec_pcs,
                                  size_t pcs_cap);
 
+/* ================ resident corpus engine (corpus.hip) ==================
+ * The manager-side corpus path the benchmark measures (BASELINE configs C2 /
+ * C3), one handle per GPU: Canonicalize every input (cover/cover.go:27-40),
+ * Go's sort.Sort(minInputArray) order (cover.go:113), first-cover Minimize
+ * (cover.go:104-131), the kept list, the sorted union (the `Union(total, cov)`
+ * fold, syz-manager/manager.go:606-610) and the resident maxCover |= union.
+ * Replaces cover.Minimize + the union fold for Manager.minimizeCorpus-sized
+ * corpora (manager.go:504-550); syzcov_minimize routes large corpora here.
+ *
+ * Modes: with `universe` (the sorted, unique PCs KCOV can report: the return
+ * addresses of the __sanitizer_cov_trace_pc calls, syz-manager/cover.go:82,
+ * 274-306, truncated to u32) every phase works on dense keys (keys.hip) and a
+ * PC outside the universe fails the step (SYZCOV_ERANGE), never aliases;
+ * without it, on PC offsets of [pc_lo, pc_lo + pc_span) (<= 2^28 PCs).
+ *
+ * Memory: one device block of syzcov_corpus_mem_size(cfg) bytes, laid out
+ * as syzcov_corpus_buffer reports; the caller may pass its own (256-byte
+ * aligned) or let the handle allocate.  Phase calls are asynchronous on the
+ * caller's stream; a handle serves one step at a time (calls on one handle
+ * are serialized by its lock, but two streams must not interleave steps).
+ *
+ * Sharded by input over `world` GPUs (n_global > n_max; rank r holds global
+ * inputs [r * n_max, r * n_max + n)), the caller runs the collectives
+ * between the phases (syzkaller_amd/dist.py does it over RCCL):
+ *   canon -> all-gather NEW_LEN[:n] into GLENS -> order(GLENS, N)
+ *   -> minimize(do_pass2 = 0)
+ *   key mode:    MIN all-reduce FIRST (int32 x span) -> pass2
+ *   window mode: all-gather + OR COVERED (bitmap_op) -> n_ids = dense_first
+ *                -> MIN all-reduce FIRST_DENSE[:n_ids] -> pass2
+ *   -> MAX all-reduce KEPT[:N] (u8) -> finish -> result. */
+typedef uint64_t syzcov_corpus;
+typedef struct syzcov_corpus_cfg {
+    size_t n_max;        /* inputs per step on this GPU */
+    size_t n_global;     /* inputs of the sharded corpus (0 = n_max: one GPU) */
+    size_t rank;         /* this shard (sharded runs) */
+    uint64_t p_max;      /* raw PCs per step on this GPU */
+    size_t max_seg_len;  /* longest input (a longer one fails the step) */
+    uint32_t pc_lo;      /* window mode: the PC window */
+    uint64_t pc_span;
+    const uint32_t *universe; /* key mode (host; read during create only) */
+    size_t universe_n;
+    int canon_in_place;  /* canonical lists overwrite the raw ones (max_seg_len <= 16384) */
+    int order_by;        /* 0: canonical lengths; 1: raw lengths (Minimize of covers as given) */
+    uint64_t rec_cap;    /* first-cover records (0 = default) */
+} syzcov_corpus_cfg;
+typedef struct syzcov_corpus_info_t {
+    uint32_t key_mode, kshift, kbase, pc_lo; /* key(pc) = (pc >> kshift) - kbase */
+    uint64_t span;       /* keys (key mode) or window PCs */
+    uint32_t win_lo, sent_key;  /* canonicalize's window; index of 0xFFFFFFFF (or ~0) */
+    uint64_t win_span, nrange, nwords, n_global, union_cap, rec_cap;
+    void *mem;
+    uint64_t mem_size;
+} syzcov_corpus_info_t;
+typedef struct syzcov_corpus_res {
+    uint32_t err_flags;  /* SYZCOV_ERR_* bits of the step */
+    uint32_t n_ids;      /* distinct keys of the corpus (sentinel included) */
+    uint32_t n_kept, n_union;
+    uint64_t max_cover;  /* |maxCover| after the merge */
+    uint64_t records;    /* first-cover records of the step */
+    const int32_t *kept_idx;   /* device: kept input indices, processing order */
+    const uint32_t *union_pcs; /* device: the sorted union */
+} syzcov_corpus_res;
+/* buffers of the layout (syzcov_corpus_buffer: byte offset in the block, size) */
+enum {
+    SYZCOV_CORPUS_CANON = 0,   /* u32 [p_max + 1] canonical lists (not in place) */
+    SYZCOV_CORPUS_NEW_LEN,     /* u32 [n_max + 1] canonical lengths */
+    SYZCOV_CORPUS_SPLIT,       /* u32 [n_max][nrange] range split points */
+    SYZCOV_CORPUS_RANGE_TOT,   /* u64 [nrange] */
+    SYZCOV_CORPUS_COVERED,     /* u32 bitmap: the step's union */
+    SYZCOV_CORPUS_MAX_COVER,   /* u32 [nwords] resident maxCover */
+    SYZCOV_CORPUS_TAB,         /* u64 [nwords] dictionary of the union */
+    SYZCOV_CORPUS_FIRST,       /* i32 [span] first-cover ranks (INT32_MAX between steps) */
+    SYZCOV_CORPUS_REC,         /* u64 [rec_cap] first-cover records */
+    SYZCOV_CORPUS_CAND,        /* u8  [n_max + 1] */
+    SYZCOV_CORPUS_KEPT,        /* u8  [n_global + 1] kept flag per global rank */
+    SYZCOV_CORPUS_LENS,        /* i64 [n_global + 1] */
+    SYZCOV_CORPUS_ORDER,       /* i32 [n_global + 1] Go's processing order */
+    SYZCOV_CORPUS_KEPT_IDX,    /* i32 [n_global + 1] kept inputs, processing order */
+    SYZCOV_CORPUS_UNION,       /* u32 [union_cap] sorted union */
+    SYZCOV_CORPUS_SCAL,        /* u64 [16] step scalars */
+    SYZCOV_CORPUS_PC_OF_KEY,   /* u32 [span] key mode */
+    SYZCOV_CORPUS_LOW_OF_KEY,  /* u8  [span] key mode: membership table */
+    SYZCOV_CORPUS_GLENS,       /* i32 [n_global] sharded: gathered lengths */
+    SYZCOV_CORPUS_SEL,         /* u8  [n_global] sharded */
+    SYZCOV_CORPUS_IOTA,        /* i32 [n_global] sharded */
+    SYZCOV_CORPUS_ITEMS,       /* i32 [n_max + 1] sharded: local inputs in order */
+    SYZCOV_CORPUS_RANKS,       /* i32 [n_max + 1] sharded: their global ranks */
+    SYZCOV_CORPUS_FIRST_DENSE, /* i32 [union_cap] sharded window mode */
+    SYZCOV_CORPUS_WS,          /* scratch */
+    SYZCOV_CORPUS_WS2,         /* sharded scratch */
+    SYZCOV_CORPUS_NBUF
+};
+int64_t syzcov_corpus_mem_size(const syzcov_corpus_cfg *cfg);
+int syzcov_corpus_create(const syzcov_corpus_cfg *cfg, void *mem, size_t mem_size,
+                         syzcov_corpus *out);
+int syzcov_corpus_destroy(syzcov_corpus h);
+int syzcov_corpus_info(syzcov_corpus h, syzcov_corpus_info_t *out);
+int syzcov_corpus_buffer(syzcov_corpus h, int which, uint64_t *offset, uint64_t *bytes);
+/* Phases (device pointers, asynchronous on `stream`).  raw is written when
+ * canon_in_place. */
+int syzcov_corpus_canon(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
+                        void *stream);
+/* lens: device int32[N] (sharded: the gathered lengths), NULL = this step's */
+int syzcov_corpus_order(syzcov_corpus h, const int32_t *lens, size_t N, void *stream);
+int syzcov_corpus_minimize(syzcov_corpus h, int do_pass2, void *stream);
+/* window mode, sharded: returns n_ids (synchronizes the stream) */
+int64_t syzcov_corpus_dense_first(syzcov_corpus h, void *stream);
+int syzcov_corpus_pass2(syzcov_corpus h, void *stream);
+int syzcov_corpus_finish(syzcov_corpus h, void *stream);
+/* canon + order + minimize + finish on one GPU */
+int syzcov_corpus_step(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
+                       void *stream);
+/* Synchronizes the stream; the step's counts and device result pointers.
+ * SYZCOV_ERANGE (a PC outside the window or the universe) or SYZCOV_ETOOLONG
+ * (an input longer than max_seg_len) if the step's results are invalid. */
+int syzcov_corpus_result(syzcov_corpus h, syzcov_corpus_res *res, void *stream);
+/* The drop-in form: cover.Minimize + the union fold of a host CSR corpus
+ * (offsets[n + 1], pcs) through the handle; out_idx (capacity n) receives the
+ * kept indices in processing order, union_out (nullable, capacity union_cap)
+ * the sorted union, *n_union (nullable) its size.  Returns the kept count. */
+int64_t syzcov_corpus_minimize_host(syzcov_corpus h, const uint64_t *offsets, const uint32_t *pcs,
+                                    size_t n, int32_t *out_idx, uint32_t *union_out,
+                                    size_t union_cap, uint64_t *n_union);
+
 /* =================== 2. device-resident launch API ==================== */
 /* All pointers below are device pointers; `stream` is a hipStream_t.
  * `ws` is caller-provided device workspace of at least the returned size.  */
@@ -376,23 +501,25 @@ int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, uint32_t *o
 /* Key mode (keys.hip): key(pc) = (pc >> kshift) - kbase over a registered PC
  * universe (the PCs KCOV reports: return addresses of the
  * __sanitizer_cov_trace_pc calls) with kshift = the largest collision-free
- * shift, at most SYZCOV_KSHIFT_MAX.  Canonicalize runs on the PCs of
- * [pc_lo, pc_lo + pc_span) exactly as syzcov_dev_canon_split; every canonical
- * PC is written as its KEY, and split[] / range_tot[] count ranges of
- * 2^range_shift keys.  The window must map into [0, nkeys).  Every canonical
- * PC is checked against the universe (low_of_key, from
- * syzcov_dev_universe_keymap): a PC outside it sets SYZCOV_ERR_UNIVERSE, and
- * the keys of that step must not be used (two PCs may share a key). */
+ * shift, at most SYZCOV_KSHIFT_MAX, nkeys <= 2^25.  Canonicalize runs on the
+ * PCs of [pc_lo, pc_lo + pc_span) exactly as syzcov_dev_canon_split; every
+ * canonical PC is written as its KEY WORD key | (pc & (2^kshift - 1)) << 26
+ * (so two PCs sharing a key stay two entries), and split[] / range_tot[]
+ * count ranges of 2^range_shift keys.  The window must map into [0, nkeys).
+ * Membership in the universe is checked where the words are consumed
+ * (syzcov_dev_minimize_range_keys). */
 int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                                 uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
                                 uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
-                                const uint8_t *low_of_key, uint32_t range_shift, uint32_t *split,
-                                uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
-                                void *stream);
+                                uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
+                                uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+/* out[i] = the PC of key word words[i] (exact, no table); in place allowed. */
+int syzcov_dev_words_to_pcs(const uint32_t *words, size_t n, uint32_t kshift, uint32_t kbase,
+                            uint32_t *out, void *stream);
 /* Key tables of a universe (univ sorted, collision-free under kshift <=
  * SYZCOV_KSHIFT_MAX, else *err_flag |= 1): pc_of_key[key(univ[i])] = univ[i]
  * (0 for keys without a universe PC) and low_of_key[key(univ[i])] =
- * univ[i] & (2^kshift - 1) (0xFF without one).  Either table may be NULL. */
+ * univ[i] & (2^kshift - 1) (0x7F without one).  Either table may be NULL. */
 int syzcov_dev_universe_keymap(const uint32_t *univ, size_t n, uint32_t kshift, uint32_t kbase,
                                uint64_t nkeys, uint32_t *pc_of_key, uint8_t *low_of_key,
                                uint32_t *err_flag, void *stream);
@@ -425,6 +552,30 @@ int syzcov_dev_minimize_range(const uint64_t *off, const uint32_t *len, const ui
                               int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
                               uint8_t *cand, uint8_t *kept, int do_pass2, size_t first_chunk,
                               uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream);
+/* Key mode (keys.hip): the same over KEY WORDS (syzcov_dev_canon_split_keys)
+ * of nkeys <= 2^25 keys in ranges of 2^range_shift <= 2^17 keys.  Every word
+ * is checked against the membership table low_of_key (syzcov_dev_universe_keymap,
+ * padded with 0x7F to nrange << range_shift bytes): a word whose PC is not in
+ * the universe sets SYZCOV_ERR_UNIVERSE in *err_flag and the step's results
+ * must not be used.  first_w / covered / records are over keys.  Sharded runs
+ * MIN all-reduce first_w and call syzcov_dev_minimize_range_keys_pass2. */
+int syzcov_dev_minimize_range_keys(const uint64_t *off, const uint32_t *len,
+                                   const uint32_t *words, const uint32_t *split,
+                                   const int32_t *order, const int32_t *ranks, size_t n_items,
+                                   uint64_t nkeys, uint32_t range_shift,
+                                   const uint64_t *range_tot, const uint8_t *low_of_key,
+                                   uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                                   uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand,
+                                   uint8_t *kept, int do_pass2, uint32_t *err_flag, void *ws,
+                                   void *stream);
+int syzcov_dev_minimize_range_keys_pass2(const uint64_t *off, const uint32_t *len,
+                                         const uint32_t *words, const uint32_t *split,
+                                         const int32_t *order, const int32_t *ranks,
+                                         size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                                         const uint64_t *range_tot, uint32_t *covered,
+                                         int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
+                                         uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
+                                         void *ws, void *stream);
 /* Sharded runs: call syzcov_dev_minimize_range with do_pass2 = 0 (first_w then
  * holds this shard's first ranks and covered its union), merge the shards'
  * covered bitmaps (OR) into the dictionary `tab` (syzcov_dev_dict_build_bits),

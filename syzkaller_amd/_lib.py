@@ -74,6 +74,21 @@ _SIGS = {
     "syzcov_state_triage": (i64, [u64, sz, p_, p_, p_, p_, p_, p_, p_, p_]),
     "syzcov_state_newcov_ws_size": (sz, [sz, u64]),
     "syzcov_state_newcov_dev": (C.c_int, [u64, p_, p_, p_, sz, u64, p_, p_, p_, sz, p_]),
+    # resident corpus engine (corpus.hip)
+    "syzcov_corpus_mem_size": (i64, [p_]),
+    "syzcov_corpus_create": (C.c_int, [p_, p_, sz, p_]),
+    "syzcov_corpus_destroy": (C.c_int, [u64]),
+    "syzcov_corpus_info": (C.c_int, [u64, p_]),
+    "syzcov_corpus_buffer": (C.c_int, [u64, C.c_int, p_, p_]),
+    "syzcov_corpus_canon": (C.c_int, [u64, p_, p_, sz, p_]),
+    "syzcov_corpus_order": (C.c_int, [u64, p_, sz, p_]),
+    "syzcov_corpus_minimize": (C.c_int, [u64, C.c_int, p_]),
+    "syzcov_corpus_dense_first": (i64, [u64, p_]),
+    "syzcov_corpus_pass2": (C.c_int, [u64, p_]),
+    "syzcov_corpus_finish": (C.c_int, [u64, p_]),
+    "syzcov_corpus_step": (C.c_int, [u64, p_, p_, sz, p_]),
+    "syzcov_corpus_result": (C.c_int, [u64, p_, p_]),
+    "syzcov_corpus_minimize_host": (i64, [u64, p_, p_, sz, p_, p_, sz, p_]),
     # device tier
     "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
     "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
@@ -90,7 +105,12 @@ _SIGS = {
     "syzcov_dev_canon_split": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, p_, p_, p_, p_, sz,
                                          p_]),
     "syzcov_dev_canon_split_keys": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, u32, u64,
-                                              p_, u32, p_, p_, p_, p_, sz, p_]),
+                                              u32, p_, p_, p_, p_, sz, p_]),
+    "syzcov_dev_words_to_pcs": (C.c_int, [p_, sz, u32, u32, p_, p_]),
+    "syzcov_dev_minimize_range_keys": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_, p_, p_,
+                                                 p_, p_, u64, p_, p_, p_, C.c_int, p_, p_, p_]),
+    "syzcov_dev_minimize_range_keys_pass2": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_,
+                                                       p_, p_, p_, u64, p_, p_, p_, p_, p_]),
     "syzcov_dev_universe_keymap": (C.c_int, [p_, sz, u32, u32, u64, p_, p_, p_, p_]),
     "syzcov_dev_keys_to_pcs": (C.c_int, [p_, u64, p_, p_, p_, sz, p_]),
     "syzcov_dev_first_to_bits": (C.c_int, [p_, u64, p_, p_]),
@@ -140,10 +160,19 @@ def lib():
         except Exception:  # pragma: no cover - torch is optional for the C-ABI
             pass
         L = C.CDLL(LIB_PATH)
+        missing = []
         for name, (res, args) in _SIGS.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                missing.append(name)
+                continue
             f.restype = res
             f.argtypes = args
+        # a tuning variant (SYZCOV_LIB) may predate an entry point; the product
+        # library must export every one
+        if missing and not os.environ.get("SYZCOV_LIB"):
+            raise ImportError(f"{LIB_PATH} lacks {missing}: rebuild it")
         _lib = L
     return _lib
 
@@ -159,3 +188,32 @@ def header_symbols() -> list[str]:
     with open(HEADER) as f:
         txt = f.read()
     return sorted(set(re.findall(r"\b(syzcov_[a-z0-9_]+)\(", txt)))
+
+
+# ---------------------------------------------------------------- corpus ABI
+class CorpusCfg(C.Structure):
+    """syzcov_corpus_cfg (include/syzcov.h)."""
+    _fields_ = [("n_max", sz), ("n_global", sz), ("rank", sz), ("p_max", u64),
+                ("max_seg_len", sz), ("pc_lo", u32), ("pc_span", u64), ("universe", p_),
+                ("universe_n", sz), ("canon_in_place", C.c_int), ("order_by", C.c_int),
+                ("rec_cap", u64)]
+
+
+class CorpusInfo(C.Structure):
+    """syzcov_corpus_info_t."""
+    _fields_ = [("key_mode", u32), ("kshift", u32), ("kbase", u32), ("pc_lo", u32),
+                ("span", u64), ("win_lo", u32), ("sent_key", u32), ("win_span", u64),
+                ("nrange", u64), ("nwords", u64), ("n_global", u64), ("union_cap", u64),
+                ("rec_cap", u64), ("mem", p_), ("mem_size", u64)]
+
+
+class CorpusRes(C.Structure):
+    """syzcov_corpus_res."""
+    _fields_ = [("err_flags", u32), ("n_ids", u32), ("n_kept", u32), ("n_union", u32),
+                ("max_cover", u64), ("records", u64), ("kept_idx", p_), ("union_pcs", p_)]
+
+
+# enum of syzcov_corpus_buffer (include/syzcov.h)
+CORPUS_BUFS = ("CANON", "NEW_LEN", "SPLIT", "RANGE_TOT", "COVERED", "MAX_COVER", "TAB", "FIRST",
+               "REC", "CAND", "KEPT", "LENS", "ORDER", "KEPT_IDX", "UNION", "SCAL", "PC_OF_KEY",
+               "LOW_OF_KEY", "GLENS", "SEL", "IOTA", "ITEMS", "RANKS", "FIRST_DENSE", "WS", "WS2")

@@ -330,6 +330,11 @@ int64_t syzcov_intersection(const uint32_t *a, size_t na, const uint32_t *b, siz
 
 // ------------------------------------------------------------------ corpus
 namespace syz {
+// cover.Minimize calls with at least this many inputs run on the corpus
+// engine (corpus.hip); smaller ones on the dictionary path below
+constexpr size_t kEngineMinInputs = 1024;
+int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n, int32_t *out_idx,
+                        int64_t *out_n);
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
 int ui_stats_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
                     uint32_t ncalls, const uint64_t *tab, uint32_t pc_lo, uint32_t nids,
@@ -434,6 +439,14 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
     if (n == 0) return 0;
     if (!offsets || !out_idx || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    // corpus-sized calls take the benchmarked engine (corpus.hip: window mode
+    // over the corpus' own PC extent, order by the raw lengths Go sorts on)
+    if (!order && sort_variant == 0 && n >= kEngineMinInputs && device_count() > 0) {
+        int64_t k = 0;
+        const int rc = minimize_via_engine(offsets, pcs, n, out_idx, &k);
+        if (rc < 0) return rc;
+        if (rc == 1) return k;
+    }
     CtxLease lease;
     Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;

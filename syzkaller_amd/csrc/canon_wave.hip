@@ -169,8 +169,7 @@ struct Params {
     uint32_t nbits;
     uint32_t kshift, kbase;   // output key = (pc >> kshift) - kbase (key mode)
     uint64_t nkeys;
-    const uint8_t *low_of_key;  // key mode: universe membership (keys.hip)
-    uint32_t lowmask;           // 2^kshift - 1
+    uint32_t lowmask;           // 2^kshift - 1 (key mode: the word's low bits)
     int key_out;              // write keys (key mode) instead of PCs
     uint32_t sent_key;        // key of PC 0xFFFFFFFF (or 0xFFFFFFFF if outside)
     uint32_t *split;          // nullable: [nseg][nrange]
@@ -415,9 +414,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        // key mode: the dense key of the PC; the key map is
-                        // monotone, so sorted unique PCs give sorted unique keys
-                        outp[pos] = P.key_out ? ((v + P.pc_lo) >> P.kshift) - P.kbase
+                        // key mode: the PC's key word (common.h); the key map
+                        // is monotone, so sorted unique PCs give sorted words
+                        outp[pos] = P.key_out ? key_word(v + P.pc_lo, P.kshift, P.kbase)
                                               : v + P.pc_lo;
                         buf[pos] = v;
                     }
@@ -429,23 +428,6 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
             continue;
         }
         if (l == 0) P.new_len[seg] = cnt;
-        if (P.key_out) {  // every canonical PC must be a universe PC (keys.hip)
-            uint32_t nm = 0;
-#pragma unroll
-            for (int q = 0; q < NQ; q++)
-                if ((uint32_t)q < nq) {
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
-                        const uint32_t pc = k[q * 4 + c] + P.pc_lo;
-                        const uint32_t key = (pc >> P.kshift) - P.kbase;
-                        const bool in = e < n && k[q * 4 + c] <= span_m1;
-                        const uint32_t t = P.low_of_key[in ? key : 0u];
-                        nm |= (uint32_t)in & (uint32_t)(t != (pc & P.lowmask));
-                    }
-                }
-            if (__ballot(nm) && l == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
-        }
         // ------------------------------------------- range splits
         if (!P.split) {
             if (l == 0) racc[0] += cnt;  // one range: its total is the PC count
@@ -501,18 +483,14 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
 // A PC outside the window is flagged (SYZCOV_ERR_WINDOW: the step's results
 // are invalid and the engine raises) and sorts as the last key, so nothing
 // downstream indexes past the key range.
-// Exactness on any input: the sorted word is key | (pc & lowmask) << 22, the
-// PC's low kshift bits riding above the 22 key bits as payload (the digits
-// never read them).  Unique compares whole words, i.e. PCs, and every
-// canonical word is checked against the universe's membership table
-// (low_of_key, keys.hip): two PCs share a key only if one of them is not in
-// the universe, and then SYZCOV_ERR_UNIVERSE is set instead of aliasing them.
-// The byte gathers of a segment are all issued before the first test (other
-// waves' LDS work hides their latency; holding them across the split searches
-// instead spilled 32 more VGPRs).
+// Key words: the sorted word is key | (pc & lowmask) << SYZ_KEY_BITS
+// (common.h), the PC's low kshift bits riding above the key bits as payload
+// (the digits never read them).  Unique compares whole words, i.e. PCs, so
+// two PCs that share a key both stay; Minimize checks every word against the
+// universe (minimize_range.hip, key mode).
 constexpr int KB = 11;
-constexpr uint32_t KEY_BITS = 2 * KB;              // keys < 2^22 in the low bits
-constexpr uint32_t KEY_MASK = (1u << KEY_BITS) - 1u;
+constexpr uint32_t KEY_BITS = SYZ_KEY_BITS;   // keys < 2^22 here: two 11-bit digits
+constexpr uint32_t KEY_MASK = SYZ_KEY_MASK;
 constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
@@ -730,7 +708,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        outp[pos] = v & KEY_MASK;
+                        outp[pos] = v;  // the key word: the PC is kept exactly
                         buf[pos] = v & KEY_MASK;
                     }
                     cnt += (uint32_t)__popcll(m);
@@ -741,29 +719,6 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
             continue;
         }
         if (l == 0) P.new_len[seg] = cnt;
-        {  // membership: one byte gather per sorted slot, 32-bit offsets from a
-           // buffer resource (64-bit addresses for 32+ gathers spilled VGPRs)
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t *>(P.low_of_key), (short)0, (int)(kmax + 1), 0x00020000);
-            uint32_t nm = 0;
-#pragma unroll
-            for (int q = 0; q < NQ; q++)
-                if ((uint32_t)q < nq) {
-                    uint32_t mt[4];
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
-                        mt[c] = __builtin_amdgcn_raw_buffer_load_b8(
-                            rs, e < n ? (int)(k[q * 4 + c] & KEY_MASK) : 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
-                        nm |= (uint32_t)(e < n) & (uint32_t)(mt[c] != k[q * 4 + c] >> KEY_BITS);
-                    }
-                }
-            if (__ballot(nm) && l == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
-        }
         if (!P.split) {
             if (l == 0) racc[0] += cnt;
         } else {
@@ -824,7 +779,8 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
                 uint32_t lo = 0, hi = cnt;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (c[mid] - (P.key_out ? 0u : P.pc_lo) < b) lo = mid + 1; else hi = mid;
+                    const uint32_t x = P.key_out ? c[mid] & SYZ_KEY_MASK : c[mid] - P.pc_lo;
+                    if (x < b) lo = mid + 1; else hi = mid;
                 }
                 s = lo;
             }
@@ -852,18 +808,13 @@ __global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_
         if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
         uint32_t *c = P.out + P.off[seg];
         const uint32_t cnt = P.new_len[seg];
-        bool bad = false, nm = false;
+        bool bad = false;
         for (uint32_t i = __lane_id(); i < cnt; i += 64) {
             const uint32_t pc = c[i];
             const bool out = pc - P.pc_lo > (uint32_t)(P.span - 1);
             bad |= out;
-            if (P.key_out && !out) {
-                const uint32_t key = (pc >> P.kshift) - P.kbase;
-                nm |= P.low_of_key[key] != (pc & P.lowmask);
-                c[i] = key;
-            }
+            if (P.key_out && !out) c[i] = key_word(pc, P.kshift, P.kbase);
         }
-        if (__ballot(nm) && __lane_id() == 0) atomicOr(P.err, SYZCOV_ERR_UNIVERSE);
         if (__ballot(bad)) {  // flagged; the segment is dropped (memory-safe downstream)
             if (__lane_id() == 0) {
                 atomicOr(P.err, SYZCOV_ERR_WINDOW);
@@ -943,7 +894,7 @@ static void launch_class(const cw::Params &P, const uint32_t *lc, const uint32_t
 static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                             uint32_t *new_len, size_t nseg, size_t max_seg_len, uint32_t pc_lo,
                             uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
-                            const uint8_t *low_of_key, int key_out, uint32_t range_shift,
+                            int key_out, uint32_t range_shift,
                             uint32_t *split,
                             uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
                             void *stream) {
@@ -952,7 +903,8 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
         return SYZCOV_ERANGE;
     if (key_out) {  // every window PC must map into [0, nkeys)
-        if (!low_of_key || kshift > SYZCOV_KSHIFT_MAX) return SYZCOV_EINVAL;
+        // key words (common.h): keys < 2^25, the low bits above them
+        if (kshift > SYZCOV_KSHIFT_MAX || nkeys > (1ull << 25)) return SYZCOV_EINVAL;
         const uint64_t k0 = pc_lo >> kshift, k1 = (pc_lo + pc_span - 1) >> kshift;
         if (nkeys == 0 || k0 < kbase || k1 - kbase >= nkeys) return SYZCOV_ERANGE;
     } else {
@@ -982,7 +934,6 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.kbase = kbase;
     P.nkeys = nkeys;
     P.key_out = key_out;
-    P.low_of_key = low_of_key;
     P.lowmask = (1u << kshift) - 1u;
     P.nbits = pc_span <= 1 ? 1 : 64 - __builtin_clzll(pc_span - 1);
     const uint64_t so = (uint64_t)(uint32_t)(0xFFFFFFFFu - pc_lo);
@@ -1011,7 +962,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     P.force_redo = (force & FORCE_REDO) ? 1u : 0u;
     cw::Params PK = P;  // the key kernel's unique loop compares (key | low bits) words
     PK.sent_key = so < pc_span ? ((0xFFFFFFFFu >> kshift) - kbase) | (P.lowmask << cw::KEY_BITS)
-                               : 0xFFFFFFFFu;  // words are < 2^29: never equal
+                               : 0xFFFFFFFFu;  // a word's key is < 2^25: never equal
     // bin by capacity class (wave-aggregated atomics), one launch per class
     // (a register bitonic network measured 20.3 ms at C2 against the LDS
     // radix's 7.8: 147 VALU ops per key)
@@ -1092,19 +1043,18 @@ extern "C" int syzcov_dev_canon_split(const uint64_t *off, const uint32_t *raw, 
                                       uint32_t *split, uint64_t *range_tot, uint32_t *err_flag,
                                       void *ws, size_t ws_size, void *stream) {
     return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, 0, pc_lo,
-                            pc_span, nullptr, 0, range_shift, split, range_tot, err_flag, ws,
-                            ws_size, stream);
+                            pc_span, 0, range_shift, split, range_tot, err_flag, ws, ws_size,
+                            stream);
 }
 
 extern "C" int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32_t *out,
                                            uint32_t *new_len, size_t nseg, size_t max_seg_len,
                                            uint32_t pc_lo, uint64_t pc_span, uint32_t kshift,
-                                           uint32_t kbase, uint64_t nkeys,
-                                           const uint8_t *low_of_key, uint32_t range_shift,
+                                           uint32_t kbase, uint64_t nkeys, uint32_t range_shift,
                                            uint32_t *split, uint64_t *range_tot,
                                            uint32_t *err_flag, void *ws, size_t ws_size,
                                            void *stream) {
     return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, kshift,
-                            kbase, nkeys, low_of_key, 1, range_shift, split, range_tot, err_flag,
-                            ws, ws_size, stream);
+                            kbase, nkeys, 1, range_shift, split, range_tot, err_flag, ws, ws_size,
+                            stream);
 }

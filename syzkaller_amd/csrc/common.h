@@ -104,6 +104,17 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tmp, u
     return res;
 }
 
+// Key mode (keys.hip): a canonical PC travels as the WORD
+//     key(pc) | (pc & (2^kshift - 1)) << SYZ_KEY_BITS,  key(pc) = (pc >> kshift) - kbase,
+// i.e. the dense key plus the low bits the shift drops, so the PC itself is
+// never lost (keys < 2^25, kshift <= SYZCOV_KSHIFT_MAX = 6: 31 bits).
+constexpr uint32_t SYZ_KEY_BITS = 26;
+constexpr uint32_t SYZ_KEY_MASK = (1u << SYZ_KEY_BITS) - 1u;
+__host__ __device__ __forceinline__ uint32_t key_word(uint32_t pc, uint32_t kshift,
+                                                      uint32_t kbase) {
+    return ((pc >> kshift) - kbase) | ((pc & ((1u << kshift) - 1u)) << SYZ_KEY_BITS);
+}
+
 // 64-bit splitmix (synthetic generator; identical to oracle/synth_oracle.c).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;

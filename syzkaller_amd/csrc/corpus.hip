@@ -1,0 +1,791 @@
+// corpus.hip — the resident corpus engine behind one C-ABI handle
+// (include/syzcov.h, "resident corpus engine"): the benchmarked C2/C3 path,
+// callable from Go over cgo exactly as bench.py drives it.
+//
+// One step over a raw corpus already in HBM (CSR off u64[n+1], raw KCOV PCs):
+//   canon    Canonicalize every input (cover/cover.go:27-40), per-range split
+//            points (canon_wave.hip)
+//   order    Go sort.Sort(minInputArray) (cover.go:113) over the canonical
+//            lengths, or the raw lengths (cover.Minimize on covers as given)
+//   minimize first-cover Minimize (cover.go:104-131; minimize_range.hip)
+//   finish   kept inputs in processing order, the sorted union (the
+//            `Union(total, cov)` fold, manager.go:606-610) and the resident
+//            maxCover |= union
+// Sharded (one handle per GPU, n_global > n_max): the caller runs the
+// collectives between the phase calls (syzkaller_amd/dist.py over RCCL, or the
+// Go host's own RCCL calls on the buffers syzcov_corpus_buffer exposes).
+//
+// Every buffer lives in one device block, carved by a fixed layout, either
+// allocated by the handle or handed in by the caller (torch's caching
+// allocator in Python), so the exchanged buffers can be wrapped as tensors.
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "common.h"
+
+namespace syz {
+
+// int64 lengths for the order: canonical (len32) or raw (from the offsets)
+__global__ void corpus_lens_kernel(const uint32_t *__restrict__ len32,
+                                   const uint64_t *__restrict__ off, uint64_t n,
+                                   int64_t *__restrict__ lens) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        lens[i] = len32 ? (int64_t)len32[i] : (int64_t)(off[i + 1] - off[i]);
+}
+
+// local work items of shard `rank`: sel[r] = order[r] lives here
+__global__ void corpus_sel_kernel(const int32_t *__restrict__ order, uint64_t N, uint32_t base,
+                                  uint32_t n_local, uint8_t *__restrict__ sel,
+                                  int32_t *__restrict__ iota) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        sel[i] = (uint32_t)order[i] - base < n_local;
+        iota[i] = (int32_t)i;
+    }
+}
+
+__global__ void corpus_sub_kernel(int32_t *__restrict__ v, uint32_t n, int32_t base) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        v[i] -= base;
+}
+
+// the union drops the sentinel (cover.go:97): its covered bit goes before the
+// maxCover merge
+__global__ void corpus_clear_bit_kernel(uint32_t *covered, uint32_t bit) {
+    covered[bit >> 5] &= ~(1u << (bit & 31));
+}
+
+// Minimize's LDS-resident ranges: 2^20 window PCs (128 KB of covered bits);
+// in key mode 2^17 keys (128 KB of membership bytes | covered bits)
+constexpr uint32_t kRangeShiftWindow = 20, kRangeShiftKeys = 17;
+
+struct Corpus {
+    std::mutex mu;
+    int dev = 0;
+    syzcov_corpus_cfg cfg{};
+    bool key_mode = false;
+    uint32_t kshift = 0, kbase = 0;
+    uint32_t win_lo = 0;    // canonicalize's PC window
+    uint64_t win_span = 0;
+    uint32_t pc_lo = 0;     // minimize / union / maxCover window (key mode: 0, nkeys)
+    uint64_t span = 0;
+    uint32_t sent_key = 0xFFFFFFFFu;  // index of PC 0xFFFFFFFF in that window, or none
+    uint32_t rshift = kRangeShiftWindow, nrange = 1;
+    uint64_t nwords = 0, n_global = 0, union_cap = 0;
+    int world = 1;
+    // layout
+    uint8_t *mem = nullptr;
+    size_t mem_size = 0;
+    bool own_mem = false;
+    size_t offs[SYZCOV_CORPUS_NBUF] = {}, sizes[SYZCOV_CORPUS_NBUF] = {};
+    size_t ws_size = 0, ws2_size = 0;
+    // per-step state
+    const uint64_t *off = nullptr;  // the step's offsets (order by raw lengths)
+    uint32_t *canon = nullptr;      // the step's canonical lists (in place: the raw buffer)
+    size_t n = 0;                   // inputs of this shard in the step
+    size_t N = 0;                   // inputs ordered (the global corpus when sharded)
+    bool dict_ready = false;        // tab holds the dictionary of the merged union
+    // device staging of the drop-in call (grow-only)
+    void *stage = nullptr;
+    size_t stage_cap = 0;
+    template <class T>
+    T *buf(int b) const {
+        return sizes[b] ? (T *)(mem + offs[b]) : nullptr;
+    }
+};
+
+static uint64_t nrange_of(uint64_t span, uint32_t rshift) {
+    return (span + (1ull << rshift) - 1) >> rshift;
+}
+
+// Largest shift <= SYZCOV_KSHIFT_MAX keeping a sorted unique universe
+// collision-free: (a >> s) != (b >> s) iff a ^ b has a bit >= s.
+static int universe_shift(const uint32_t *u, size_t n, uint32_t *ks) {
+    uint32_t s = SYZCOV_KSHIFT_MAX;
+    for (size_t i = 1; i < n; i++) {
+        if (u[i] <= u[i - 1]) return SYZCOV_EINVAL;
+        const uint32_t x = u[i] ^ u[i - 1];
+        const uint32_t hb = 31u - (uint32_t)__builtin_clz(x);
+        if (hb < s) s = hb;
+    }
+    *ks = n < 2 ? 0 : s;
+    return 0;
+}
+
+// Plans the layout (sizes only); returns the total bytes or < 0.
+static int64_t plan(Corpus &c) {
+    const syzcov_corpus_cfg &g = c.cfg;
+    const size_t n = g.n_max, N = c.n_global;
+    size_t *sz = c.sizes;
+    for (int b = 0; b < SYZCOV_CORPUS_NBUF; b++) sz[b] = 0;
+    sz[SYZCOV_CORPUS_CANON] = g.canon_in_place ? 0 : (g.p_max + 1) * 4;
+    sz[SYZCOV_CORPUS_NEW_LEN] = (n + 1) * 4;
+    sz[SYZCOV_CORPUS_SPLIT] = c.nrange > 1 ? n * c.nrange * 4 : 0;
+    sz[SYZCOV_CORPUS_RANGE_TOT] = c.nrange * 8;
+    sz[SYZCOV_CORPUS_COVERED] = ((uint64_t)c.nrange << c.rshift) / 8;
+    sz[SYZCOV_CORPUS_MAX_COVER] = c.nwords * 4;
+    sz[SYZCOV_CORPUS_TAB] = c.nwords * 8;
+    sz[SYZCOV_CORPUS_FIRST] = c.span * 4;
+    sz[SYZCOV_CORPUS_REC] = g.rec_cap * 8;
+    sz[SYZCOV_CORPUS_CAND] = n + 1;
+    sz[SYZCOV_CORPUS_KEPT] = N + 1;
+    sz[SYZCOV_CORPUS_LENS] = (N + 1) * 8;
+    sz[SYZCOV_CORPUS_ORDER] = (N + 1) * 4;
+    sz[SYZCOV_CORPUS_KEPT_IDX] = (N + 1) * 4;
+    sz[SYZCOV_CORPUS_UNION] = c.union_cap * 4;
+    sz[SYZCOV_CORPUS_SCAL] = 16 * 8;
+    sz[SYZCOV_CORPUS_PC_OF_KEY] = c.key_mode ? c.span * 4 : 0;
+    sz[SYZCOV_CORPUS_LOW_OF_KEY] = c.key_mode ? (uint64_t)c.nrange << c.rshift : 0;
+    if (c.world > 1) {
+        sz[SYZCOV_CORPUS_GLENS] = N * 4;
+        sz[SYZCOV_CORPUS_SEL] = N;
+        sz[SYZCOV_CORPUS_IOTA] = N * 4;
+        sz[SYZCOV_CORPUS_ITEMS] = (n + 1) * 4;
+        sz[SYZCOV_CORPUS_RANKS] = (n + 1) * 4;
+        sz[SYZCOV_CORPUS_FIRST_DENSE] = c.key_mode ? 0 : c.union_cap * 4;
+    }
+    c.ws_size = std::max({syzcov_dev_canon_split_ws_size(n), syzcov_dev_dict_ws_size(c.span),
+                          syzcov_dev_compact_ws_size(N), syzcov_dev_sort_ws_size(N),
+                          syzcov_dev_minimize_range_ws_size(N, c.span, c.rshift)});
+    sz[SYZCOV_CORPUS_WS] = c.ws_size;
+    // sharded: dictionary / compaction scratch apart from ws, which carries
+    // minimize's rank-ordered descriptors from pass 1 to pass 2
+    c.ws2_size = c.world > 1 ? std::max(syzcov_dev_dict_ws_size(c.span),
+                                        syzcov_dev_compact_ws_size(N))
+                             : 0;
+    sz[SYZCOV_CORPUS_WS2] = c.ws2_size;
+    size_t tot = 0;
+    for (int b = 0; b < SYZCOV_CORPUS_NBUF; b++) {
+        c.offs[b] = tot;
+        tot += align_up(sz[b], 256);
+    }
+    return (int64_t)tot;
+}
+
+// Validates cfg and derives the windows; host reads of the universe only.
+static int setup(Corpus &c, const syzcov_corpus_cfg *cfg) {
+    if (!cfg || cfg->n_max == 0 || cfg->n_max > 0x7FFFFFFF || cfg->p_max == 0 ||
+        cfg->max_seg_len == 0)
+        return SYZCOV_EINVAL;
+    c.cfg = *cfg;
+    syzcov_corpus_cfg &g = c.cfg;
+    c.n_global = g.n_global ? g.n_global : g.n_max;
+    if (c.n_global < g.n_max || c.n_global > 0x7FFFFFFF) return SYZCOV_EINVAL;
+    c.world = (int)((c.n_global + g.n_max - 1) / g.n_max);
+    if (g.canon_in_place && g.max_seg_len > 16384) return SYZCOV_EINVAL;
+    c.key_mode = g.universe != nullptr;
+    if (c.key_mode) {
+        if (g.universe_n == 0) return SYZCOV_EINVAL;
+        int rc = universe_shift(g.universe, g.universe_n, &c.kshift);
+        if (rc) {
+            set_error("the PC universe must be sorted and unique");
+            return rc;
+        }
+        const uint32_t lo = g.universe[0], hi = g.universe[g.universe_n - 1];
+        c.kbase = lo >> c.kshift;
+        c.win_lo = lo;
+        c.win_span = (uint64_t)hi - lo + 1;
+        c.pc_lo = 0;
+        c.span = (uint64_t)(hi >> c.kshift) - c.kbase + 1;
+    } else {
+        if (g.pc_span == 0 || (uint64_t)g.pc_lo + g.pc_span > (1ull << 32)) return SYZCOV_ERANGE;
+        c.win_lo = c.pc_lo = g.pc_lo;
+        c.win_span = c.span = g.pc_span;
+    }
+    const uint64_t so = c.key_mode ? (uint64_t)(0xFFFFFFFFu >> c.kshift) - c.kbase
+                                   : (uint64_t)(0xFFFFFFFFu - c.pc_lo);
+    c.sent_key = so < c.span ? (uint32_t)so : 0xFFFFFFFFu;
+    c.rshift = c.key_mode ? kRangeShiftKeys : kRangeShiftWindow;
+    if (c.key_mode && c.span > (1ull << 25)) {
+        set_error("key space of %llu keys > 2^25", (unsigned long long)c.span);
+        return SYZCOV_ERANGE;
+    }
+    c.nrange = (uint32_t)nrange_of(c.span, c.rshift);
+    if (c.nrange > 256) {
+        set_error("PC window too wide for the range engine (> 256 ranges of 2^20)");
+        return SYZCOV_ERANGE;
+    }
+    c.nwords = (c.span + 31) / 32;
+    if (g.rec_cap == 0)
+        g.rec_cap = std::max<uint64_t>(1ull << 22, std::min<uint64_t>(g.p_max, 1ull << 26));
+    c.union_cap = std::min<uint64_t>(c.span, g.p_max * (uint64_t)c.world) + 1;
+    if (g.order_by != 0 && g.order_by != 1) return SYZCOV_EINVAL;
+    return 0;
+}
+
+static int init_device(Corpus &c, hipStream_t s) {
+    const syzcov_corpus_cfg &g = c.cfg;
+    SYZ_HIP(hipMemsetAsync(c.mem, 0, c.mem_size, s));
+    SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)c.buf<int32_t>(SYZCOV_CORPUS_FIRST), INT32_MAX,
+                              c.span, s));
+    if (!c.key_mode) return 0;
+    // key tables of the universe (keys.hip), from a staged copy; the
+    // membership table is padded to whole ranges with "no universe PC"
+    uint32_t *err = (uint32_t *)c.buf<uint64_t>(SYZCOV_CORPUS_SCAL);
+    SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_LOW_OF_KEY), 0x7F,
+                           c.sizes[SYZCOV_CORPUS_LOW_OF_KEY], s));
+    uint32_t *stage = nullptr;
+    SYZ_HIP(hipMalloc(&stage, g.universe_n * 4));
+    int rc = 0;
+    if (hipMemcpyAsync(stage, g.universe, g.universe_n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        rc = SYZCOV_EHIP;
+    if (!rc)
+        rc = syzcov_dev_universe_keymap(stage, g.universe_n, c.kshift, c.kbase, c.span,
+                                        c.buf<uint32_t>(SYZCOV_CORPUS_PC_OF_KEY),
+                                        c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY), err, s);
+    uint32_t h = 0;
+    if (!rc && (hipMemcpyAsync(&h, err, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess))
+        rc = SYZCOV_EHIP;
+    hipFree(stage);
+    if (rc) return rc;
+    if (h) {
+        set_error("universe keymap failed (unsorted or colliding universe)");
+        return SYZCOV_EINVAL;
+    }
+    SYZ_HIP(hipMemsetAsync(err, 0, 8, s));
+    return 0;
+}
+
+static Corpus *get(syzcov_corpus h) { return reinterpret_cast<Corpus *>(h); }
+
+// Scalars (u64 words of SCAL): 0 err flags (u32), 1 n_ids (u32), 2 n_kept
+// (u32), 3 n_union (u32), 4 |maxCover| (u64), 5 / 6 local ranks / items
+// (u32), 7 record count (u64).
+enum { SC_ERR = 0, SC_NIDS = 1, SC_NKEPT = 2, SC_NUNION = 3, SC_MAXCOV = 4, SC_CR = 5,
+       SC_CI = 6, SC_REC = 7 };
+
+static uint64_t *scal(const Corpus &c) { return c.buf<uint64_t>(SYZCOV_CORPUS_SCAL); }
+static bool sharded(const Corpus &c) { return c.N > c.n; }
+
+// --------------------------------------------------------------- phases
+static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hipStream_t s) {
+    if (!off || !raw || n == 0 || n > c.cfg.n_max) return SYZCOV_EINVAL;
+    c.off = off;
+    c.n = n;
+    c.N = n;
+    c.dict_ready = false;
+    uint64_t *sc = scal(c);
+    SYZ_HIP(hipMemsetAsync(sc, 0, 16 * 8, s));
+    uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
+    SYZ_HIP(hipMemsetAsync(rt, 0, c.nrange * 8, s));
+    c.canon = c.cfg.canon_in_place ? raw : c.buf<uint32_t>(SYZCOV_CORPUS_CANON);
+    uint32_t *nl = c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN);
+    uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
+    void *ws = c.buf<void>(SYZCOV_CORPUS_WS);
+    if (c.key_mode)
+        return syzcov_dev_canon_split_keys(off, raw, c.canon, nl, n, c.cfg.max_seg_len, c.win_lo,
+                                           c.win_span, c.kshift, c.kbase, c.span, c.rshift, split,
+                                           rt, (uint32_t *)sc, ws, c.ws_size, s);
+    return syzcov_dev_canon_split(off, raw, c.canon, nl, n, c.cfg.max_seg_len, c.pc_lo, c.span,
+                                  c.rshift, split, rt, (uint32_t *)sc, ws, c.ws_size, s);
+}
+
+// Go's order over N lengths; also clears Minimize's inputs (queued ahead of
+// the sort, whose read-backs leave the GPU idle while the host issues).
+static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
+    if (!c.canon) return SYZCOV_EINVAL;  // no canon phase yet
+    if (!lens32 && N != c.n) return SYZCOV_EINVAL;
+    if (N < c.n || N > c.n_global) return SYZCOV_EINVAL;
+    if (N > c.n && (uint64_t)c.cfg.rank * c.cfg.n_max + c.n > N) return SYZCOV_EINVAL;
+    c.N = N;
+    SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_COVERED), 0, c.sizes[SYZCOV_CORPUS_COVERED],
+                           s));
+    SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_CAND), 0, c.n, s));
+    SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_KEPT), 0, c.sizes[SYZCOV_CORPUS_KEPT], s));
+    int64_t *lens = c.buf<int64_t>(SYZCOV_CORPUS_LENS);
+    const uint32_t *l32 = lens32 ? (const uint32_t *)lens32
+                                 : (c.cfg.order_by ? nullptr
+                                                   : c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN));
+    hipLaunchKernelGGL(corpus_lens_kernel, dim3(grid_for(N, 256, 8192)), dim3(256), 0, s, l32,
+                       c.off, (uint64_t)N, lens);
+    SYZ_LAUNCH_CHECK();
+    return syzcov_dev_sort_order(lens, N, 0, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
+                                 c.buf<void>(SYZCOV_CORPUS_WS), c.ws_size, s);
+}
+
+// Work items: (input, rank).  One GPU: every input, ranks = positions of
+// the order.  Sharded: this shard's inputs in global processing order with
+// their GLOBAL ranks, by two ordered compactions (no host sync).
+static int items_of(Corpus &c, const int32_t **items, const int32_t **ranks, hipStream_t s) {
+    if (!sharded(c)) {
+        *items = c.buf<int32_t>(SYZCOV_CORPUS_ORDER);
+        *ranks = nullptr;
+        return 0;
+    }
+    const uint32_t base = (uint32_t)(c.cfg.rank * c.cfg.n_max);
+    uint8_t *sel = c.buf<uint8_t>(SYZCOV_CORPUS_SEL);
+    int32_t *iota = c.buf<int32_t>(SYZCOV_CORPUS_IOTA);
+    int32_t *it = c.buf<int32_t>(SYZCOV_CORPUS_ITEMS), *rk = c.buf<int32_t>(SYZCOV_CORPUS_RANKS);
+    const int32_t *order = c.buf<int32_t>(SYZCOV_CORPUS_ORDER);
+    void *ws2 = c.buf<void>(SYZCOV_CORPUS_WS2);
+    hipLaunchKernelGGL(corpus_sel_kernel, dim3(grid_for(c.N, 256, 8192)), dim3(256), 0, s, order,
+                       (uint64_t)c.N, base, (uint32_t)c.n, sel, iota);
+    SYZ_LAUNCH_CHECK();
+    int rc = syzcov_dev_compact_kept(sel, iota, c.N, rk, (uint32_t *)(scal(c) + SC_CR), ws2, s);
+    if (rc) return rc;
+    rc = syzcov_dev_compact_kept(sel, order, c.N, it, (uint32_t *)(scal(c) + SC_CI), ws2, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(corpus_sub_kernel, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s, it,
+                       (uint32_t)c.n, (int32_t)base);
+    SYZ_LAUNCH_CHECK();
+    *items = it;
+    *ranks = rk;
+    return 0;
+}
+
+static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
+    if (!c.canon || !c.N) return SYZCOV_EINVAL;
+    if (do_pass2 && sharded(c)) return SYZCOV_EINVAL;  // pass 2 follows the exchange
+    const int32_t *items, *ranks;
+    int rc = items_of(c, &items, &ranks, s);
+    if (rc) return rc;
+    const uint32_t *nl = c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN);
+    const uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
+    const uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
+    if (c.key_mode)
+        return syzcov_dev_minimize_range_keys(
+            c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
+            c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY), c.buf<uint32_t>(SYZCOV_CORPUS_COVERED),
+            c.buf<int32_t>(SYZCOV_CORPUS_FIRST), c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap,
+            scal(c) + SC_REC, c.buf<uint8_t>(SYZCOV_CORPUS_CAND),
+            c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, (uint32_t *)(scal(c) + SC_ERR),
+            c.buf<void>(SYZCOV_CORPUS_WS), s);
+    return syzcov_dev_minimize_range(
+        c.off, nl, c.canon, split, items, ranks, c.n, c.pc_lo, c.span, c.rshift, rt,
+        c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.buf<int32_t>(SYZCOV_CORPUS_FIRST),
+        c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
+        c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, 0, 0, 0,
+        c.buf<void>(SYZCOV_CORPUS_WS), s);
+}
+
+// Window mode, sharded: the dictionary of the merged covered set and this
+// shard's first ranks over it (the MIN exchange moves n_ids entries).
+static int64_t ph_dense_first(Corpus &c, hipStream_t s) {
+    if (c.key_mode || !sharded(c)) return SYZCOV_EINVAL;
+    uint64_t *tab = c.buf<uint64_t>(SYZCOV_CORPUS_TAB);
+    int rc = syzcov_dev_dict_build_bits(c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.span, tab,
+                                        (uint32_t *)(scal(c) + SC_NIDS),
+                                        c.buf<void>(SYZCOV_CORPUS_WS2), s);
+    if (rc) return rc;
+    rc = syzcov_dev_first_dense(tab, c.span, c.buf<int32_t>(SYZCOV_CORPUS_FIRST),
+                                c.buf<int32_t>(SYZCOV_CORPUS_FIRST_DENSE), 1, s);
+    if (rc) return rc;
+    uint32_t nids = 0;
+    SYZ_HIP(hipMemcpyAsync(&nids, scal(c) + SC_NIDS, 4, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    c.dict_ready = true;
+    return nids;
+}
+
+// Sharded pass 2 against the exchanged first ranks: key mode reads the MIN
+// all-reduced first-cover array itself (its union = keys with a first cover),
+// window mode the MIN-merged dense table.
+static int ph_pass2(Corpus &c, hipStream_t s) {
+    if (!sharded(c)) return SYZCOV_EINVAL;
+    const int32_t *items = c.buf<int32_t>(SYZCOV_CORPUS_ITEMS);
+    const int32_t *ranks = c.buf<int32_t>(SYZCOV_CORPUS_RANKS);
+    int32_t *first = c.buf<int32_t>(SYZCOV_CORPUS_FIRST);
+    if (c.key_mode) {
+        int rc = syzcov_dev_first_to_bits(first, c.span, c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), s);
+        if (rc) return rc;
+    } else if (!c.dict_ready) {
+        return SYZCOV_EINVAL;
+    }
+    const uint32_t *nl = c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN);
+    const uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
+    const uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
+    uint32_t *cov = c.buf<uint32_t>(SYZCOV_CORPUS_COVERED);
+    uint64_t *rec = c.buf<uint64_t>(SYZCOV_CORPUS_REC);
+    uint8_t *cand = c.buf<uint8_t>(SYZCOV_CORPUS_CAND), *kept = c.buf<uint8_t>(SYZCOV_CORPUS_KEPT);
+    int rc = c.key_mode
+                 ? syzcov_dev_minimize_range_keys_pass2(
+                       c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt, cov,
+                       first, rec, c.cfg.rec_cap, scal(c) + SC_REC, cand, kept,
+                       c.buf<void>(SYZCOV_CORPUS_WS), s)
+                 : syzcov_dev_minimize_range_pass2(
+                       c.off, nl, c.canon, split, items, ranks, c.n, c.pc_lo, c.span, c.rshift, rt,
+                       cov, first, rec, c.cfg.rec_cap, scal(c) + SC_REC, cand,
+                       c.buf<uint64_t>(SYZCOV_CORPUS_TAB),
+                       c.buf<int32_t>(SYZCOV_CORPUS_FIRST_DENSE), kept,
+                       c.buf<void>(SYZCOV_CORPUS_WS), s);
+    if (rc) return rc;
+    // the other ranks' entries of the merged array too (pass 2 resets only
+    // this shard's records above the fill threshold)
+    if (c.key_mode) SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)first, INT32_MAX, c.span, s));
+    return 0;
+}
+
+// kept list in processing order, the sorted union, maxCover |= union.
+static int ph_finish(Corpus &c, hipStream_t s) {
+    if (!c.N) return SYZCOV_EINVAL;
+    uint64_t *sc = scal(c);
+    void *wsx = sharded(c) ? c.buf<void>(SYZCOV_CORPUS_WS2) : c.buf<void>(SYZCOV_CORPUS_WS);
+    uint64_t *tab = c.buf<uint64_t>(SYZCOV_CORPUS_TAB);
+    uint32_t *covered = c.buf<uint32_t>(SYZCOV_CORPUS_COVERED);
+    int rc = syzcov_dev_compact_kept(c.buf<uint8_t>(SYZCOV_CORPUS_KEPT),
+                                     c.buf<int32_t>(SYZCOV_CORPUS_ORDER), c.N,
+                                     c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX),
+                                     (uint32_t *)(sc + SC_NKEPT), wsx, s);
+    if (rc) return rc;
+    if (!c.dict_ready) {
+        rc = syzcov_dev_dict_build_bits(covered, c.span, tab, (uint32_t *)(sc + SC_NIDS), wsx, s);
+        if (rc) return rc;
+    }
+    // Union drops 0xFFFFFFFF (cover.go:97): in key mode, its key
+    uint32_t *un = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
+    rc = syzcov_dev_dict_to_list_drop(tab, c.span, c.pc_lo,
+                                      c.key_mode ? c.sent_key : 0xFFFFFFFFu, un,
+                                      (uint32_t *)(sc + SC_NUNION), s);
+    if (rc) return rc;
+    if (c.key_mode) {  // sorted keys -> sorted PCs (the key map is monotone)
+        rc = syzcov_dev_keys_to_pcs(c.buf<uint32_t>(SYZCOV_CORPUS_PC_OF_KEY), c.span, un, un,
+                                    (const uint32_t *)(sc + SC_NUNION), c.union_cap, s);
+        if (rc) return rc;
+    }
+    if (c.sent_key != 0xFFFFFFFFu) {
+        hipLaunchKernelGGL(corpus_clear_bit_kernel, dim3(1), dim3(1), 0, s, covered, c.sent_key);
+        SYZ_LAUNCH_CHECK();
+    }
+    return syzcov_dev_bitmap_op(0, c.buf<uint32_t>(SYZCOV_CORPUS_MAX_COVER), covered, c.nwords,
+                                sc + SC_MAXCOV, s);
+}
+
+static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
+    uint64_t h[16];
+    SYZ_HIP(hipMemcpyAsync(h, scal(c), sizeof h, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    const uint32_t err = (uint32_t)h[SC_ERR];
+    r->err_flags = err;
+    r->n_ids = (uint32_t)h[SC_NIDS];
+    r->n_kept = (uint32_t)h[SC_NKEPT];
+    r->n_union = (uint32_t)h[SC_NUNION];
+    r->max_cover = h[SC_MAXCOV];
+    r->records = h[SC_REC];
+    r->kept_idx = c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX);
+    r->union_pcs = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
+    if (err & SYZCOV_ERR_SEGLEN) {
+        set_error("an input is longer than max_seg_len=%zu", c.cfg.max_seg_len);
+        return SYZCOV_ETOOLONG;
+    }
+    if (err & SYZCOV_ERR_WINDOW) {
+        set_error("a PC fell outside the engine's PC window");
+        return SYZCOV_ERANGE;
+    }
+    if (err & SYZCOV_ERR_UNIVERSE) {
+        set_error("a PC is not in the registered PC universe");
+        return SYZCOV_ERANGE;
+    }
+    if (err) {
+        set_error("engine error flags %#x", err);
+        return SYZCOV_EHIP;
+    }
+    return 0;
+}
+
+// RAII: the handle's device current, the handle locked.
+class Use {
+  public:
+    explicit Use(Corpus *c) : c_(c), g_(c->mu) {
+        hipGetDevice(&prev_);
+        if (prev_ != c->dev) hipSetDevice(c->dev);
+    }
+    ~Use() {
+        if (prev_ != c_->dev) hipSetDevice(prev_);
+    }
+
+  private:
+    Corpus *c_;
+    std::lock_guard<std::mutex> g_;
+    int prev_ = 0;
+};
+
+// cover.Minimize through an engine handle on host buffers (the drop-in
+// call): stage, step, read back.
+static int64_t minimize_host(Corpus &c, const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                             int32_t *out_idx, uint32_t *union_out, size_t union_out_cap,
+                             uint64_t *n_union_out, hipStream_t s) {
+    const uint64_t base = offsets[0], P = offsets[n] - base;
+    if (P > c.cfg.p_max) return SYZCOV_EINVAL;
+    std::vector<uint64_t> hoff(n + 1);
+    for (size_t i = 0; i <= n; i++) {
+        hoff[i] = offsets[i] - base;
+        if (i && hoff[i] < hoff[i - 1]) return SYZCOV_EINVAL;
+        if (i && hoff[i] - hoff[i - 1] > c.cfg.max_seg_len) {
+            set_error("an input is longer than max_seg_len=%zu", c.cfg.max_seg_len);
+            return SYZCOV_ETOOLONG;
+        }
+    }
+    const size_t need = align_up((n + 1) * 8, 256) + (P + 1) * 4;
+    if (need > c.stage_cap) {
+        if (c.stage) {
+            SYZ_HIP(hipStreamSynchronize(s));
+            hipFree(c.stage);
+            c.stage = nullptr;
+            c.stage_cap = 0;
+        }
+        if (hipMalloc(&c.stage, need) != hipSuccess) {
+            set_error("hipMalloc(%zu) failed", need);
+            return SYZCOV_ENOMEM;
+        }
+        c.stage_cap = need;
+    }
+    uint64_t *d_off = (uint64_t *)c.stage;
+    uint32_t *d_pcs = (uint32_t *)((uint8_t *)c.stage + align_up((n + 1) * 8, 256));
+    SYZ_HIP(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (P) SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
+    int rc = ph_canon(c, d_off, d_pcs, n, s);
+    if (!rc) rc = ph_order(c, nullptr, n, s);
+    if (!rc) rc = ph_minimize(c, 1, s);
+    if (!rc) rc = ph_finish(c, s);
+    syzcov_corpus_res r{};
+    if (!rc) rc = ph_result(c, &r, s);
+    if (rc) {
+        hipStreamSynchronize(s);
+        return rc;
+    }
+    if (r.n_kept)
+        SYZ_HIP(hipMemcpyAsync(out_idx, r.kept_idx, (size_t)r.n_kept * 4, hipMemcpyDeviceToHost, s));
+    if (n_union_out) *n_union_out = r.n_union;
+    if (union_out && r.n_union) {
+        if (union_out_cap < r.n_union) {
+            hipStreamSynchronize(s);
+            set_error("union capacity %zu < %u", union_out_cap, r.n_union);
+            return SYZCOV_ERANGE;
+        }
+        SYZ_HIP(hipMemcpyAsync(union_out, r.union_pcs, (size_t)r.n_union * 4,
+                               hipMemcpyDeviceToHost, s));
+    }
+    SYZ_HIP(hipStreamSynchronize(s));
+    return r.n_kept;
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int64_t syzcov_corpus_mem_size(const syzcov_corpus_cfg *cfg) {
+    Corpus c;
+    int rc = setup(c, cfg);
+    if (rc) return rc;
+    return plan(c);
+}
+
+int syzcov_corpus_create(const syzcov_corpus_cfg *cfg, void *mem, size_t mem_size,
+                         syzcov_corpus *out) {
+    if (!out) return SYZCOV_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device (libsyzcov has no CPU path)");
+        return SYZCOV_ENODEV;
+    }
+    Corpus *c = new (std::nothrow) Corpus();
+    if (!c) return SYZCOV_ENOMEM;
+    int rc = setup(*c, cfg);
+    const int64_t need = rc ? rc : plan(*c);
+    if (need < 0) {
+        delete c;
+        return (int)need;
+    }
+    hipGetDevice(&c->dev);
+    c->cfg.universe = nullptr;  // host memory is not retained past the call
+    if (mem) {
+        if (mem_size < (size_t)need || ((uintptr_t)mem & 255)) {
+            delete c;
+            set_error("caller memory: %zu bytes at %p, need %lld 256-byte aligned", mem_size, mem,
+                      (long long)need);
+            return SYZCOV_EINVAL;
+        }
+        c->mem = (uint8_t *)mem;
+    } else {
+        if (hipMalloc(&c->mem, (size_t)need) != hipSuccess) {
+            delete c;
+            set_error("hipMalloc(%lld) failed", (long long)need);
+            return SYZCOV_ENOMEM;
+        }
+        c->own_mem = true;
+    }
+    c->mem_size = (size_t)need;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        rc = SYZCOV_EHIP;
+    } else {
+        c->cfg.universe = cfg->universe;
+        rc = init_device(*c, s);
+        c->cfg.universe = nullptr;
+        if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = SYZCOV_EHIP;
+        hipStreamDestroy(s);
+    }
+    if (rc) {
+        if (c->own_mem) hipFree(c->mem);
+        delete c;
+        return rc;
+    }
+    *out = reinterpret_cast<syzcov_corpus>(c);
+    return 0;
+}
+
+int syzcov_corpus_destroy(syzcov_corpus h) {
+    Corpus *c = get(h);
+    if (!c) return 0;
+    {
+        Use u(c);
+        hipDeviceSynchronize();
+        if (c->own_mem) hipFree(c->mem);
+        if (c->stage) hipFree(c->stage);
+    }
+    delete c;
+    return 0;
+}
+
+int syzcov_corpus_info(syzcov_corpus h, syzcov_corpus_info_t *out) {
+    Corpus *c = get(h);
+    if (!c || !out) return SYZCOV_EINVAL;
+    out->key_mode = c->key_mode;
+    out->kshift = c->kshift;
+    out->kbase = c->kbase;
+    out->pc_lo = c->pc_lo;
+    out->span = c->span;
+    out->win_lo = c->win_lo;
+    out->win_span = c->win_span;
+    out->nrange = c->nrange;
+    out->nwords = c->nwords;
+    out->n_global = c->n_global;
+    out->union_cap = c->union_cap;
+    out->rec_cap = c->cfg.rec_cap;
+    out->sent_key = c->sent_key;
+    out->mem = c->mem;
+    out->mem_size = c->mem_size;
+    return 0;
+}
+
+int syzcov_corpus_buffer(syzcov_corpus h, int which, uint64_t *offset, uint64_t *bytes) {
+    Corpus *c = get(h);
+    if (!c || which < 0 || which >= SYZCOV_CORPUS_NBUF) return SYZCOV_EINVAL;
+    if (offset) *offset = c->offs[which];
+    if (bytes) *bytes = c->sizes[which];
+    return 0;
+}
+
+int syzcov_corpus_canon(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
+                        void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_canon(*c, off, raw, n, (hipStream_t)stream);
+}
+
+int syzcov_corpus_order(syzcov_corpus h, const int32_t *lens, size_t N, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_order(*c, lens, N, (hipStream_t)stream);
+}
+
+int syzcov_corpus_minimize(syzcov_corpus h, int do_pass2, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_minimize(*c, do_pass2, (hipStream_t)stream);
+}
+
+int64_t syzcov_corpus_dense_first(syzcov_corpus h, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_dense_first(*c, (hipStream_t)stream);
+}
+
+int syzcov_corpus_pass2(syzcov_corpus h, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_pass2(*c, (hipStream_t)stream);
+}
+
+int syzcov_corpus_finish(syzcov_corpus h, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_finish(*c, (hipStream_t)stream);
+}
+
+int syzcov_corpus_step(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
+                       void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ph_canon(*c, off, raw, n, s);
+    if (!rc) rc = ph_order(*c, nullptr, n, s);
+    if (!rc) rc = ph_minimize(*c, 1, s);
+    if (!rc) rc = ph_finish(*c, s);
+    return rc;
+}
+
+int syzcov_corpus_result(syzcov_corpus h, syzcov_corpus_res *res, void *stream) {
+    Corpus *c = get(h);
+    if (!c || !res) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_result(*c, res, (hipStream_t)stream);
+}
+
+int64_t syzcov_corpus_minimize_host(syzcov_corpus h, const uint64_t *offsets, const uint32_t *pcs,
+                                    size_t n, int32_t *out_idx, uint32_t *union_out,
+                                    size_t union_cap, uint64_t *n_union) {
+    Corpus *c = get(h);
+    if (!c || !offsets || !out_idx || n == 0 || n > c->cfg.n_max) return SYZCOV_EINVAL;
+    if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    Use u(c);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
+    const int64_t rc = minimize_host(*c, offsets, pcs, n, out_idx, union_out, union_cap, n_union, s);
+    hipStreamDestroy(s);
+    return rc;
+}
+
+}  // extern "C"
+
+// cover.Minimize (syzcov_minimize, api.cc) on large corpora: a transient
+// window-mode engine over the corpus' own PC extent.  Returns 1 with the
+// count in *out_n, 0 if the corpus does not suit the engine (the caller takes
+// the dictionary path), < 0 on error.
+namespace syz {
+int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n, int32_t *out_idx,
+                        int64_t *out_n) {
+    const uint64_t base = offsets[0], P = offsets[n] - base;
+    if (P == 0) return 0;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    size_t max_len = 1;
+    for (size_t i = 0; i < n; i++) {
+        if (offsets[i + 1] < offsets[i]) return SYZCOV_EINVAL;
+        max_len = std::max<size_t>(max_len, offsets[i + 1] - offsets[i]);
+    }
+    for (uint64_t k = base; k < base + P; k++) {
+        lo = std::min(lo, pcs[k]);
+        hi = std::max(hi, pcs[k]);
+    }
+    const uint64_t span = (uint64_t)hi - lo + 1;
+    if (nrange_of(span, kRangeShiftWindow) > 256) return 0;
+    syzcov_corpus_cfg cfg{};
+    cfg.n_max = n;
+    cfg.p_max = P;
+    cfg.max_seg_len = max_len;
+    cfg.pc_lo = lo;
+    cfg.pc_span = span;
+    cfg.order_by = 1;  // Go sorts by len(cov), duplicates included
+    cfg.canon_in_place = max_len <= 16384;  // the staged copy is the caller's own
+    syzcov_corpus h = 0;
+    int rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
+    if (rc) return rc;
+    const int64_t k = syzcov_corpus_minimize_host(h, offsets, pcs, n, out_idx, nullptr, 0, nullptr);
+    syzcov_corpus_destroy(h);
+    if (k < 0) return (int)k;
+    *out_n = k;
+    return 1;
+}
+}  // namespace syz

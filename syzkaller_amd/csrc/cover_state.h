@@ -59,6 +59,9 @@ struct CoverState {
     uint32_t *grp = nullptr;
     bool dirty = false;          // maxCover touched: the universe can no longer change
     hipStream_t s = nullptr;
+    // device-tier batches run on the caller's stream: ordered after the
+    // handle's stream (ev_state) and the handle's stream after them (ev_dev)
+    hipEvent_t ev_state = nullptr, ev_dev = nullptr;
     std::mutex mu;  // the reference's coverMu
     // grow-only scratch
     void *scratch = nullptr;

@@ -15,14 +15,17 @@
 // kernel's return addresses are >= 5 bytes apart, so kshift >= 2 there.
 //
 // EXACT ON ANY INPUT.  Two PCs can share a key only if one of them is not in
-// the universe, so every place that forms a key also checks membership:
+// the universe, so a key never stands for a PC by itself: canonical lists hold
+// KEY WORDS, key | (pc & lowmask) << SYZ_KEY_BITS (common.h), and whatever
+// indexes by key also checks membership,
 //     low_of_key[key] == (pc & lowmask),  lowmask = 2^kshift - 1
-// (one byte per key: the universe PC's low kshift bits, 0xFF for a key with no
-// universe PC; kshift <= 7 keeps 0xFF out of reach).  A PC that fails it sets
-// SYZCOV_ERR_UNIVERSE and the step / batch raises instead of aliasing it with
-// its neighbour: canon_wave.hip carries the low bits through the key sort as
-// payload and checks every canonical PC; the fuzzer state's pc_index checks
-// every PC it indexes (cover_state.h).
+// (one byte per key: the universe PC's low kshift bits, 0x7F for a key with no
+// universe PC; kshift <= 6 keeps 0x7F out of reach and bit 7 free for
+// Minimize's covered flag).  A PC that fails it sets SYZCOV_ERR_UNIVERSE and
+// the step / batch raises instead of aliasing it with its neighbour:
+// Minimize pass 1 checks every canonical word against the table staged in LDS
+// next to its covered bits (minimize_range.hip); the fuzzer state's pc_index
+// checks every PC it indexes (cover_state.h).
 #include "common.h"
 
 namespace syz {
@@ -54,6 +57,17 @@ __global__ void keys_to_pcs_kernel(const uint32_t *__restrict__ pc_of_key, uint6
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t k = keys[i];
         out[i] = k < nkeys ? pc_of_key[k] : 0xFFFFFFFFu;
+    }
+}
+
+// out[i] = the PC of key word words[i] (common.h): exact for any word, no
+// table (the canonical lists of a key-mode step back as PCs).
+__global__ void words_to_pcs_kernel(const uint32_t *words, uint64_t n, uint32_t kshift,
+                                    uint32_t kbase, uint32_t *out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t w = words[i];
+        out[i] = (((w & SYZ_KEY_MASK) + kbase) << kshift) | (w >> SYZ_KEY_BITS);
     }
 }
 
@@ -92,9 +106,9 @@ extern "C" int syzcov_dev_universe_keymap(const uint32_t *univ, size_t n, uint32
         return SYZCOV_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     // keys without a universe PC: pc_of_key 0 (never read for a valid key),
-    // low_of_key 0xFF (no PC's low kshift <= 7 bits equal it)
+    // low_of_key 0x7F (no PC's low kshift <= 6 bits equal it)
     if (pc_of_key) SYZ_HIP(hipMemsetAsync(pc_of_key, 0, nkeys * 4, s));
-    if (low_of_key) SYZ_HIP(hipMemsetAsync(low_of_key, 0xFF, nkeys, s));
+    if (low_of_key) SYZ_HIP(hipMemsetAsync(low_of_key, 0x7F, nkeys, s));
     if (n == 0) return 0;
     hipLaunchKernelGGL(keymap_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, univ,
                        (uint64_t)n, kshift, kbase, nkeys, pc_of_key, low_of_key, err_flag);
@@ -110,6 +124,16 @@ extern "C" int syzcov_dev_keys_to_pcs(const uint32_t *pc_of_key, uint64_t nkeys,
     hipLaunchKernelGGL(keys_to_pcs_kernel, dim3(grid_for(n_max, 256, 4096)), dim3(256), 0,
                        (hipStream_t)stream, pc_of_key, nkeys, keys, out, n_dev,
                        (uint64_t)n_max);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_words_to_pcs(const uint32_t *words, size_t n, uint32_t kshift,
+                                       uint32_t kbase, uint32_t *out, void *stream) {
+    if (n == 0) return 0;
+    if (!words || !out || kshift > SYZCOV_KSHIFT_MAX) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(words_to_pcs_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0,
+                       (hipStream_t)stream, words, (uint64_t)n, kshift, kbase, out);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -93,6 +93,11 @@ struct Args {
     uint64_t *stamp;           // [G][4] per-workgroup timing stamps (debug builds)
     uint32_t *pctr;            // dynamic pieces: this chunk's next-piece counter
     uint32_t npieces;          // dynamic pieces: pieces of this chunk (G)
+    // key mode: pcs are key words (common.h); every word is checked against the
+    // universe's membership table (keys.hip) staged with the covered bits
+    uint32_t keymask;          // SYZ_KEY_MASK in key mode, ~0 otherwise
+    const uint8_t *low_of_key; // [nrange << rshift] bytes, 0x7F past the keys
+    uint32_t *err;             // SYZCOV_ERR_UNIVERSE
 };
 
 #ifdef SYZ_MR_DEBUG
@@ -482,7 +487,14 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
 // DYN: a grid of one workgroup per CU takes pieces from a counter in
 // range-major order (a piece of the same range keeps the LDS bitmap), so the
 // chunk has no tail of late, unevenly sized workgroups.
-template <int UG, bool TEST = true, bool DYN = false>
+// KEYM (key mode): LDS holds one byte per key of the range, the universe
+// PC's low bits (0x7F: no universe PC) | covered << 7, so the per-PC work is
+// still one LDS read: covered = byte >> 7, and the word's low bits must equal
+// byte & 0x7F (membership, keys.hip); a word that fails sets
+// SYZCOV_ERR_UNIVERSE.  Ranges are 2^17 keys (128 KB of bytes).
+// The next batch's item descriptors are loaded while the current batch
+// streams (short sub-runs at 32 ranges made their round trip per batch show).
+template <int UG, bool TEST = true, bool DYN = false, bool KEYM = false>
 __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t a, uint32_t b,
                                                                uint32_t P, int load_cov) {
     extern __shared__ uint32_t s_cov[];
@@ -501,7 +513,9 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
     unsigned long long *const rrec = A.rec + region * A.cap_k;
     const uint32_t nwords = (1u << A.rshift) >> 5;
+    const uint8_t *const s_cov8 = reinterpret_cast<const uint8_t *>(s_cov);
     uint32_t cur_rho = 0xFFFFFFFFu;
+    uint32_t nonmem = 0;  // lanes that saw a word outside the universe (KEYM)
     for (;;) {
     uint32_t g = blockIdx.x;
     if (DYN) {
@@ -519,13 +533,34 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         return;
     }
     if (rho != cur_rho) {
-        const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
-        if (load_cov) {
-            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
+        if (KEYM) {  // table bytes | covered << 7, 16 keys per uint4
+            const uint32_t nq = (1u << A.rshift) >> 4;
+            const uint4 *t4 = reinterpret_cast<const uint4 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
+            const uint32_t *cw = A.covered + (uint64_t)rho * nwords;
+            for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
+                uint4 t = t4[q];
+                if (load_cov) {
+                    const uint32_t cb = (cw[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+                    auto spread = [](uint32_t x) {  // bit i -> bit 8i + 7
+                        return ((x & 1u) << 7) | ((x & 2u) << 14) | ((x & 4u) << 21) |
+                               ((x & 8u) << 28);
+                    };
+                    t.x |= spread(cb);
+                    t.y |= spread(cb >> 4);
+                    t.z |= spread(cb >> 8);
+                    t.w |= spread(cb >> 12);
+                }
+                s4[q] = t;
+            }
         } else {
-            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
-                s4[q] = make_uint4(0, 0, 0, 0);
+            const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
+            if (load_cov) {
+                for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
+            } else {
+                for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
+                    s4[q] = make_uint4(0, 0, 0, 0);
+            }
         }
         cur_rho = rho;
         __syncthreads();
@@ -536,28 +571,43 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     const uint32_t l = __lane_id();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t rbase = rho << A.rshift;
-    const uint32_t bmask = nwords * 32 - 1;
+    const uint32_t bmask = (1u << A.rshift) - 1u;
     const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
     const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+    // item descriptors of batch ib (lane l: item ib + l), loaded one batch ahead
+    uint32_t d_s0 = 0, d_s1 = 0;
+    uint64_t d_base = 0;
+    int32_t d_rk = 0;
+    auto load_desc = [&](uint32_t ib_) {
+        const uint32_t item = ib_ + l;
+        d_s0 = d_s1 = 0;
+        d_base = 0;
+        d_rk = 0;
+        if (item < w1) {
+            d_rk = A.ranks ? A.ranks[item] : (int32_t)item;
+            d_s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            d_s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            d_base = A.base_r[item];
+        }
+    };
+    if (w0 < w1) load_desc(w0);
     for (uint32_t ib = w0; ib < w1; ib += 64) {
         const uint32_t item = ib + l;
         uint32_t m = 0, nch = 0, he = 0;
         uint64_t a0 = 0;
-        int32_t rk = 0;
+        const int32_t rk = d_rk;
         if (item < w1) {
-            rk = A.ranks ? A.ranks[item] : (int32_t)item;
-            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
-            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
-            const uint64_t st = A.base_r[item] + s0;
-            m = s1 - s0;
+            const uint64_t st = d_base + d_s0;
+            m = d_s1 - d_s0;
 #ifdef SYZ_MR_DEBUG
-            if (s1 < s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
+            if (d_s1 < d_s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
 #endif
             a0 = st & ~3ull;
             const uint32_t head = (uint32_t)(st - a0);
             he = ((head + m) << 2) | head;
             nch = m ? (head + m + 3) >> 2 : 0u;
         }
+        if (ib + 64 < w1) load_desc(ib + 64);
         const uint32_t incl = wave_incl_scan(nch);
         const uint32_t ex_l = incl - nch;  // lane j: item j's first chunk
         const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
@@ -617,26 +667,32 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                 const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    bit[u * 4 + k] = (vv[k] - A.pc_lo - rbase) & bmask;
-                    if (TEST) wv[u * 4 + k] = s_cov[bit[u * 4 + k] >> 5];
+                    bit[u * 4 + k] = ((vv[k] & A.keymask) - A.pc_lo - rbase) & bmask;
+                    if (TEST) wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
+                                                   : s_cov[bit[u * 4 + k] >> 5];
                 }
             }
 #pragma unroll
             for (int u = 0; u < UG; u++) {
                 const uint32_t head = hv[u] & 3u, end = hv[u] >> 2;
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const uint32_t idx = co[u] * 4 + k;
                     const uint32_t valid =
                         (uint32_t)(cj[u] < 64) & (uint32_t)(idx >= head) & (uint32_t)(idx < end);
 #ifdef SYZ_MR_DEBUG
-                    {
-                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                        if (valid) MR_CHK(A, 8, vv[k] - A.pc_lo - rbase, nwords * 32);
-                    }
+                    if (valid) MR_CHK(A, 8, bit[u * 4 + k], nwords * 32);
 #endif
-                    // TEST = false: tuning probe, the stream alone (not exact)
-                    const uint32_t unc = TEST ? ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u : 0u;
+                    uint32_t unc;
+                    if (KEYM) {
+                        const uint32_t t = wv[u * 4 + k];
+                        unc = TEST ? (~t >> 7) & 1u : 0u;
+                        nonmem |= valid & (uint32_t)((t & 0x7Fu) != (vv[k] >> SYZ_KEY_BITS));
+                    } else {
+                        // TEST = false: tuning probe, the stream alone (not exact)
+                        unc = TEST ? ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u : 0u;
+                    }
                     um |= (valid & unc) << (u * 4 + k);
                 }
             }
@@ -657,7 +713,8 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
 #pragma unroll
                         for (int k = 0; k < 4; k++)
                             if ((um >> (u * 4 + k)) & 1u) {
-                                const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
+                                const uint32_t wo =
+                                    MR_CHK(A, 4, (vv[k] & A.keymask) - A.pc_lo, A.dbg_span);
                                 if (slot < A.cap_k)
                                     rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
                                 else  // no room: its min cannot wait
@@ -694,6 +751,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     if (!DYN) break;
     __syncthreads();  // every wave is done before the LDS bitmap is replaced
     }
+    if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
 }
 
 // Region loops: block b serves region b % NCTR (the grid is a multiple of
@@ -793,7 +851,7 @@ __global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_
         const uint32_t n = A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + j];
         bool hit = false;
         for (uint32_t q = threadIdx.x; q < n; q += blockDim.x)
-            hit |= first_of(first_w, tab, first_d, A.pcs[o + q] - A.pc_lo) == rank;
+            hit |= first_of(first_w, tab, first_d, (A.pcs[o + q] & A.keymask) - A.pc_lo) == rank;
         if (__syncthreads_or(hit) && threadIdx.x == 0) kept[rank] = 1;
     }
 }
@@ -909,6 +967,9 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.stamp = nullptr;
     A.pctr = nullptr;
     A.npieces = 0;
+    A.keymask = 0xFFFFFFFFu;
+    A.low_of_key = nullptr;
+    A.err = nullptr;
     A.dbg_npcs = A.dbg_nseg = ~0ull;
     A.dbg_span = pc_span;
 #ifdef SYZ_MR_DEBUG
@@ -951,12 +1012,13 @@ static int mr_pass2(const mr::Args &A, uint64_t pc_span, const uint64_t *tab,
     return 0;
 }
 
-extern "C" int syzcov_dev_minimize_range(
+static int minimize_range_impl(
     const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
     const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
     uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
     uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
-    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream) {
+    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, const uint8_t *low_of_key,
+    uint32_t *err_flag, void *ws, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (n_items == 0) {
         if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
@@ -967,6 +1029,14 @@ extern "C" int syzcov_dev_minimize_range(
     int rc = mr_args(A, off, len, pcs, split, order, ranks, n_items, pc_lo, pc_span, range_shift,
                      range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
     if (rc) return rc;
+    const bool keym = low_of_key != nullptr;
+    if (keym) {  // key words over <= 2^25 keys, 2^rshift table bytes in LDS
+        if (!err_flag || pc_lo != 0 || range_shift > 17 || pc_span > (1ull << 25))
+            return SYZCOV_EINVAL;
+        A.keymask = SYZ_KEY_MASK;
+        A.low_of_key = low_of_key;
+        A.err = err_flag;
+    }
     const uint64_t nrange = A.nrange;
     SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters and done marks
 #ifdef SYZ_MR_DEBUG
@@ -986,7 +1056,7 @@ extern "C" int syzcov_dev_minimize_range(
         if (e1 != hipSuccess) return SYZCOV_EHIP;
     }
 #endif
-    const size_t lds = ((size_t)1 << range_shift) / 8;
+    const size_t lds = ((size_t)1 << range_shift) / (keym ? 1 : 8);
     // SYZCOV_MR_CFG="variant,pmode" (tuning): variant 0 = lane groups with the
     // first-cover atomics in the streaming loop (round 1), 1 = lane groups with
     // deferred first covers, 2 = the same with whole-wave sub-runs above 512
@@ -995,15 +1065,17 @@ extern "C" int syzcov_dev_minimize_range(
     // k >= 3 = P = kR.  C2 key mode, minimize ms (tools/gpu_mrvar.sh): lane
     // groups + whole wave 3.07 (deferred 3.00), stream 2.75 at P = 2R, 2.35 at
     // 8R, 2.26-2.30 at 12R..32R, dynamic pieces 2.13-2.15 at 8R..32R.
-    int variant = nrange <= 16 ? 4 : 1, pmode = nrange <= 16 ? 16 : 0;
+    int variant = (nrange <= 16 || keym) ? 4 : 1, pmode = (nrange <= 16 || keym) ? 16 : 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    constexpr int NVAR = 5;
+    constexpr int NVAR = 6;
     const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>,
                           mr::pass1_kernel<0x40000000, true, false, 4, 4, true>,
                           mr::pass1_kernel<512, true, false, 4, 4, true>,
-                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<4, true, true>};
-    const int vi = variant >= 0 && variant < NVAR ? variant : 0;
+                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<4, true, true>,
+                          mr::pass1_stream_kernel<4, true, true, true>};
+    int vi = variant >= 0 && variant < NVAR - 1 ? variant : 0;
+    if (keym) vi = 5;  // the only pass 1 that reads key words
     const K k1 = kern[vi];
     const bool defer = vi >= 1;
     static std::atomic<uint32_t> attr_set[NVAR];
@@ -1039,7 +1111,7 @@ extern "C" int syzcov_dev_minimize_range(
         else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // more pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         unsigned grid = (unsigned)G;
-        if (vi == 4) {  // dynamic pieces: one workgroup per CU draws them
+        if (vi >= 4) {  // dynamic pieces: one workgroup per CU draws them
             if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
             A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
                                   (size_t)nchunk * 256);
@@ -1160,6 +1232,30 @@ extern "C" int syzcov_dev_minimize_range(
     return rc;
 }
 
+extern "C" int syzcov_dev_minimize_range(
+    const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
+    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
+    size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, void *ws, void *stream) {
+    return minimize_range_impl(off, len, pcs, split, order, ranks, n_items, pc_lo, pc_span,
+                               range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt,
+                               cand, kept, do_pass2, first_chunk, growth, pcs_per_wg_hint, nullptr,
+                               nullptr, ws, stream);
+}
+
+extern "C" int syzcov_dev_minimize_range_keys(
+    const uint64_t *off, const uint32_t *len, const uint32_t *words, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint64_t nkeys,
+    uint32_t range_shift, const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered,
+    int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand,
+    uint8_t *kept, int do_pass2, uint32_t *err_flag, void *ws, void *stream) {
+    if (!low_of_key) return SYZCOV_EINVAL;
+    return minimize_range_impl(off, len, words, split, order, ranks, n_items, 0, nkeys, range_shift,
+                               range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, kept,
+                               do_pass2, 0, 0, 0, low_of_key, err_flag, ws, stream);
+}
+
 extern "C" int syzcov_dev_minimize_range_pass2(
     const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,
     const int32_t *order, const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span,
@@ -1173,6 +1269,22 @@ extern "C" int syzcov_dev_minimize_range_pass2(
                      range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
     if (rc) return rc;
     return mr_pass2(A, pc_span, tab, first_dense, kept, (hipStream_t)stream);
+}
+
+extern "C" int syzcov_dev_minimize_range_keys_pass2(
+    const uint64_t *off, const uint32_t *len, const uint32_t *words, const uint32_t *split,
+    const int32_t *order, const int32_t *ranks, size_t n_items, uint64_t nkeys,
+    uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, void *ws,
+    void *stream) {
+    if (n_items == 0) return 0;
+    if (!kept) return SYZCOV_EINVAL;
+    mr::Args A;
+    int rc = mr_args(A, off, len, words, split, order, ranks, n_items, 0, nkeys, range_shift,
+                     range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
+    if (rc) return rc;
+    A.keymask = SYZ_KEY_MASK;  // the overflow fallback reads the words
+    return mr_pass2(A, nkeys, nullptr, nullptr, kept, (hipStream_t)stream);
 }
 
 extern "C" int syzcov_dev_first_dense(const uint64_t *tab, uint64_t pc_span, int32_t *first_w,

@@ -936,6 +936,8 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     if (st->low_of_key) hipFree(st->low_of_key);
     if (st->grp) hipFree(st->grp);
     if (st->scratch) hipFree(st->scratch);
+    if (st->ev_state) hipEventDestroy(st->ev_state);
+    if (st->ev_dev) hipEventDestroy(st->ev_dev);
     hipStreamDestroy(st->s);
     delete st;
     return 0;
@@ -1065,7 +1067,7 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
             break;
         }
         if (hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
-        // (the keymap zero-fills pc_of_key and 0xFF-fills low_of_key first)
+        // (the keymap zero-fills pc_of_key and 0x7F-fills low_of_key first)
         if ((rc = syzcov_dev_universe_keymap(lst, hn, ks, kbase, nkeys, st->pc_of_key,
                                              st->low_of_key, d_n, st->s)))
             break;
@@ -1336,10 +1338,29 @@ extern "C" int syzcov_state_newcov_dev(syzcov_cover_state h, const int32_t *call
     if (ws_size < syzcov_state_newcov_ws_size(nrec, npc)) return SYZCOV_EINVAL;
     if (nrec == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
+    // the handle's lock (the reference's coverMu) for the launch: the batch
+    // uses the handle's grouping scratch and maxCover.  The caller's stream
+    // waits for the handle's earlier work, and the handle's stream (the host
+    // tier: state_add, triage, ...) for this batch.
+    std::lock_guard<std::mutex> g(st->mu);
+    hipSetDevice(st->dev);
+    if (!st->ev_state) {
+        SYZ_HIP(hipEventCreateWithFlags(&st->ev_state, hipEventDisableTiming));
+        SYZ_HIP(hipEventCreateWithFlags(&st->ev_dev, hipEventDisableTiming));
+    }
+    if (s != st->s) {
+        SYZ_HIP(hipEventRecord(st->ev_state, st->s));
+        SYZ_HIP(hipStreamWaitEvent(s, st->ev_state, 0));
+    }
     st->dirty = true;
     uint32_t *dstats = nullptr;
-    return newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws, &dstats, stats,
-                         s);
+    const int rc = newcov_launch(st, callid, rec_off, pcs, nrec, npc, is_new, (uint8_t *)ws,
+                                 &dstats, stats, s);
+    if (s != st->s) {
+        SYZ_HIP(hipEventRecord(st->ev_dev, s));
+        SYZ_HIP(hipStreamWaitEvent(st->s, st->ev_dev, 0));
+    }
+    return rc;
 }
 
 // The host-buffer batch of execute() (add_input false) or addInput

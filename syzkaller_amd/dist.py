@@ -6,20 +6,22 @@ The only exchanges are the reductions the first-cover formulation needs
 (SURVEY §8e):
 
     canonical lens all-gather              -> identical Go sort.Sort order
-    covered bitmap all-gather + OR          -> the corpus union = identical dictionary
-    first[]        int32 MIN all-reduce    -> global first-cover rank per dense PC id
+    first[]        int32 MIN all-reduce    -> global first-cover rank per key
+                                              (key mode: the union = keys with one)
+    covered bitmap all-gather + OR          -> window mode: the union = identical
+                                              dictionary, first[] MIN over its ids
     kept flags     uint8 MAX all-reduce    -> identical kept list on every rank
 
 The collective glue below is device-agnostic (it runs under gloo on CPU
 tensors in tests/test_dist_gloo.py); the per-shard compute is libsyzcov's
-HIP kernels via engine.CorpusEngine.
+corpus handle (corpus.hip) via engine.CorpusEngine.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from .engine import INT32_MAX, CorpusEngine, _p, _stream
+from .engine import CorpusEngine, _p, _stream
 from ._lib import check
 
 
@@ -102,60 +104,29 @@ def local_items(order: torch.Tensor, rank: int, n_local: int):
 # ---------------------------------------------------------------- engine
 class ShardedEngine(CorpusEngine):
     """Rank `rank` of `world`: n local inputs of a global corpus of n*world
-    (global input i lives on rank i // n)."""
+    (global input i lives on rank i // n).  The per-shard compute is the
+    library's corpus handle (corpus.hip); the collectives run between its
+    phase calls, on the buffers of its layout (include/syzcov.h)."""
+
+    # "exchange": the MIN merge of first ranks (key mode: the first-cover array
+    # itself; window mode: over the dictionary of the OR-merged covered sets),
+    # pass 2 and the MAX merge of kept flags
+    PHASES = ("canon", "order", "minimize", "exchange", "finish")
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 rank: int, world: int, device="cuda", sort_variant: int = 0, universe=None):
+                 rank: int, world: int, device="cuda", universe=None):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
-                         n_global=n * world, sort_variant=sort_variant, universe=universe)
+                         n_global=n * world, rank=rank, universe=universe)
         self.rank, self.world, self.n_local = rank, world, n
-        self.glens = torch.empty(n * world, dtype=torch.int32, device=self.dev)
-        # the merged union can be larger than this shard's PC count
-        gcap = min(pc_span, p_max * world) + 1
-        self.union = torch.empty(gcap, dtype=torch.int32, device=self.dev)
-        # compact first-cover exchange: one int32 per PC of the merged union
-        self.first_dense = torch.empty(gcap, dtype=torch.int32, device=self.dev)
-        # dictionary/compaction scratch apart from ws, which carries minimize's
-        # rank-ordered descriptors from pass 1 to pass 2
-        self.ws2 = torch.empty(max(self.L.syzcov_dev_dict_ws_size(pc_span),
-                                   self.L.syzcov_dev_compact_ws_size(n * world)),
-                               dtype=torch.uint8, device=self.dev)
-        # local work items: global ranks of this shard's inputs and the inputs
-        # themselves, by two ordered compactions (exactly n of them: the order
-        # is a permutation of the N global inputs)
-        self.iota = torch.arange(n * world, dtype=torch.int32, device=self.dev)
-        self.sel = torch.empty(n * world, dtype=torch.uint8, device=self.dev)
-        self.ranks_l = torch.empty(n + 1, dtype=torch.int32, device=self.dev)
-        self.items_l = torch.empty(n + 1, dtype=torch.int32, device=self.dev)
-        self.cnt_l = torch.zeros(2, dtype=torch.int32, device=self.dev)
-
-    # "exchange": the covered OR, the dictionary, the first-rank MIN merge,
-    # pass 2 and the kept merge (the only phase with collectives besides order)
-    PHASES = ("canon", "order", "minimize", "exchange", "compact", "union", "merge")
-
-    def _local_items(self, N: int):
-        """(local input index, global rank) of this shard's items in global
-        processing order, on the device with no host sync."""
-        n, base, s = self.n_local, self.rank * self.n_local, _stream()
-        order = self.order[:N]
-        torch.logical_and(order >= base, order < base + n, out=self.sel.view(torch.bool))
-        check(self.L.syzcov_dev_compact_kept(_p(self.sel), _p(self.iota), N, _p(self.ranks_l),
-                                             _p(self.cnt_l[0:1]), _p(self.ws2), s),
-              "dev_compact_kept")
-        check(self.L.syzcov_dev_compact_kept(_p(self.sel), _p(order), N, _p(self.items_l),
-                                             _p(self.cnt_l[1:2]), _p(self.ws2), s),
-              "dev_compact_kept")
-        self.items_l[:n].sub_(base)
-        return self.items_l[:n], self.ranks_l[:n]
 
     def _or_into(self, dst, src):
         check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
               "dev_bitmap_op")
 
     def step(self, off, raw, n, sync: bool = True, ev=None):
-        """One rank's step.  Exchanges: canonical lengths (all-gather), covered
-        bitmaps (all-gather + OR), first ranks over the merged dictionary (int32
-        MIN), kept flags by global rank (uint8 MAX)."""
+        """One rank's step.  Exchanges: canonical lengths (all-gather), first
+        ranks (int32 MIN; window mode after an all-gather + OR of the covered
+        bitmaps and over their dictionary), kept flags by global rank (u8 MAX)."""
         k = [0]
 
         def mark_ev():
@@ -164,48 +135,26 @@ class ShardedEngine(CorpusEngine):
             k[0] += 1
         assert n == self.n_local
         N = n * self.world
-        L, s = self.L, _stream()
+        L, h, s = self.L, self.h, _stream()
         mark_ev()
         self.canonicalize(off, raw, n)
         mark_ev()
-        self.glens = gather_lens(self.new_len[:n], self.world)   # RCCL all-gather
-        self.sort_order(self.glens, N)                          # identical on every rank
+        _all_gather(self.glens[:N], self.new_len[:n].contiguous())  # RCCL all-gather
+        self.sort_order(self.glens, N)                              # identical on every rank
         mark_ev()
-        items, ranks = self._local_items(N)
-        m = n
-        self.minimize(off, items, ranks, m, do_pass2=False)
+        self.minimize(do_pass2=False)
         mark_ev()
         if self.key_mode:
             # dense key space: the first-cover array itself is the exchange
             # (nkeys int32, 16 MB at 2^22 keys; no dictionary, no host sync)
-            merge_first(self.first[:self.span])                  # RCCL int32 MIN
-            check(L.syzcov_dev_first_to_bits(_p(self.first), self.span, _p(self.covered), s),
-                  "dev_first_to_bits")                          # union = keys with a first cover
-            self.minimize_pass2(off, items, ranks, m)            # kept against the global first
-            self.first[:self.span].fill_(INT32_MAX)              # other ranks' entries too
-            merge_kept(self.kept[:N])                            # RCCL uint8 MAX
-            self.build_dict(self.ws2)
-            mark_ev()
-            self.compact(N, self.ws2)
-            mark_ev()
-            self.union_list()
-            mark_ev()
-            self.merge_max_cover()
-            mark_ev()
-            return self.result() if sync else None
-        merge_covered(self.covered[:self.nwords], self.world, self._or_into)
-        self.build_dict(self.ws2)
-        n_ids = int(self.scal[1].item()) & 0xFFFFFFFF
-        check(L.syzcov_dev_first_dense(_p(self.tab), self.span, _p(self.first),
-                                       _p(self.first_dense), 1, s), "dev_first_dense")
-        merge_first(self.first_dense[:n_ids])                    # RCCL int32 MIN
-        self.minimize_pass2(off, items, ranks, m, tab=self.tab, first_dense=self.first_dense)
-        merge_kept(self.kept[:N])                                 # RCCL uint8 MAX
+            merge_first(self.first[:self.span])                      # RCCL int32 MIN
+        else:
+            merge_covered(self.covered[:self.nwords], self.world, self._or_into)
+            n_ids = check(L.syzcov_corpus_dense_first(h, s), "corpus_dense_first")
+            merge_first(self.first_dense[:n_ids])                   # RCCL int32 MIN
+        check(L.syzcov_corpus_pass2(h, s), "corpus_pass2")          # kept against the global first
+        merge_kept(self.kept[:N])                                    # RCCL uint8 MAX
         mark_ev()
-        self.compact(N, self.ws2)
-        mark_ev()
-        self.union_list()
-        mark_ev()
-        self.merge_max_cover()
+        self.finish()
         mark_ev()
         return self.result() if sync else None

@@ -26,12 +26,11 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ._lib import check, lib
+from ._lib import CORPUS_BUFS, CorpusCfg, CorpusInfo, CorpusRes, check, lib
 
 INT32_MAX = 0x7FFFFFFF
 SYZCOV_ERR_WINDOW, SYZCOV_ERR_SEGLEN, SYZCOV_ERR_UNIVERSE = 1, 2, 4  # err_flag bits (syzcov.h)
-KSHIFT_MAX = 7  # SYZCOV_KSHIFT_MAX: a universe PC's low bits fit the membership byte
-RANGE_SHIFT = 20  # 2^20 PCs per LDS-resident range (128 KB covered bitmap)
+KSHIFT_MAX = 6  # SYZCOV_KSHIFT_MAX: a universe PC's low bits fit the membership byte
 
 
 def _p(t: torch.Tensor | None):
@@ -56,78 +55,93 @@ class StepResult:
     max_cover: int              # |maxCover| after the merge
 
 
-class CorpusEngine:
-    """Buffers sized for up to `n_max` inputs / `p_max` raw PCs (longest input
-    `max_seg_len`) over the PC window [pc_lo, pc_lo + pc_span), at most 256
-    ranges of 2^20 PCs.  `n_global` > n_max: a shard of a larger corpus
-    (ranks, kept flags and the order span the whole corpus)."""
+_DT = {"CANON": torch.int32, "NEW_LEN": torch.int32, "SPLIT": torch.int32,
+       "RANGE_TOT": torch.int64, "COVERED": torch.int32, "MAX_COVER": torch.int32,
+       "TAB": torch.int64, "FIRST": torch.int32, "REC": torch.int64, "CAND": torch.uint8,
+       "KEPT": torch.uint8, "LENS": torch.int64, "ORDER": torch.int32, "KEPT_IDX": torch.int32,
+       "UNION": torch.int32, "SCAL": torch.int64, "PC_OF_KEY": torch.int32,
+       "LOW_OF_KEY": torch.uint8, "GLENS": torch.int32, "SEL": torch.uint8,
+       "IOTA": torch.int32, "ITEMS": torch.int32, "RANKS": torch.int32,
+       "FIRST_DENSE": torch.int32, "WS": torch.uint8, "WS2": torch.uint8}
 
-    PHASES = ("canon", "order", "minimize", "compact", "union", "merge")
+
+class CorpusEngine:
+    """The resident corpus engine of libsyzcov (corpus.hip, include/syzcov.h
+    "resident corpus engine") behind one handle: the device memory is one
+    torch allocation laid out by the library, every phase a C-ABI call on
+    torch's current stream, so bench.py measures exactly what a Go host would
+    call over cgo.  Sized for up to `n_max` inputs / `p_max` raw PCs (longest
+    input `max_seg_len`) over the PC window [pc_lo, pc_lo + pc_span), or over
+    the dense keys of a registered PC `universe` (key mode).  `n_global` >
+    n_max: shard `rank` of a larger corpus (dist.ShardedEngine)."""
+
+    PHASES = ("canon", "order", "minimize", "finish")
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 device="cuda", n_global: int | None = None, sort_variant: int = 0,
-                 rec_cap: int = 0, canon_in_place: bool = False, universe=None):
+                 device="cuda", n_global: int | None = None, rank: int = 0, rec_cap: int = 0,
+                 canon_in_place: bool = False, universe=None, order_by: int = 0):
         L = lib()
         dev = torch.device(device)
-        self.dev, self.L = dev, L
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.dev, self.L, self.h = dev, L, None
         self.n_max, self.p_max, self.max_seg = n_max, p_max, max_seg_len
-        # Key mode (keys.hip): with the PC universe registered, every phase works
-        # on dense keys (pc >> kshift) - kbase instead of window offsets
-        self.key_mode = universe is not None
-        self.kshift, self.kbase = 0, pc_lo
-        self.win_lo, self.win_span = pc_lo, pc_span  # Canonicalize's sort window
-        if self.key_mode:
-            (self.kshift, self.kbase, nkeys, self.pc_of_key, self.low_of_key, ulo,
-             uhi) = universe_keymap(universe, dev)
-            self.win_lo, self.win_span = ulo, uhi - ulo + 1  # the universe's extent
-            pc_lo, pc_span = 0, nkeys  # minimize / union / maxCover window = the key range
-        self.pc_lo, self.span = pc_lo, pc_span
-        so = (0xFFFFFFFF >> self.kshift) - self.kbase  # key of the 0xFFFFFFFF sentinel
-        self.sent_key = so if 0 <= so < pc_span else None
-        self.sort_variant = sort_variant
         self.n_global = n_global or n_max
-        self.rshift = RANGE_SHIFT
-        self.nrange = (pc_span + (1 << RANGE_SHIFT) - 1) >> RANGE_SHIFT
-        if self.nrange > 256:
-            raise ValueError("PC window too wide for the range engine (> 256 ranges of 2^20)")
-        nwords = (pc_span + 31) // 32
-        self.nwords = nwords
-        # canonical covers: their own buffer, or the raw CSR slots themselves
-        # (canon_in_place: halves the corpus footprint; the raw lists are consumed)
         self.canon_in_place = canon_in_place
-        if canon_in_place and max_seg_len > 16384:
-            raise ValueError("in-place canonicalization needs max_seg_len <= 16384")
-        self.canon = None if canon_in_place else _u32(p_max + 1, dev)
-        self.new_len = _u32(n_max + 1, dev)
-        # split points (columns per segment) and PCs per range, from canon
-        self.split = (torch.empty(n_max * self.nrange, dtype=torch.int32, device=dev)
-                      if self.nrange > 1 else None)
-        self.range_tot = torch.zeros(self.nrange, dtype=torch.int64, device=dev)
-        # covered set (one bit per window PC; ends up as the corpus union) and
-        # the resident maxCover
-        self.covered = torch.zeros((self.nrange << RANGE_SHIFT) // 32, dtype=torch.int32,
-                                   device=dev)
-        self.max_cover = torch.zeros(nwords, dtype=torch.int32, device=dev)
-        self.tab = torch.empty(nwords, dtype=torch.int64, device=dev)
-        # first-cover rank per window PC: INT32_MAX outside a step's records
-        self.first = torch.full((pc_span,), INT32_MAX, dtype=torch.int32, device=dev)
-        self.rec_cap = rec_cap or max(1 << 22, min(p_max, 1 << 26))
-        self.rec = torch.empty(self.rec_cap, dtype=torch.int64, device=dev)
-        self.rec_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.cand = torch.empty(n_max + 1, dtype=torch.uint8, device=dev)
-        self.kept = torch.zeros(self.n_global + 1, dtype=torch.uint8, device=dev)
-        self.lens64 = torch.empty(self.n_global + 1, dtype=torch.int64, device=dev)
-        self.order = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
-        self.out_idx = torch.empty(self.n_global + 1, dtype=torch.int32, device=dev)
-        self.union = _u32(min(pc_span, p_max) + 1, dev)
-        self.scal = torch.zeros(16, dtype=torch.int64, device=dev)  # err, n_ids, n_kept, ...
-        ws = max(L.syzcov_dev_canon_split_ws_size(n_max),
-                 L.syzcov_dev_dict_ws_size(pc_span),
-                 L.syzcov_dev_compact_ws_size(self.n_global),
-                 L.syzcov_dev_sort_ws_size(self.n_global),
-                 L.syzcov_dev_minimize_range_ws_size(self.n_global, pc_span, RANGE_SHIFT))
-        self.ws = torch.empty(ws, dtype=torch.uint8, device=dev)
-        self.ws_size = ws
+        self._univ = None
+        if universe is not None:  # host copy (read by create only)
+            if isinstance(universe, torch.Tensor):
+                universe = universe.cpu().numpy().view(np.uint32)
+            self._univ = np.ascontiguousarray(universe, dtype=np.uint32)
+        cfg = CorpusCfg(n_max=n_max, n_global=self.n_global, rank=rank, p_max=p_max,
+                        max_seg_len=max_seg_len, pc_lo=pc_lo, pc_span=pc_span,
+                        universe=None if self._univ is None else self._univ.ctypes.data,
+                        universe_n=0 if self._univ is None else self._univ.size,
+                        canon_in_place=int(canon_in_place), order_by=order_by, rec_cap=rec_cap)
+        size = check(L.syzcov_corpus_mem_size(C.byref(cfg)), "corpus_mem_size")
+        with torch.cuda.device(dev):
+            self.mem = torch.empty(size, dtype=torch.uint8, device=dev)
+            h = C.c_uint64(0)
+            check(L.syzcov_corpus_create(C.byref(cfg), _p(self.mem), size, C.byref(h)),
+                  "corpus_create")
+        self.h = h.value
+        self._univ = None
+        info = CorpusInfo()
+        check(L.syzcov_corpus_info(self.h, C.byref(info)), "corpus_info")
+        self.key_mode = bool(info.key_mode)
+        self.kshift, self.kbase = info.kshift, info.kbase
+        self.pc_lo, self.span = info.pc_lo, info.span
+        self.win_lo, self.win_span = info.win_lo, info.win_span
+        self.nrange, self.nwords = info.nrange, info.nwords
+        self.rec_cap = info.rec_cap
+        self.sent_key = None if info.sent_key == 0xFFFFFFFF else info.sent_key
+        for name in CORPUS_BUFS:
+            setattr(self, name.lower(), self._view(name))
+        self.canon_buf = self.canon           # the CANON buffer (None when in place)
+        self.canon = None                     # the step's canonical lists
+        self.union = self.union               # noqa: PLW0127 (named for callers)
+        self.scal = self.scal
+        self.rec_cnt = self.scal[7:8]
+        self.out_idx = self.kept_idx
+
+    def _view(self, name: str):
+        off, nb = C.c_uint64(0), C.c_uint64(0)
+        check(self.L.syzcov_corpus_buffer(self.h, CORPUS_BUFS.index(name), C.byref(off),
+                                          C.byref(nb)), "corpus_buffer")
+        if nb.value == 0:
+            return None
+        return self.mem[off.value:off.value + nb.value].view(_DT[name])
+
+    def close(self):
+        if self.h:
+            self.L.syzcov_corpus_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     def alg_bytes(self, raw_pcs: int, canon_pcs: int) -> dict:
         """Algorithmic HBM bytes per launch of the streaming phases (DESIGN.md
@@ -137,91 +151,26 @@ class CorpusEngine:
 
     # ---------------------------------------------------------------- phases
     def canonicalize(self, off: torch.Tensor, raw: torch.Tensor, n: int):
-        """Wavefront canonicalize + per-range split points and range totals."""
-        self.scal.zero_()
-        self.range_tot.zero_()
-        if self.canon_in_place:
-            self.canon = raw
-        if self.key_mode:
-            check(self.L.syzcov_dev_canon_split_keys(
-                _p(off), _p(raw), _p(self.canon), _p(self.new_len), n, self.max_seg, self.win_lo,
-                self.win_span, self.kshift, self.kbase, self.span, _p(self.low_of_key),
-                self.rshift, _p(self.split),
-                _p(self.range_tot), _p(self.scal), _p(self.ws), self.ws_size, _stream()),
-                "dev_canon_split_keys")
-            return
-        check(self.L.syzcov_dev_canon_split(_p(off), _p(raw), _p(self.canon), _p(self.new_len), n,
-                                            self.max_seg, self.pc_lo, self.span, self.rshift,
-                                            _p(self.split), _p(self.range_tot), _p(self.scal),
-                                            _p(self.ws), self.ws_size, _stream()),
-              "dev_canon_split")
+        """Wavefront canonicalize + per-range split points and range totals
+        (key mode: key words, common.h)."""
+        check(self.L.syzcov_corpus_canon(self.h, _p(off), _p(raw), n, _stream()), "corpus_canon")
+        self.canon = raw if self.canon_in_place else self.canon_buf
 
-    def sort_order(self, lens32: torch.Tensor, n: int):
-        """Go sort.Sort order over canonical lengths (lens32: int32 [n])."""
-        self.lens64[:n].copy_(lens32[:n])  # int32 -> int64 in the copy kernel
-        check(self.L.syzcov_dev_sort_order(_p(self.lens64), n, self.sort_variant, _p(self.order),
-                                           _p(self.ws), self.ws_size, _stream()), "dev_sort_order")
+    def sort_order(self, lens32: torch.Tensor | None = None, n: int | None = None):
+        """Go sort.Sort order over int32 lengths (None: this step's own);
+        clears Minimize's inputs."""
+        own = lens32 is None or lens32.data_ptr() == self.new_len.data_ptr()
+        check(self.L.syzcov_corpus_order(self.h, None if own else _p(lens32), n, _stream()),
+              "corpus_order")
 
-    def minimize_clear(self, n_items):
-        """Zero minimize's inputs (covered, cand, kept)."""
-        self.covered.zero_()
-        self.cand[:n_items].zero_()
-        self.kept.zero_()
+    def minimize(self, do_pass2: bool = True):
+        """First-cover Minimize over this step's items (sharded: this shard's,
+        with global ranks; pass 2 after the exchange)."""
+        check(self.L.syzcov_corpus_minimize(self.h, int(do_pass2), _stream()), "corpus_minimize")
 
-    def minimize(self, off, order, ranks, n_items, do_pass2=True, cleared=False):
-        """Range-partitioned first-cover Minimize; leaves the union in covered.
-        cleared: minimize_clear() already ran on this stream."""
-        if not cleared:
-            self.minimize_clear(n_items)
-        check(self.L.syzcov_dev_minimize_range(
-            _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
-            n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
-            _p(self.first), _p(self.rec), self.rec_cap, _p(self.rec_cnt), _p(self.cand),
-            _p(self.kept), int(do_pass2), 0, 0, 0, _p(self.ws), _stream()), "dev_minimize_range")
-
-    def minimize_pass2(self, off, order, ranks, n_items, tab=None, first_dense=None):
-        """Pass 2 over the records (sharded: against the MIN-merged dense table)."""
-        check(self.L.syzcov_dev_minimize_range_pass2(
-            _p(off), _p(self.new_len), _p(self.canon), _p(self.split), _p(order), _p(ranks),
-            n_items, self.pc_lo, self.span, self.rshift, _p(self.range_tot), _p(self.covered),
-            _p(self.first), _p(self.rec), self.rec_cap, _p(self.rec_cnt), _p(self.cand), _p(tab),
-            _p(first_dense), _p(self.kept), _p(self.ws), _stream()), "dev_minimize_range_pass2")
-
-    def compact(self, n_ranks: int, ws=None):
-        check(self.L.syzcov_dev_compact_kept(_p(self.kept), _p(self.order), n_ranks,
-                                             _p(self.out_idx), _p(self.scal[2:3]),
-                                             _p(self.ws if ws is None else ws), _stream()),
-              "dev_compact_kept")
-
-    def build_dict(self, ws=None):
-        """Dense-id dictionary of the covered set; *n_ids -> scal[1]."""
-        check(self.L.syzcov_dev_dict_build_bits(_p(self.covered), self.span, _p(self.tab),
-                                                _p(self.scal[1:2]),
-                                                _p(self.ws if ws is None else ws), _stream()),
-              "dev_dict_build_bits")
-
-    def union_list(self):
-        # Union drops 0xFFFFFFFF (cover.go:97): in key mode, its key
-        drop = 0xFFFFFFFF
-        if self.key_mode:
-            drop = self.sent_key if self.sent_key is not None else 0xFFFFFFFF
-        check(self.L.syzcov_dev_dict_to_list_drop(_p(self.tab), self.span, self.pc_lo, drop,
-                                                  _p(self.union), _p(self.scal[3:4]), _stream()),
-              "dev_dict_to_list_drop")
-        if self.key_mode:  # sorted keys -> sorted PCs (the key map is monotone)
-            check(self.L.syzcov_dev_keys_to_pcs(_p(self.pc_of_key), self.span, _p(self.union),
-                                                _p(self.union),
-                                                _p(self.scal[3:4]), self.union.numel(), _stream()),
-                  "dev_keys_to_pcs")
-
-    def merge_max_cover(self):
-        """maxCover |= union.  The union (Union fold) drops 0xFFFFFFFF
-        (cover.go:97): if the window holds it, its covered bit goes first."""
-        so = self.sent_key
-        if so is not None:
-            self.covered[so >> 5] &= ~(1 << (so & 31)) if (so & 31) != 31 else 0x7FFFFFFF
-        check(self.L.syzcov_dev_bitmap_op(0, _p(self.max_cover), _p(self.covered), self.nwords,
-                                          _p(self.scal[4:5]), _stream()), "dev_bitmap_op")
+    def finish(self):
+        """Kept list, sorted union, maxCover |= union."""
+        check(self.L.syzcov_corpus_finish(self.h, _stream()), "corpus_finish")
 
     # ------------------------------------------------------------------ step
     def step(self, off: torch.Tensor, raw: torch.Tensor, n: int, sync: bool = True, ev=None):
@@ -234,46 +183,33 @@ class CorpusEngine:
         mark_ev()
         self.canonicalize(off, raw, n)
         mark_ev()
-        # queued ahead of the sort, whose final read-back leaves the GPU idle
-        # while the host issues the next launches
-        self.minimize_clear(n)
-        self.sort_order(self.new_len, n)
+        self.sort_order(None, n)
         mark_ev()
-        self.minimize(off, self.order, None, n, cleared=True)
+        self.minimize(True)
         mark_ev()
-        self.compact(n)
-        mark_ev()
-        self.build_dict()
-        self.union_list()
-        mark_ev()
-        self.merge_max_cover()
+        self.finish()
         mark_ev()
         return self.result() if sync else None
 
     def result(self) -> StepResult:
-        sc = self.scal.cpu().tolist()
-        if sc[0] & SYZCOV_ERR_WINDOW:
-            raise RuntimeError("a PC fell outside the engine's PC window")
-        if sc[0] & SYZCOV_ERR_SEGLEN:
-            raise RuntimeError(f"an input is longer than max_seg_len={self.max_seg}")
-        if sc[0] & SYZCOV_ERR_UNIVERSE:
-            raise RuntimeError("a PC is not in the registered PC universe (key mode would alias "
-                               "it with a universe PC; keys.hip)")
-        if sc[0] & 0xFFFFFFFF:
-            raise RuntimeError(f"engine error flags {sc[0] & 0xFFFFFFFF:#x}")
-        n_ids, n_kept, n_union = (int(x) & 0xFFFFFFFF for x in sc[1:4])
-        return StepResult(self.out_idx[:n_kept], n_kept, self.union[:n_union], n_union, n_ids,
-                          int(sc[4]))
+        r = CorpusRes()
+        rc = self.L.syzcov_corpus_result(self.h, C.byref(r), _stream())
+        if rc < 0:
+            msg = self.L.syzcov_last_error().decode(errors="replace")
+            if r.err_flags & SYZCOV_ERR_UNIVERSE:
+                msg += " (key mode would alias it with a universe PC; keys.hip)"
+            raise RuntimeError(msg)
+        return StepResult(self.kept_idx[:r.n_kept], r.n_kept, self.union[:r.n_union], r.n_union,
+                          r.n_ids, r.max_cover)
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """The canonical covers as PCs, in the CSR slots of `off` (key mode:
-        mapped back from the keys canon wrote there)."""
+        decoded from the key words canon wrote there)."""
         if not self.key_mode:
             return self.canon
         out = torch.empty_like(self.canon)
-        check(self.L.syzcov_dev_keys_to_pcs(_p(self.pc_of_key), self.span, _p(self.canon), _p(out),
-                                            None, int(off[n].item()), _stream()),
-              "dev_keys_to_pcs")
+        check(self.L.syzcov_dev_words_to_pcs(_p(self.canon), int(off[n].item()), self.kshift,
+                                             self.kbase, _p(out), _stream()), "dev_words_to_pcs")
         return out
 
 

@@ -18,11 +18,6 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smo
 rc=$?; tail -2 $o/smoke.log; fatal $rc smoke
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $o/bench.json 2> $o/bench.err
 rc=$?; cat $o/bench.json; [ $rc -ne 0 ] && tail -20 $o/bench.err; fatal $rc bench
-if [ "$STAMPS" = 1 ]; then  # minimize chunk stamps (debug build, C2-sized C3-seed corpus)
-  SYZCOV_LIB=$PWD/syzkaller_amd/variants/mrdbg.so SYZCOV_MR_DBG=2100000000,1000000 \
-    timeout -k 10 200 python -u tools/diag_c3.py 1000000 > $o/stamps.log 2>&1
-  rc=$?; grep "mr dbg\]   wgs\|minimize ok\|step ok" $o/stamps.log; fatal $rc stamps
-fi
 [ "$NOPROF" = 1 ] && exit 0
 [ $SECONDS -gt 650 ] && { echo "no time left for profiles ($SECONDS s)"; exit 0; }
-timeout -k 10 $((1100 - SECONDS)) bash tools/profile_r02.sh
+timeout -k 10 $((1100 - SECONDS)) bash tools/profile_r03.sh

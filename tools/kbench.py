@@ -50,7 +50,7 @@ def main():
     torch.cuda.synchronize()
     fns = {
         "canon": lambda: eng.canonicalize(off, raw, n),
-        "minimize": lambda: eng.minimize(off, eng.order, None, n),
+        "minimize": lambda: (eng.sort_order(None, n), eng.minimize()),
         "step": lambda: eng.step(off, raw, n, sync=False),
     }
     f = fns[a.what]

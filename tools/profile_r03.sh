@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-2 rocprofv3 evidence (run on the GPU box from the repo root):
+# Round-3 rocprofv3 evidence (run on the GPU box from the repo root):
 #   corpus C2 (key mode): kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes -> traffic
 #   newcov C5: the same;  prio C4: trace + stats
 # counters never combined with tracing; each pass its own run (MI355X_MICROARCH.md)
 set -o pipefail
 export TMPDIR=/tmp
-o=gpurun_out/prof_r02
+o=gpurun_out/prof_r03
 mkdir -p $o
 B="python3 bench.py --no-cpu"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/corpus_trace -o run -- $B --steps 5 --warmup 2 > $o/corpus_trace.log 2>&1 || { tail -20 $o/corpus_trace.log; exit 1; }
