@@ -54,8 +54,10 @@ def parse():
     ap.add_argument("--workload", choices=["corpus", "prio", "newcov"], default="corpus")
     ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
     ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
-    ap.add_argument("--history", type=int, default=32,
-                    help="newcov: batches streamed through the check before the bench")
+    ap.add_argument("--history", type=int, default=512,
+                    help="newcov: batches streamed through the check before the bench (512: "
+                         "maxCover near saturation, a long-running fuzzer; 32: the early, "
+                         "candidate-heavy regime)")
     ap.add_argument("--inputs", type=int, default=1_000_000,
                     help="inputs (programs) per GPU at N=1 (config C2)")
     ap.add_argument("--global-inputs", type=int, default=None,
@@ -70,6 +72,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prio-dense", action="store_true",
                     help="prio: contract over all C keys instead of the active positional keys")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="N=1: skip the C3-on-one-GPU sub-record (the strong-scaling anchor)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="N=1: skip the drop-in legs (cover.Minimize from host buffers)")
     ap.add_argument("--no-universe", action="store_true",
                     help="window offsets instead of the dense keys of the registered PC "
                          "universe (keys.hip), for the corpus engine and newcov's maxCover")
@@ -288,12 +294,111 @@ def bench_corpus(args):
         pk = stream_peak(dev)
         out["roofline"]["peak_measured"] = pk
         out["roofline"]["frac_of_measured"] = achieved / pk
+    if world == 1 and glob is None:
+        eng.close()
+        del eng, off, raw
+        torch.cuda.empty_cache()
+        if not args.no_c3:
+            out["c3_single_gpu"] = c3_single(args, dev)
+        if not args.no_dropin:
+            out["dropin"] = dropin_legs(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         cb = out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = value / cb["value"]
         out["vs_cpu_minimize_union"] = (out["minimize_union_pcs_per_s"]
                                         / cb["minimize_canonical_pcs_per_s"])
     return rank, world, out
+
+
+def c3_single(args, dev):
+    """C3 (10M inputs, seed 0x5EED0003, 20.5 G raw PCs = 82 GB) on ONE GPU,
+    canonicalized out of place (82 + 81 GB): the same-workload anchor of the
+    driver's 1 -> 8 GPU strong-scaling curve (N > 1 runs C3 sharded)."""
+    import torch
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n = C3_INPUTS
+    lo, span = synth_window(args.log2_space)
+    off, raw, lens, total = synth_corpus(n, SEED_C3, mean=args.mean, sigma=args.sigma,
+                                         log2_space=args.log2_space, device=dev)
+    univ = None if args.no_universe else synth_universe(args.log2_space, SEED_C3, device=dev)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, device=dev, universe=univ)
+    del univ, lens
+    eng.step(off, raw, n)  # warmup
+    torch.cuda.synchronize()
+    steps = 3
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(eng.PHASES) + 1)]
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        eng.step(off, raw, n, sync=False, ev=ev[k])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    res = eng.result()
+    ph = {p: round(sum(e[i].elapsed_time(e[i + 1]) for e in ev) / steps, 3)
+          for i, p in enumerate(eng.PHASES)}
+    out = {"workload": f"C3: {n} inputs on one GPU (seed {SEED_C3:#x}), out-of-place canon",
+           "ms_per_step": dt * 1e3, "value": total / dt, "unit": "input-PCs/s", "steps": steps,
+           "raw_pcs": total, "phases_ms": ph,
+           "results": {"kept": res.n_kept, "union": res.n_union}}
+    eng.close()
+    del eng, off, raw
+    torch.cuda.empty_cache()
+    return out
+
+
+def dropin_legs(args, dev):
+    """cover.Minimize through the drop-in C-ABI from HOST buffers (what the cgo
+    shim of INTEGRATION.md calls): syzcov_minimize (stateless: stage, a
+    transient window-mode engine over the corpus' PC extent, read back) and
+    syzcov_corpus_minimize_host on a persistent key-mode handle (the manager's
+    form).  PCIe-inclusive; the corpora are the C1 / C2 synthetic ones."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe
+    L = _lib.lib()
+    legs = {}
+    for name, n, seed in (("C1", 10_000, SEED_C1), ("C2", args.inputs, SEED)):
+        off, raw, lens, total = synth_corpus(n, seed, mean=args.mean, sigma=args.sigma,
+                                             log2_space=args.log2_space, device=dev)
+        h_off = off.cpu().numpy().astype(np.uint64)
+        h_pcs = raw[:total].cpu().numpy().view(np.uint32)
+        max_len = int(lens.max().item())
+        del off, raw, lens
+        torch.cuda.empty_cache()
+        out = np.empty(n, np.int32)
+        t0 = time.perf_counter()
+        k = _lib.check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n, None, 0,
+                                         out.ctypes.data), "minimize")
+        t1 = time.perf_counter()
+        univ = synth_universe(args.log2_space, seed, device=dev).cpu().numpy().view(np.uint32)
+        cfg = _lib.CorpusCfg(n_max=n, p_max=total, max_seg_len=max_len,
+                             universe=univ.ctypes.data, universe_n=univ.size)
+        h = C.c_uint64(0)
+        _lib.check(L.syzcov_corpus_create(C.byref(cfg), None, 0, C.byref(h)), "corpus_create")
+        un = np.empty(1 << args.log2_space, np.uint32)
+        nu = C.c_uint64(0)
+        reps, tk = 2, []
+        for _ in range(reps + 1):
+            ta = time.perf_counter()
+            k2 = _lib.check(L.syzcov_corpus_minimize_host(h.value, h_off.ctypes.data,
+                                                          h_pcs.ctypes.data, n, out.ctypes.data,
+                                                          un.ctypes.data, un.size, C.byref(nu)),
+                            "corpus_minimize_host")
+            tk.append(time.perf_counter() - ta)
+        L.syzcov_corpus_destroy(h.value)
+        legs[name] = {
+            "inputs": n, "raw_pcs": total,
+            "syzcov_minimize_ms": round((t1 - t0) * 1e3, 2), "syzcov_minimize_kept": k,
+            "syzcov_minimize_input_pcs_per_s": total / (t1 - t0),
+            "handle_minimize_host_ms": round(min(tk[1:]) * 1e3, 2),
+            "handle_minimize_host_kept": k2, "handle_union": nu.value,
+            "handle_minimize_host_input_pcs_per_s": total / min(tk[1:]),
+            "note": "host buffers in and out, PCIe transfers included; syzcov_minimize orders "
+                    "by the raw lengths it is given (Minimize of covers as given)"}
+        del h_pcs, h_off
+    return legs
 
 
 def bench_prio(args):

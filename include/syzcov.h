@@ -324,7 +324,7 @@ int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncal
 typedef uint64_t syzcov_corpus;
 typedef struct syzcov_corpus_cfg {
     size_t n_max;        /* inputs per step on this GPU */
-    size_t n_global;     /* inputs of the sharded corpus (0 = n_max: one GPU) */
+    size_t n_global;     /* 0: one GPU; else the sharded protocol over n_global inputs */
     size_t rank;         /* this shard (sharded runs) */
     uint64_t p_max;      /* raw PCs per step on this GPU */
     size_t max_seg_len;  /* longest input (a longer one fails the step) */

@@ -75,6 +75,7 @@ struct Corpus {
     uint32_t rshift = kRangeShiftWindow, nrange = 1;
     uint64_t nwords = 0, n_global = 0, union_cap = 0;
     int world = 1;
+    bool shard = false;  // the sharded protocol (cfg.n_global given, even at world 1)
     // layout
     uint8_t *mem = nullptr;
     size_t mem_size = 0;
@@ -138,7 +139,7 @@ static int64_t plan(Corpus &c) {
     sz[SYZCOV_CORPUS_SCAL] = 16 * 8;
     sz[SYZCOV_CORPUS_PC_OF_KEY] = c.key_mode ? c.span * 4 : 0;
     sz[SYZCOV_CORPUS_LOW_OF_KEY] = c.key_mode ? (uint64_t)c.nrange << c.rshift : 0;
-    if (c.world > 1) {
+    if (c.shard) {
         sz[SYZCOV_CORPUS_GLENS] = N * 4;
         sz[SYZCOV_CORPUS_SEL] = N;
         sz[SYZCOV_CORPUS_IOTA] = N * 4;
@@ -152,7 +153,7 @@ static int64_t plan(Corpus &c) {
     sz[SYZCOV_CORPUS_WS] = c.ws_size;
     // sharded: dictionary / compaction scratch apart from ws, which carries
     // minimize's rank-ordered descriptors from pass 1 to pass 2
-    c.ws2_size = c.world > 1 ? std::max(syzcov_dev_dict_ws_size(c.span),
+    c.ws2_size = c.shard ? std::max(syzcov_dev_dict_ws_size(c.span),
                                         syzcov_dev_compact_ws_size(N))
                              : 0;
     sz[SYZCOV_CORPUS_WS2] = c.ws2_size;
@@ -174,6 +175,7 @@ static int setup(Corpus &c, const syzcov_corpus_cfg *cfg) {
     c.n_global = g.n_global ? g.n_global : g.n_max;
     if (c.n_global < g.n_max || c.n_global > 0x7FFFFFFF) return SYZCOV_EINVAL;
     c.world = (int)((c.n_global + g.n_max - 1) / g.n_max);
+    c.shard = g.n_global != 0;
     if (g.canon_in_place && g.max_seg_len > 16384) return SYZCOV_EINVAL;
     c.key_mode = g.universe != nullptr;
     if (c.key_mode) {
@@ -258,7 +260,7 @@ enum { SC_ERR = 0, SC_NIDS = 1, SC_NKEPT = 2, SC_NUNION = 3, SC_MAXCOV = 4, SC_C
        SC_CI = 6, SC_REC = 7 };
 
 static uint64_t *scal(const Corpus &c) { return c.buf<uint64_t>(SYZCOV_CORPUS_SCAL); }
-static bool sharded(const Corpus &c) { return c.N > c.n; }
+static bool sharded(const Corpus &c) { return c.shard; }
 
 // --------------------------------------------------------------- phases
 static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hipStream_t s) {
@@ -289,7 +291,7 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
     if (!c.canon) return SYZCOV_EINVAL;  // no canon phase yet
     if (!lens32 && N != c.n) return SYZCOV_EINVAL;
     if (N < c.n || N > c.n_global) return SYZCOV_EINVAL;
-    if (N > c.n && (uint64_t)c.cfg.rank * c.cfg.n_max + c.n > N) return SYZCOV_EINVAL;
+    if (c.shard && (uint64_t)c.cfg.rank * c.cfg.n_max + c.n > N) return SYZCOV_EINVAL;
     c.N = N;
     SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_COVERED), 0, c.sizes[SYZCOV_CORPUS_COVERED],
                            s));

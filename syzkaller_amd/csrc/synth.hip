@@ -69,21 +69,31 @@ __global__ void synth_universe_kernel(uint64_t seed, uint32_t n, uint32_t *__res
         out[k] = synth_universe(seed, k);
 }
 
-// Streaming copy, 16 B per lane, 4 loads in flight: the measured HBM peak the
-// bench reports next to the 8 TB/s vendor figure (roofline.peak_measured).
-__global__ __launch_bounds__(256) void stream_copy_kernel(const uint4 *__restrict__ src,
-                                                          uint4 *__restrict__ dst, uint64_t n4) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
-                    d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+// Streaming copy, 16 B per lane: the measured HBM peak the bench reports
+// next to the 8 TB/s vendor figure (roofline.peak_measured).  Each workgroup
+// copies whole contiguous 8 x 16 KB tiles (8 loads of 16 B per lane in flight
+// before the first store) with non-temporal stores, so the written lines do
+// not evict the lines being read.
+constexpr int SC_THREADS = 1024, SC_U = 8;
+typedef unsigned int sc_v4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(SC_THREADS) void stream_copy_kernel(const uint4 *__restrict__ src,
+                                                                 uint4 *__restrict__ dst,
+                                                                 uint64_t n4) {
+    constexpr uint64_t TILE = (uint64_t)SC_THREADS * SC_U;
+    const uint64_t ntile = n4 / TILE;
+    for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+        const uint64_t b = t * TILE + threadIdx.x;
+        const sc_v4 *s4 = reinterpret_cast<const sc_v4 *>(src);
+        sc_v4 *d4 = reinterpret_cast<sc_v4 *>(dst);
+        sc_v4 v[SC_U];
+#pragma unroll
+        for (int u = 0; u < SC_U; u++) v[u] = s4[b + (uint64_t)u * SC_THREADS];
+#pragma unroll
+        for (int u = 0; u < SC_U; u++) __builtin_nontemporal_store(v[u], d4 + b + (uint64_t)u * SC_THREADS);
     }
-    for (; i < n4; i += stride) dst[i] = src[i];
+    for (uint64_t i = ntile * TILE + (uint64_t)blockIdx.x * SC_THREADS + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * SC_THREADS)
+        dst[i] = src[i];
 }
 
 }  // namespace syz
@@ -93,7 +103,7 @@ using namespace syz;
 extern "C" int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes, void *stream) {
     if (!src || !dst || nbytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return SYZCOV_EINVAL;
     if (nbytes == 0) return 0;
-    hipLaunchKernelGGL(stream_copy_kernel, dim3(256 * 16), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(stream_copy_kernel, dim3(256 * 2), dim3(SC_THREADS), 0, (hipStream_t)stream,
                        (const uint4 *)src, (uint4 *)dst, (uint64_t)(nbytes / 16));
     SYZ_LAUNCH_CHECK();
     return 0;

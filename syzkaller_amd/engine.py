@@ -93,7 +93,7 @@ class CorpusEngine:
             if isinstance(universe, torch.Tensor):
                 universe = universe.cpu().numpy().view(np.uint32)
             self._univ = np.ascontiguousarray(universe, dtype=np.uint32)
-        cfg = CorpusCfg(n_max=n_max, n_global=self.n_global, rank=rank, p_max=p_max,
+        cfg = CorpusCfg(n_max=n_max, n_global=n_global or 0, rank=rank, p_max=p_max,
                         max_seg_len=max_seg_len, pc_lo=pc_lo, pc_span=pc_span,
                         universe=None if self._univ is None else self._univ.ctypes.data,
                         universe_n=0 if self._univ is None else self._univ.size,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel micro-bench on the C2 corpus: times one engine phase at a time.
-    python tools/kbench.py canon|minimize|step [--inputs N] [--reps R]"""
+    python tools/kbench.py canon|minimize|step|order [--keys] [--inputs N] [--reps R]"""
 import argparse
 import os
 import sys
@@ -11,7 +11,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window  # noqa: E402
+from syzkaller_amd.engine import (CorpusEngine, synth_corpus, synth_universe,  # noqa: E402
+                                  synth_window)
 
 
 def main():
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--mean", type=int, default=2048)
     ap.add_argument("--sigma", type=int, default=512)
     ap.add_argument("--log2-space", type=int, default=22)
+    ap.add_argument("--keys", action="store_true", help="key mode (the synthetic PC universe)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n = a.inputs
@@ -45,7 +47,8 @@ def main():
     lo, span = synth_window(a.log2_space)
     off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
                                          log2_space=a.log2_space)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    univ = synth_universe(a.log2_space, 0x5EED0002) if a.keys else None
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=univ)
     eng.step(off, raw, n)
     torch.cuda.synchronize()
     fns = {
