@@ -20,6 +20,15 @@ struct Index {
     const uint8_t *low_of_key;     // key mode: universe membership (keys.hip)
 };
 
+// Bitmap index of pc; false only if it is outside the window / key range (no
+// membership test: for positions, e.g. range boundaries, where the PC itself
+// is checked elsewhere).
+__device__ __forceinline__ bool pc_index_range(const Index &X, uint32_t pc, uint32_t *idx) {
+    const uint32_t k = X.key_mode ? (pc >> X.kshift) - X.kbase : pc - X.pc_lo;
+    *idx = k;
+    return k < X.span;
+}
+
 // Bitmap index of pc; false if pc is outside the window / key range, or, in
 // key mode, not a universe PC (its key belongs to another PC or to none: the
 // caller rejects it instead of aliasing it, keys.hip).

@@ -98,6 +98,7 @@ struct Args {
     uint32_t keymask;          // SYZ_KEY_MASK in key mode, ~0 otherwise
     const uint8_t *low_of_key; // [nrange << rshift] bytes, 0x7F past the keys
     uint32_t *err;             // SYZCOV_ERR_UNIVERSE
+    int slice_major;           // dynamic pieces drawn slice by slice (else range by range)
 };
 
 #ifdef SYZ_MR_DEBUG
@@ -524,8 +525,10 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         g = s_next;
         __syncthreads();
         if (g >= G) break;
-        const uint32_t S = G / P;  // range-major: g = position * S + slice
-        g = (g % S) * P + g / S;
+        if (!A.slice_major) {
+            const uint32_t S = G / P;  // range-major: g = position * S + slice
+            g = (g % S) * P + g / S;
+        }
     }
     uint32_t rho, i0, i1;
     if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) {
@@ -754,6 +757,260 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
 }
 
+// Pass 1 as ONE chunk stream per wave across its 64-item batches (FLOW).
+// The stream kernel above drains its load pipeline at every batch boundary
+// (the next batch's descriptors and first loads wait for the last test), which
+// short sub-runs make frequent: at 2^17-key ranges (key mode) a sub-run is ~64
+// PCs and a batch ~4 windows.  Here the item descriptors live in registers
+// (looked up with ds_bpermute, no LDS), three batches deep: C (being tested),
+// N (scanned, its first window issued while C's last one is tested) and R
+// (its descriptor loads in flight), so the window after C's last is N's first.
+template <int UG, bool KEYM>
+__global__ __launch_bounds__(THREADS) void pass1_flow_kernel(Args A, uint32_t a, uint32_t b,
+                                                             uint32_t P, int load_cov) {
+    extern __shared__ uint32_t s_cov[];
+    __shared__ uint32_t s_plan[MAX_R + 1];
+    __shared__ uint32_t s_next;
+    const uint32_t G = A.npieces;
+    plan_pieces(A, G, P, s_plan);
+    const uint32_t region = blockIdx.x % NCTR;
+    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
+    unsigned long long *const rrec = A.rec + region * A.cap_k;
+    const uint32_t nwords = (1u << A.rshift) >> 5;
+    const uint8_t *const s_cov8 = reinterpret_cast<const uint8_t *>(s_cov);
+    const uint32_t l = __lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t cur_rho = 0xFFFFFFFFu;
+    uint32_t nonmem = 0;
+    for (;;) {
+        if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+        __syncthreads();
+        uint32_t g = s_next;
+        __syncthreads();
+        if (g >= G) break;
+        {
+            const uint32_t S = G / P;  // range-major: g = position * S + slice
+            g = (g % S) * P + g / S;
+        }
+        uint32_t rho, i0, i1;
+        if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
+        if (rho != cur_rho) {
+            __syncthreads();  // every wave is done with the previous range
+            uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
+            if (KEYM) {  // table bytes | covered << 7, 16 keys per uint4
+                const uint32_t nq = (1u << A.rshift) >> 4;
+                const uint4 *t4 =
+                    reinterpret_cast<const uint4 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
+                const uint32_t *cw = A.covered + (uint64_t)rho * nwords;
+                for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
+                    uint4 t = t4[q];
+                    if (load_cov) {
+                        const uint32_t cb = (cw[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+                        auto spread = [](uint32_t x) {  // bit i -> bit 8i + 7
+                            return ((x & 1u) << 7) | ((x & 2u) << 14) | ((x & 4u) << 21) |
+                                   ((x & 8u) << 28);
+                        };
+                        t.x |= spread(cb);
+                        t.y |= spread(cb >> 4);
+                        t.z |= spread(cb >> 8);
+                        t.w |= spread(cb >> 12);
+                    }
+                    s4[q] = t;
+                }
+            } else {
+                const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
+                for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
+                    s4[q] = load_cov ? g4[q] : make_uint4(0, 0, 0, 0);
+            }
+            cur_rho = rho;
+            __syncthreads();
+        }
+        const uint32_t rbase = rho << A.rshift;
+        const uint32_t bmask = (1u << A.rshift) - 1u;
+        const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+        const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+        if (w0 >= w1) continue;
+        // ---- batch descriptors (lane j: item ib + j)
+        struct Raw {
+            uint32_t s0, s1;
+            uint64_t base;
+            int32_t rk;
+        };
+        struct Bat {
+            uint32_t a0lo, a0hi, he, ex, ib, tot;  // ib, tot wave-uniform
+            int32_t rk;
+        };
+        auto load_raw = [&](uint32_t ib_) {
+            Raw r{0, 0, 0, 0};
+            const uint32_t item = ib_ + l;
+            if (item < w1) {
+                r.rk = A.ranks ? A.ranks[item] : (int32_t)item;
+                r.s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+                r.s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+                r.base = A.base_r[item];
+            }
+            return r;
+        };
+        auto make = [&](uint32_t ib_, const Raw &r) {
+            Bat t;
+            const uint32_t item = ib_ + l;
+            uint32_t m = 0, nch = 0, he = 0;
+            uint64_t a0 = 0;
+            if (item < w1) {
+                const uint64_t st = r.base + r.s0;
+                m = r.s1 - r.s0;
+                a0 = st & ~3ull;
+                const uint32_t head = (uint32_t)(st - a0);
+                he = ((head + m) << 2) | head;
+                nch = m ? (head + m + 3) >> 2 : 0u;
+            }
+            const uint32_t incl = wave_incl_scan(nch);
+            t.a0lo = (uint32_t)a0;
+            t.a0hi = (uint32_t)(a0 >> 32);
+            t.he = he;
+            t.ex = incl - nch;
+            t.ib = ib_;
+            t.tot = __builtin_amdgcn_readlane(incl, 63);
+            t.rk = r.rk;
+            return t;
+        };
+        Bat C = make(w0, load_raw(w0));
+        const uint32_t ibN0 = w0 + 64;
+        Bat N = make(ibN0, load_raw(ibN0));  // empty (tot 0) past w1
+        uint32_t ibR = ibN0 + 64;
+        Raw R = load_raw(ibR);
+        // window (batch X, chunk c0): lane l takes chunk c0 + u * 64 + l of X's stream
+        uint32_t sj = 0;  // uniform: item of the window's first chunk (walk state of the batch)
+        auto issue = [&](const Bat &X, uint32_t c0, bool fresh, uint4 (&dst)[UG],
+                         uint32_t (&dj)[UG], uint32_t (&dc)[UG], uint32_t (&dh)[UG]) {
+            if (fresh) sj = 0;
+            uint32_t jj[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t cb = c0 + u * 64;  // uniform
+                auto ex_at = [&](uint32_t t) -> uint32_t {
+                    return t < 64 ? (uint32_t)__builtin_amdgcn_readlane(X.ex, t) : X.tot;
+                };
+                while (sj < 63 && ex_at(sj + 1) <= cb) sj++;
+                uint32_t j = sj;
+                const uint32_t c = cb + l;
+                for (uint32_t t = sj + 1; t < 64 && ex_at(t) < cb + 64; t++)
+                    j = c >= ex_at(t) ? t : j;
+                jj[u] = j;
+                dj[u] = c < X.tot ? j : 64u;
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t lo = (uint32_t)__shfl((int)X.a0lo, (int)jj[u], 64);
+                const uint32_t hi = (uint32_t)__shfl((int)X.a0hi, (int)jj[u], 64);
+                const uint32_t bx = (uint32_t)__shfl((int)X.ex, (int)jj[u], 64);
+                dh[u] = (uint32_t)__shfl((int)X.he, (int)jj[u], 64);
+                const uint32_t c = c0 + u * 64 + l;
+                dc[u] = dj[u] < 64 ? c - bx : 0u;  // past the end: chunk 0, never tested
+                const uint64_t ba = (uint64_t)lo | ((uint64_t)hi << 32);
+                dst[u] = reinterpret_cast<const uint4 *>(A.pcs + ba)[dc[u]];
+            }
+        };
+        uint4 v[UG];
+        uint32_t cj[UG], co[UG], hv[UG];
+        uint32_t c0 = 0;
+        issue(C, 0, true, v, cj, co, hv);
+        constexpr uint32_t WIN = 64 * UG;
+        for (;;) {
+            // the next window: C's next one, else N's first (N empty: nothing)
+            const bool in_c = c0 + WIN < C.tot;
+            const bool more = in_c || N.tot != 0;
+            uint4 vn[UG];
+            uint32_t nj[UG], nc[UG], nh[UG];
+            {  // straight-line: the batch is a register select, not a branch
+                Bat X;
+                X.a0lo = in_c ? C.a0lo : N.a0lo;
+                X.a0hi = in_c ? C.a0hi : N.a0hi;
+                X.he = in_c ? C.he : N.he;
+                X.ex = in_c ? C.ex : N.ex;
+                X.tot = in_c ? C.tot : N.tot;
+                issue(X, in_c ? c0 + WIN : 0u, !in_c, vn, nj, nc, nh);
+            }
+            // ---- test window v of batch C
+            uint32_t um = 0;
+            uint32_t wv[UG * 4], bit[UG * 4];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    bit[u * 4 + k] = ((vv[k] & A.keymask) - A.pc_lo - rbase) & bmask;
+                    wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
+                                         : s_cov[bit[u * 4 + k] >> 5];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t head = hv[u] & 3u, end = hv[u] >> 2;
+                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t idx = co[u] * 4 + k;
+                    const uint32_t valid =
+                        (uint32_t)(cj[u] < 64) & (uint32_t)(idx >= head) & (uint32_t)(idx < end);
+                    uint32_t unc;
+                    if (KEYM) {
+                        const uint32_t t = wv[u * 4 + k];
+                        unc = (~t >> 7) & 1u;
+                        nonmem |= valid & (uint32_t)((t & 0x7Fu) != (vv[k] >> SYZ_KEY_BITS));
+                    } else {
+                        unc = ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u;
+                    }
+                    um |= (valid & unc) << (u * 4 + k);
+                }
+            }
+            if (__ballot(um != 0)) {
+                const uint32_t cnt = (uint32_t)__popc(um);
+                const uint32_t inc2 = wave_incl_scan(cnt);
+                const uint32_t t2 = __shfl(inc2, 63, 64);
+                unsigned long long basei = 0;
+                if (l == 0) basei = atomicAdd(rctr, (unsigned long long)t2);
+                uint64_t slot = __shfl(basei, 0, 64) + (inc2 - cnt);
+#pragma unroll
+                for (int u = 0; u < UG; u++) {
+                    const int32_t rki = __shfl(C.rk, (int)(cj[u] & 63u), 64);
+                    if (!((um >> (u * 4)) & 15u)) continue;
+                    A.cand[C.ib + cj[u]] = 1;
+                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if ((um >> (u * 4 + k)) & 1u) {
+                            const uint32_t wo = (vv[k] & A.keymask) - A.pc_lo;
+                            if (slot < A.cap_k)
+                                rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                            else  // no room: its min cannot wait
+                                atomicMin(&A.first_w[wo], rki);
+                            slot++;
+                        }
+                }
+            }
+            if (!more) break;
+            if (in_c) {
+                c0 += WIN;
+            } else {  // rotate: N becomes current, R is scanned, the next raw loads go out
+                C = N;
+                N = make(ibR, R);
+                ibR += 64;
+                R = load_raw(ibR);
+                c0 = 0;
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                v[u] = vn[u];
+                cj[u] = nj[u];
+                co[u] = nc[u];
+                hv[u] = nh[u];
+            }
+        }
+    }
+    if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
+}
+
 // Region loops: block b serves region b % NCTR (the grid is a multiple of
 // NCTR), records [lo_k, min(ctr_k, cap_k)) of it.
 #define SYZ_FOR_RECORDS(A, LO, i, r)                                                          \
@@ -970,6 +1227,7 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.keymask = 0xFFFFFFFFu;
     A.low_of_key = nullptr;
     A.err = nullptr;
+    A.slice_major = getenv("SYZCOV_MR_SLICE") ? 1 : 0;  // PROBE
     A.dbg_npcs = A.dbg_nseg = ~0ull;
     A.dbg_span = pc_span;
 #ifdef SYZ_MR_DEBUG
@@ -1068,14 +1326,21 @@ static int minimize_range_impl(
     int variant = (nrange <= 16 || keym) ? 4 : 1, pmode = (nrange <= 16 || keym) ? 16 : 0;
     if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    constexpr int NVAR = 6;
+    constexpr int NVAR = 10;
     const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>,
                           mr::pass1_kernel<0x40000000, true, false, 4, 4, true>,
                           mr::pass1_kernel<512, true, false, 4, 4, true>,
                           mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<4, true, true>,
-                          mr::pass1_stream_kernel<4, true, true, true>};
-    int vi = variant >= 0 && variant < NVAR - 1 ? variant : 0;
-    if (keym) vi = 5;  // the only pass 1 that reads key words
+                          mr::pass1_stream_kernel<4, true, true, true>,
+                          mr::pass1_flow_kernel<4, false>, mr::pass1_flow_kernel<4, true>,
+                          mr::pass1_flow_kernel<3, false>, mr::pass1_flow_kernel<3, true>};
+    int vi = variant >= 0 && variant < NVAR ? variant : 0;
+    if (const char *e = getenv("SYZCOV_MR_FLOW")) {  // A/B: flow kernel, UG = 3 or 4
+        const int ug = atoi(e);
+        vi = keym ? (ug == 3 ? 9 : 7) : (ug == 3 ? 8 : 6);
+    } else if (keym) {
+        vi = 5;
+    }
     const K k1 = kern[vi];
     const bool defer = vi >= 1;
     static std::atomic<uint32_t> attr_set[NVAR];

@@ -235,7 +235,9 @@ static_assert(SPLIT_NS <= 64, "one sample per lane");
 // 0xFFFFFFFF, which is never a candidate, cover.go:43-48).  Sorted records
 // only: a record out of order is caught here at the boundaries (stats 3)
 // or inside its sub-runs by the candidate pass; non-monotone boundaries
-// become empty sub-runs.  An end outside the index space: stats 1.
+// become empty sub-runs.  An end outside the index space: stats 1.  Key
+// positions only (pc_index_range): the candidate pass checks every PC's
+// membership in the universe.
 __global__ __launch_bounds__(256) void newcov_split_kernel(
     const uint64_t *__restrict__ rec_off, const uint32_t *__restrict__ pcs,
     const uint32_t *__restrict__ perm, const uint32_t *__restrict__ coff, int ncalls, Index X,
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
         const uint32_t sl = n <= SPLIT_NS ? l : (uint32_t)(((uint64_t)l * n) >> SPLIT_LNS);
         const uint32_t x = l < ns ? p[sl] : SENT;
         uint32_t kx;
-        const bool xin = pc_index(X, x, &kx);
+        const bool xin = pc_index_range(X, x, &kx);
         uint32_t bad = (uint32_t)(l < ns && x != SENT && !xin);
         if (x == SENT || !xin) kx = 0xFFFFFFFFu;  // sorts after every query
         const uint32_t nqry = nr;  // queries 0..nr-2: range bounds; nr-1: the sentinel
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
 #pragma unroll
                 for (int g = 0; g < SQ_G; g++) {
                     uint32_t ke;
-                    const bool ein = pc_index(X, e[g], &ke);
+                    const bool ein = pc_index_range(X, e[g], &ke);
                     if (e[g] == SENT || !ein) ke = 0xFFFFFFFFu;
                     cnt[g] += (uint32_t)__popcll(__ballot(lo[g] + o + l < hi[g] && ke < v[g]));
                 }
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
         // the record's last PC, and each boundary's neighbours
         if (l == 0 && neff) {
             uint32_t kl;
-            bad |= (uint32_t)!pc_index(X, p[neff - 1], &kl);
+            bad |= (uint32_t)!pc_index_range(X, p[neff - 1], &kl);
         }
         if (l + 1 < nr && res_mine > 0 && res_mine < neff && p[res_mine - 1] > p[res_mine])
             bad |= 2u;
@@ -486,8 +488,11 @@ __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {
 // SGPRs capped: above 80 the hardware admits one 1024-thread workgroup per
 // CU instead of two (MI355X_MICROARCH.md, residency), whatever the
 // occupancy API reports.
+#ifndef SYZ_NC_KEY_WPE
+#define SYZ_NC_KEY_WPE 4  // key mode: 128 VGPRs (the deferred membership bytes) at one workgroup per CU: 0.97 vs 1.41 ms per C5 batch at 8
+#endif
 template <bool KEY>
-__global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72))) void newcov_cand_lds_kernel(
+__global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__((amdgpu_num_sgpr(72))) void newcov_cand_lds_kernel(
     const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
     uint64_t words_per_call, Index X, uint32_t nr, const uint32_t *__restrict__ ipre, uint32_t ne,
     const uint4 *__restrict__ desc, const uint4 *__restrict__ rows,
@@ -585,6 +590,28 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
         }
     };
     uint32_t sink = 0;
+    // key mode: the membership bytes of a step's rows, gathered BEFORE the next
+    // step's loads are issued, so testing them waits for this step's loads
+    // only (gathered inside the test, each wait also drained the prefetched
+    // next step: C5 1.23 ms per batch)
+    uint32_t mb[LC_U * 4];
+    auto gather = [&](uint32_t s0, const uint4 *pc) {
+        if (!KEY) return;
+#pragma unroll
+        for (int u = 0; u < LC_U; u++) {
+            const uint32_t i = (s0 + u) & 63;
+            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
+            const bool row = s0 + u < nrow;  // wave-uniform
+            const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const bool in = row && 4 * l + c >= lo && 4 * l + c < hi;
+                mb[u * 4 + c] = __builtin_amdgcn_raw_buffer_load_b8(
+                    lr, in ? (v[c] >> ks) - obase + (q << RSH) : 0xFFFFFFF0u, 0, 0);
+            }
+        }
+    };
     auto test = [&](uint32_t s0, const uint4 *pc) {
         if (dbg & 32) {  // timing probe: loads only
 #pragma unroll
@@ -601,16 +628,11 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
             // bitmap words of the four components (the word index is masked
             // into the staged range, so reads are unconditional and in flight
             // together)
-            uint32_t o[4], wd[4], mb[4];
+            uint32_t o[4], wd[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 o[c] = (KEY ? v[c] >> ks : v[c]) - obase;
                 wd[c] = s_m[(o[c] >> 5) & ((1u << (RSH - 5)) - 1)];
-                if (KEY) {
-                    const bool in = 4 * l + c >= lo && 4 * l + c < hi;
-                    mb[c] = __builtin_amdgcn_raw_buffer_load_b8(
-                        lr, in ? o[c] + (q << RSH) : 0xFFFFFFF0u, 0, 0);
-                }
             }
             // element 4l's predecessor: lane l-1's last element (DPP wave shift),
             // for lane 0 the PC before the row
@@ -626,7 +648,7 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
                 const uint64_t pm = lane_range(lo1 > (uint32_t)c ? (lo1 - c + 3) >> 2 : 0u,
                                                hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
                 bad |= __ballot((c ? v[c - 1] : p0) > v[c]) & pm;
-                if (KEY) nonmem |= __ballot(mb[c] != (v[c] & lowmask)) & vm;
+                if (KEY) nonmem |= __ballot(mb[u * 4 + c] != (v[c] & lowmask)) & vm;
                 const uint64_t cm = __ballot(!((wd[c] >> (o[c] & 31)) & 1u)) & vm;
                 if (cm) emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);  // rare
             }
@@ -654,8 +676,10 @@ __global__ __launch_bounds__(LC_THREADS, 8) __attribute__((amdgpu_num_sgpr(72)))
         // unconditional issues: a load under a branch makes the compiler drain
         // every load at the loop head, which would serialise the two buffers
         for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * LC_U) {
+            gather(s0, pcA);
             issue(s0 + LC_U, pcB);
             test(s0, pcA);
+            gather(s0 + LC_U, pcB);
             issue(s0 + 2 * LC_U, pcA);
             test(s0 + LC_U, pcB);
         }

@@ -161,17 +161,22 @@ def test_c4_closed_form_1m(torch):
     assert out is eng.out
 
 
-@pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
-def test_c5_newcov_stream_fullsize(torch, keys):
+@pytest.mark.parametrize("name,keys", [("C5", True), ("C5", False), ("C5S", True)],
+                         ids=["early-key-mode", "early-window-mode", "steady-key-mode"])
+def test_c5_newcov_stream_fullsize(torch, name, keys):
     """Config C5 at its own size (syz-fuzzer/fuzzer.go:456-480): the stream
     bench.py --workload newcov times (seed 0x5EED0005, batch b = records
     b * 65536 ..), every batch through syzcov_state_newcov_dev, is_new of each
-    batch and every call's maxCover at the end bit-identical to the oracle."""
+    batch and every call's maxCover at the end bit-identical to the oracle.
+    C5: 32 history batches + the 2 timed ones (every record still new);
+    C5S: 512 + 2, the steady state the bench reports (maxCover near
+    saturation; new counts of every batch, digests of the last two)."""
     import ctypes as C
     from syzkaller_amd import _lib
     from syzkaller_amd.engine import synth_corpus, synth_records, synth_universe, synth_window
     from syzkaller_amd.fuzzer import CoverState
-    g = golden("C5")
+    g = golden(name)
+    first_digest = g.get("is_new_sha256_first_batch", 0)
     L = _lib.lib()
     P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
     s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
@@ -198,8 +203,10 @@ def test_c5_newcov_stream_fullsize(torch, keys):
         _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc, P(is_new),
                                              P(stats), P(ws), wsz, s()), "state_newcov_dev")
         assert int(stats[0].item()) == 0, b
-        h = hashlib.sha256(is_new.cpu().numpy().tobytes()).hexdigest()
-        assert (int(is_new.sum().item()), h) == (g["new_per_batch"][b], g["is_new_sha256"][b]), b
+        assert int(is_new.sum().item()) == g["new_per_batch"][b], b
+        if b >= first_digest:
+            h = hashlib.sha256(is_new.cpu().numpy().tobytes()).hexdigest()
+            assert h == g["is_new_sha256"][b - first_digest], b
         del ws, pcs
     assert total == g["record_pcs"]
     mn = np.array([st.max_cover(c).size for c in range(g["ncalls"])], np.uint32)
