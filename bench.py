@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
 # this same bench command (tools/profile.sh -> tools/traffic.py), committed per round
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED_C1 = 0x5EED0001  # BASELINE.json configs[0]: the CPU (reference) config
 SEED = 0x5EED0002     # configs[1]: 1M inputs, one GPU
