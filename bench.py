@@ -437,7 +437,7 @@ def bench_prio(args):
                                + (", all C keys contracted" if args.prio_dense
                                   else f", active keys 0..{eng.max_len - 1}"),
                    "programs_per_gpu": nprog, "calls": eng.C,
-                   "at_rows": eng.rows if args.prio_dense else -(-eng.max_len // 128) * 128,
+                   "at_rows": eng.rows if args.prio_dense else -(-(eng.max_len + 1) // 128) * 128,
                    "at_cols": eng.ldp,
                    "parallelism": f"shard-by-program x{world}"
                                   + (", int32 SUM all-reduce of counts" if world > 1 else "")},

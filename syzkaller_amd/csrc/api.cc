@@ -31,18 +31,22 @@ void set_error(const char *fmt, ...) {
     va_end(ap);
 }
 
-// The library's one run-time override (tests of the exact fallbacks; every
-// tuning choice is a compile-time default): SYZCOV_FORCE, a comma-separated
-// list of "canon3" (key mode canonicalizes with the 3-pass window-offset sort
-// instead of the 2-pass key sort) and "redo" (every wave-canonicalized segment
-// takes the order-check-failure path, the workgroup sort of canon.hip).  Read
-// at every call, so a test can set and clear it.
+// The library's one run-time override (tests of the exact fallbacks and of
+// both candidate passes; every tuning choice is a compile-time default):
+// SYZCOV_FORCE, a comma-separated list of "canon3" (key mode canonicalizes
+// with the 3-pass window-offset sort instead of the 2-pass key sort), "redo"
+// (every wave-canonicalized segment takes the order-check-failure path, the
+// workgroup sort of canon.hip), "nc_lds" / "nc_probe" (newcov's LDS-staged or
+// global-probe candidate pass instead of the one the batch's shape picks).
+// Read at every call, so a test can set and clear it.
 uint32_t force_flags() {
     const char *e = getenv("SYZCOV_FORCE");
     if (!e || !*e) return 0;
     uint32_t f = 0;
     if (strstr(e, "canon3")) f |= FORCE_CANON3;
     if (strstr(e, "redo")) f |= FORCE_REDO;
+    if (strstr(e, "nc_lds")) f |= FORCE_NC_LDS;
+    if (strstr(e, "nc_probe")) f |= FORCE_NC_PROBE;
     return f;
 }
 

@@ -24,8 +24,7 @@
 // sub-run with a group of 4 lanes (16 items per step, 16-byte chunks, 4 in
 // flight per lane), so a load instruction covers 16 sub-runs in 64-B pieces
 // instead of 64 scattered 16-B pieces; the per-PC work is a subtract, a shift
-// and one LDS bit test.  (A whole-wave path for long
-// sub-runs remains for the SMALL_M variants.)
+// and one LDS test.
 //
 // Records go to NCTR regions of the record buffer, each with its own counter
 // (workgroup b appends to region b mod NCTR): one counter for the whole chip
@@ -53,7 +52,6 @@ namespace mr {
 
 constexpr int THREADS = 1024;
 constexpr int NWAVE = THREADS / 64;
-constexpr int UB = 4;            // 256-PC rows in flight per wave (long sub-runs)
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
@@ -98,7 +96,6 @@ struct Args {
     uint32_t keymask;          // SYZ_KEY_MASK in key mode, ~0 otherwise
     const uint8_t *low_of_key; // [nrange << rshift] bytes, 0x7F past the keys
     uint32_t *err;             // SYZCOV_ERR_UNIVERSE
-    int slice_major;           // dynamic pieces drawn slice by slice (else range by range)
 };
 
 #ifdef SYZ_MR_DEBUG
@@ -153,31 +150,6 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
         }
         __syncthreads();
     }
-}
-
-// Drop from `um` every uncovered occurrence whose PC already has a first
-// cover below rank rk: first(pc) <= first_w[pc] < rk, so the record could
-// never make rk kept and the atomicMin cannot lower first_w.  first_w only
-// decreases, so a stale read prunes less, never wrongly.  This takes the
-// same-address atomics of hot PCs out of the early chunks, where nearly every
-// PC is uncovered and the chunk's items share them.
-template <int NU>
-__device__ __forceinline__ uint32_t prune_ranked(uint32_t um, const uint4 (&v)[NU], int32_t rk,
-                                                 const Args &A) {
-    int32_t f[NU * 4];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            f[u * 4 + k] = ((um >> (u * 4 + k)) & 1u)
-                               ? A.first_w[MR_CHK(A, 2, vv[k] - A.pc_lo, A.dbg_span)]
-                               : INT32_MAX;
-    }
-#pragma unroll
-    for (int q = 0; q < NU * 4; q++)
-        if (f[q] < rk) um &= ~(1u << q);
-    return um;
 }
 
 // The range plan of a chunk: sh[j] = first piece position of range j (wave 0
@@ -238,20 +210,19 @@ __device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint
     return map_piece(A, G, P, a, b, blockIdx.x, rho, i0, i1, sh);
 }
 
-// Pass 1 over items [a, b) (one chunk).
-// SMALL_M: sub-runs up to this length take the lane-per-item path.
-// TEST = false is a tuning variant that streams the data without the
-// covered tests (not exact; selected only through SYZCOV_MR_CFG).
-template <uint32_t SMALL_M, bool TEST, bool WHOLE = false, int GS = 8, int UG = 4,
-          bool DEFER = false>
+// Pass 1 over items [a, b) (one chunk), lane groups: the window-mode form
+// for many ranges (64 at C2's 2^26-PC window, where the chunk stream measured
+// 5.2 against 3.98 ms).  GS lanes per item, 64 / GS items per step: a lane
+// group reads its sub-run in consecutive 16-byte chunks (GS * 16 B per load
+// instruction and item), so one instruction touches a few whole lines instead
+// of 64 scattered ones; UG chunks per lane are in flight.  First covers are
+// deferred to min_records_kernel.
+template <int GS = 4, int UG = 4>
 __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b, uint32_t P,
                                                         int load_cov) {
     extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
     __shared__ uint32_t s_plan[MAX_R + 1];
     uint32_t rho, i0, i1;
-#ifdef SYZ_MR_DEBUG
-    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
-#endif
     if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
     const uint32_t region = blockIdx.x % NCTR;
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
@@ -260,17 +231,10 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
     {
         const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
-        if (load_cov) {
-            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS) s4[q] = g4[q];
-        } else {  // first chunk: nothing is covered yet
-            for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
-                s4[q] = make_uint4(0, 0, 0, 0);
-        }
+        for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
+            s4[q] = load_cov ? g4[q] : make_uint4(0, 0, 0, 0);  // first chunk: none covered
     }
     __syncthreads();
-#ifdef SYZ_MR_DEBUG
-    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
-#endif
     const uint32_t l = __lane_id();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t rbase = rho << A.rshift;  // window offset of the range
@@ -285,25 +249,14 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
         int32_t rk = 0;
         if (item < w1) {
             rk = A.ranks ? A.ranks[item] : (int32_t)item;
-            uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
-            uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
-            if (WHOLE) {  // tuning probe: the whole canonical list, one range
-                s0 = 0;
-                s1 = rho == 0 ? A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + item] : 0u;
-            }
+            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
             st = A.base_r[item] + s0;
             m = s1 - s0;
 #ifdef SYZ_MR_DEBUG
             if (s1 < s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
 #endif
         }
-        // ---- (1) sub-runs up to SMALL_M PCs: GS lanes per item, 64 / GS
-        // items per step.  A lane group reads its sub-run in consecutive
-        // 16-byte chunks (GS * 16 B per load instruction and item), so one
-        // instruction touches a few whole lines instead of 64 scattered ones;
-        // UG chunks per lane are in flight.  Default GS = 4, UG = 4 (256 B
-        // per item and step): minimize 7.0 -> 4.6 ms at C2 against one lane
-        // per item (sweep: tools/sweep_mr_parity.sh).
         for (uint32_t pss = 0; pss < (uint32_t)GS; pss++) {  // 64 / GS items per step
             const uint32_t gi = l / GS, gl = l % GS, sl = pss * (64 / GS) + gi;
             const uint32_t st_lo = __shfl((uint32_t)st, sl, 64);
@@ -311,10 +264,9 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
             const uint32_t mi = __shfl(m, sl, 64);
             const int32_t rki = __shfl(rk, sl, 64);
             const uint64_t sti = (uint64_t)st_lo | ((uint64_t)st_hi << 32);
-            const bool mine = mi > 0 && mi <= SMALL_M;
             const uint64_t a0 = sti & ~3ull;
             const uint32_t head = (uint32_t)(sti - a0), end = head + mi;
-            const uint32_t nch = mine ? (end + 3) >> 2 : 0u;
+            const uint32_t nch = mi ? (end + 3) >> 2 : 0u;
             const uint32_t maxch = wave_max(nch);
             const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
             for (uint32_t c0 = 0; c0 < maxch; c0 += GS * UG) {
@@ -338,19 +290,11 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                         if (valid && bit >= nwords * 32)
                             MR_CAP8(A, 1u, ib + sl, sti, mi, idx, head, vv[k], rho);
 #endif
-                        if (TEST && WHOLE) {  // probe: window-wide test in global memory
-                            const uint32_t wo = valid ? vv[k] - A.pc_lo : 0u;
-                            um |= (uint32_t)(valid && !((A.covered[wo >> 5] >> (wo & 31)) & 1u))
-                                  << (u * 4 + k);
-                        } else if (TEST)
-                            um |= (uint32_t)(valid && !((s_cov[MR_CHK(A, 8, bit, nwords * 32) >> 5] >>
-                                                         (bit & 31)) & 1u))
-                                  << (u * 4 + k);
-                        else
-                            um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
+                        um |= (uint32_t)(valid && !((s_cov[MR_CHK(A, 8, bit, nwords * 32) >> 5] >>
+                                                     (bit & 31)) & 1u))
+                              << (u * 4 + k);
                     }
                 }
-                if (!DEFER && __ballot(um != 0)) um = prune_ranked<UG>(um, v, rki, A);
                 if (__ballot(um != 0)) {
                     // reserve this lane's records, then write them
                     const uint32_t cnt = (uint32_t)__popc(um);
@@ -368,88 +312,9 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
                             for (int k = 0; k < 4; k++)
                                 if ((um >> (u * 4 + k)) & 1u) {
                                     const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
-                                    if (!DEFER) atomicMin(&A.first_w[wo], rki);
                                     if (slot < A.cap_k)
                                         rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
-                                    else if (DEFER)  // no room: its min cannot wait
-                                        atomicMin(&A.first_w[wo], rki);
-                                    slot++;
-                                }
-                        }
-                    }
-                }
-            }
-        }
-        // ---- (2) long sub-runs: the whole wave per item, 256 PCs per row
-        uint64_t big = __ballot(m > SMALL_M);
-        while (big) {
-            const uint32_t i = __builtin_ctzll(big);
-            big &= big - 1;
-            // readlane returns int: widen through uint32_t, or a low half >= 2^31
-            // sign-extends over the high half (corpus offsets past 2^31 PCs, C3)
-            const uint64_t sti =
-                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)st, i) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(st >> 32), i) << 32);
-            const uint32_t mi = __builtin_amdgcn_readlane(m, i);
-            const int32_t rki = __builtin_amdgcn_readlane(rk, i);
-            const uint64_t a0 = sti & ~3ull;
-            const uint32_t head = (uint32_t)(sti - a0), end = head + mi;
-            const uint32_t nch = (end + 3) >> 2;
-            const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
-            for (uint32_t c0 = 0; c0 < nch; c0 += 64 * UB) {
-                uint4 v[UB];
-#pragma unroll
-                for (int u = 0; u < UB; u++) {
-                    const uint32_t ch = c0 + u * 64 + l;
-                    v[u] = ch < nch ? src[ch] : make_uint4(0, 0, 0, 0);
-                }
-                uint32_t um = 0;
-#pragma unroll
-                for (int u = 0; u < UB; u++) {
-                    const uint32_t ch = c0 + u * 64 + l;
-                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const uint32_t idx = ch * 4 + k;
-                        const bool valid = ch < nch && idx >= head && idx < end;
-                        const uint32_t bit = valid ? vv[k] - A.pc_lo - rbase : 0u;
-#ifdef SYZ_MR_DEBUG
-                        if (valid && bit >= nwords * 32)
-                            MR_CAP8(A, 2u, ib + i, sti, mi, idx, head, vv[k], rho);
-#endif
-                        if (TEST && WHOLE) {  // probe: window-wide test in global memory
-                            const uint32_t wo = valid ? vv[k] - A.pc_lo : 0u;
-                            um |= (uint32_t)(valid && !((A.covered[wo >> 5] >> (wo & 31)) & 1u))
-                                  << (u * 4 + k);
-                        } else if (TEST)
-                            um |= (uint32_t)(valid && !((s_cov[MR_CHK(A, 8, bit, nwords * 32) >> 5] >>
-                                                         (bit & 31)) & 1u))
-                                  << (u * 4 + k);
-                        else
-                            um |= (uint32_t)(valid && bit == 0xFFFFFFFFu) << (u * 4 + k);
-                    }
-                }
-                if (!DEFER && __ballot(um != 0)) um = prune_ranked<UB>(um, v, rki, A);
-                if (__ballot(um != 0)) {
-                    const uint32_t cnt = (uint32_t)__popc(um);
-                    const uint32_t incl = wave_incl_scan(cnt);
-                    const uint32_t tot = __shfl(incl, 63, 64);
-                    unsigned long long basei = 0;
-                    if (l == 0) basei = atomicAdd(rctr, (unsigned long long)tot);
-                    uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
-                    if (l == 0) A.cand[ib + i] = 1;
-                    if (um) {
-#pragma unroll
-                        for (int u = 0; u < UB; u++) {
-                            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int k = 0; k < 4; k++)
-                                if ((um >> (u * 4 + k)) & 1u) {
-                                    const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
-                                    if (!DEFER) atomicMin(&A.first_w[wo], rki);
-                                    if (slot < A.cap_k)
-                                        rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
-                                    else if (DEFER)  // no room: its min cannot wait
+                                    else  // no room: its min cannot wait
                                         atomicMin(&A.first_w[wo], rki);
                                     slot++;
                                 }
@@ -459,16 +324,6 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
             }
         }
     }
-#ifdef SYZ_MR_DEBUG
-    __syncthreads();
-    if (threadIdx.x == 0 && A.stamp) {
-        uint64_t *st = A.stamp + 4 * (uint64_t)blockIdx.x;
-        st[0] = ts0;
-        st[1] = ts1;
-        st[2] = __builtin_amdgcn_s_memrealtime();
-        st[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
-    }
-#endif
 }
 
 // Pass 1 as a CHUNK STREAM (first covers deferred to min_records_kernel).
@@ -485,9 +340,9 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
 // straight-line code, so the next UG x 64 chunks stay in flight while the
 // current ones are tested (a conditional load or test made the compiler wait
 // for every outstanding load, vmcnt(0), and for each LDS read in turn).
-// DYN: a grid of one workgroup per CU takes pieces from a counter in
-// range-major order (a piece of the same range keeps the LDS bitmap), so the
-// chunk has no tail of late, unevenly sized workgroups.
+// A grid of one workgroup per CU takes pieces from a counter in range-major
+// order (a piece of the same range keeps the LDS bitmap), so the chunk has no
+// tail of late, unevenly sized workgroups (dynamic pieces).
 // KEYM (key mode): LDS holds one byte per key of the range, the universe
 // PC's low bits (0x7F: no universe PC) | covered << 7, so the per-PC work is
 // still one LDS read: covered = byte >> 7, and the word's low bits must equal
@@ -495,7 +350,7 @@ __global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint
 // SYZCOV_ERR_UNIVERSE.  Ranges are 2^17 keys (128 KB of bytes).
 // The next batch's item descriptors are loaded while the current batch
 // streams (short sub-runs at 32 ranges made their round trip per batch show).
-template <int UG, bool TEST = true, bool DYN = false, bool KEYM = false>
+template <int UG, bool KEYM = false>
 __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t a, uint32_t b,
                                                                uint32_t P, int load_cov) {
     extern __shared__ uint32_t s_cov[];
@@ -505,10 +360,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     __shared__ uint32_t s_ex[NWAVE][64];   // first chunk of the item in the stream
     __shared__ int32_t s_rk[NWAVE][64];
     __shared__ uint32_t s_next;
-#ifdef SYZ_MR_DEBUG
-    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint32_t G = DYN ? A.npieces : gridDim.x;
+    const uint32_t G = A.npieces;
     plan_pieces(A, G, P, s_plan);
     const uint32_t region = blockIdx.x % NCTR;
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
@@ -518,23 +370,17 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     uint32_t cur_rho = 0xFFFFFFFFu;
     uint32_t nonmem = 0;  // lanes that saw a word outside the universe (KEYM)
     for (;;) {
-    uint32_t g = blockIdx.x;
-    if (DYN) {
-        if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
-        __syncthreads();
-        g = s_next;
-        __syncthreads();
-        if (g >= G) break;
-        if (!A.slice_major) {
-            const uint32_t S = G / P;  // range-major: g = position * S + slice
-            g = (g % S) * P + g / S;
-        }
+    if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+    __syncthreads();
+    uint32_t g = s_next;
+    __syncthreads();
+    if (g >= G) break;
+    {
+        const uint32_t S = G / P;  // range-major: g = position * S + slice
+        g = (g % S) * P + g / S;
     }
     uint32_t rho, i0, i1;
-    if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) {
-        if (DYN) continue;
-        return;
-    }
+    if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
     if (rho != cur_rho) {
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
         if (KEYM) {  // table bytes | covered << 7, 16 keys per uint4
@@ -568,9 +414,6 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         cur_rho = rho;
         __syncthreads();
     }
-#ifdef SYZ_MR_DEBUG
-    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();
-#endif
     const uint32_t l = __lane_id();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t rbase = rho << A.rshift;
@@ -671,8 +514,8 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     bit[u * 4 + k] = ((vv[k] & A.keymask) - A.pc_lo - rbase) & bmask;
-                    if (TEST) wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
-                                                   : s_cov[bit[u * 4 + k] >> 5];
+                    wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
+                                         : s_cov[bit[u * 4 + k] >> 5];
                 }
             }
 #pragma unroll
@@ -690,11 +533,10 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                     uint32_t unc;
                     if (KEYM) {
                         const uint32_t t = wv[u * 4 + k];
-                        unc = TEST ? (~t >> 7) & 1u : 0u;
+                        unc = (~t >> 7) & 1u;
                         nonmem |= valid & (uint32_t)((t & 0x7Fu) != (vv[k] >> SYZ_KEY_BITS));
                     } else {
-                        // TEST = false: tuning probe, the stream alone (not exact)
-                        unc = TEST ? ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u : 0u;
+                        unc = ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u;
                     }
                     um |= (valid & unc) << (u * 4 + k);
                 }
@@ -739,274 +581,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-#ifdef SYZ_MR_DEBUG
-    if (!DYN) {
-        __syncthreads();
-        if (threadIdx.x == 0 && A.stamp) {
-            uint64_t *stp = A.stamp + 4 * (uint64_t)blockIdx.x;
-            stp[0] = ts0;
-            stp[1] = ts1;
-            stp[2] = __builtin_amdgcn_s_memrealtime();
-            stp[3] = (uint64_t)rho | (uint64_t)(i1 - i0) << 8;
-        }
-    }
-#endif
-    if (!DYN) break;
     __syncthreads();  // every wave is done before the LDS bitmap is replaced
-    }
-    if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
-}
-
-// Pass 1 as ONE chunk stream per wave across its 64-item batches (FLOW).
-// The stream kernel above drains its load pipeline at every batch boundary
-// (the next batch's descriptors and first loads wait for the last test), which
-// short sub-runs make frequent: at 2^17-key ranges (key mode) a sub-run is ~64
-// PCs and a batch ~4 windows.  Here the item descriptors live in registers
-// (looked up with ds_bpermute, no LDS), three batches deep: C (being tested),
-// N (scanned, its first window issued while C's last one is tested) and R
-// (its descriptor loads in flight), so the window after C's last is N's first.
-template <int UG, bool KEYM>
-__global__ __launch_bounds__(THREADS) void pass1_flow_kernel(Args A, uint32_t a, uint32_t b,
-                                                             uint32_t P, int load_cov) {
-    extern __shared__ uint32_t s_cov[];
-    __shared__ uint32_t s_plan[MAX_R + 1];
-    __shared__ uint32_t s_next;
-    const uint32_t G = A.npieces;
-    plan_pieces(A, G, P, s_plan);
-    const uint32_t region = blockIdx.x % NCTR;
-    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
-    unsigned long long *const rrec = A.rec + region * A.cap_k;
-    const uint32_t nwords = (1u << A.rshift) >> 5;
-    const uint8_t *const s_cov8 = reinterpret_cast<const uint8_t *>(s_cov);
-    const uint32_t l = __lane_id();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t cur_rho = 0xFFFFFFFFu;
-    uint32_t nonmem = 0;
-    for (;;) {
-        if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
-        __syncthreads();
-        uint32_t g = s_next;
-        __syncthreads();
-        if (g >= G) break;
-        {
-            const uint32_t S = G / P;  // range-major: g = position * S + slice
-            g = (g % S) * P + g / S;
-        }
-        uint32_t rho, i0, i1;
-        if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
-        if (rho != cur_rho) {
-            __syncthreads();  // every wave is done with the previous range
-            uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
-            if (KEYM) {  // table bytes | covered << 7, 16 keys per uint4
-                const uint32_t nq = (1u << A.rshift) >> 4;
-                const uint4 *t4 =
-                    reinterpret_cast<const uint4 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
-                const uint32_t *cw = A.covered + (uint64_t)rho * nwords;
-                for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
-                    uint4 t = t4[q];
-                    if (load_cov) {
-                        const uint32_t cb = (cw[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
-                        auto spread = [](uint32_t x) {  // bit i -> bit 8i + 7
-                            return ((x & 1u) << 7) | ((x & 2u) << 14) | ((x & 4u) << 21) |
-                                   ((x & 8u) << 28);
-                        };
-                        t.x |= spread(cb);
-                        t.y |= spread(cb >> 4);
-                        t.z |= spread(cb >> 8);
-                        t.w |= spread(cb >> 12);
-                    }
-                    s4[q] = t;
-                }
-            } else {
-                const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
-                for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
-                    s4[q] = load_cov ? g4[q] : make_uint4(0, 0, 0, 0);
-            }
-            cur_rho = rho;
-            __syncthreads();
-        }
-        const uint32_t rbase = rho << A.rshift;
-        const uint32_t bmask = (1u << A.rshift) - 1u;
-        const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
-        const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
-        if (w0 >= w1) continue;
-        // ---- batch descriptors (lane j: item ib + j)
-        struct Raw {
-            uint32_t s0, s1;
-            uint64_t base;
-            int32_t rk;
-        };
-        struct Bat {
-            uint32_t a0lo, a0hi, he, ex, ib, tot;  // ib, tot wave-uniform
-            int32_t rk;
-        };
-        auto load_raw = [&](uint32_t ib_) {
-            Raw r{0, 0, 0, 0};
-            const uint32_t item = ib_ + l;
-            if (item < w1) {
-                r.rk = A.ranks ? A.ranks[item] : (int32_t)item;
-                r.s1 = A.split_t[(uint64_t)rho * A.n_items + item];
-                r.s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
-                r.base = A.base_r[item];
-            }
-            return r;
-        };
-        auto make = [&](uint32_t ib_, const Raw &r) {
-            Bat t;
-            const uint32_t item = ib_ + l;
-            uint32_t m = 0, nch = 0, he = 0;
-            uint64_t a0 = 0;
-            if (item < w1) {
-                const uint64_t st = r.base + r.s0;
-                m = r.s1 - r.s0;
-                a0 = st & ~3ull;
-                const uint32_t head = (uint32_t)(st - a0);
-                he = ((head + m) << 2) | head;
-                nch = m ? (head + m + 3) >> 2 : 0u;
-            }
-            const uint32_t incl = wave_incl_scan(nch);
-            t.a0lo = (uint32_t)a0;
-            t.a0hi = (uint32_t)(a0 >> 32);
-            t.he = he;
-            t.ex = incl - nch;
-            t.ib = ib_;
-            t.tot = __builtin_amdgcn_readlane(incl, 63);
-            t.rk = r.rk;
-            return t;
-        };
-        Bat C = make(w0, load_raw(w0));
-        const uint32_t ibN0 = w0 + 64;
-        Bat N = make(ibN0, load_raw(ibN0));  // empty (tot 0) past w1
-        uint32_t ibR = ibN0 + 64;
-        Raw R = load_raw(ibR);
-        // window (batch X, chunk c0): lane l takes chunk c0 + u * 64 + l of X's stream
-        uint32_t sj = 0;  // uniform: item of the window's first chunk (walk state of the batch)
-        auto issue = [&](const Bat &X, uint32_t c0, bool fresh, uint4 (&dst)[UG],
-                         uint32_t (&dj)[UG], uint32_t (&dc)[UG], uint32_t (&dh)[UG]) {
-            if (fresh) sj = 0;
-            uint32_t jj[UG];
-#pragma unroll
-            for (int u = 0; u < UG; u++) {
-                const uint32_t cb = c0 + u * 64;  // uniform
-                auto ex_at = [&](uint32_t t) -> uint32_t {
-                    return t < 64 ? (uint32_t)__builtin_amdgcn_readlane(X.ex, t) : X.tot;
-                };
-                while (sj < 63 && ex_at(sj + 1) <= cb) sj++;
-                uint32_t j = sj;
-                const uint32_t c = cb + l;
-                for (uint32_t t = sj + 1; t < 64 && ex_at(t) < cb + 64; t++)
-                    j = c >= ex_at(t) ? t : j;
-                jj[u] = j;
-                dj[u] = c < X.tot ? j : 64u;
-            }
-#pragma unroll
-            for (int u = 0; u < UG; u++) {
-                const uint32_t lo = (uint32_t)__shfl((int)X.a0lo, (int)jj[u], 64);
-                const uint32_t hi = (uint32_t)__shfl((int)X.a0hi, (int)jj[u], 64);
-                const uint32_t bx = (uint32_t)__shfl((int)X.ex, (int)jj[u], 64);
-                dh[u] = (uint32_t)__shfl((int)X.he, (int)jj[u], 64);
-                const uint32_t c = c0 + u * 64 + l;
-                dc[u] = dj[u] < 64 ? c - bx : 0u;  // past the end: chunk 0, never tested
-                const uint64_t ba = (uint64_t)lo | ((uint64_t)hi << 32);
-                dst[u] = reinterpret_cast<const uint4 *>(A.pcs + ba)[dc[u]];
-            }
-        };
-        uint4 v[UG];
-        uint32_t cj[UG], co[UG], hv[UG];
-        uint32_t c0 = 0;
-        issue(C, 0, true, v, cj, co, hv);
-        constexpr uint32_t WIN = 64 * UG;
-        for (;;) {
-            // the next window: C's next one, else N's first (N empty: nothing)
-            const bool in_c = c0 + WIN < C.tot;
-            const bool more = in_c || N.tot != 0;
-            uint4 vn[UG];
-            uint32_t nj[UG], nc[UG], nh[UG];
-            {  // straight-line: the batch is a register select, not a branch
-                Bat X;
-                X.a0lo = in_c ? C.a0lo : N.a0lo;
-                X.a0hi = in_c ? C.a0hi : N.a0hi;
-                X.he = in_c ? C.he : N.he;
-                X.ex = in_c ? C.ex : N.ex;
-                X.tot = in_c ? C.tot : N.tot;
-                issue(X, in_c ? c0 + WIN : 0u, !in_c, vn, nj, nc, nh);
-            }
-            // ---- test window v of batch C
-            uint32_t um = 0;
-            uint32_t wv[UG * 4], bit[UG * 4];
-#pragma unroll
-            for (int u = 0; u < UG; u++) {
-                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    bit[u * 4 + k] = ((vv[k] & A.keymask) - A.pc_lo - rbase) & bmask;
-                    wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
-                                         : s_cov[bit[u * 4 + k] >> 5];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < UG; u++) {
-                const uint32_t head = hv[u] & 3u, end = hv[u] >> 2;
-                const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t idx = co[u] * 4 + k;
-                    const uint32_t valid =
-                        (uint32_t)(cj[u] < 64) & (uint32_t)(idx >= head) & (uint32_t)(idx < end);
-                    uint32_t unc;
-                    if (KEYM) {
-                        const uint32_t t = wv[u * 4 + k];
-                        unc = (~t >> 7) & 1u;
-                        nonmem |= valid & (uint32_t)((t & 0x7Fu) != (vv[k] >> SYZ_KEY_BITS));
-                    } else {
-                        unc = ~(wv[u * 4 + k] >> (bit[u * 4 + k] & 31)) & 1u;
-                    }
-                    um |= (valid & unc) << (u * 4 + k);
-                }
-            }
-            if (__ballot(um != 0)) {
-                const uint32_t cnt = (uint32_t)__popc(um);
-                const uint32_t inc2 = wave_incl_scan(cnt);
-                const uint32_t t2 = __shfl(inc2, 63, 64);
-                unsigned long long basei = 0;
-                if (l == 0) basei = atomicAdd(rctr, (unsigned long long)t2);
-                uint64_t slot = __shfl(basei, 0, 64) + (inc2 - cnt);
-#pragma unroll
-                for (int u = 0; u < UG; u++) {
-                    const int32_t rki = __shfl(C.rk, (int)(cj[u] & 63u), 64);
-                    if (!((um >> (u * 4)) & 15u)) continue;
-                    A.cand[C.ib + cj[u]] = 1;
-                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        if ((um >> (u * 4 + k)) & 1u) {
-                            const uint32_t wo = (vv[k] & A.keymask) - A.pc_lo;
-                            if (slot < A.cap_k)
-                                rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
-                            else  // no room: its min cannot wait
-                                atomicMin(&A.first_w[wo], rki);
-                            slot++;
-                        }
-                }
-            }
-            if (!more) break;
-            if (in_c) {
-                c0 += WIN;
-            } else {  // rotate: N becomes current, R is scanned, the next raw loads go out
-                C = N;
-                N = make(ibR, R);
-                ibR += 64;
-                R = load_raw(ibR);
-                c0 = 0;
-            }
-#pragma unroll
-            for (int u = 0; u < UG; u++) {
-                v[u] = vn[u];
-                cj[u] = nj[u];
-                co[u] = nc[u];
-                hv[u] = nh[u];
-            }
-        }
     }
     if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
 }
@@ -1021,23 +596,7 @@ __global__ __launch_bounds__(THREADS) void pass1_flow_kernel(Args A, uint32_t a,
          i += (uint64_t)nsub_ * blockDim.x)                                                   \
         if (const unsigned long long r = rk_[i]; true)
 
-// covered |= the records appended since the last chunk.  The done marks are
-// double-buffered: chunk c reads set c % 2 and one thread per region writes
-// the new mark into the other set, so no separate advance launch is needed.
-__global__ void cover_records_kernel(Args A, int par) {
-    const unsigned long long *done_in = A.done + (par ? 1 : 0) * NCTR * CTR_STRIDE;
-    unsigned long long *done_out = A.done + (par ? 0 : 1) * NCTR * CTR_STRIDE;
-    if (blockIdx.x < NCTR && threadIdx.x == 0)
-        done_out[blockIdx.x * CTR_STRIDE] =
-            std::min<uint64_t>(A.ctr[blockIdx.x * CTR_STRIDE], A.cap_k);
-    SYZ_FOR_RECORDS(A, done_in[(blockIdx.x % NCTR) * CTR_STRIDE], i, r) {
-        const uint32_t wo = (uint32_t)r;
-        const uint32_t mbit = 1u << (wo & 31);
-        if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
-    }
-}
-
-// Deferred first covers (pass1 DEFER): first_w[pc] = min over the records
+// Deferred first covers: first_w[pc] = min over the records
 // appended since the last chunk, and covered |= them unless the caller
 // rebuilds covered from first_w.  Pass 1 then never waits on an atomic: on
 // gfx950 one counter (vmcnt) tracks loads, stores and atomics together, so an
@@ -1227,7 +786,6 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.keymask = 0xFFFFFFFFu;
     A.low_of_key = nullptr;
     A.err = nullptr;
-    A.slice_major = getenv("SYZCOV_MR_SLICE") ? 1 : 0;  // PROBE
     A.dbg_npcs = A.dbg_nseg = ~0ull;
     A.dbg_span = pc_span;
 #ifdef SYZ_MR_DEBUG
@@ -1315,53 +873,27 @@ static int minimize_range_impl(
     }
 #endif
     const size_t lds = ((size_t)1 << range_shift) / (keym ? 1 : 8);
-    // SYZCOV_MR_CFG="variant,pmode" (tuning): variant 0 = lane groups with the
-    // first-cover atomics in the streaming loop (round 1), 1 = lane groups with
-    // deferred first covers, 2 = the same with whole-wave sub-runs above 512
-    // PCs, 3 = the chunk stream over a fixed grid, 4 = the chunk stream over
-    // dynamic pieces; pmode 0 = P = 2R pieces per slice, 1 = one slice,
-    // k >= 3 = P = kR.  C2 key mode, minimize ms (tools/gpu_mrvar.sh): lane
-    // groups + whole wave 3.07 (deferred 3.00), stream 2.75 at P = 2R, 2.35 at
-    // 8R, 2.26-2.30 at 12R..32R, dynamic pieces 2.13-2.15 at 8R..32R.
-    int variant = (nrange <= 16 || keym) ? 4 : 1, pmode = (nrange <= 16 || keym) ? 16 : 0;
-    if (const char *e = getenv("SYZCOV_MR_CFG")) sscanf(e, "%d,%d", &variant, &pmode);
+    // Pass 1 form: the chunk stream over dynamic pieces for up to 16 ranges
+    // and in key mode (C2 key mode, 4 ranges: lane groups 3.00 ms, stream 2.75
+    // at P = 2R pieces per slice, 2.26-2.30 at 12R..32R, dynamic pieces 2.13 at
+    // 16R); lane groups over a fixed grid at P = 2R for the many ranges of
+    // window mode (64 at C2: 3.98 against the stream's 5.2).
+    const bool chunk_stream = nrange <= 16 || keym;
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    constexpr int NVAR = 10;
-    const K kern[NVAR] = {mr::pass1_kernel<0x40000000, true, false, 4, 4>,
-                          mr::pass1_kernel<0x40000000, true, false, 4, 4, true>,
-                          mr::pass1_kernel<512, true, false, 4, 4, true>,
-                          mr::pass1_stream_kernel<4>, mr::pass1_stream_kernel<4, true, true>,
-                          mr::pass1_stream_kernel<4, true, true, true>,
-                          mr::pass1_flow_kernel<4, false>, mr::pass1_flow_kernel<4, true>,
-                          mr::pass1_flow_kernel<3, false>, mr::pass1_flow_kernel<3, true>};
-    int vi = variant >= 0 && variant < NVAR ? variant : 0;
-    if (const char *e = getenv("SYZCOV_MR_FLOW")) {  // A/B: flow kernel, UG = 3 or 4
-        const int ug = atoi(e);
-        vi = keym ? (ug == 3 ? 9 : 7) : (ug == 3 ? 8 : 6);
-    } else if (keym) {
-        vi = 5;
-    }
-    const K k1 = kern[vi];
-    const bool defer = vi >= 1;
-    static std::atomic<uint32_t> attr_set[NVAR];
-    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[vi]))) return rc;
-    if (const char *e = getenv("SYZCOV_MR_CHUNK")) {  // tuning: "first,growth"
-        unsigned long fc = 0, gr = 0;
-        if (sscanf(e, "%lu,%lu", &fc, &gr) == 2) {
-            first_chunk = fc;
-            growth = (uint32_t)gr;
-        }
-    }
+    const K k1 = keym ? mr::pass1_stream_kernel<4, true>
+                      : chunk_stream ? mr::pass1_stream_kernel<4, false> : mr::pass1_kernel<4, 4>;
+    static std::atomic<uint32_t> attr_set[3];
+    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024,
+                               attr_set[keym ? 2 : chunk_stream ? 1 : 0])))
+        return rc;
     if (first_chunk == 0) first_chunk = 64;
     if (growth < 2) growth = 4;
-    if (const char *e = getenv("SYZCOV_MR_WG")) pcs_per_wg_hint = strtoull(e, nullptr, 0);  // tuning
-    uint64_t g_min = 256;  // at least one workgroup per CU
-    if (const char *e = getenv("SYZCOV_MR_GMIN")) g_min = strtoull(e, nullptr, 0);  // tuning
-    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;  // sweep: 2^17 4.03, 2^19 4.00, 2^20 4.40 ms
+    // sweep at C2: 2^17 PCs per workgroup 4.03, 2^19 4.00, 2^20 4.40 ms
+    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;
+    const uint64_t g_min = 256;     // at least one workgroup per CU
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
-    // below 2^24 PCs (64 MB of first_w) the covered set is rebuilt from first_w
-    bool cover_from_first = pc_span <= (1ull << 24);
-    if (const char *e = getenv("SYZCOV_MR_COVER")) cover_from_first = atoi(e) == 1;  // tuning
+    // below 2^24 keys (64 MB of first_w) the covered set is rebuilt from first_w
+    const bool cover_from_first = pc_span <= (1ull << 24);
     uint64_t a = 0, step = first_chunk;
     int par = 0;  // done-mark set of this chunk
     uint32_t nchunk = 0;
@@ -1371,12 +903,10 @@ static int minimize_range_impl(
         // P = 2R workgroups per item slice
         uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
         G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
-        uint64_t P = 2 * nrange;
-        if (pmode == 1) P = G;
-        else if (pmode >= 3) P = (uint64_t)pmode * nrange;  // more pieces per slice
+        const uint64_t P = (chunk_stream ? 16 : 2) * (uint64_t)nrange;  // pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         unsigned grid = (unsigned)G;
-        if (vi >= 4) {  // dynamic pieces: one workgroup per CU draws them
+        if (chunk_stream) {  // dynamic pieces: one workgroup per CU draws them
             if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
             A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
                                   (size_t)nchunk * 256);
@@ -1450,17 +980,14 @@ static int minimize_range_impl(
             if (b >= strtoull(e, nullptr, 0)) return SYZCOV_EINVAL;  // debug: stop before the fault
         }
 #endif
-        if (defer)  // the chunk's first covers (+ covered, unless rebuilt below)
-            hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
-                               (int)!cover_from_first);
-        if (cover_from_first) {
-            // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
-            // first_w (16 MB at 2^22 keys) instead of an atomicOr per record
-            // (C2 key mode: 5 vs 74-274 us per early chunk)
-            if (b < n_items) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
-        } else if (!defer) {
-            hipLaunchKernelGGL(mr::cover_records_kernel, dim3(1024), dim3(256), 0, s, A, par);
-        }
+        // the chunk's first covers (+ covered, unless rebuilt below)
+        hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
+                           (int)!cover_from_first);
+        // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
+        // first_w (16 MB at 2^22 keys) instead of an atomicOr per record (C2 key
+        // mode: 5 vs 74-274 us per early chunk)
+        if (cover_from_first && b < n_items)
+            RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
         par ^= 1;
         a = b;
         step *= growth;

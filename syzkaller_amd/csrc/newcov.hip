@@ -496,13 +496,11 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
     const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
     uint64_t words_per_call, Index X, uint32_t nr, const uint32_t *__restrict__ ipre, uint32_t ne,
     const uint4 *__restrict__ desc, const uint4 *__restrict__ rows,
-    const uint32_t *__restrict__ qoff, uint2 *__restrict__ clist, uint32_t *__restrict__ stats,
-    uint32_t dbg, uint64_t *__restrict__ stamp) {
+    const uint32_t *__restrict__ qoff, uint2 *__restrict__ clist, uint32_t *__restrict__ stats) {
     extern __shared__ uint4 s_m4[];  // (1 << RSH) / 128 uint4
     __shared__ uint2 s_cb[LC_THREADS / 64 * LC_CBW];  // per wave: pending candidates
     const uint32_t t = threadIdx.x, w = blockIdx.x, l = __lane_id(), wv = t >> 6;
     if (w >= ipre[ne]) return;  // grid is an upper bound
-    const uint64_t ts0 = (dbg & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint4 d = desc[w];
     const uint32_t e = d.x, c = e / nr, q = e - c * nr, r0 = d.y, r1 = d.z;
     const uint4 *R = rows + qoff[q];
@@ -589,7 +587,6 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
                                                   pr, any ? l * 16u : 0xFFFFFFF0u, any ? ra * 4u : 0u, 0));
         }
     };
-    uint32_t sink = 0;
     // key mode: the membership bytes of a step's rows, gathered BEFORE the next
     // step's loads are issued, so testing them waits for this step's loads
     // only (gathered inside the test, each wait also drained the prefetched
@@ -613,11 +610,6 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
         }
     };
     auto test = [&](uint32_t s0, const uint4 *pc) {
-        if (dbg & 32) {  // timing probe: loads only
-#pragma unroll
-            for (int u = 0; u < LC_U; u++) sink += pc[u].x ^ pc[u].w;
-            return;
-        }
 #pragma unroll
         for (int u = 0; u < LC_U; u++) {
             if (s0 + u >= nrow) break;  // wave-uniform
@@ -663,11 +655,9 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
 #pragma unroll
     for (int i = 0; i < SV; i++) {
         const uint32_t j = t + i * LC_THREADS;
-        s_m4[j] = j < nv && !(dbg & 1) ? sv[i] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        s_m4[j] = j < nv ? sv[i] : make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     __syncthreads();
-    const uint64_t ts1 = (dbg & 8) ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (dbg & 2) return;  // timing probe: staging and first loads only
     for (; rb < w1; rb += 64) {
         if (rb != w0) {
             rows64(rb);
@@ -685,22 +675,8 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
         }
     }
     if (nc) flush();
-    if (sink == 0x9E3779B9u) stats[2] = sink;
     if (bad && l == 0) stats[0] = 3u;
     if (nonmem && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
-    if (dbg & 8) {  // timing probe: per-workgroup stamps (100 MHz clock)
-        __syncthreads();
-        if (t == 0) {
-            stamp[4 * w] = ts0;
-            stamp[4 * w + 1] = ts1;
-            stamp[4 * w + 2] = __builtin_amdgcn_s_memrealtime();
-            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // XCC_ID
-            stamp[4 * w + 3] = (uint64_t)(r1 - r0) | (uint64_t)q << 24 |
-                               (uint64_t)((hw >> 8) & 0xFF) << 32 | (uint64_t)(hw >> 13 & 7) << 40 |
-                               (uint64_t)(xcc & 15) << 48;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1175,53 +1151,13 @@ extern "C" size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc) {
 // Candidate pass choice.  LDS staging (ranges of 2^19 indices, nr <= 32)
 // pays when the bitmap bytes staged (about nr x calls x 64 KB) stay well
 // under the PCs streamed; otherwise (sparse calls, huge windows) every PC
-// probes the bitmap in global memory.  SYZCOV_NEWCOV_PATH=lds|probe forces one.
-static int env_path() {  // read per batch (tests switch it)
-    const char *e = getenv("SYZCOV_NEWCOV_PATH");
-    return e ? (!strcmp(e, "lds") ? 1 : !strcmp(e, "probe") ? 2 : 0) : 0;
+// probes the bitmap in global memory.  SYZCOV_FORCE=nc_lds|nc_probe forces one.
+static int forced_path() {
+    const uint32_t f = force_flags();
+    return (f & FORCE_NC_LDS) ? 1 : (f & FORCE_NC_PROBE) ? 2 : 0;
 }
-static uint32_t env_dbg() {  // timing probes of the LDS pass (results invalid)
-    const char *e = getenv("SYZCOV_NC_DBG");
-    return e ? (uint32_t)atoi(e) : 0u;
-}
-// timing probe (SYZCOV_NC_DBG & 8): per-workgroup stamps of the LDS pass,
-// summarised to SYZCOV_NC_STAMP_FILE after each launch
-static uint64_t *g_stamp = nullptr;
-static size_t g_stamp_n = 0;
-static uint64_t *stamp_buf(uint64_t items) {
-    if (!(env_dbg() & 8)) return nullptr;
-    if (g_stamp_n < items) {
-        if (g_stamp) hipFree(g_stamp);
-        g_stamp = nullptr;
-        if (hipMalloc(&g_stamp, items * 32) != hipSuccess) return nullptr;
-        g_stamp_n = items;
-    }
-    hipMemset(g_stamp, 0, items * 32);
-    return g_stamp;
-}
-static void stamp_dump(hipStream_t s, uint64_t items) {
-    const char *fn = getenv("SYZCOV_NC_STAMP_FILE");
-    if (!g_stamp || !fn) return;
-    std::vector<uint64_t> h(items * 4);
-    hipStreamSynchronize(s);
-    hipMemcpy(h.data(), g_stamp, items * 32, hipMemcpyDeviceToHost);
-    FILE *f = fopen(fn, "a");
-    if (!f) return;
-    for (uint64_t w = 0; w < items; w++)
-        if (h[4 * w + 2])
-            fprintf(f, "%llu %llu %llu %llu %llu\n", (unsigned long long)w,
-                    (unsigned long long)h[4 * w], (unsigned long long)h[4 * w + 1],
-                    (unsigned long long)h[4 * w + 2], (unsigned long long)h[4 * w + 3]);
-    fprintf(f, "--\n");
-    fclose(f);
-}
-static uint32_t env_items() {
-    static const uint32_t v = [] {
-        const char *e = getenv("SYZCOV_NEWCOV_ITEMS");
-        return e ? (uint32_t)atoi(e) : 1024u;
-    }();
-    return v ? std::min(v, ITEMS_MAX) : 1024u;
-}
+// work items of the LDS pass per batch (64 rows at least per item)
+constexpr uint32_t NC_ITEMS = 1024;
 
 static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
                          const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
@@ -1253,7 +1189,7 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                        dim3(GS_THREADS), nc <= GRP_MAX_CALLS ? (size_t)nc * 4 : 0, s, callid,
                        (uint32_t)nrec, st->ncalls, cur, perm);
     const uint64_t nr64 = (st->X.span + (1ull << RSH) - 1) >> RSH;
-    const int forced = env_path();
+    const int forced = forced_path();
     const uint64_t range_bytes = std::min<uint64_t>(st->words * 4, 1u << (RSH - 3));
     const bool lds = nr64 <= NR_MAX && npc < (1ull << 30) &&  // buffer offsets: 4 GB of PCs
                      (forced == 1 ||
@@ -1283,13 +1219,13 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         uint32_t *rq = (uint32_t *)(ws + Lw.rq), *qoff = (uint32_t *)(ws + Lw.qoff);
         uint64_t *bq = (uint64_t *)(ws + Lw.bq);
         uint4 *rows = (uint4 *)(ws + Lw.rows);
-        // chunk: about env_items() work items over the batch, >= 64 rows, and
+        // chunk: about NC_ITEMS work items over the batch, >= 64 rows, and
         // rows <= nrows / CHR <= ITEMS_MAX, so the descriptors fit ITEMS_MAX +
         // the pairs
         const uint64_t nrows = npc / 256 + 2 * std::min<uint64_t>(npc, (uint64_t)nrec * nr) + 1;
         const uint64_t est = npc / 256 + (uint64_t)nrec * nr / 2;  // ~half a row of slack per sub-run
         const uint32_t CHR = (uint32_t)std::max<uint64_t>(
-            std::max<uint64_t>(64, (est + env_items() - 1) / env_items()),
+            std::max<uint64_t>(64, (est + NC_ITEMS - 1) / NC_ITEMS),
             (nrows + ITEMS_MAX - 1) / ITEMS_MAX);
         // sub-runs of the grouped records (records with a bad call id are not
         // grouped: coff[nc] <= nrec)
@@ -1318,15 +1254,7 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS), (size_t)(1u << (RSH - 3)), s, pcs,
                            (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
                            st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
-                           (const uint4 *)rows, (const uint32_t *)qoff, clist, stats, env_dbg(),
-                           stamp_buf(items));
-        if (env_dbg() & 8) stamp_dump(s, items);
-        if (env_dbg() & 16) {  // timing probe: occupancy of the LDS pass
-            int nb = 0;
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, LC_THREADS, 1u << (RSH - 3));
-            fprintf(stderr, "newcov LDS pass: %d workgroups/CU, %llu launched\n", nb,
-                    (unsigned long long)items);
-        }
+                           (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
     } else {
         const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
         hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off,

@@ -624,7 +624,6 @@ extern "C" int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog
     const size_t nk = ldp / PK;
     int gpx = (int)std::max<size_t>(1, std::min<size_t>((nk + 7) / 8,
                                                               (768 / 8 + ntiles - 1) / ntiles));
-    if (const char *e = getenv("SYZCOV_PRIO_GPX")) gpx = std::max(1, atoi(e));  // tuning sweeps
     const size_t splits = 8 * (size_t)gpx;
     const size_t kchunk = (nk + splits - 1) / splits * PK;
     hipLaunchKernelGGL(prio_gemm_kernel<false>, dim3((unsigned)(ntiles * splits)), dim3(256), 0,

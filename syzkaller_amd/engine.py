@@ -253,7 +253,9 @@ class PrioEngine:
         """MFMA ops one counts launch executes (upper-triangle 128x128 tiles)."""
         nt = self.rows // 128
         if self.active_rows and self.max_len is not None:
-            nt = max(1, -(-min(self.max_len, self.C) // 128))
+            # the active block holds the ones row too: roundup(min(max_len, C) + 1, 128)
+            # rows, as pos_plan sizes it (prio.hip)
+            nt = max(1, -(-(min(self.max_len, self.C) + 1) // 128))
         return nt * (nt + 1) // 2 * 128 * 128 * 2 * self.ldp
 
     def step(self, lens: torch.Tensor, ev=None, reduce=None):

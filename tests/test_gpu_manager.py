@@ -97,7 +97,7 @@ def test_new_inputs_vs_sequential():
 def newcov_path(request, monkeypatch):
     """Both candidate passes of newcov.hip: LDS-staged key ranges and global
     bitmap probes (the library picks one per batch from its shape)."""
-    monkeypatch.setenv("SYZCOV_NEWCOV_PATH", request.param)
+    monkeypatch.setenv("SYZCOV_FORCE", "nc_" + request.param)
     return request.param
 
 
