@@ -61,6 +61,20 @@ static inline unsigned grid_for(size_t n, unsigned block, unsigned cap = 1u << 1
 // ---------------------------------------------------------------- device side
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Issue fence of a software-pipelined loop: loads issued before it stay
+// before it (memory clobber), and code that reads the returned value stays
+// after it.  Without it the scheduler sinks the next batch's loads below the
+// current batch's consumers, so the in-order vmcnt wait for the current batch
+// also drains the next one (one batch in flight instead of two).
+// -DSYZ_NO_ISSUE_FENCE builds the unfenced schedule for A/B runs.
+template <typename T>
+__device__ __forceinline__ T issue_fence(T x) {
+#ifndef SYZ_NO_ISSUE_FENCE
+    asm volatile("" : "+s"(x) : : "memory");
+#endif
+    return x;
+}
+
 // Wave-wide inclusive scan of a u32 (64 lanes) in DPP, no LDS: row_shr 1, 2,
 // 4, 8 scan each row of 16 lanes (lanes shifted in from outside the row read
 // the identity 0), then row_bcast:15 adds row r-1's total to rows 1 and 3 and

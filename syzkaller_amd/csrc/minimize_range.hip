@@ -58,6 +58,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
     return v;
 }
+// inclusive prefix max over the wave's lanes (DPP, as wave_incl_scan)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
 constexpr int MAX_R = 256;
 constexpr int NCTR = 64;        // record regions (counters)
 constexpr int CTR_STRIDE = 32;  // u64s between counters (256 B: separate lines)
@@ -200,146 +210,24 @@ __device__ bool map_piece(const Args &A, uint32_t G, uint32_t P, uint32_t a, uin
     return true;
 }
 
-// Workgroup -> piece for the fixed-grid kernels.  Consecutive workgroups read
-// different ranges of the SAME segments at the same time: the sub-runs of one
-// segment are neighbours in HBM and a line shared by two ranges is still in
-// L2 when the second one asks for it.
-__device__ bool piece_of(const Args &A, uint32_t G, uint32_t P, uint32_t a, uint32_t b,
-                         uint32_t *rho, uint32_t *i0, uint32_t *i1, uint32_t *sh) {
-    plan_pieces(A, G, P, sh);
-    return map_piece(A, G, P, a, b, blockIdx.x, rho, i0, i1, sh);
-}
-
-// Pass 1 over items [a, b) (one chunk), lane groups: the window-mode form
-// for many ranges (64 at C2's 2^26-PC window, where the chunk stream measured
-// 5.2 against 3.98 ms).  GS lanes per item, 64 / GS items per step: a lane
-// group reads its sub-run in consecutive 16-byte chunks (GS * 16 B per load
-// instruction and item), so one instruction touches a few whole lines instead
-// of 64 scattered ones; UG chunks per lane are in flight.  First covers are
-// deferred to min_records_kernel.
-template <int GS = 4, int UG = 4>
-__global__ __launch_bounds__(THREADS) void pass1_kernel(Args A, uint32_t a, uint32_t b, uint32_t P,
-                                                        int load_cov) {
-    extern __shared__ uint32_t s_cov[];          // (1 << rshift) / 32 words
-    __shared__ uint32_t s_plan[MAX_R + 1];
-    uint32_t rho, i0, i1;
-    if (!piece_of(A, gridDim.x, P, a, b, &rho, &i0, &i1, s_plan)) return;
-    const uint32_t region = blockIdx.x % NCTR;
-    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
-    unsigned long long *const rrec = A.rec + region * A.cap_k;
-    const uint32_t nwords = (1u << A.rshift) >> 5;
-    {
-        const uint4 *g4 = reinterpret_cast<const uint4 *>(A.covered + (uint64_t)rho * nwords);
-        uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
-        for (uint32_t q = threadIdx.x; q < nwords / 4; q += THREADS)
-            s4[q] = load_cov ? g4[q] : make_uint4(0, 0, 0, 0);  // first chunk: none covered
-    }
-    __syncthreads();
-    const uint32_t l = __lane_id();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t rbase = rho << A.rshift;  // window offset of the range
-    // the slice is split evenly over the waves, 64 items per batch
-    const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
-    const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
-    for (uint32_t ib = w0; ib < w1; ib += 64) {
-        // ---- per-lane item descriptor: sub-run of range rho
-        const uint32_t item = ib + l;
-        uint64_t st = 0;
-        uint32_t m = 0;
-        int32_t rk = 0;
-        if (item < w1) {
-            rk = A.ranks ? A.ranks[item] : (int32_t)item;
-            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
-            const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
-            st = A.base_r[item] + s0;
-            m = s1 - s0;
-#ifdef SYZ_MR_DEBUG
-            if (s1 < s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
-#endif
-        }
-        for (uint32_t pss = 0; pss < (uint32_t)GS; pss++) {  // 64 / GS items per step
-            const uint32_t gi = l / GS, gl = l % GS, sl = pss * (64 / GS) + gi;
-            const uint32_t st_lo = __shfl((uint32_t)st, sl, 64);
-            const uint32_t st_hi = __shfl((uint32_t)(st >> 32), sl, 64);
-            const uint32_t mi = __shfl(m, sl, 64);
-            const int32_t rki = __shfl(rk, sl, 64);
-            const uint64_t sti = (uint64_t)st_lo | ((uint64_t)st_hi << 32);
-            const uint64_t a0 = sti & ~3ull;
-            const uint32_t head = (uint32_t)(sti - a0), end = head + mi;
-            const uint32_t nch = mi ? (end + 3) >> 2 : 0u;
-            const uint32_t maxch = wave_max(nch);
-            const uint4 *src = reinterpret_cast<const uint4 *>(A.pcs + a0);
-            for (uint32_t c0 = 0; c0 < maxch; c0 += GS * UG) {
-                uint4 v[UG];
-#pragma unroll
-                for (int u = 0; u < UG; u++) {
-                    const uint32_t ch = c0 + u * GS + gl;
-                    v[u] = ch < nch ? src[ch] : make_uint4(0, 0, 0, 0);
-                }
-                uint32_t um = 0;
-#pragma unroll
-                for (int u = 0; u < UG; u++) {
-                    const uint32_t ch = c0 + u * GS + gl;
-                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const uint32_t idx = ch * 4 + k;
-                        const bool valid = ch < nch && idx >= head && idx < end;
-                        const uint32_t bit = valid ? vv[k] - A.pc_lo - rbase : 0u;
-#ifdef SYZ_MR_DEBUG
-                        if (valid && bit >= nwords * 32)
-                            MR_CAP8(A, 1u, ib + sl, sti, mi, idx, head, vv[k], rho);
-#endif
-                        um |= (uint32_t)(valid && !((s_cov[MR_CHK(A, 8, bit, nwords * 32) >> 5] >>
-                                                     (bit & 31)) & 1u))
-                              << (u * 4 + k);
-                    }
-                }
-                if (__ballot(um != 0)) {
-                    // reserve this lane's records, then write them
-                    const uint32_t cnt = (uint32_t)__popc(um);
-                    const uint32_t incl = wave_incl_scan(cnt);
-                    const uint32_t tot = __shfl(incl, 63, 64);
-                    unsigned long long basei = 0;
-                    if (l == 0) basei = atomicAdd(rctr, (unsigned long long)tot);
-                    uint64_t slot = __shfl(basei, 0, 64) + (incl - cnt);
-                    if (um) {
-                        A.cand[ib + sl] = 1;
-#pragma unroll
-                        for (int u = 0; u < UG; u++) {
-                            const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int k = 0; k < 4; k++)
-                                if ((um >> (u * 4 + k)) & 1u) {
-                                    const uint32_t wo = MR_CHK(A, 4, vv[k] - A.pc_lo, A.dbg_span);
-                                    if (slot < A.cap_k)
-                                        rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
-                                    else  // no room: its min cannot wait
-                                        atomicMin(&A.first_w[wo], rki);
-                                    slot++;
-                                }
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
 // Pass 1 as a CHUNK STREAM (first covers deferred to min_records_kernel).
 // A wave takes 64 items at a time and concatenates their sub-runs into one
 // list of 16-byte chunks (an exclusive scan of the per-item chunk counts;
 // lane j holds item j's start); lane l then loads chunks l, l + 64, l + 128,
 // ... of that list.  Every load instruction is a full wave of useful 16-byte
-// pieces whatever the sub-run lengths (the lane-group and whole-wave paths
-// above idle the lanes of short or ragged sub-runs), and consecutive lanes
-// read consecutive chunks of one sub-run.  The item of a chunk comes from a
-// WAVE-UNIFORM walk over the item starts (readlane, no LDS round trips): the
-// 64 chunks of one load instruction are contiguous, so only the items that
-// start inside them are visited.  Loads and the covered tests are branch-free
-// straight-line code, so the next UG x 64 chunks stay in flight while the
-// current ones are tested (a conditional load or test made the compiler wait
-// for every outstanding load, vmcnt(0), and for each LDS read in turn).
+// pieces whatever the sub-run lengths (lane groups per item idle the lanes of
+// short or ragged sub-runs: 4.82 against 3.99 ms in window mode at C2's 64
+// ranges), and consecutive lanes read consecutive chunks of one sub-run.
+// The item of a chunk: the items starting inside a 64-chunk window mark
+// their start in a per-wave LDS row, and a DPP prefix max over the lanes
+// carries each mark forward — branch-free, three LDS operations per window.
+// (A wave-uniform walk over the item starts by readlane, serial scalar loops
+// of ~10 steps per window at 32 ranges, held pass 1 at 3.4 ms of C2's
+// 3.95 ms Minimize; the marks: 2.87 ms.)  Loads and covered tests are
+// branch-free straight-line code, so the next UG x 64 chunks stay in flight
+// while the current ones are tested (a conditional load or test made the
+// compiler wait for every outstanding load, vmcnt(0), and for each LDS read
+// in turn).  UG = 2 (UG 2 / 3 / 4: 2.85 / 2.89 / 2.95 ms key mode).
 // A grid of one workgroup per CU takes pieces from a counter in range-major
 // order (a piece of the same range keeps the LDS bitmap), so the chunk has no
 // tail of late, unevenly sized workgroups (dynamic pieces).
@@ -359,8 +247,10 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     __shared__ uint32_t s_he[NWAVE][64];   // (end << 2) | head, in PCs from s_a0
     __shared__ uint32_t s_ex[NWAVE][64];   // first chunk of the item in the stream
     __shared__ int32_t s_rk[NWAVE][64];
+    __shared__ uint32_t s_own[NWAVE][64];  // item + 1 starting at each chunk of a window
     __shared__ uint32_t s_next;
     const uint32_t G = A.npieces;
+    s_own[threadIdx.x >> 6][__lane_id()] = 0u;
     plan_pieces(A, G, P, s_plan);
     const uint32_t region = blockIdx.x % NCTR;
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
@@ -463,11 +353,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         s_rk[w][l] = rk;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        // start of item t (t <= 64; item 64 = the end of the stream)
-        auto ex_at = [&](uint32_t t) -> uint32_t {
-            return t < 64 ? (uint32_t)__builtin_amdgcn_readlane(ex_l, t) : tot;
-        };
-        uint32_t sj = 0;  // uniform: the item of the first chunk of the window
+        uint32_t sj = 0;  // uniform: the item covering the window's first chunk
         uint4 v[UG];
         uint32_t cj[UG], co[UG], hv[UG];  // item (64: past the end), chunk in it, its (end, head)
         auto issue = [&](uint32_t c0, uint4 (&dst)[UG], uint32_t (&dj)[UG], uint32_t (&dc)[UG],
@@ -476,11 +362,21 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
 #pragma unroll
             for (int u = 0; u < UG; u++) {
                 const uint32_t cb = c0 + u * 64;  // uniform
-                while (sj < 63 && ex_at(sj + 1) <= cb) sj++;
-                uint32_t j = sj;
                 const uint32_t c = cb + l;
-                for (uint32_t t = sj + 1; t < 64 && ex_at(t) < cb + 64; t++)
-                    j = c >= ex_at(t) ? t : j;
+                // the item of chunk c is the last item starting at or before c:
+                // items starting inside the window mark their start (max
+                // index + 1: empty sub-runs share a start with the next item),
+                // a prefix max over the lanes carries each mark forward, and
+                // the item covering the previous window's last chunk (sj)
+                // covers the chunks before the first mark
+                if (ex_l - cb < 64u) atomicMax(&s_own[w][ex_l - cb], l + 1u);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mk = s_own[w][l];
+                s_own[w][l] = 0u;
+                const uint32_t pm = wave_incl_max(mk);
+                const uint32_t j = pm ? max(sj, pm - 1u) : sj;
+                sj = __builtin_amdgcn_readlane(j, 63);
                 jj[u] = j;
                 dj[u] = c < tot ? j : 64u;
             }
@@ -506,6 +402,8 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
             uint4 vn[UG];
             uint32_t nj[UG], nc[UG], nh[UG];
             issue(c0 + 64 * UG, vn, nj, nc, nh);
+            // the next chunks' loads stay ahead of the current ones' tests
+            const uint32_t kmask = issue_fence(A.keymask);
             uint32_t um = 0;
             uint32_t wv[UG * 4], bit[UG * 4];
 #pragma unroll
@@ -513,7 +411,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                 const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    bit[u * 4 + k] = ((vv[k] & A.keymask) - A.pc_lo - rbase) & bmask;
+                    bit[u * 4 + k] = ((vv[k] & kmask) - A.pc_lo - rbase) & bmask;
                     wv[u * 4 + k] = KEYM ? (uint32_t)s_cov8[bit[u * 4 + k]]
                                          : s_cov[bit[u * 4 + k] >> 5];
                 }
@@ -873,19 +771,10 @@ static int minimize_range_impl(
     }
 #endif
     const size_t lds = ((size_t)1 << range_shift) / (keym ? 1 : 8);
-    // Pass 1 form: the chunk stream over dynamic pieces for up to 16 ranges
-    // and in key mode (C2 key mode, 4 ranges: lane groups 3.00 ms, stream 2.75
-    // at P = 2R pieces per slice, 2.26-2.30 at 12R..32R, dynamic pieces 2.13 at
-    // 16R); lane groups over a fixed grid at P = 2R for the many ranges of
-    // window mode (64 at C2: 3.98 against the stream's 5.2).
-    const bool chunk_stream = nrange <= 16 || keym;
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
-    const K k1 = keym ? mr::pass1_stream_kernel<4, true>
-                      : chunk_stream ? mr::pass1_stream_kernel<4, false> : mr::pass1_kernel<4, 4>;
-    static std::atomic<uint32_t> attr_set[3];
-    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024,
-                               attr_set[keym ? 2 : chunk_stream ? 1 : 0])))
-        return rc;
+    const K k1 = keym ? mr::pass1_stream_kernel<2, true> : mr::pass1_stream_kernel<2, false>;
+    static std::atomic<uint32_t> attr_set[2];
+    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[keym ? 1 : 0]))) return rc;
     if (first_chunk == 0) first_chunk = 64;
     if (growth < 2) growth = 4;
     // sweep at C2: 2^17 PCs per workgroup 4.03, 2^19 4.00, 2^20 4.40 ms
@@ -900,19 +789,16 @@ static int minimize_range_impl(
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
         // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
-        // P = 2R workgroups per item slice
         uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
         G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
-        const uint64_t P = (chunk_stream ? 16 : 2) * (uint64_t)nrange;  // pieces per slice
+        const uint64_t P = 16 * (uint64_t)nrange;  // pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
-        unsigned grid = (unsigned)G;
-        if (chunk_stream) {  // dynamic pieces: one workgroup per CU draws them
-            if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
-            A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
-                                  (size_t)nchunk * 256);
-            A.npieces = (uint32_t)G;
-            grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
-        }
+        // dynamic pieces: one workgroup per CU draws them
+        if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
+        A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
+                              (size_t)nchunk * 256);
+        A.npieces = (uint32_t)G;
+        const unsigned grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
         nchunk++;
         hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));

@@ -153,6 +153,59 @@ def test_engine_key_mode_sentinel(torch, force, monkeypatch):
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
 
 
+@pytest.mark.parametrize("force", ["", "canon3"])
+def test_engine_key_mode_clustered(torch, force, monkeypatch):
+    """Covers as real kernels produce them: runs of neighbouring PCs (a few
+    functions), repeated PCs, a few far-away PCs, in execution order: the
+    digits of a sort pass concentrate on a few histogram bins (same-address
+    LDS atomics in every wave instruction).  The key sort and the 3-pass
+    window-offset sort must give the oracle's canonical covers and Minimize
+    result (cover.go:28-40, 104-131)."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
+    from syzkaller_amd.engine import CorpusEngine
+    rng = np.random.default_rng(91)
+    univ = (np.uint64(0x81000000) + 16 * np.arange(1 << 18, dtype=np.uint64)
+            + rng.integers(0, 16, 1 << 18).astype(np.uint64)).astype(np.uint32)
+    covers = []
+    for i in range(1500):
+        kind = i % 4
+        if kind == 0:  # one dense run of neighbouring PCs
+            a = int(rng.integers(0, univ.size - 4000))
+            c = univ[a:a + int(rng.integers(1, 3500))]
+        elif kind == 1:  # a dense run plus far-away PCs: coarse buckets, a full one
+            a = int(rng.integers(0, univ.size - 2000))
+            c = np.concatenate([univ[a:a + int(rng.integers(200, 1800))],
+                                univ[rng.integers(0, univ.size, size=int(rng.integers(1, 300)))]])
+        elif kind == 2:  # few distinct PCs, each repeated (loops)
+            c = np.repeat(univ[rng.integers(0, univ.size, size=int(rng.integers(1, 60)))],
+                          int(rng.integers(1, 50)))
+        else:  # several runs
+            runs = [univ[a:a + int(rng.integers(5, 400))]
+                    for a in rng.integers(0, univ.size - 400, size=int(rng.integers(1, 8)))]
+            c = np.concatenate(runs)
+        c = c[rng.permutation(c.size)][:8000]
+        covers.append(c.astype(np.uint32))
+    lens = np.array([c.size for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers + [np.zeros(1, np.uint32)])
+    n = len(covers)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
+    eng = CorpusEngine(n, int(lens.sum()), int(lens.max()), int(univ[0]),
+                       int(univ[-1]) - int(univ[0]) + 1, universe=univ)
+    assert eng.key_mode
+    res = eng.step(off, raw, n)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs[:int(lens.sum())])
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    canon = eng.canonical_pcs(off, n).cpu().numpy().view(np.uint32)
+    for i in range(n):
+        a, b = int(o_off[i]), int(o_off[i]) + int(c_off[i + 1] - c_off[i])
+        assert np.array_equal(canon[a:b], c_pcs[c_off[i]:c_off[i + 1]]), i
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
+
+
 def _stray(u: np.ndarray, i: int) -> int:
     """A PC next to universe PC u[i] that is not in the universe."""
     us = set(u.tolist())

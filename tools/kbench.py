@@ -49,7 +49,10 @@ def main():
                                          log2_space=a.log2_space)
     univ = synth_universe(a.log2_space, 0x5EED0002) if a.keys else None
     eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=univ)
-    eng.step(off, raw, n)
+    if a.what == "canon":  # canon alone (experimental builds may not order correctly)
+        eng.canonicalize(off, raw, n)
+    else:
+        eng.step(off, raw, n)
     torch.cuda.synchronize()
     fns = {
         "canon": lambda: eng.canonicalize(off, raw, n),
