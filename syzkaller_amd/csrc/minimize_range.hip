@@ -775,8 +775,14 @@ static int minimize_range_impl(
     const K k1 = keym ? mr::pass1_stream_kernel<2, true> : mr::pass1_stream_kernel<2, false>;
     static std::atomic<uint32_t> attr_set[2];
     if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[keym ? 1 : 0]))) return rc;
-    if (first_chunk == 0) first_chunk = 64;
-    if (growth < 2) growth = 4;
+#ifndef SYZ_MR_FIRST
+#define SYZ_MR_FIRST 64
+#endif
+#ifndef SYZ_MR_GROWTH
+#define SYZ_MR_GROWTH 4
+#endif
+    if (first_chunk == 0) first_chunk = SYZ_MR_FIRST;
+    if (growth < 2) growth = SYZ_MR_GROWTH;
     // sweep at C2: 2^17 PCs per workgroup 4.03, 2^19 4.00, 2^20 4.40 ms
     if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;
     const uint64_t g_min = 256;     // at least one workgroup per CU
@@ -789,6 +795,8 @@ static int minimize_range_impl(
     while (a < n_items) {
         const uint64_t b = std::min<uint64_t>(n_items, a + step);
         // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
+        // P = 16R pieces per slice (fewer, larger pieces in the small chunks,
+        // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2)
         uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
         G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
         const uint64_t P = 16 * (uint64_t)nrange;  // pieces per slice
