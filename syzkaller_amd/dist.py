@@ -114,9 +114,10 @@ class ShardedEngine(CorpusEngine):
     PHASES = ("canon", "order", "minimize", "exchange", "finish")
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 rank: int, world: int, device="cuda", universe=None):
+                 rank: int, world: int, device="cuda", universe=None, canon_in_place=False):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
-                         n_global=n * world, rank=rank, universe=universe)
+                         n_global=n * world, rank=rank, universe=universe,
+                         canon_in_place=canon_in_place)
         self.rank, self.world, self.n_local = rank, world, n
 
     def _or_into(self, dst, src):

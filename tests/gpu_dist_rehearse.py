@@ -1,6 +1,7 @@
-"""Subprocess body for tests/test_gpu_fullsize.py::test_world8_rehearsal_c2:
+"""Subprocess body for tests/test_gpu_fullsize.py::test_world8_rehearsal_*:
 WORLD ranks of the sharded engine share cuda:0 (collectives over gloo, staged
-through the host) and process config C2's 1M-input corpus split by input
+through the host) and process config C2's 1M-input corpus (or C3's 10M,
+canonicalized in place: 82 GB of raw PCs on the one GPU) split by input
 (rank r holds global inputs [r*n, (r+1)*n)).  Rank 0 compares the kept list
 and the union with the CPU oracle's full-size digests
 (tests/golden/fullsize_digests.json) and prints OK.
@@ -28,7 +29,8 @@ def worker(rank, world, port, cfg, keys):
     off, raw, lens, total = synth_corpus(n, cfg["seed"], first=rank * n, mean=cfg["mean"],
                                          sigma=cfg["sigma"], log2_space=cfg["log2_space"])
     univ = synth_universe(cfg["log2_space"], cfg["seed"]) if keys else None
-    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world, universe=univ)
+    eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world, universe=univ,
+                        canon_in_place=cfg["n"] > 1_000_000)
     for step in range(2):  # the second step must find the engine state clean
         res = eng.step(off, raw, n)
         kept = res.kept_idx.cpu().numpy().astype("<i4").tobytes()
@@ -62,7 +64,7 @@ def main():
     for p in ps:
         p.start()
     for p in ps:
-        p.join(timeout=240)
+        p.join(timeout=240 if cfg["n"] <= 1_000_000 else 520)
     codes = [p.exitcode for p in ps]
     for p in ps:
         if p.exitcode is None:

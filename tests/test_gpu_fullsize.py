@@ -6,6 +6,7 @@ tools/gen_golden_fullsize.py from oracle/fullsize.c).
   C3  10M inputs (82 GB raw), one GPU         kept / union / order / lens digests
   C3  canonical lengths in 1M chunks + the 10M Go sort order on the device
   C2  world-8 sharded rehearsal on one GPU    kept / union / order digests
+  C3  world-8 sharded rehearsal on one GPU    kept / union / order digests (in place)
   C4  1M programs: raw co-occurrence counts against the closed form
       D[i][j] = #{p : len(p) > max(i, j)}, D[i][i] = 0 (prio.go:137-154)
   C5  the bench's new-coverage stream: 32 history batches + 2 more of 65,536
@@ -122,6 +123,21 @@ def test_world8_rehearsal_c2(torch, keys):
     import sys
     r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "8", "C2",
                         keys], capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and r.stdout.count("OK") == 8, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_world8_rehearsal_c3(torch):
+    """Eight ranks over C3 (10M inputs, 82 GB of raw PCs, 1.25M per rank,
+    canonicalized in place) on one GPU: the 8-GPU bench's workload and data
+    path, rehearsed against the ORACLE's C3 digests (kept list, union, Go
+    order over all 10M canonical lengths)."""
+    import subprocess
+    import sys
+    free, _ = torch.cuda.mem_get_info()
+    if free < 140 << 30:
+        pytest.skip(f"the C3 rehearsal needs ~110 GB of HBM, {free >> 30} GB free")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "8", "C3",
+                        "keys"], capture_output=True, text=True, timeout=560)
     assert r.returncode == 0 and r.stdout.count("OK") == 8, r.stdout[-3000:] + r.stderr[-3000:]
 
 
