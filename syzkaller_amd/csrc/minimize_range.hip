@@ -784,7 +784,13 @@ static int minimize_range_impl(
     if (first_chunk == 0) first_chunk = SYZ_MR_FIRST;
     if (growth < 2) growth = SYZ_MR_GROWTH;
     // sweep at C2: 2^17 PCs per workgroup 4.03, 2^19 4.00, 2^20 4.40 ms
-    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << 19;
+#ifndef SYZ_MR_HINT_LOG
+#define SYZ_MR_HINT_LOG 19
+#endif
+#ifndef SYZ_MR_PPS
+#define SYZ_MR_PPS 16
+#endif
+    if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << SYZ_MR_HINT_LOG;
     const uint64_t g_min = 256;     // at least one workgroup per CU
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     // below 2^24 keys (64 MB of first_w) the covered set is rebuilt from first_w
@@ -799,7 +805,7 @@ static int minimize_range_impl(
         // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2)
         uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
         G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
-        const uint64_t P = 16 * (uint64_t)nrange;  // pieces per slice
+        const uint64_t P = SYZ_MR_PPS * (uint64_t)nrange;  // pieces per slice
         G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
         // dynamic pieces: one workgroup per CU draws them
         if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
