@@ -79,7 +79,69 @@ def parse():
     ap.add_argument("--no-universe", action="store_true",
                     help="window offsets instead of the dense keys of the registered PC "
                          "universe (keys.hip), for the corpus engine and newcov's maxCover")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and the process group, run no workload (a check of "
+                         "the --gpus N launcher; runs on a host without a GPU)")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed launcher: start N rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rank r on GPU r), relay rank 0's JSON line and return the first failing
+    exit code.  This process never touches the GPU (no torch import): every
+    rank is a fresh child, never an exec of a GPU-initialised process."""
+    import socket
+    import subprocess
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      text=True))
+    import threading
+    out0 = []  # rank 0 prints one line; read on a thread so a failing rank is seen at once
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    while rc == 0 and any(p.poll() is None for p in procs):
+        time.sleep(0.2)
+        rc = next((p.returncode for p in procs if p.returncode not in (None, 0)), 0)
+    if rc != 0:  # one rank failed: the others would wait in a collective forever
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p in procs:
+        c = p.wait()
+        if rc == 0 and c != 0:
+            rc = c
+    reader.join(timeout=10)
+    sys.stdout.write("".join(out0))
+    sys.stdout.flush()
+    return rc
+
+
+def bench_dry(args):
+    """The launcher and the process group without a workload: one line with
+    the world the ranks actually formed."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = __import__("torch").ones(1)
+        dist.all_reduce(t)
+        assert int(t.item()) == world
+    out = {"metric": "dry run (no workload)", "value": None, "n_gpus": world,
+           "rccl_ranks": dist.get_world_size() if world > 1 else 1,
+           "backend": dist.get_backend() if world > 1 else None}
+    return rank, world, out
 
 
 def cpu_baseline(args):
@@ -588,8 +650,19 @@ def bench_newcov(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} ranks",
+              file=sys.stderr)
     fn = {"prio": bench_prio, "newcov": bench_newcov}.get(args.workload, bench_corpus)
-    rank, world, out = fn(args)
+    rank, world, out = (bench_dry if args.dry_run else fn)(args)
+    if world > 1:
+        import torch.distributed as dist
+        # the ranks the collectives actually ran over, and their backend
+        out["rccl_ranks"] = dist.get_world_size()
+        out["backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

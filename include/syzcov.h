@@ -320,7 +320,14 @@ int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncal
  *   key mode:    MIN all-reduce FIRST (int32 x span) -> pass2
  *   window mode: all-gather + OR COVERED (bitmap_op) -> n_ids = dense_first
  *                -> MIN all-reduce FIRST_DENSE[:n_ids] -> pass2
- *   -> MAX all-reduce KEPT[:N] (u8) -> finish -> result. */
+ *   -> MAX all-reduce KEPT[:N + 1] (u8): pass2 puts this shard's SYZCOV_ERR_*
+ *      flags in KEPT[N] and finish ORs the merged byte into the step's flags,
+ *      so every rank fails a step any shard flagged (its aliased first covers
+ *      went into the MIN merge)
+ *   -> finish -> result.
+ * A step abandoned between minimize(do_pass2 = 0) and pass2 is cleaned up by
+ * the next canon (FIRST refilled).  canon_in_place: the canonical key words
+ * replace the raw PCs, so every step must be fed raw PCs again. */
 typedef uint64_t syzcov_corpus;
 typedef struct syzcov_corpus_cfg {
     size_t n_max;        /* inputs per step on this GPU */

@@ -57,6 +57,16 @@ __global__ void corpus_clear_bit_kernel(uint32_t *covered, uint32_t bit) {
     covered[bit >> 5] &= ~(1u << (bit & 31));
 }
 
+// sharded: this shard's error flags ride in the spare kept byte through the
+// kept MAX all-reduce; finish ORs the merged byte back (every rank fails a step
+// any shard flagged: its aliased first covers went into the MIN merge)
+__global__ void corpus_err_to_kept_kernel(const uint32_t *err, uint8_t *kept_n) {
+    *kept_n = (uint8_t)(*err > 255u ? 255u : *err);
+}
+__global__ void corpus_err_from_kept_kernel(uint32_t *err, const uint8_t *kept_n) {
+    *err |= *kept_n;
+}
+
 // Minimize's LDS-resident ranges: 2^20 window PCs (128 KB of covered bits);
 // in key mode 2^17 keys (128 KB of membership bytes | covered bits)
 constexpr uint32_t kRangeShiftWindow = 20, kRangeShiftKeys = 17;
@@ -88,6 +98,7 @@ struct Corpus {
     size_t n = 0;                   // inputs of this shard in the step
     size_t N = 0;                   // inputs ordered (the global corpus when sharded)
     bool dict_ready = false;        // tab holds the dictionary of the merged union
+    bool pass2_pending = false;     // sharded pass 1 ran, its pass 2 (which resets FIRST) not yet
     // device staging of the drop-in call (grow-only)
     void *stage = nullptr;
     size_t stage_cap = 0;
@@ -196,9 +207,15 @@ static int setup(Corpus &c, const syzcov_corpus_cfg *cfg) {
         c.win_lo = c.pc_lo = g.pc_lo;
         c.win_span = c.span = g.pc_span;
     }
-    const uint64_t so = c.key_mode ? (uint64_t)(0xFFFFFFFFu >> c.kshift) - c.kbase
-                                   : (uint64_t)(0xFFFFFFFFu - c.pc_lo);
-    c.sent_key = so < c.span ? (uint32_t)so : 0xFFFFFFFFu;
+    // the key of PC 0xFFFFFFFF, which Union drops (cover.go:97).  In key mode
+    // only a universe that holds the sentinel has one: another universe PC
+    // sharing its key (pc >= 0xFFFFFFC0 at kshift 6) is an ordinary PC
+    if (c.key_mode)
+        c.sent_key = g.universe[g.universe_n - 1] == 0xFFFFFFFFu ? (uint32_t)(c.span - 1)
+                                                                 : 0xFFFFFFFFu;
+    else
+        c.sent_key = (uint64_t)(0xFFFFFFFFu - c.pc_lo) < c.span ? 0xFFFFFFFFu - c.pc_lo
+                                                                : 0xFFFFFFFFu;
     c.rshift = c.key_mode ? kRangeShiftKeys : kRangeShiftWindow;
     if (c.key_mode && c.span > (1ull << 25)) {
         set_error("key space of %llu keys > 2^25", (unsigned long long)c.span);
@@ -269,6 +286,14 @@ static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hip
     c.n = n;
     c.N = n;
     c.dict_ready = false;
+    if (c.pass2_pending) {
+        // a sharded step abandoned between pass 1 and pass 2 (e.g. a failed
+        // collective) left its ranks, and in key mode the merged ranks of every
+        // shard, in FIRST: pass 1 would atomicMin against them
+        SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)c.buf<int32_t>(SYZCOV_CORPUS_FIRST), INT32_MAX,
+                                  c.span, s));
+        c.pass2_pending = false;
+    }
     uint64_t *sc = scal(c);
     SYZ_HIP(hipMemsetAsync(sc, 0, 16 * 8, s));
     uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
@@ -347,6 +372,7 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
     const uint32_t *nl = c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN);
     const uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
     const uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
+    if (!do_pass2) c.pass2_pending = true;
     if (c.key_mode)
         return syzcov_dev_minimize_range_keys(
             c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
@@ -417,6 +443,10 @@ static int ph_pass2(Corpus &c, hipStream_t s) {
     // the other ranks' entries of the merged array too (pass 2 resets only
     // this shard's records above the fill threshold)
     if (c.key_mode) SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)first, INT32_MAX, c.span, s));
+    c.pass2_pending = false;
+    hipLaunchKernelGGL(corpus_err_to_kept_kernel, dim3(1), dim3(1), 0, s,
+                       (const uint32_t *)(scal(c) + SC_ERR), kept + c.N);
+    SYZ_LAUNCH_CHECK();
     return 0;
 }
 
@@ -424,6 +454,11 @@ static int ph_pass2(Corpus &c, hipStream_t s) {
 static int ph_finish(Corpus &c, hipStream_t s) {
     if (!c.N) return SYZCOV_EINVAL;
     uint64_t *sc = scal(c);
+    if (sharded(c)) {  // the MAX-merged error byte of every shard (ph_pass2)
+        hipLaunchKernelGGL(corpus_err_from_kept_kernel, dim3(1), dim3(1), 0, s,
+                           (uint32_t *)(sc + SC_ERR), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT) + c.N);
+        SYZ_LAUNCH_CHECK();
+    }
     void *wsx = sharded(c) ? c.buf<void>(SYZCOV_CORPUS_WS2) : c.buf<void>(SYZCOV_CORPUS_WS);
     uint64_t *tab = c.buf<uint64_t>(SYZCOV_CORPUS_TAB);
     uint32_t *covered = c.buf<uint32_t>(SYZCOV_CORPUS_COVERED);
@@ -635,8 +670,9 @@ int syzcov_corpus_destroy(syzcov_corpus h) {
     Corpus *c = get(h);
     if (!c) return 0;
     {
+        // no device-wide sync: hipFree waits for the work on the memory it
+        // frees, and caller-provided memory stays the caller's to retire
         Use u(c);
-        hipDeviceSynchronize();
         if (c->own_mem) hipFree(c->mem);
         if (c->stage) hipFree(c->stage);
     }
@@ -783,6 +819,7 @@ int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n, 
     cfg.canon_in_place = max_len <= 16384;  // the staged copy is the caller's own
     syzcov_corpus h = 0;
     int rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
+    if (rc == SYZCOV_ENOMEM) return 0;  // too big for the device now: the dictionary path
     if (rc) return rc;
     const int64_t k = syzcov_corpus_minimize_host(h, offsets, pcs, n, out_idx, nullptr, 0, nullptr);
     syzcov_corpus_destroy(h);

@@ -32,9 +32,15 @@ def worker(rank, world, port, cfg, keys):
     inplace = cfg["n"] > 1_000_000
     eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world, universe=univ,
                         canon_in_place=inplace)
-    # the second step must find the engine state clean (in place, the first
-    # step's canonical key words replaced the raw PCs: one step)
-    for step in range(1 if inplace else 2):
+    # the second step must find the engine state clean.  In place, the first
+    # step's canonical key words replaced the raw PCs, so the second step is fed
+    # raw PCs again, as a host re-feeds KCOV lists each step (syzcov.h)
+    for step in range(2):
+        if step and inplace:
+            del off, raw
+            off, raw, lens, total = synth_corpus(n, cfg["seed"], first=rank * n,
+                                                 mean=cfg["mean"], sigma=cfg["sigma"],
+                                                 log2_space=cfg["log2_space"])
         res = eng.step(off, raw, n)
         kept = res.kept_idx.cpu().numpy().astype("<i4").tobytes()
         union = res.union.cpu().numpy().astype("<i4").tobytes()

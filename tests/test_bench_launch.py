@@ -1,0 +1,48 @@
+"""bench.py --gpus N starts its own N ranks when no torch.distributed
+launcher did (the driver's `python bench.py --gpus 8`): one JSON line from
+rank 0 carrying the world the ranks formed, and a failing rank ends the run
+instead of leaving its peers in a collective."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_launcher_forms_world():
+    for n in (2, 3):
+        r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run"],
+                           capture_output=True, text=True, timeout=120, env=_env())
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        d = json.loads(lines[0])
+        assert d["n_gpus"] == n and d["rccl_ranks"] == n, d
+
+
+def test_single_rank_unchanged():
+    r = subprocess.run([sys.executable, BENCH, "--dry-run"], capture_output=True, text=True,
+                       timeout=120, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["rccl_ranks"] == 1 and d["backend"] is None
+
+
+def test_failing_ranks_end_the_run():
+    # without a GPU every rank of the real workload fails at device setup: the
+    # launcher must return their error, not hang
+    env = _env()
+    env["HIP_VISIBLE_DEVICES"] = ""  # no device even on a GPU host
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -118,3 +118,4 @@ def test_sharded_prio_counts_sum():
     exp = orc.dynamic_raw(lens, 64).astype(np.int32)
     for rank, c in res:
         assert np.array_equal(c, exp), rank
+

@@ -139,6 +139,19 @@ def test_sharded_engine_two_ranks(torch):
     assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout + r.stderr
 
 
+def test_sharded_error_reaches_every_rank(torch):
+    """Key mode, two ranks on one GPU: a non-universe PC on ONE shard fails
+    the step on EVERY rank (its aliased first covers went into the MIN merge);
+    a step abandoned after pass 1 does not poison the next one."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_dist_err.py"), "2"],
+                       capture_output=True, text=True, timeout=160)
+    assert r.returncode == 0 and r.stdout.count("OK") == 2, r.stdout + r.stderr
+
+
 def test_engine_properties_large(torch):
     """Size-independent properties at 200k inputs: union(kept) == union(all),
     kept order follows non-increasing canonical length, first kept = rank 0."""

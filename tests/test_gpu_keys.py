@@ -300,3 +300,30 @@ def test_engine_segment_longer_than_declared(torch, keys):
                        universe=synth_universe(log2, seed) if keys else None)
     with pytest.raises(RuntimeError, match="max_seg_len"):
         eng.step(off, raw, n)
+
+
+def test_engine_key_mode_top_key_not_sentinel(torch):
+    """A universe whose last PC shares the sentinel's key (0xFFFFFFC0 at
+    kshift 6) but does not hold 0xFFFFFFFF: that PC is an ordinary PC and
+    stays in the union (only 0xFFFFFFFF itself is dropped, cover.go:97)."""
+    from syzkaller_amd.engine import CorpusEngine
+    univ = (0xFFFF0000 + 64 * np.arange(1024, dtype=np.uint64)).astype(np.uint32)
+    assert univ[-1] == 0xFFFFFFC0
+    rng = np.random.default_rng(11)
+    covers = [np.sort(rng.choice(univ, size=int(rng.integers(1, 200)), replace=False))
+              for _ in range(300)]
+    covers[17] = np.array([0xFFFFFFC0], np.uint32)  # the top key alone in one input
+    lens = np.array([c.size for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers).astype(np.uint32)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32).copy()).cuda()
+    eng = CorpusEngine(len(covers), int(lens.sum()), int(lens.max()), int(univ[0]),
+                       int(univ[-1]) - int(univ[0]) + 1, universe=univ)
+    assert eng.kshift == 6 and eng.sent_key is None
+    res = eng.step(off, raw, len(covers))
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
+    un = res.union.cpu().numpy().view(np.uint32)
+    assert np.array_equal(un, orc.union_fold_csr(c_off, c_pcs)) and un[-1] == 0xFFFFFFC0
