@@ -53,6 +53,7 @@ extern "C" {
 #define SYZCOV_ERR_WINDOW 1u  /* a PC outside the configured PC window */
 #define SYZCOV_ERR_SEGLEN 2u  /* a segment longer than the declared max_seg_len */
 #define SYZCOV_ERR_UNIVERSE 4u /* key mode: a PC that is not in the registered universe */
+#define SYZCOV_ERR_ORDER 8u   /* a caller order entry outside [0, N) */
 /* Key mode: the key shift is capped so a universe PC's low kshift bits fit
  * one byte of the membership table with bit 7 free and 0x7F left for "no
  * universe PC", and a canonical key word (key | low << 26) fits 32 bits. */
@@ -359,6 +360,9 @@ typedef struct syzcov_corpus_res {
     uint64_t records;    /* first-cover records of the step */
     const int32_t *kept_idx;   /* device: kept input indices, processing order */
     const uint32_t *union_pcs; /* device: the sorted union */
+    uint32_t fallback;   /* 1: the step saw a PC outside the key space (err_flags says
+                            which) and was recomputed in window mode; results exact */
+    uint32_t reserved_;
 } syzcov_corpus_res;
 /* buffers of the layout (syzcov_corpus_buffer: byte offset in the block, size) */
 enum {
@@ -402,6 +406,12 @@ int syzcov_corpus_canon(syzcov_corpus h, const uint64_t *off, uint32_t *raw, siz
                         void *stream);
 /* lens: device int32[N] (sharded: the gathered lengths), NULL = this step's */
 int syzcov_corpus_order(syzcov_corpus h, const int32_t *lens, size_t N, void *stream);
+/* The caller's processing order instead (device int32[N]: order[r] = the
+ * input of rank r, e.g. the Go shim's own sort.Sort(minInputArray),
+ * cover.go:113; sharded: the global order, identical on every rank).  An
+ * entry outside [0, N) is replaced by 0 and fails the step (SYZCOV_ERR_ORDER);
+ * a permutation is the caller's contract (the host form checks it). */
+int syzcov_corpus_order_given(syzcov_corpus h, const int32_t *order, size_t N, void *stream);
 int syzcov_corpus_minimize(syzcov_corpus h, int do_pass2, void *stream);
 /* window mode, sharded: returns n_ids (synchronizes the stream) */
 int64_t syzcov_corpus_dense_first(syzcov_corpus h, void *stream);
@@ -411,8 +421,13 @@ int syzcov_corpus_finish(syzcov_corpus h, void *stream);
 int syzcov_corpus_step(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
                        void *stream);
 /* Synchronizes the stream; the step's counts and device result pointers.
- * SYZCOV_ERANGE (a PC outside the window or the universe) or SYZCOV_ETOOLONG
- * (an input longer than max_seg_len) if the step's results are invalid. */
+ * A PC outside the key space (key mode: not in the universe; either mode:
+ * outside the window) does not fail the step: like cover.Minimize on any u32
+ * input, it is recomputed by a window-mode engine over the step's own PC
+ * extent (res.fallback = 1; maxCover takes the union's PCs it can represent).
+ * That needs the raw PCs, so a step canonicalized in place (on device) or
+ * sharded returns SYZCOV_ERANGE instead, as does a corpus wider than 2^28 PCs;
+ * SYZCOV_ETOOLONG: an input longer than max_seg_len. */
 int syzcov_corpus_result(syzcov_corpus h, syzcov_corpus_res *res, void *stream);
 /* The drop-in form: cover.Minimize + the union fold of a host CSR corpus
  * (offsets[n + 1], pcs) through the handle; out_idx (capacity n) receives the
@@ -421,6 +436,12 @@ int syzcov_corpus_result(syzcov_corpus h, syzcov_corpus_res *res, void *stream);
 int64_t syzcov_corpus_minimize_host(syzcov_corpus h, const uint64_t *offsets, const uint32_t *pcs,
                                     size_t n, int32_t *out_idx, uint32_t *union_out,
                                     size_t union_cap, uint64_t *n_union);
+/* The same with the caller's processing order (host int32[n], a permutation
+ * of [0, n); SYZCOV_EINVAL otherwise): what the cover.Minimize shim passes. */
+int64_t syzcov_corpus_minimize_host_order(syzcov_corpus h, const uint64_t *offsets,
+                                          const uint32_t *pcs, size_t n, const int32_t *order,
+                                          int32_t *out_idx, uint32_t *union_out, size_t union_cap,
+                                          uint64_t *n_union);
 
 /* =================== 2. device-resident launch API ==================== */
 /* All pointers below are device pointers; `stream` is a hipStream_t.

@@ -82,6 +82,7 @@ _SIGS = {
     "syzcov_corpus_buffer": (C.c_int, [u64, C.c_int, p_, p_]),
     "syzcov_corpus_canon": (C.c_int, [u64, p_, p_, sz, p_]),
     "syzcov_corpus_order": (C.c_int, [u64, p_, sz, p_]),
+    "syzcov_corpus_order_given": (C.c_int, [u64, p_, sz, p_]),
     "syzcov_corpus_minimize": (C.c_int, [u64, C.c_int, p_]),
     "syzcov_corpus_dense_first": (i64, [u64, p_]),
     "syzcov_corpus_pass2": (C.c_int, [u64, p_]),
@@ -89,6 +90,7 @@ _SIGS = {
     "syzcov_corpus_step": (C.c_int, [u64, p_, p_, sz, p_]),
     "syzcov_corpus_result": (C.c_int, [u64, p_, p_]),
     "syzcov_corpus_minimize_host": (i64, [u64, p_, p_, sz, p_, p_, sz, p_]),
+    "syzcov_corpus_minimize_host_order": (i64, [u64, p_, p_, sz, p_, p_, p_, sz, p_]),
     # device tier
     "syzcov_dev_canon_ws_size": (sz, [sz, sz]),
     "syzcov_dev_canonicalize": (C.c_int, [p_, p_, p_, p_, sz, sz, p_, u32, u64, p_, p_, sz, p_]),
@@ -210,7 +212,8 @@ class CorpusInfo(C.Structure):
 class CorpusRes(C.Structure):
     """syzcov_corpus_res."""
     _fields_ = [("err_flags", u32), ("n_ids", u32), ("n_kept", u32), ("n_union", u32),
-                ("max_cover", u64), ("records", u64), ("kept_idx", p_), ("union_pcs", p_)]
+                ("max_cover", u64), ("records", u64), ("kept_idx", p_), ("union_pcs", p_),
+                ("fallback", u32), ("reserved_", u32)]
 
 
 # enum of syzcov_corpus_buffer (include/syzcov.h)

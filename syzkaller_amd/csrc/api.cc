@@ -215,12 +215,16 @@ static void release_large(Ctx *c) {
 }  // namespace syz
 
 using namespace syz;
+namespace syz {
+void dropin_trim();
+}
 
 extern "C" {
 
 const char *syzcov_version(void) { return "syzcov 0.2 gfx950"; }
 
 int syzcov_pool_trim(void) {
+    dropin_trim();  // the cached cover.Minimize engine (corpus.hip)
     CtxPool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
     int cur = 0;
@@ -337,8 +341,8 @@ namespace syz {
 // cover.Minimize calls with at least this many inputs run on the corpus
 // engine (corpus.hip); smaller ones on the dictionary path below
 constexpr size_t kEngineMinInputs = 1024;
-int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n, int32_t *out_idx,
-                        int64_t *out_n);
+int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                        const int32_t *order, int32_t *out_idx, int64_t *out_n);
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
 int ui_stats_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
                     uint32_t ncalls, const uint64_t *tab, uint32_t pc_lo, uint32_t nids,
@@ -443,11 +447,12 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
     if (n == 0) return 0;
     if (!offsets || !out_idx || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
-    // corpus-sized calls take the benchmarked engine (corpus.hip: window mode
-    // over the corpus' own PC extent, order by the raw lengths Go sorts on)
-    if (!order && sort_variant == 0 && n >= kEngineMinInputs && device_count() > 0) {
+    // corpus-sized calls take the benchmarked engine (corpus.hip: a cached
+    // window-mode handle over the corpus' own PC extent; the caller's order,
+    // or the restated sort over the raw lengths Go sorts on)
+    if ((order || sort_variant == 0) && n >= kEngineMinInputs && device_count() > 0) {
         int64_t k = 0;
-        const int rc = minimize_via_engine(offsets, pcs, n, out_idx, &k);
+        const int rc = minimize_via_engine(offsets, pcs, n, order, out_idx, &k);
         if (rc < 0) return rc;
         if (rc == 1) return k;
     }

@@ -495,6 +495,19 @@ constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
 
+// The 11-bit digit of a key.  SYZ_PROBE_NOCONF (timing probe only, wrong
+// results): a digit whose histogram word is lane-distinct within every 32-lane
+// group, i.e. the same LDS operations without bank conflicts.
+__device__ __forceinline__ uint32_t digit11(uint32_t k, uint32_t sh, uint32_t l) {
+#ifdef SYZ_PROBE_NOCONF
+    const uint32_t x = k >> sh;
+    return ((l & 31u) << 1) | (x & 1u) | (((x >> 1) & 15u) << 6);
+#else
+    (void)l;
+    return (k >> sh) & 2047u;
+#endif
+}
+
 // exclusive scan of the 2048 u16 counts in bin order, in place
 __device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(h);
@@ -539,7 +552,7 @@ __device__ __forceinline__ void count16(const uint32_t (&k)[NK], uint32_t nq, ui
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 const bool ok = real_slot<RAW, NK>(q * 4 + c, l, lo, hi);
-                const uint32_t d = (k[q * 4 + c] >> sh) & 2047u;
+                const uint32_t d = digit11(k[q * 4 + c], sh, l);
                 atomicAdd(&h[ok ? d >> 1 : KWORDS + l], ok ? hinc(d) : 1u);
             }
         }
@@ -561,7 +574,7 @@ __device__ __forceinline__ void scatter16(const uint32_t (&k)[NK], uint32_t nq, 
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++) {  // branch-free, as scatter_rows
             ok[j] = (uint32_t)(q0 + j / 4) < nq && real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
-            const uint32_t d = (k[q0 * 4 + j] >> sh) & 2047u;
+            const uint32_t d = digit11(k[q0 * 4 + j], sh, l);
             pos[j] = atomicAdd(&h[ok[j] ? d >> 1 : KWORDS + l], ok[j] ? hinc(d) : 1u) >>
                      ((d & 1u) << 4);
         }
@@ -670,6 +683,11 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
         uint32_t bad = P.force_redo;
+#ifdef SYZ_PROBE_NOCONF
+        const uint32_t probe_ok = 0;  // the probe's order is not a sort: never redo
+#else
+        const uint32_t probe_ok = 1;
+#endif
         if (inplace) {  // nothing may be written before the order is known
             uint32_t carry = P.sent_key;
 #pragma unroll
@@ -681,7 +699,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
-                        bad |= (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                        bad |= probe_ok & (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
                                (uint32_t)(e - 1u < n - 1u);
                     }
                 }
@@ -701,7 +719,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                    bad |= probe_ok & (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
                            (uint32_t)(e - 1u < n - 1u);
                     // whole words: distinct PCs stay distinct even if they share a key
                     const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);

@@ -46,6 +46,21 @@ __global__ void corpus_sel_kernel(const int32_t *__restrict__ order, uint64_t N,
     }
 }
 
+// a caller's order into ORDER; an entry outside [0, N) becomes 0 (no kernel
+// indexes past the corpus) and fails the step
+__global__ void corpus_order_copy_kernel(const int32_t *__restrict__ src, uint64_t N,
+                                         int32_t *__restrict__ dst, uint32_t *err) {
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t v = src[i];
+        const bool ok = (uint64_t)(uint32_t)v < N;
+        dst[i] = ok ? v : 0;
+        bad |= !ok;
+    }
+    if (__ballot(bad) && __lane_id() == 0) atomicOr(err, SYZCOV_ERR_ORDER);
+}
+
 __global__ void corpus_sub_kernel(int32_t *__restrict__ v, uint32_t n, int32_t base) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         v[i] -= base;
@@ -65,6 +80,56 @@ __global__ void corpus_err_to_kept_kernel(const uint32_t *err, uint8_t *kept_n) 
 }
 __global__ void corpus_err_from_kept_kernel(uint32_t *err, const uint8_t *kept_n) {
     *err |= *kept_n;
+}
+
+// maxCover |= covered, unless the step saw a PC outside the key space (its
+// covered bits may then stand for an aliased PC: the union is recomputed in
+// window mode, corpus_fallback); the popcount either way.
+__global__ __launch_bounds__(256) void corpus_merge_kernel(uint32_t *__restrict__ maxc,
+                                                           const uint32_t *__restrict__ cov,
+                                                           uint64_t nwords, const uint32_t *err,
+                                                           unsigned long long *pop) {
+    const bool skip = (*err & (SYZCOV_ERR_UNIVERSE | SYZCOV_ERR_WINDOW)) != 0;
+    uint32_t cnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t m = skip ? maxc[i] : (maxc[i] | cov[i]);
+        if (!skip) maxc[i] = m;
+        cnt += __popc(m);
+    }
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+    if (__lane_id() == 0 && cnt) atomicAdd(pop, (unsigned long long)cnt);
+}
+
+// The representable PCs of a window-mode fallback union into maxCover: key
+// mode, a PC that is its key's universe PC; window mode, a PC in the window.
+__global__ void corpus_merge_pcs_kernel(const uint32_t *__restrict__ pcs, uint32_t n,
+                                        const uint32_t *__restrict__ pc_of_key, uint32_t kshift,
+                                        uint32_t kbase, uint32_t lo, uint64_t span,
+                                        uint32_t *__restrict__ maxc) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t pc = pcs[i];
+        uint64_t b;
+        if (pc_of_key) {
+            b = (uint64_t)(pc >> kshift) - kbase;
+            if ((pc >> kshift) < kbase || b >= span || pc_of_key[b] != pc) continue;
+        } else {
+            b = (uint64_t)pc - lo;
+            if (pc < lo || b >= span) continue;
+        }
+        atomicOr(&maxc[b >> 5], 1u << (b & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void corpus_popcount_kernel(const uint32_t *__restrict__ w,
+                                                              uint64_t nwords,
+                                                              unsigned long long *pop) {
+    uint32_t cnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        cnt += __popc(w[i]);
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+    if (__lane_id() == 0 && cnt) atomicAdd(pop, (unsigned long long)cnt);
 }
 
 // Minimize's LDS-resident ranges: 2^20 window PCs (128 KB of covered bits);
@@ -94,6 +159,9 @@ struct Corpus {
     size_t ws_size = 0, ws2_size = 0;
     // per-step state
     const uint64_t *off = nullptr;  // the step's offsets (order by raw lengths)
+    const uint32_t *raw_in = nullptr;  // the step's raw PCs when canon is out of place
+    bool allow_fallback = true;     // a PC outside the key space: window-mode recompute
+    bool order_given = false;       // the step's order came from the caller (ORDER)
     uint32_t *canon = nullptr;      // the step's canonical lists (in place: the raw buffer)
     size_t n = 0;                   // inputs of this shard in the step
     size_t N = 0;                   // inputs ordered (the global corpus when sharded)
@@ -276,6 +344,9 @@ static Corpus *get(syzcov_corpus h) { return reinterpret_cast<Corpus *>(h); }
 enum { SC_ERR = 0, SC_NIDS = 1, SC_NKEPT = 2, SC_NUNION = 3, SC_MAXCOV = 4, SC_CR = 5,
        SC_CI = 6, SC_REC = 7 };
 
+// SCAL[0] bit: the step was recomputed by corpus_fallback (results valid)
+constexpr uint32_t kErrRecomputed = 1u << 31;
+
 static uint64_t *scal(const Corpus &c) { return c.buf<uint64_t>(SYZCOV_CORPUS_SCAL); }
 static bool sharded(const Corpus &c) { return c.shard; }
 
@@ -283,6 +354,7 @@ static bool sharded(const Corpus &c) { return c.shard; }
 static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hipStream_t s) {
     if (!off || !raw || n == 0 || n > c.cfg.n_max) return SYZCOV_EINVAL;
     c.off = off;
+    c.raw_in = c.cfg.canon_in_place ? nullptr : raw;
     c.n = n;
     c.N = n;
     c.dict_ready = false;
@@ -312,9 +384,9 @@ static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hip
 
 // Go's order over N lengths; also clears Minimize's inputs (queued ahead of
 // the sort, whose read-backs leave the GPU idle while the host issues).
-static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
+static int order_begin(Corpus &c, bool global, size_t N, hipStream_t s) {
     if (!c.canon) return SYZCOV_EINVAL;  // no canon phase yet
-    if (!lens32 && N != c.n) return SYZCOV_EINVAL;
+    if (!global && N != c.n) return SYZCOV_EINVAL;
     if (N < c.n || N > c.n_global) return SYZCOV_EINVAL;
     if (c.shard && (uint64_t)c.cfg.rank * c.cfg.n_max + c.n > N) return SYZCOV_EINVAL;
     c.N = N;
@@ -322,6 +394,26 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
                            s));
     SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_CAND), 0, c.n, s));
     SYZ_HIP(hipMemsetAsync(c.buf<void>(SYZCOV_CORPUS_KEPT), 0, c.sizes[SYZCOV_CORPUS_KEPT], s));
+    return 0;
+}
+
+// The caller's order (device int32[N]) instead of the restated sort.
+static int ph_order_given(Corpus &c, const int32_t *order, size_t N, hipStream_t s) {
+    if (!order) return SYZCOV_EINVAL;
+    int rc = order_begin(c, c.shard, N, s);
+    if (rc) return rc;
+    c.order_given = true;
+    hipLaunchKernelGGL(corpus_order_copy_kernel, dim3(grid_for(N, 256, 8192)), dim3(256), 0, s,
+                       order, (uint64_t)N, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
+                       (uint32_t *)(scal(c) + SC_ERR));
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
+    int rc = order_begin(c, lens32 != nullptr, N, s);
+    if (rc) return rc;
+    c.order_given = false;
     int64_t *lens = c.buf<int64_t>(SYZCOV_CORPUS_LENS);
     const uint32_t *l32 = lens32 ? (const uint32_t *)lens32
                                  : (c.cfg.order_by ? nullptr
@@ -486,8 +578,116 @@ static int ph_finish(Corpus &c, hipStream_t s) {
         hipLaunchKernelGGL(corpus_clear_bit_kernel, dim3(1), dim3(1), 0, s, covered, c.sent_key);
         SYZ_LAUNCH_CHECK();
     }
-    return syzcov_dev_bitmap_op(0, c.buf<uint32_t>(SYZCOV_CORPUS_MAX_COVER), covered, c.nwords,
-                                sc + SC_MAXCOV, s);
+    SYZ_HIP(hipMemsetAsync(sc + SC_MAXCOV, 0, 8, s));
+    hipLaunchKernelGGL(corpus_merge_kernel, dim3(grid_for(c.nwords, 256, 1024)), dim3(256), 0, s,
+                       c.buf<uint32_t>(SYZCOV_CORPUS_MAX_COVER), (const uint32_t *)covered,
+                       (uint64_t)c.nwords, (const uint32_t *)(sc + SC_ERR),
+                       (unsigned long long *)(sc + SC_MAXCOV));
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+static int ph_order_given(Corpus &c, const int32_t *order, size_t N, hipStream_t s);
+static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s);
+int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *mm, hipStream_t s);
+
+// A step that saw a PC outside the handle's key space (key mode: a PC not in
+// the registered universe, which would alias a universe PC; either mode: a PC
+// outside the window) is recomputed by a transient window-mode engine over the
+// step's own PC extent: cover.Minimize (cover.go:104-131) never fails on a u32
+// input, so neither does the handle.  It needs the raw PCs (out-of-place
+// canon; the host form restages them) and one GPU (a sharded step fails on
+// every rank instead).  The kept list and the union land in this handle's
+// buffers; maxCover takes the union's PCs it can represent.  `order`: the
+// step's own order when the caller gave it, else canonical / raw lengths as cfg.
+static int corpus_fallback(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
+    const int32_t *order = c.order_given ? c.buf<int32_t>(SYZCOV_CORPUS_ORDER) : nullptr;
+    if (c.shard || !c.raw_in || !c.off || !c.n || !c.allow_fallback) return 1;
+    uint64_t ends[2];
+    SYZ_HIP(hipMemcpyAsync(&ends[0], c.off, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipMemcpyAsync(&ends[1], c.off + c.n, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (ends[1] <= ends[0]) return 1;
+    uint32_t *mm = (uint32_t *)(scal(c) + 10);  // spare scalar words
+    int rc = minmax_pcs(c.raw_in + ends[0], ends[1] - ends[0], mm, s);
+    if (rc) return rc;
+    uint32_t hm[2];
+    SYZ_HIP(hipMemcpyAsync(hm, mm, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    const uint64_t span = (uint64_t)hm[1] - hm[0] + 1;
+    if (nrange_of(span, kRangeShiftWindow) > 256) return 1;  // too wide: the error stands
+    syzcov_corpus_cfg cfg{};
+    cfg.n_max = c.n;
+    cfg.p_max = ends[1];  // the CANON buffer is indexed by the step's absolute offsets
+    cfg.max_seg_len = c.cfg.max_seg_len;
+    cfg.pc_lo = hm[0];
+    cfg.pc_span = span;
+    cfg.order_by = c.cfg.order_by;
+    syzcov_corpus h = 0;
+    rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
+    if (rc) return rc;
+    Corpus &w = *get(h);
+    w.allow_fallback = false;
+    syzcov_corpus_res rw{};
+    {
+        std::lock_guard<std::mutex> g(w.mu);  // same device as c
+        rc = ph_canon(w, c.off, const_cast<uint32_t *>(c.raw_in), c.n, s);
+        if (!rc) rc = order ? ph_order_given(w, order, c.n, s) : ph_order(w, nullptr, c.n, s);
+        if (!rc) rc = ph_minimize(w, 1, s);
+        if (!rc) rc = ph_finish(w, s);
+        if (!rc) rc = ph_result(w, &rw, s);
+        if (!rc && rw.n_union > c.sizes[SYZCOV_CORPUS_UNION] / 4) {
+            set_error("window-mode fallback: union of %u PCs > capacity %zu", rw.n_union,
+                      c.sizes[SYZCOV_CORPUS_UNION] / 4);
+            rc = SYZCOV_ERANGE;
+        }
+        uint32_t *un = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
+        if (!rc && rw.n_kept)
+            rc = hipMemcpyAsync(c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX), rw.kept_idx,
+                                (size_t)rw.n_kept * 4, hipMemcpyDeviceToDevice, s) == hipSuccess
+                     ? 0 : SYZCOV_EHIP;
+        if (!rc && rw.n_union)
+            rc = hipMemcpyAsync(un, rw.union_pcs, (size_t)rw.n_union * 4, hipMemcpyDeviceToDevice,
+                                s) == hipSuccess ? 0 : SYZCOV_EHIP;
+        if (!rc) {  // maxCover |= the union's representable PCs
+            uint64_t *sc = scal(c);
+            uint32_t *maxc = c.buf<uint32_t>(SYZCOV_CORPUS_MAX_COVER);
+            if (rw.n_union)
+                hipLaunchKernelGGL(corpus_merge_pcs_kernel, dim3(grid_for(rw.n_union, 256, 1024)),
+                                   dim3(256), 0, s, (const uint32_t *)un, rw.n_union,
+                                   c.key_mode ? c.buf<uint32_t>(SYZCOV_CORPUS_PC_OF_KEY) : nullptr,
+                                   c.kshift, c.kbase, c.pc_lo, c.span, maxc);
+            SYZ_HIP(hipMemsetAsync(sc + SC_MAXCOV, 0, 8, s));
+            hipLaunchKernelGGL(corpus_popcount_kernel, dim3(grid_for(c.nwords, 256, 1024)),
+                               dim3(256), 0, s, (const uint32_t *)maxc, (uint64_t)c.nwords,
+                               (unsigned long long *)(sc + SC_MAXCOV));
+            SYZ_LAUNCH_CHECK();
+            uint64_t mc = 0;
+            SYZ_HIP(hipMemcpyAsync(&mc, sc + SC_MAXCOV, 8, hipMemcpyDeviceToHost, s));
+            SYZ_HIP(hipStreamSynchronize(s));
+            r->n_ids = rw.n_ids;
+            r->n_kept = rw.n_kept;
+            r->n_union = rw.n_union;
+            r->records = rw.records;
+            r->max_cover = mc;
+            r->fallback = 1;
+            // the step's scalars now describe the recomputed results (a second
+            // result call returns them without recomputing)
+            uint64_t hs[8];
+            SYZ_HIP(hipMemcpyAsync(hs, sc, sizeof hs, hipMemcpyDeviceToHost, s));
+            SYZ_HIP(hipStreamSynchronize(s));
+            hs[SC_ERR] |= kErrRecomputed;
+            hs[SC_NIDS] = rw.n_ids;
+            hs[SC_NKEPT] = rw.n_kept;
+            hs[SC_NUNION] = rw.n_union;
+            hs[SC_MAXCOV] = mc;
+            hs[SC_REC] = rw.records;
+            SYZ_HIP(hipMemcpyAsync(sc, hs, sizeof hs, hipMemcpyHostToDevice, s));
+        }
+        hipStreamSynchronize(s);
+    }
+    syzcov_corpus_destroy(h);
+    return rc;
 }
 
 static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
@@ -503,6 +703,17 @@ static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
     r->records = h[SC_REC];
     r->kept_idx = c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX);
     r->union_pcs = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
+    r->fallback = 0;
+    if (err & kErrRecomputed) {  // corpus_fallback already ran for this step
+        r->err_flags = err & ~kErrRecomputed;
+        r->fallback = 1;
+        return 0;
+    }
+    if ((err & (SYZCOV_ERR_WINDOW | SYZCOV_ERR_UNIVERSE)) &&
+        !(err & (SYZCOV_ERR_SEGLEN | SYZCOV_ERR_ORDER))) {
+        const int rc = corpus_fallback(c, r, s);
+        if (rc <= 0) return rc;  // recomputed (0) or failed (< 0); 1: not possible here
+    }
     if (err & SYZCOV_ERR_SEGLEN) {
         set_error("an input is longer than max_seg_len=%zu", c.cfg.max_seg_len);
         return SYZCOV_ETOOLONG;
@@ -514,6 +725,10 @@ static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
     if (err & SYZCOV_ERR_UNIVERSE) {
         set_error("a PC is not in the registered PC universe");
         return SYZCOV_ERANGE;
+    }
+    if (err & SYZCOV_ERR_ORDER) {
+        set_error("the processing order holds an entry outside [0, %zu)", c.N);
+        return SYZCOV_EINVAL;
     }
     if (err) {
         set_error("engine error flags %#x", err);
@@ -541,11 +756,26 @@ class Use {
 
 // cover.Minimize through an engine handle on host buffers (the drop-in
 // call): stage, step, read back.
+// Go's order must be a permutation of the inputs (host check, O(n)).
+static bool is_permutation(const int32_t *order, size_t n) {
+    std::vector<uint8_t> seen(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t v = (uint32_t)order[i];
+        if (v >= n || seen[v]) return false;
+        seen[v] = 1;
+    }
+    return true;
+}
+
 static int64_t minimize_host(Corpus &c, const uint64_t *offsets, const uint32_t *pcs, size_t n,
-                             int32_t *out_idx, uint32_t *union_out, size_t union_out_cap,
-                             uint64_t *n_union_out, hipStream_t s) {
+                             const int32_t *order, int32_t *out_idx, uint32_t *union_out,
+                             size_t union_out_cap, uint64_t *n_union_out, hipStream_t s) {
     const uint64_t base = offsets[0], P = offsets[n] - base;
     if (P > c.cfg.p_max) return SYZCOV_EINVAL;
+    if (order && !is_permutation(order, n)) {
+        set_error("the processing order is not a permutation of the %zu inputs", n);
+        return SYZCOV_EINVAL;
+    }
     std::vector<uint64_t> hoff(n + 1);
     for (size_t i = 0; i <= n; i++) {
         hoff[i] = offsets[i] - base;
@@ -555,7 +785,7 @@ static int64_t minimize_host(Corpus &c, const uint64_t *offsets, const uint32_t 
             return SYZCOV_ETOOLONG;
         }
     }
-    const size_t need = align_up((n + 1) * 8, 256) + (P + 1) * 4;
+    const size_t need = align_up((n + 1) * 8, 256) + align_up((P + 1) * 4, 256) + n * 4;
     if (need > c.stage_cap) {
         if (c.stage) {
             SYZ_HIP(hipStreamSynchronize(s));
@@ -571,14 +801,26 @@ static int64_t minimize_host(Corpus &c, const uint64_t *offsets, const uint32_t 
     }
     uint64_t *d_off = (uint64_t *)c.stage;
     uint32_t *d_pcs = (uint32_t *)((uint8_t *)c.stage + align_up((n + 1) * 8, 256));
+    int32_t *d_ord = (int32_t *)((uint8_t *)d_pcs + align_up((P + 1) * 4, 256));
     SYZ_HIP(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (P) SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
+    if (order) SYZ_HIP(hipMemcpyAsync(d_ord, order, n * 4, hipMemcpyHostToDevice, s));
     int rc = ph_canon(c, d_off, d_pcs, n, s);
-    if (!rc) rc = ph_order(c, nullptr, n, s);
+    if (!rc) rc = order ? ph_order_given(c, d_ord, n, s) : ph_order(c, nullptr, n, s);
     if (!rc) rc = ph_minimize(c, 1, s);
     if (!rc) rc = ph_finish(c, s);
     syzcov_corpus_res r{};
     if (!rc) rc = ph_result(c, &r, s);
+    if (rc == SYZCOV_ERANGE && !c.raw_in && (r.err_flags & (SYZCOV_ERR_WINDOW | SYZCOV_ERR_UNIVERSE)) &&
+        !(r.err_flags & (SYZCOV_ERR_SEGLEN | SYZCOV_ERR_ORDER)) && P) {
+        // canonicalized in place: restage the raw PCs for the window-mode recompute
+        if (hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s) == hipSuccess) {
+            c.raw_in = d_pcs;
+            const int fr = corpus_fallback(c, &r, s);
+            c.raw_in = nullptr;
+            if (fr <= 0) rc = fr;
+        }
+    }
     if (rc) {
         hipStreamSynchronize(s);
         return rc;
@@ -781,50 +1023,200 @@ int64_t syzcov_corpus_minimize_host(syzcov_corpus h, const uint64_t *offsets, co
     Use u(c);
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
-    const int64_t rc = minimize_host(*c, offsets, pcs, n, out_idx, union_out, union_cap, n_union, s);
+    const int64_t rc =
+        minimize_host(*c, offsets, pcs, n, nullptr, out_idx, union_out, union_cap, n_union, s);
     hipStreamDestroy(s);
     return rc;
 }
 
+int64_t syzcov_corpus_minimize_host_order(syzcov_corpus h, const uint64_t *offsets,
+                                          const uint32_t *pcs, size_t n, const int32_t *order,
+                                          int32_t *out_idx, uint32_t *union_out, size_t union_cap,
+                                          uint64_t *n_union) {
+    Corpus *c = get(h);
+    if (!c || !offsets || !order || !out_idx || n == 0 || n > c->cfg.n_max) return SYZCOV_EINVAL;
+    if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    Use u(c);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
+    const int64_t rc =
+        minimize_host(*c, offsets, pcs, n, order, out_idx, union_out, union_cap, n_union, s);
+    hipStreamDestroy(s);
+    return rc;
+}
+
+int syzcov_corpus_order_given(syzcov_corpus h, const int32_t *order, size_t N, void *stream) {
+    Corpus *c = get(h);
+    if (!c) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_order_given(*c, order, N, (hipStream_t)stream);
+}
+
 }  // extern "C"
 
-// cover.Minimize (syzcov_minimize, api.cc) on large corpora: a transient
-// window-mode engine over the corpus' own PC extent.  Returns 1 with the
-// count in *out_n, 0 if the corpus does not suit the engine (the caller takes
-// the dictionary path), < 0 on error.
+// cover.Minimize (syzcov_minimize, api.cc) on large corpora: a window-mode
+// engine over the corpus' own PC extent, CACHED per device across calls (a
+// manager minimizes corpora of similar size over the same kernel text, so the
+// handle is created once and reused while the corpus fits its capacity and
+// window; syzcov_pool_trim releases it).  The corpus is staged once into the
+// cache's device buffer, its PC extent taken there (one min/max pass, no host
+// scan), and the order is the caller's (Go's own sort.Sort, the shim) or the
+// restated sort over the raw lengths (Go sorts by len(cov), duplicates
+// included).  Returns 1 with the count in *out_n, 0 if the corpus does not
+// suit the engine or the device is short of memory or the cache is busy (the
+// caller takes the dictionary path), < 0 on error.
 namespace syz {
-int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n, int32_t *out_idx,
-                        int64_t *out_n) {
-    const uint64_t base = offsets[0], P = offsets[n] - base;
-    if (P == 0) return 0;
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    size_t max_len = 1;
-    for (size_t i = 0; i < n; i++) {
-        if (offsets[i + 1] < offsets[i]) return SYZCOV_EINVAL;
-        max_len = std::max<size_t>(max_len, offsets[i + 1] - offsets[i]);
-    }
-    for (uint64_t k = base; k < base + P; k++) {
-        lo = std::min(lo, pcs[k]);
-        hi = std::max(hi, pcs[k]);
-    }
-    const uint64_t span = (uint64_t)hi - lo + 1;
-    if (nrange_of(span, kRangeShiftWindow) > 256) return 0;
-    syzcov_corpus_cfg cfg{};
-    cfg.n_max = n;
-    cfg.p_max = P;
-    cfg.max_seg_len = max_len;
-    cfg.pc_lo = lo;
-    cfg.pc_span = span;
-    cfg.order_by = 1;  // Go sorts by len(cov), duplicates included
-    cfg.canon_in_place = max_len <= 16384;  // the staged copy is the caller's own
+int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *mm, hipStream_t s);
+
+struct DropinCache {
+    std::mutex mu;
     syzcov_corpus h = 0;
-    int rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
-    if (rc == SYZCOV_ENOMEM) return 0;  // too big for the device now: the dictionary path
+    size_t n_cap = 0, seg_cap = 0;
+    uint64_t p_cap = 0;
+    uint32_t lo = 0;
+    uint64_t span = 0;
+    void *stage = nullptr;  // off u64[n+1] | pcs u32[P+1] | order i32[n] | min/max
+    size_t stage_cap = 0;
+};
+constexpr int kMaxDev = 16;
+static DropinCache g_dropin[kMaxDev];
+
+static void dropin_release(DropinCache &dc) {
+    if (dc.h) syzcov_corpus_destroy(dc.h);
+    if (dc.stage) hipFree(dc.stage);
+    dc.h = 0;
+    dc.stage = nullptr;
+    dc.stage_cap = dc.n_cap = dc.seg_cap = dc.p_cap = dc.span = 0;
+}
+
+void dropin_trim() {
+    int cur = 0;
+    hipGetDevice(&cur);
+    for (int d = 0; d < kMaxDev; d++) {
+        std::lock_guard<std::mutex> g(g_dropin[d].mu);
+        if (!g_dropin[d].h && !g_dropin[d].stage) continue;
+        hipSetDevice(d);
+        dropin_release(g_dropin[d]);
+    }
+    hipSetDevice(cur);
+}
+
+// the handle for a corpus of n inputs / P PCs / longest max_len over [lo, hi]
+static int dropin_handle(DropinCache &dc, size_t n, uint64_t P, size_t max_len, uint32_t lo,
+                         uint32_t hi) {
+    if (dc.h && n <= dc.n_cap && P <= dc.p_cap && max_len <= dc.seg_cap && lo >= dc.lo &&
+        (uint64_t)hi - dc.lo < dc.span)
+        return 1;
+    // grow: capacities only rise, the window widens to cover both corpora
+    // (whole 2^20-PC ranges) while it stays within the engine's 256 ranges
+    uint64_t nlo = lo, nhi = hi;
+    if (dc.h) {
+        nlo = std::min<uint64_t>(lo, dc.lo);
+        nhi = std::max<uint64_t>(hi, dc.lo + dc.span - 1);
+    }
+    nlo &= ~((1ull << kRangeShiftWindow) - 1);
+    if (nrange_of(nhi - nlo + 1, kRangeShiftWindow) > 256) {
+        nlo = lo & ~((1ull << kRangeShiftWindow) - 1);
+        nhi = hi;
+    }
+    nhi = std::min<uint64_t>(0xFFFFFFFFull, nhi);
+    syzcov_corpus_cfg cfg{};
+    cfg.n_max = std::max(n, dc.n_cap);
+    cfg.p_max = std::max<uint64_t>(P, dc.p_cap);
+    cfg.max_seg_len = std::max(max_len, dc.seg_cap);
+    cfg.pc_lo = (uint32_t)nlo;
+    cfg.pc_span = nhi - nlo + 1;
+    cfg.order_by = 1;  // Go sorts by len(cov), duplicates included
+    cfg.canon_in_place = cfg.max_seg_len <= 16384;  // the staged copy is the cache's own
+    if (dc.h) syzcov_corpus_destroy(dc.h);
+    dc.h = 0;
+    int rc = syzcov_corpus_create(&cfg, nullptr, 0, &dc.h);
+    if (rc == SYZCOV_ENOMEM && (cfg.n_max > n || cfg.p_max > P)) {  // retry at this corpus' size
+        cfg.n_max = n;
+        cfg.p_max = P;
+        rc = syzcov_corpus_create(&cfg, nullptr, 0, &dc.h);
+    }
+    if (rc) {
+        dc.h = 0;
+        return rc == SYZCOV_ENOMEM ? 0 : rc;
+    }
+    dc.n_cap = cfg.n_max;
+    dc.p_cap = cfg.p_max;
+    dc.seg_cap = cfg.max_seg_len;
+    dc.lo = cfg.pc_lo;
+    dc.span = cfg.pc_span;
+    return 1;
+}
+
+static int64_t dropin_run(DropinCache &dc, const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                          const int32_t *order, int32_t *out_idx, hipStream_t s) {
+    const uint64_t base = offsets[0], P = offsets[n] - base;
+    size_t max_len = 1;
+    std::vector<uint64_t> hoff(n + 1);
+    for (size_t i = 0; i <= n; i++) {
+        hoff[i] = offsets[i] - base;
+        if (i && hoff[i] < hoff[i - 1]) return SYZCOV_EINVAL;
+        if (i) max_len = std::max<size_t>(max_len, hoff[i] - hoff[i - 1]);
+    }
+    if (order && !is_permutation(order, n)) {
+        set_error("the processing order is not a permutation of the %zu inputs", n);
+        return SYZCOV_EINVAL;
+    }
+    const size_t o_pcs = align_up((n + 1) * 8, 256), o_ord = o_pcs + align_up((P + 1) * 4, 256),
+                 o_mm = o_ord + align_up(n * 4, 256), need = o_mm + 256;
+    if (need > dc.stage_cap) {
+        if (dc.stage) hipFree(dc.stage);
+        dc.stage = nullptr;
+        dc.stage_cap = 0;
+        if (hipMalloc(&dc.stage, need) != hipSuccess) return 0;  // short of memory: dictionary path
+        dc.stage_cap = need;
+    }
+    uint8_t *st = (uint8_t *)dc.stage;
+    uint64_t *d_off = (uint64_t *)st;
+    uint32_t *d_pcs = (uint32_t *)(st + o_pcs), *d_mm = (uint32_t *)(st + o_mm);
+    int32_t *d_ord = (int32_t *)(st + o_ord);
+    SYZ_HIP(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
+    if (order) SYZ_HIP(hipMemcpyAsync(d_ord, order, n * 4, hipMemcpyHostToDevice, s));
+    int rc = minmax_pcs(d_pcs, P, d_mm, s);
     if (rc) return rc;
-    const int64_t k = syzcov_corpus_minimize_host(h, offsets, pcs, n, out_idx, nullptr, 0, nullptr);
-    syzcov_corpus_destroy(h);
-    if (k < 0) return (int)k;
-    *out_n = k;
+    uint32_t mm[2];
+    SYZ_HIP(hipMemcpyAsync(mm, d_mm, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (nrange_of((uint64_t)mm[1] - mm[0] + 1, kRangeShiftWindow) > 256) return 0;
+    rc = dropin_handle(dc, n, P, max_len, mm[0], mm[1]);
+    if (rc <= 0) return rc;
+    Corpus &c = *get(dc.h);
+    Use u(&c);
+    rc = ph_canon(c, d_off, d_pcs, n, s);
+    if (!rc) rc = order ? ph_order_given(c, d_ord, n, s) : ph_order(c, nullptr, n, s);
+    if (!rc) rc = ph_minimize(c, 1, s);
+    if (!rc) rc = ph_finish(c, s);
+    syzcov_corpus_res r{};
+    if (!rc) rc = ph_result(c, &r, s);
+    if (!rc && r.n_kept)
+        rc = hipMemcpyAsync(out_idx, r.kept_idx, (size_t)r.n_kept * 4, hipMemcpyDeviceToHost, s) ==
+                     hipSuccess
+                 ? 0
+                 : SYZCOV_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = SYZCOV_EHIP;
+    return rc ? rc : (int64_t)r.n_kept + 1;  // + 1: 0 means "not taken"
+}
+
+int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,
+                        const int32_t *order, int32_t *out_idx, int64_t *out_n) {
+    if (offsets[n] == offsets[0]) return 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    DropinCache &dc = g_dropin[dev];
+    std::unique_lock<std::mutex> lk(dc.mu, std::try_to_lock);
+    if (!lk.owns_lock()) return 0;  // another caller holds the cached engine
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
+    const int64_t k = dropin_run(dc, offsets, pcs, n, order, out_idx, s);
+    hipStreamDestroy(s);
+    if (k <= 0) return (int)k;
+    *out_n = k - 1;
     return 1;
 }
 }  // namespace syz

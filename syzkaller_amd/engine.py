@@ -53,6 +53,8 @@ class StepResult:
     n_union: int
     n_ids: int                  # distinct PCs in the corpus (incl. a 0xFFFFFFFF sentinel)
     max_cover: int              # |maxCover| after the merge
+    fallback: bool = False      # a PC outside the key space: recomputed in window mode
+    err_flags: int = 0          # SYZCOV_ERR_* bits the step saw (with fallback: why)
 
 
 _DT = {"CANON": torch.int32, "NEW_LEN": torch.int32, "SPLIT": torch.int32,
@@ -197,10 +199,11 @@ class CorpusEngine:
         if rc < 0:
             msg = self.L.syzcov_last_error().decode(errors="replace")
             if r.err_flags & SYZCOV_ERR_UNIVERSE:
-                msg += " (key mode would alias it with a universe PC; keys.hip)"
+                msg += (" (key mode would alias it with a universe PC; keys.hip; the window-mode "
+                        "recompute needs the raw PCs: canon in place or sharded cannot)")
             raise RuntimeError(msg)
         return StepResult(self.kept_idx[:r.n_kept], r.n_kept, self.union[:r.n_union], r.n_union,
-                          r.n_ids, r.max_cover)
+                          r.n_ids, r.max_cover, bool(r.fallback), r.err_flags)
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """The canonical covers as PCs, in the CSR slots of `off` (key mode:

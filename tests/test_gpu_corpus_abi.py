@@ -182,9 +182,11 @@ def test_corpus_minimize_host_vs_oracle(L, raw, keys):
 
 
 def test_corpus_handle_errors(L):
-    """A PC outside the window, or (key mode) next to a universe PC but not in
-    the universe, fails the call with SYZCOV_ERANGE; the handle then serves
-    the clean corpus again."""
+    """A PC far outside the window (a PC extent too wide for the window-mode
+    recompute) fails the call with SYZCOV_ERANGE.  Key mode, a PC next to a
+    universe PC but not in the universe is never aliased: the step is
+    recomputed in window mode and returns the reference's result.  The handle
+    then serves the clean corpus again."""
     rng = np.random.default_rng(5)
     univ = (0x90000000 + 16 * np.arange(1 << 15) + rng.integers(0, 16, 1 << 15)).astype(np.uint32)
     n = 1500
@@ -209,7 +211,10 @@ def test_corpus_handle_errors(L):
                 stray = u + 1 if (u + 1) not in set(univ.tolist()) else u - 1
                 bad[j] = stray
                 bad[int(off[700]):int(off[701])].sort()
-                assert _minimize_host(L, h, off, bad, n, univ.size + 1)[0] == -5
+                c_off, c_pcs = orc.canonicalize_csr(off, bad)
+                kb, keptb, unb = _minimize_host(L, h, off, bad, n, univ.size + 1)
+                assert keptb.tolist() == list(orc.minimize_csr(c_off, c_pcs))
+                assert np.array_equal(unb, orc.union_fold_csr(c_off, c_pcs))
             k1, kept1, _ = _minimize_host(L, h, off, pcs, n, univ.size + 1)
             assert k1 == k0 and kept1.tolist() == kept0.tolist()
         finally:

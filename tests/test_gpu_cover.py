@@ -244,3 +244,37 @@ def test_bitmap_and_bytemap_ops(op):
         exp = npf((a != 0).astype(np.uint8), (b != 0).astype(np.uint8)) & 1
         assert np.array_equal(d.cpu().numpy(), exp.astype(np.uint8)), (op, nbytes)
         assert int(pop.item()) == int(exp.sum())
+
+
+def _minimize_in_order(covs, order):
+    """cover.go:114-129 over a given processing order (Python restatement)."""
+    seen, out = set(), []
+    for i in order:
+        c = covs[i]
+        if any(int(p) not in seen for p in c):
+            out.append(int(i))
+        seen.update(int(p) for p in c)
+    return out
+
+
+def test_minimize_engine_with_caller_order(cover):
+    """cover.Minimize as the Go shim calls it (its own sort.Sort order, raw
+    covers with duplicates) at engine size (>= 1024 inputs): the cached
+    window-mode engine takes the caller's order.  Three corpora in a row: the
+    cache is reused, then grows (a wider PC window, more inputs)."""
+    from syzkaller_amd import SyzcovError, _lib
+    rng = np.random.default_rng(21)
+    for trial, (n, hi) in enumerate(((3000, 1 << 16), (2500, 1 << 16), (5000, 1 << 21))):
+        base = 0x81000000 + trial * 4096
+        covs = [(base + rng.integers(0, hi, size=int(rng.integers(0, 300)))).astype(np.uint32)
+                for _ in range(n)]
+        legacy = orc.sort_order([len(c) for c in covs], orc.LEGACY)
+        assert cover.Minimize(covs, order=legacy) == list(orc.minimize(covs, orc.LEGACY)), trial
+        perm = rng.permutation(n).astype(np.int32)
+        assert cover.Minimize(covs, order=perm) == _minimize_in_order(covs, perm), trial
+        assert cover.Minimize(covs) == list(orc.minimize(covs)), trial
+    bad = np.zeros(n, np.int32)  # not a permutation
+    with pytest.raises(SyzcovError):
+        cover.Minimize(covs, order=bad)
+    assert _lib.lib().syzcov_pool_trim() == 0  # releases the cached engine too
+    assert cover.Minimize(covs, order=perm) == _minimize_in_order(covs, perm)

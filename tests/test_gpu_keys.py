@@ -72,8 +72,9 @@ def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2):
 
 
 def test_engine_key_mode_window_error(torch):
-    """A PC below the universe's first key is out of the key range: the
-    step raises instead of returning a wrong result."""
+    """A PC far below the universe's first key: out of the key range, and the
+    corpus' PC extent (2^31 PCs) is too wide for the window-mode recompute, so
+    the step raises instead of returning a wrong result."""
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     n, log2 = 300, 14
     off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=200, sigma=50, log2_space=log2)
@@ -213,13 +214,22 @@ def _stray(u: np.ndarray, i: int) -> int:
                 if int(u[j]) + d not in us and int(u[j]) + d <= int(u[-1]))
 
 
+def _oracle_of(off, raw, n):
+    o_off = off[:n + 1].cpu().numpy().astype(np.uint64)
+    o_pcs = raw[:int(o_off[-1])].cpu().numpy().view(np.uint32)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    return list(orc.minimize_csr(c_off, c_pcs)), orc.union_fold_csr(c_off, c_pcs)
+
+
 @pytest.mark.parametrize("force", ["", "canon3", "redo"])
 @pytest.mark.parametrize("in_place", [False, True], ids=["out-of-place", "in-place"])
 def test_engine_key_mode_nonuniverse(torch, force, in_place, monkeypatch):
     """A PC inside the universe's key range that is not a universe PC (it
-    shares its key with a universe PC, cover.go would treat them as two PCs):
-    the step raises, never returns an aliased result.  Every canonicalization
-    path checks membership (keys.hip)."""
+    shares its key with a universe PC, cover.go would treat them as two PCs)
+    is never aliased.  Out of place the step is recomputed in window mode over
+    the corpus' PC extent and returns the reference's results (cover.Minimize
+    never fails, cover.go:104-131); in place the raw PCs are gone and the step
+    raises.  Every canonicalization path checks membership (keys.hip)."""
     monkeypatch.setenv("SYZCOV_FORCE", force)
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     n, log2, seed = 2000, 16, 0x5EED0002
@@ -231,19 +241,82 @@ def test_engine_key_mode_nonuniverse(torch, force, in_place, monkeypatch):
         eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u,
                            canon_in_place=in_place)
         res = eng.step(off, raw, n)  # clean corpus: fine
-        assert res.n_kept > 0
+        assert res.n_kept > 0 and not res.fallback
+        mc0 = res.max_cover
         off, raw, lens, total = synth_corpus(n, seed, mean=1500, sigma=600, log2_space=log2)
         j = int(off[where].item()) + int(lens[where].item()) // 2
         k = int(raw[j].item()) & 0xFFFFFFFF
         raw[j] = np.int32(np.uint32(_stray(uh, int(np.searchsorted(uh, k)))))
-        with pytest.raises(RuntimeError, match="universe"):
-            eng.step(off, raw, n)
+        if in_place:
+            with pytest.raises(RuntimeError, match="universe"):
+                eng.step(off, raw, n)
+            continue
+        exp_kept, exp_union = _oracle_of(off, raw, n)
+        res = eng.step(off, raw, n)
+        assert res.fallback and res.err_flags & 4, where
+        assert res.kept_idx.cpu().numpy().tolist() == exp_kept, where
+        assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union), where
+        assert res.max_cover == mc0  # the stray PC has no key of its own
+        res2 = eng.result()  # a second read returns the recomputed step
+        assert res2.fallback and res2.n_kept == res.n_kept
+        res3 = eng.step(off, raw, n)  # and the next step recomputes again
+        assert res3.kept_idx.cpu().numpy().tolist() == exp_kept
+
+
+def test_engine_key_mode_fallback_outside_extent(torch):
+    """PCs above the universe's last PC (outside the key range, SYZCOV_ERR_WINDOW)
+    and a caller order: the window-mode recompute keeps the caller's order,
+    the host drop-in form restages its in-place PCs, maxCover takes only the
+    union's universe PCs."""
+    import ctypes as C
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 1500, 15, 0x5EED0002
+    u = synth_universe(log2, seed)
+    uh = u.cpu().numpy().view(np.uint32)
+    lo, span = synth_window(log2)
+    off, raw, lens, total = synth_corpus(n, seed, mean=900, sigma=300, log2_space=log2)
+    for i in (3, 700, 1499):  # a few PCs past the universe's extent
+        raw[int(off[i].item())] = np.int32(np.uint32(int(uh[-1]) + 1000 + i))
+    exp_kept, exp_union = _oracle_of(off, raw, n)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u)
+    res = eng.step(off, raw, n)
+    assert res.fallback and res.err_flags & 1
+    assert res.kept_idx.cpu().numpy().tolist() == exp_kept
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
+    univ_in_union = np.intersect1d(exp_union, uh).size
+    assert res.max_cover == univ_in_union
+    # host form, canon in place inside the handle, with a caller order
+    L = _lib.lib()
+    h_off = off.cpu().numpy().astype(np.uint64)
+    h_pcs = raw[:total].cpu().numpy().view(np.uint32).copy()
+    covs = [h_pcs[h_off[i]:h_off[i + 1]] for i in range(n)]
+    perm = np.random.default_rng(4).permutation(n).astype(np.int32)
+    seen, exp_p = set(), []
+    for i in perm:
+        if any(int(p) not in seen for p in covs[i]):
+            exp_p.append(int(i))
+        seen.update(int(p) for p in covs[i])
+    cfg = _lib.CorpusCfg(n_max=n, p_max=total, max_seg_len=int(lens.max().item()),
+                         universe=uh.ctypes.data, universe_n=uh.size, canon_in_place=1)
+    h = C.c_uint64(0)
+    _lib.check(L.syzcov_corpus_create(C.byref(cfg), None, 0, C.byref(h)), "corpus_create")
+    out = np.empty(n, np.int32)
+    un = np.empty(total, np.uint32)
+    nu = C.c_uint64(0)
+    k = _lib.check(L.syzcov_corpus_minimize_host_order(h.value, h_off.ctypes.data, h_pcs.ctypes.data,
+                                                       n, perm.ctypes.data, out.ctypes.data,
+                                                       un.ctypes.data, un.size, C.byref(nu)),
+                   "corpus_minimize_host_order")
+    L.syzcov_corpus_destroy(h.value)
+    assert out[:k].tolist() == exp_p
+    assert np.array_equal(un[:nu.value], exp_union)
 
 
 def test_engine_key_mode_gap_key(torch):
-    """A universe with keys that hold no PC (every other synthetic PC): a PC
-    on such a key is rejected; the universe's own PCs give the oracle's
-    results."""
+    """A universe with keys that hold no PC (every other synthetic PC): the
+    universe's own PCs give the oracle's results; a PC on such a key is never
+    aliased (the step is recomputed in window mode)."""
     from syzkaller_amd.engine import CorpusEngine
     rng = np.random.default_rng(7)
     full = np.array([orc.lib().orc_synth_universe(0x5EED0002, k) for k in range(1 << 14)],
@@ -263,8 +336,11 @@ def test_engine_key_mode_gap_key(torch):
     assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
     raw[int(o_off[300]) + 0] = np.int32(full[101].view(np.int32))  # a removed PC: a gap key
-    with pytest.raises(RuntimeError, match="universe"):
-        eng.step(off, raw, len(covers))
+    exp_kept, exp_union = _oracle_of(off, raw, len(covers))
+    res = eng.step(off, raw, len(covers))  # recomputed in window mode, exact
+    assert res.fallback
+    assert res.kept_idx.cpu().numpy().tolist() == exp_kept
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
 
 
 @pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
