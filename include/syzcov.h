@@ -316,8 +316,9 @@ int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncal
  * Sharded by input over `world` GPUs (n_global > n_max; rank r holds global
  * inputs [r * n_max, r * n_max + n)), the caller runs the collectives
  * between the phases (syzkaller_amd/dist.py does it over RCCL):
- *   canon -> all-gather NEW_LEN[:n] into GLENS -> order(GLENS, N)
- *   -> minimize(do_pass2 = 0)
+ *   canon -> all-gather NEW_LEN[:n] into GLENS -> order(GLENS, N), or
+ *   order_part(GLENS, N) + MAX all-reduce ORDER[:N] (the order split over the
+ *   ranks) -> minimize(do_pass2 = 0)
  *   key mode:    MIN all-reduce FIRST (int32 x span) -> pass2
  *   window mode: all-gather + OR COVERED (bitmap_op) -> n_ids = dense_first
  *                -> MIN all-reduce FIRST_DENSE[:n_ids] -> pass2
@@ -406,6 +407,11 @@ int syzcov_corpus_canon(syzcov_corpus h, const uint64_t *off, uint32_t *raw, siz
                         void *stream);
 /* lens: device int32[N] (sharded: the gathered lengths), NULL = this step's */
 int syzcov_corpus_order(syzcov_corpus h, const int32_t *lens, size_t N, void *stream);
+/* Sharded: this rank's PART of the order over the gathered lengths (the ranks
+ * split the late pdqsort rounds and the finisher, syzcov_dev_sort_order_part);
+ * the caller then MAX all-reduces ORDER[:N] (int32), which gives every rank
+ * the full order, before minimize. */
+int syzcov_corpus_order_part(syzcov_corpus h, const int32_t *lens, size_t N, void *stream);
 /* The caller's processing order instead (device int32[N]: order[r] = the
  * input of rank r, e.g. the Go shim's own sort.Sort(minInputArray),
  * cover.go:113; sharded: the global order, identical on every rank).  An
@@ -629,6 +635,14 @@ int syzcov_dev_compact_kept(const uint8_t *kept, const int32_t *order, size_t n,
 size_t syzcov_dev_sort_ws_size(size_t n);
 int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order,
                           void *ws, size_t ws_size, void *stream);
+/* One part of the order for a corpus sharded over `nparts` ranks: the parts
+ * run the same level-synchronous rounds until the order holds >= 4 * nparts
+ * segments, then each finishes only the segments starting in its block of
+ * positions and leaves -1 in the others'; an int32 MAX all-reduce of the
+ * parts' `order` arrays is the full order (cover.go:113).  Same workspace as
+ * syzcov_dev_sort_order. */
+int syzcov_dev_sort_order_part(const int64_t *lens, size_t n, uint32_t part, uint32_t nparts,
+                               int32_t *order, void *ws, size_t ws_size, void *stream);
 /* Segmented form: an independent Go sort.Sort per group, group g = lens
  * [goff[g], goff[g+1]) (device u64, ngroups >= 1, every group non-empty,
  * lengths < 0xFFFFFFFF).  order[i] for i in group g is a grouped index inside

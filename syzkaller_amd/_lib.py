@@ -83,6 +83,7 @@ _SIGS = {
     "syzcov_corpus_canon": (C.c_int, [u64, p_, p_, sz, p_]),
     "syzcov_corpus_order": (C.c_int, [u64, p_, sz, p_]),
     "syzcov_corpus_order_given": (C.c_int, [u64, p_, sz, p_]),
+    "syzcov_corpus_order_part": (C.c_int, [u64, p_, sz, p_]),
     "syzcov_corpus_minimize": (C.c_int, [u64, C.c_int, p_]),
     "syzcov_corpus_dense_first": (i64, [u64, p_]),
     "syzcov_corpus_pass2": (C.c_int, [u64, p_]),
@@ -126,6 +127,7 @@ _SIGS = {
     "syzcov_dev_compact_kept": (C.c_int, [p_, p_, sz, p_, p_, p_, p_]),
     "syzcov_dev_sort_ws_size": (sz, [sz]),
     "syzcov_dev_sort_order": (C.c_int, [p_, sz, C.c_int, p_, p_, sz, p_]),
+    "syzcov_dev_sort_order_part": (C.c_int, [p_, sz, u32, u32, p_, p_, sz, p_]),
     "syzcov_dev_sort_seg_ws_size": (sz, [sz, sz]),
     "syzcov_dev_sort_order_segmented": (C.c_int, [p_, p_, sz, sz, C.c_int, p_, p_, sz, p_]),
     "syzcov_dev_bytemap_op": (C.c_int, [C.c_int, p_, p_, u64, p_, p_]),

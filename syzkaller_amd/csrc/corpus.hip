@@ -410,7 +410,10 @@ static int ph_order_given(Corpus &c, const int32_t *order, size_t N, hipStream_t
     return 0;
 }
 
-static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
+// nparts > 1: this shard's part of the order only (syzcov_dev_sort_order_part);
+// the caller MAX all-reduces ORDER[:N] before minimize
+static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s, uint32_t part = 0,
+                    uint32_t nparts = 1) {
     int rc = order_begin(c, lens32 != nullptr, N, s);
     if (rc) return rc;
     c.order_given = false;
@@ -421,8 +424,8 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s) {
     hipLaunchKernelGGL(corpus_lens_kernel, dim3(grid_for(N, 256, 8192)), dim3(256), 0, s, l32,
                        c.off, (uint64_t)N, lens);
     SYZ_LAUNCH_CHECK();
-    return syzcov_dev_sort_order(lens, N, 0, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
-                                 c.buf<void>(SYZCOV_CORPUS_WS), c.ws_size, s);
+    return syzcov_dev_sort_order_part(lens, N, part, nparts, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
+                                      c.buf<void>(SYZCOV_CORPUS_WS), c.ws_size, s);
 }
 
 // Work items: (input, rank).  One GPU: every input, ranks = positions of
@@ -1043,6 +1046,13 @@ int64_t syzcov_corpus_minimize_host_order(syzcov_corpus h, const uint64_t *offse
         minimize_host(*c, offsets, pcs, n, order, out_idx, union_out, union_cap, n_union, s);
     hipStreamDestroy(s);
     return rc;
+}
+
+int syzcov_corpus_order_part(syzcov_corpus h, const int32_t *lens, size_t N, void *stream) {
+    Corpus *c = get(h);
+    if (!c || !c->shard || !lens) return SYZCOV_EINVAL;
+    Use u(c);
+    return ph_order(*c, lens, N, (hipStream_t)stream, (uint32_t)c->cfg.rank, (uint32_t)c->world);
 }
 
 int syzcov_corpus_order_given(syzcov_corpus h, const int32_t *order, size_t N, void *stream) {

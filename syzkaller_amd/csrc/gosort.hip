@@ -474,6 +474,65 @@ __global__ __launch_bounds__(WG) void swap_kernel(const Seg *__restrict__ cur,
     }
 }
 
+
+// ------------------------------------------------------ sharded order
+// One part of `nparts` (a rank of a sharded corpus, dist.py): from the round
+// that first holds >= 4 * nparts large segments (or the finisher, whichever
+// comes first), this part keeps only the live segments that START in its block
+// of positions [part * n / nparts, (part + 1) * n / nparts), with their
+// descendants (the owner is fixed at that round), and sets the positions of
+// every other live segment to -1.  Every position is then final on at least
+// one part, with the same value wherever it is (segments are independent:
+// pdqsort reads nothing outside [a, b) but the finished pivot at a-1), so an
+// int32 MAX all-reduce of the parts' arrays is Go's order.
+__device__ __forceinline__ bool seg_mine(const Seg &g, uint32_t n, uint32_t part, uint32_t nparts) {
+    return (uint32_t)(((uint64_t)(uint32_t)g.a * nparts) / n) == part;
+}
+
+// positions of the segments this part drops: -1 (block per segment)
+__global__ __launch_bounds__(WG) void shard_fill_kernel(const Seg *__restrict__ cur,
+                                                        const uint32_t *__restrict__ ccount,
+                                                        const Seg *__restrict__ small,
+                                                        const uint32_t *__restrict__ scount,
+                                                        uint32_t small_cap, uint32_t n,
+                                                        uint32_t part, uint32_t nparts,
+                                                        int32_t *__restrict__ I) {
+    const uint32_t nc = *ccount, ns = min(*scount, small_cap);
+    for (uint32_t i = blockIdx.x; i < nc + ns; i += gridDim.x) {
+        const Seg g = i < nc ? cur[i] : small[i - nc];
+        if (seg_mine(g, n, part, nparts)) continue;
+        for (int p = g.a + (int)threadIdx.x; p < g.b; p += WG) I[p] = -1;
+    }
+}
+
+// the lists compacted to this part's segments (one workgroup; list order is
+// free: segments are independent)
+__device__ void shard_compact(Seg *list, uint32_t *count, uint32_t cap, uint32_t n, uint32_t part,
+                              uint32_t nparts, uint32_t *s_n) {
+    const uint32_t tot = min(*count, cap);
+    if (threadIdx.x == 0) *s_n = 0;
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < tot; i0 += WG) {
+        const uint32_t i = i0 + threadIdx.x;
+        Seg g{};
+        const bool keep = i < tot && seg_mine(g = list[i], n, part, nparts);
+        __syncthreads();  // the chunk is read before any slot of it is written
+        if (keep) list[atomicAdd(s_n, 1u)] = g;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = *s_n;
+}
+
+__global__ __launch_bounds__(WG) void shard_compact_kernel(Seg *cur, uint32_t *ccount, Seg *small,
+                                                           uint32_t *scount, uint32_t small_cap,
+                                                           uint32_t cur_cap, uint32_t n,
+                                                           uint32_t part, uint32_t nparts) {
+    __shared__ uint32_t s_n;
+    shard_compact(cur, ccount, cur_cap, n, part, nparts, &s_n);
+    __syncthreads();
+    shard_compact(small, scount, small_cap, n, part, nparts, &s_n);
+}
+
 // ------------------------------------------------------- in-LDS finisher
 // One workgroup per segment of <= SMALL elements: tasks are popped by lane 0
 // (O(1) control steps), partitions of tasks longer than MID run WG-parallel;
@@ -890,8 +949,21 @@ static int read_ctl(uint32_t *h, const uint32_t *ctl, size_t n, uint32_t *pin, h
     return 0;
 }
 
-static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
+static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t part = 0,
+                      uint32_t nparts = 1) {
     PinnedCtl pin;
+    bool split = nparts <= 1;  // this part's segments selected (or nothing to split)
+    auto split_now = [&](Seg *cur_, uint32_t *ccount_, uint32_t ncur_) {
+        hipLaunchKernelGGL(shard_fill_kernel, dim3(std::min<uint32_t>(ncur_ + 4096, 8192)), dim3(WG),
+                           0, s, (const Seg *)cur_, (const uint32_t *)ccount_, (const Seg *)w.small,
+                           (const uint32_t *)(w.ctl + 3), w.small_cap, (uint32_t)w.n, part, nparts,
+                           w.I);
+        hipLaunchKernelGGL(shard_compact_kernel, dim3(1), dim3(WG), 0, s, cur_, ccount_, w.small,
+                           w.ctl + 3, w.small_cap, w.seg_cap, (uint32_t)w.n, part, nparts);
+        SYZ_LAUNCH_CHECK();
+        split = true;
+        return 0;
+    };
     Seg *cur = w.segA, *nxt = w.segB;
     uint32_t *ccount = w.ctl + 1, *ncount = w.ctl + 2, *cmax = w.ctl + 4, *nmax = w.ctl + 5;
     uint32_t *citems = w.ctl + 6, *nitems = w.ctl + 7;
@@ -916,8 +988,11 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     constexpr int SYNC_EVERY = 8;  // 4 and 16 measured no faster
     const uint32_t cap_seg = std::min<uint32_t>(w.seg_cap, w.n / (SMALL + 1) + 1);
     uint32_t ncur = h[1], maxlen = h[4];
+    bool exact = true;  // ncur is the device's count (a read-back), not a bound
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
+        if (!split && exact && ncur >= 4 * nparts) split_now(cur, ccount, ncur);
+        exact = false;
         // the children of this round go to nxt
         // (lead_kernel zeroes ncount / nmax)
         Ctl cn{nxt, ncount, nmax, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
@@ -945,7 +1020,12 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
             if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
             ncur = h[ccount - w.ctl];
             maxlen = h[cmax - w.ctl];
+            exact = true;
         }
+    }
+    if (!split && !h[0]) {  // the finisher's segments are split at least
+        split_now(cur, ccount, 0);
+        if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
     }
     if (!h[0] && h[3]) {
         hipLaunchKernelGGL(small_kernel, dim3(std::min<uint32_t>(h[3], 8192)), dim3(WG), 0, s, w.small,
@@ -962,8 +1042,23 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1) {
     return 0;
 }
 
+static int sort_order_part(const int64_t *lens, size_t n, int sort_variant, uint32_t part,
+                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream);
+
 extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
                                      int32_t *order, void *ws, size_t ws_size, void *stream) {
+    return sort_order_part(lens, n, sort_variant, 0, 1, order, ws, ws_size, stream);
+}
+
+extern "C" int syzcov_dev_sort_order_part(const int64_t *lens, size_t n, uint32_t part,
+                                          uint32_t nparts, int32_t *order, void *ws,
+                                          size_t ws_size, void *stream) {
+    if (nparts == 0 || part >= nparts) return SYZCOV_EINVAL;
+    return sort_order_part(lens, n, 0, part, nparts, order, ws, ws_size, stream);
+}
+
+static int sort_order_part(const int64_t *lens, size_t n, int sort_variant, uint32_t part,
+                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream) {
     if (n == 0) return 0;
     if (!lens || !order || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (sort_variant != 0) {
@@ -980,7 +1075,7 @@ extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_var
     Ctl c{w.segA, w.ctl + 1, w.ctl + 4, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
     if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
     SYZ_LAUNCH_CHECK();
-    if (int rc = run_rounds(w, s, (int64_t)n)) return rc;
+    if (int rc = run_rounds(w, s, (int64_t)n, part, nparts)) return rc;
     SYZ_HIP(hipMemcpyAsync(order, w.I, n * 4, hipMemcpyDeviceToDevice, s));
     return 0;
 }

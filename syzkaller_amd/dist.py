@@ -5,7 +5,8 @@ One process per GPU, torch.distributed over RCCL ("nccl" backend on ROCm).
 The only exchanges are the reductions the first-cover formulation needs
 (SURVEY §8e):
 
-    canonical lens all-gather              -> identical Go sort.Sort order
+    canonical lens all-gather              -> the Go sort.Sort order's rounds
+    order          int32 MAX all-reduce    -> each rank finished its part of it
     first[]        int32 MIN all-reduce    -> global first-cover rank per key
                                               (key mode: the union = keys with one)
     covered bitmap all-gather + OR          -> window mode: the union = identical
@@ -53,6 +54,13 @@ def _all_gather(out: torch.Tensor, t: torch.Tensor) -> None:
 def merge_first(first: torch.Tensor) -> None:
     """Global first-cover rank per dense PC id."""
     _all_reduce(first, dist.ReduceOp.MIN)
+
+
+def merge_order(order: torch.Tensor) -> None:
+    """The Go order split over the ranks (syzcov_corpus_order_part): each
+    rank holds its segments' positions and -1 in the others'; every position
+    is final on some rank with the same value wherever it is, so MAX."""
+    _all_reduce(order, dist.ReduceOp.MAX)
 
 
 def merge_counts(counts: torch.Tensor) -> None:
@@ -114,11 +122,15 @@ class ShardedEngine(CorpusEngine):
     PHASES = ("canon", "order", "minimize", "exchange", "finish")
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
-                 rank: int, world: int, device="cuda", universe=None, canon_in_place=False):
+                 rank: int, world: int, device="cuda", universe=None, canon_in_place=False,
+                 split_order: bool = True):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
                          n_global=n * world, rank=rank, universe=universe,
                          canon_in_place=canon_in_place)
         self.rank, self.world, self.n_local = rank, world, n
+        # the ranks split the Go order's late rounds and finisher (each finishes
+        # the segments starting in its block), merged by an int32 MAX all-reduce
+        self.split_order = split_order and world > 1
 
     def _or_into(self, dst, src):
         check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
@@ -141,7 +153,11 @@ class ShardedEngine(CorpusEngine):
         self.canonicalize(off, raw, n)
         mark_ev()
         _all_gather(self.glens[:N], self.new_len[:n].contiguous())  # RCCL all-gather
-        self.sort_order(self.glens, N)                              # identical on every rank
+        if self.split_order:
+            check(L.syzcov_corpus_order_part(h, _p(self.glens), N, s), "corpus_order_part")
+            merge_order(self.order[:N])                             # RCCL int32 MAX
+        else:
+            self.sort_order(self.glens, N)                          # identical on every rank
         mark_ev()
         self.minimize(do_pass2=False)
         mark_ev()

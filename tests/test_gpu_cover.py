@@ -278,3 +278,36 @@ def test_minimize_engine_with_caller_order(cover):
         cover.Minimize(covs, order=bad)
     assert _lib.lib().syzcov_pool_trim() == 0  # releases the cached engine too
     assert cover.Minimize(covs, order=perm) == _minimize_in_order(covs, perm)
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_sort_order_parts_merge_to_go_order(cover, nparts):
+    """The order split over ranks (syzcov_dev_sort_order_part): every part's
+    array MAX-merged is Go's order (cover.go:113), for tie-heavy lengths at
+    small and C2 scale (the split happens mid-rounds at 1M, at the finisher
+    for a single small segment)."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(41 + nparts)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for n in (1, 5, 3000, 1_000_000):
+        lens = rng.normal(2048, 512, size=n).astype(np.int64).clip(1, 65535)
+        exp = orc.sort_order(lens)
+        d_lens = torch.from_numpy(lens).cuda()
+        ws = torch.empty(L.syzcov_dev_sort_ws_size(n), dtype=torch.uint8, device="cuda")
+        merged = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        seen = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for part in range(nparts):
+            out = torch.empty(n, dtype=torch.int32, device="cuda")
+            _lib.check(L.syzcov_dev_sort_order_part(C.c_void_p(d_lens.data_ptr()), n, part, nparts,
+                                                    C.c_void_p(out.data_ptr()),
+                                                    C.c_void_p(ws.data_ptr()), ws.numel(), s),
+                       "sort_order_part")
+            torch.maximum(merged, out, out=merged)
+            seen += (out >= 0).to(torch.int32)
+        assert np.array_equal(merged.cpu().numpy(), exp), (n, nparts)
+        assert int(seen.min().item()) >= 1  # every position final on some part
+        if n == 1_000_000:  # the late rounds were split: most positions on one part only
+            assert float((seen == 1).float().mean().item()) > 0.5
