@@ -162,6 +162,9 @@ struct Corpus {
     const uint32_t *raw_in = nullptr;  // the step's raw PCs when canon is out of place
     bool allow_fallback = true;     // a PC outside the key space: window-mode recompute
     bool order_given = false;       // the step's order came from the caller (ORDER)
+    uint32_t *fb_union = nullptr;   // a fallback union larger than UNION (grow-only)
+    size_t fb_union_cap = 0;
+    bool fb_union_used = false;     // this step's union lives in fb_union
     uint32_t *canon = nullptr;      // the step's canonical lists (in place: the raw buffer)
     size_t n = 0;                   // inputs of this shard in the step
     size_t N = 0;                   // inputs ordered (the global corpus when sharded)
@@ -355,6 +358,7 @@ static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hip
     if (!off || !raw || n == 0 || n > c.cfg.n_max) return SYZCOV_EINVAL;
     c.off = off;
     c.raw_in = c.cfg.canon_in_place ? nullptr : raw;
+    c.fb_union_used = false;
     c.n = n;
     c.N = n;
     c.dict_ready = false;
@@ -639,12 +643,21 @@ static int corpus_fallback(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
         if (!rc) rc = ph_minimize(w, 1, s);
         if (!rc) rc = ph_finish(w, s);
         if (!rc) rc = ph_result(w, &rw, s);
-        if (!rc && rw.n_union > c.sizes[SYZCOV_CORPUS_UNION] / 4) {
-            set_error("window-mode fallback: union of %u PCs > capacity %zu", rw.n_union,
-                      c.sizes[SYZCOV_CORPUS_UNION] / 4);
-            rc = SYZCOV_ERANGE;
-        }
+        // PCs outside the universe can make the union larger than the key
+        // space the UNION buffer is sized for: then it goes to a side buffer
         uint32_t *un = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
+        if (!rc && rw.n_union > c.sizes[SYZCOV_CORPUS_UNION] / 4) {
+            if (rw.n_union > c.fb_union_cap) {
+                if (c.fb_union) hipFree(c.fb_union);
+                c.fb_union = nullptr;
+                c.fb_union_cap = 0;
+                if (hipMalloc(&c.fb_union, align_up((size_t)rw.n_union * 4, 256)) != hipSuccess)
+                    rc = SYZCOV_ENOMEM;
+                else c.fb_union_cap = rw.n_union;
+            }
+            un = c.fb_union;
+            c.fb_union_used = true;
+        }
         if (!rc && rw.n_kept)
             rc = hipMemcpyAsync(c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX), rw.kept_idx,
                                 (size_t)rw.n_kept * 4, hipMemcpyDeviceToDevice, s) == hipSuccess
@@ -674,6 +687,7 @@ static int corpus_fallback(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
             r->records = rw.records;
             r->max_cover = mc;
             r->fallback = 1;
+            r->union_pcs = un;
             // the step's scalars now describe the recomputed results (a second
             // result call returns them without recomputing)
             uint64_t hs[8];
@@ -710,6 +724,7 @@ static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
     if (err & kErrRecomputed) {  // corpus_fallback already ran for this step
         r->err_flags = err & ~kErrRecomputed;
         r->fallback = 1;
+        if (c.fb_union_used) r->union_pcs = c.fb_union;
         return 0;
     }
     if ((err & (SYZCOV_ERR_WINDOW | SYZCOV_ERR_UNIVERSE)) &&
@@ -920,6 +935,7 @@ int syzcov_corpus_destroy(syzcov_corpus h) {
         Use u(c);
         if (c->own_mem) hipFree(c->mem);
         if (c->stage) hipFree(c->stage);
+        if (c->fb_union) hipFree(c->fb_union);
     }
     delete c;
     return 0;

@@ -202,7 +202,15 @@ class CorpusEngine:
                 msg += (" (key mode would alias it with a universe PC; keys.hip; the window-mode "
                         "recompute needs the raw PCs: canon in place or sharded cannot)")
             raise RuntimeError(msg)
-        return StepResult(self.kept_idx[:r.n_kept], r.n_kept, self.union[:r.n_union], r.n_union,
+        union = self.union[:r.n_union]
+        if r.n_union and r.union_pcs != self.union.data_ptr():
+            # a window-mode recompute whose union outgrew the key space's buffer
+            # (PCs outside the universe): the handle's side buffer, copied out
+            union = torch.empty(-(-r.n_union // 4) * 4, dtype=torch.int32, device=self.dev)
+            check(self.L.syzcov_dev_stream_copy(C.c_void_p(r.union_pcs), _p(union), union.numel() * 4,
+                                                _stream()), "dev_stream_copy")
+            union = union[:r.n_union]
+        return StepResult(self.kept_idx[:r.n_kept], r.n_kept, union, r.n_union,
                           r.n_ids, r.max_cover, bool(r.fallback), r.err_flags)
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:

@@ -5,8 +5,10 @@ set -o pipefail
 export TMPDIR=/tmp
 o=gpurun_out/r04b; mkdir -p $o
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit 1;; esac; }
-timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_manager.py tests/test_gpu_triage.py "tests/test_gpu_fullsize.py::test_c5_newcov_stream_fullsize" > $o/pytest.log 2>&1
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_keys.py tests/test_gpu_corpus_abi.py "tests/test_gpu_cover.py::test_sort_order_parts_merge_to_go_order" \
+  tests/test_gpu_manager.py tests/test_gpu_triage.py "tests/test_gpu_fullsize.py::test_c5_newcov_stream_fullsize" \
+  "tests/test_gpu_fullsize.py::test_world8_rehearsal_c2" "tests/test_gpu_fullsize.py::test_world8_rehearsal_c3" > $o/pytest.log 2>&1
 rc=$?; tail -5 $o/pytest.log; grep -q "illegal memory access\|HSA_STATUS_ERROR\|Memory access fault" $o/pytest.log && { echo "GPU fault"; exit 1; }
 fatal $rc pytest
 for v in keym gather; do
