@@ -675,6 +675,9 @@ int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out,
 /* dst <- src, 16-byte aligned, nbytes % 16 == 0: the streaming-copy kernel
  * whose rate the bench reports as the measured HBM peak. */
 int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes, void *stream);
+/* HBM copy-rate probes for the bench's measured peak: form 0 = the streaming
+ * copy above, 1 = one 16-byte element per thread, one pass (<= 2^36 bytes). */
+int syzcov_dev_copy_peak(const void *src, void *dst, size_t nbytes, int form, void *stream);
 
 /* Dynamic priority counts as a dense contraction on i8 MFMA with i32
  * accumulation: counts = AᵀA over the matrix AT (rows = syzcov_dev_prio_rows(C)

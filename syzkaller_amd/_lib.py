@@ -136,6 +136,7 @@ _SIGS = {
     "syzcov_dev_synth_universe": (C.c_int, [u64, u32, p_, p_]),
     "syzcov_dev_synth_callids": (C.c_int, [u64, u64, sz, u32, p_, p_]),
     "syzcov_dev_stream_copy": (C.c_int, [p_, p_, sz, p_]),
+    "syzcov_dev_copy_peak": (C.c_int, [p_, p_, sz, C.c_int, p_]),
     "syzcov_dev_prio_rows": (sz, [C.c_int]),
     "syzcov_dev_prio_ldp": (sz, [sz]),
     "syzcov_dev_prio_build_at": (C.c_int, [C.c_int, p_, p_, p_, sz, C.c_int, p_, sz, p_, p_]),

@@ -38,8 +38,6 @@
 #include "common.h"
 
 #include <algorithm>
-#include <cstdio>
-#include <cstdlib>
 
 #define RC_(expr)                 \
     do {                          \
@@ -95,10 +93,6 @@ struct Args {
     const uint64_t *base_r;    // [items] off[order[j]]
     const uint32_t *split_t;   // [nrange][items] split[order[j]][rho]
     uint32_t n_items;
-    // SYZ_MR_DEBUG builds only: bounds of the global arrays and a report word
-    uint32_t *dbg;             // [0] first failing check id, [1..2] its value
-    uint64_t dbg_npcs, dbg_nseg, dbg_span;
-    uint64_t *stamp;           // [G][4] per-workgroup timing stamps (debug builds)
     uint32_t *pctr;            // dynamic pieces: this chunk's next-piece counter
     uint32_t npieces;          // dynamic pieces: pieces of this chunk (G)
     // key mode: pcs are key words (common.h); every word is checked against the
@@ -108,24 +102,6 @@ struct Args {
     uint32_t *err;             // SYZCOV_ERR_UNIVERSE
 };
 
-#ifdef SYZ_MR_DEBUG
-// index check of a debug build: report the first failure and clamp the index
-#define MR_CHK(A, id, idx, bound)                                                    \
-    ((idx) < (bound) ? (idx)                                                         \
-                     : (atomicCAS((A).dbg, 0u, (uint32_t)(id)) == 0u                 \
-                            ? ((A).dbg[1] = (uint32_t)(uint64_t)(idx),               \
-                               (A).dbg[2] = (uint32_t)((uint64_t)(idx) >> 32), 0)    \
-                            : 0))
-// detailed capture of the first out-of-range covered-bit index (debug builds)
-#define MR_CAP8(A, path, item, sti, mi, idx, head, vv, rho)                             \
-    if (atomicCAS((A).dbg + 4, 0u, 1u) == 0u) {                                         \
-        (A).dbg[5] = (path); (A).dbg[6] = (item); (A).dbg[7] = (uint32_t)(sti);           \
-        (A).dbg[8] = (uint32_t)((uint64_t)(sti) >> 32); (A).dbg[9] = (mi);                \
-        (A).dbg[10] = (idx); (A).dbg[11] = (head); (A).dbg[12] = (vv); (A).dbg[13] = (rho); \
-    }
-#else
-#define MR_CHK(A, id, idx, bound) (idx)
-#endif
 
 // Gather the items' CSR bases and split columns into rank order, transposed
 // so that a workgroup owning range rho reads split_t[rho][i0..i1) contiguously.
@@ -140,7 +116,7 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
     for (uint32_t t0 = blockIdx.x * 64; t0 < n; t0 += gridDim.x * 64) {
         const uint32_t rows = min(64u, n - t0);
         if (threadIdx.x < rows) {
-            const uint32_t seg = MR_CHK(A, 1, (uint32_t)A.order[t0 + threadIdx.x], A.dbg_nseg);
+            const uint32_t seg = (uint32_t)A.order[t0 + threadIdx.x];
             s_seg[threadIdx.x] = seg;
             base_r[t0 + threadIdx.x] = A.off[seg];
         }
@@ -335,9 +311,6 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         if (item < w1) {
             const uint64_t st = d_base + d_s0;
             m = d_s1 - d_s0;
-#ifdef SYZ_MR_DEBUG
-            if (d_s1 < d_s0 || st + m > A.dbg_npcs) { MR_CHK(A, 3, st + m, 0ull); m = 0; }
-#endif
             a0 = st & ~3ull;
             const uint32_t head = (uint32_t)(st - a0);
             he = ((head + m) << 2) | head;
@@ -425,9 +398,6 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                     const uint32_t idx = co[u] * 4 + k;
                     const uint32_t valid =
                         (uint32_t)(cj[u] < 64) & (uint32_t)(idx >= head) & (uint32_t)(idx < end);
-#ifdef SYZ_MR_DEBUG
-                    if (valid) MR_CHK(A, 8, bit[u * 4 + k], nwords * 32);
-#endif
                     uint32_t unc;
                     if (KEYM) {
                         const uint32_t t = wv[u * 4 + k];
@@ -457,7 +427,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                         for (int k = 0; k < 4; k++)
                             if ((um >> (u * 4 + k)) & 1u) {
                                 const uint32_t wo =
-                                    MR_CHK(A, 4, (vv[k] & A.keymask) - A.pc_lo, A.dbg_span);
+                                    (vv[k] & A.keymask) - A.pc_lo;
                                 if (slot < A.cap_k)
                                     rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
                                 else  // no room: its min cannot wait
@@ -544,14 +514,14 @@ __device__ __forceinline__ int32_t first_of(const int32_t *first_w, const uint64
 __global__ void pass2_kernel(Args A, const uint64_t *tab, const int32_t *first_d, uint8_t *kept) {
     SYZ_FOR_RECORDS(A, 0, i, r) {
         const int32_t rank = (int32_t)(r >> 32);
-        if (first_of(A.first_w, tab, first_d, MR_CHK(A, 5, (uint32_t)r, A.dbg_span)) == rank)
-            kept[MR_CHK(A, 6, (uint32_t)rank, A.dbg_nseg)] = 1;
+        if (first_of(A.first_w, tab, first_d, (uint32_t)r) == rank)
+            kept[(uint32_t)rank] = 1;
     }
 }
 
 // first_w back to INT32_MAX at every recorded offset (after pass 2).
 __global__ void reset_kernel(Args A) {
-    SYZ_FOR_RECORDS(A, 0, i, r) A.first_w[MR_CHK(A, 7, (uint32_t)r, A.dbg_span)] = INT32_MAX;
+    SYZ_FOR_RECORDS(A, 0, i, r) A.first_w[(uint32_t)r] = INT32_MAX;
 }
 
 // ---- overflow fallbacks (early exit unless *cnt > cap)
@@ -677,28 +647,11 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.cap_k = rec_cap / mr::NCTR;
     A.base_r = (uint64_t *)((uint8_t *)ws + MR_HDR);
     A.split_t = (uint32_t *)((uint8_t *)A.base_r + align_up(n_items * 8, 256));
-    A.dbg = nullptr;
-    A.stamp = nullptr;
     A.pctr = nullptr;
     A.npieces = 0;
     A.keymask = 0xFFFFFFFFu;
     A.low_of_key = nullptr;
     A.err = nullptr;
-    A.dbg_npcs = A.dbg_nseg = ~0ull;
-    A.dbg_span = pc_span;
-#ifdef SYZ_MR_DEBUG
-    // debug build: SYZCOV_MR_DBG="<pcs array length>,<inputs>" bounds the index checks
-    static uint32_t *dbg = nullptr;
-    if (!dbg && hipMalloc(&dbg, 64) != hipSuccess) return SYZCOV_EHIP;
-    A.dbg = dbg;
-    static uint64_t *stamp = nullptr;
-    if (!stamp && hipMalloc(&stamp, 8192 * 32) != hipSuccess) return SYZCOV_EHIP;
-    A.stamp = stamp;
-    if (const char *e = getenv("SYZCOV_MR_DBG")) {
-        unsigned long long a = 0, b = 0;
-        if (sscanf(e, "%llu,%llu", &a, &b) == 2) { A.dbg_npcs = a; A.dbg_nseg = b; }
-    }
-#endif
     return 0;
 }
 
@@ -753,23 +706,11 @@ static int minimize_range_impl(
     }
     const uint64_t nrange = A.nrange;
     SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters and done marks
-#ifdef SYZ_MR_DEBUG
-    SYZ_HIP(hipMemsetAsync(A.dbg, 0, 64, s));
-#endif
     static std::atomic<uint32_t> prep_attr{0};  // nrange = 256 needs 65.8 KB of dynamic LDS
     if ((rc = set_dyn_lds_once((const void *)mr::prep_kernel, 80 * 1024, prep_attr))) return rc;
     hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256),
                        split ? 64 * (nrange + 1) * sizeof(uint32_t) : 0, s, A,
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
-#ifdef SYZ_MR_DEBUG
-    {
-        uint32_t h[4] = {0, 0, 0, 0};
-        hipError_t e1 = hipStreamSynchronize(s);
-        hipMemcpy(h, A.dbg, 16, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[mr dbg] prep: %s, check %u\n", hipGetErrorString(e1), h[0]);
-        if (e1 != hipSuccess) return SYZCOV_EHIP;
-    }
-#endif
     const size_t lds = ((size_t)1 << range_shift) / (keym ? 1 : 8);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
     const K k1 = keym ? mr::pass1_stream_kernel<2, true> : mr::pass1_stream_kernel<2, false>;
@@ -816,70 +757,6 @@ static int minimize_range_impl(
         nchunk++;
         hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
                            (uint32_t)b, (uint32_t)P, (int)(a != 0));
-#ifdef SYZ_MR_DEBUG
-        {
-            uint32_t h[4] = {0, 0, 0, 0};
-            hipError_t e1 = hipStreamSynchronize(s);
-            hipMemcpy(h, A.dbg, 16, hipMemcpyDeviceToHost);
-            fprintf(stderr, "[mr dbg] pass1 chunk [%llu, %llu) G %llu P %llu: %s, check %u value %#llx\n",
-                    (unsigned long long)a, (unsigned long long)b, (unsigned long long)G,
-                    (unsigned long long)P, hipGetErrorString(e1), h[0],
-                    (unsigned long long)h[1] | ((unsigned long long)h[2] << 32));
-        {
-            static uint64_t hs[8192 * 4];
-            hipMemcpy(hs, A.stamp, G * 32, hipMemcpyDeviceToHost);
-            uint64_t t0 = ~0ull, tend = 0, fmax = 0, lmax = 0, lsum = 0, nwg = 0, slow = 0;
-            for (uint64_t g = 0; g < G; g++) {
-                const uint64_t *q = hs + 4 * g;
-                if (!q[2]) continue;
-                nwg++;
-                t0 = std::min(t0, q[0]);
-                if (q[2] > tend) { tend = q[2]; slow = g; }
-                fmax = std::max(fmax, q[1] - q[0]);
-                lmax = std::max(lmax, q[2] - q[1]);
-                lsum += q[2] - q[1];
-            }
-            if (nwg)
-                fprintf(stderr, "[mr dbg]   wgs %llu span %.1f us, fill max %.1f us, loop avg %.1f max "
-                        "%.1f us, last wg %llu rho %llu items %llu start %.1f fill %.1f loop %.1f\n",
-                        (unsigned long long)nwg, (tend - t0) / 100.0, fmax / 100.0,
-                        lsum / 100.0 / nwg, lmax / 100.0, (unsigned long long)slow,
-                        (unsigned long long)(hs[4 * slow + 3] & 255),
-                        (unsigned long long)(hs[4 * slow + 3] >> 8), (hs[4 * slow] - t0) / 100.0,
-                        (hs[4 * slow + 1] - hs[4 * slow]) / 100.0,
-                        (hs[4 * slow + 2] - hs[4 * slow + 1]) / 100.0);
-            hipMemset(A.stamp, 0, G * 32);
-        }
-        uint32_t d[16];
-        hipMemcpy(d, A.dbg, 64, hipMemcpyDeviceToHost);
-        if (d[4])
-            fprintf(stderr, "[mr dbg]   bit: path %u item %u sti %#llx m %u idx %u head %u vv %#x rho %u\n",
-                    d[5], d[6], (unsigned long long)d[7] | ((unsigned long long)d[8] << 32), d[9],
-                    d[10], d[11], d[12], d[13]);
-        if (d[4] && e1 == hipSuccess) {
-            int32_t seg = -1;
-            uint64_t o = 0, br = 0;
-            uint32_t sp[8] = {0}, st4[4] = {0}, pv[8] = {0};
-            hipMemcpy(&seg, A.order + d[6], 4, hipMemcpyDeviceToHost);
-            hipMemcpy(&o, A.off + seg, 8, hipMemcpyDeviceToHost);
-            hipMemcpy(&br, A.base_r + d[6], 8, hipMemcpyDeviceToHost);
-            hipMemcpy(sp, A.split + (uint64_t)seg * A.nrange, 4 * A.nrange, hipMemcpyDeviceToHost);
-            for (uint32_t r = 0; r < A.nrange && r < 4; r++)
-                hipMemcpy(st4 + r, A.split_t + (uint64_t)r * A.n_items + d[6], 4,
-                          hipMemcpyDeviceToHost);
-            const uint64_t sti = (uint64_t)d[7] | ((uint64_t)d[8] << 32);
-            hipMemcpy(pv, A.pcs + (sti & ~3ull), 32, hipMemcpyDeviceToHost);
-            fprintf(stderr, "[mr dbg]   order[item] %d off %#llx base_r %#llx split %u %u %u %u "
-                    "split_t %u %u %u %u pcs@a0 %#x %#x %#x %#x %#x %#x %#x %#x\n", seg,
-                    (unsigned long long)o, (unsigned long long)br, sp[0], sp[1], sp[2], sp[3],
-                    st4[0], st4[1], st4[2], st4[3], pv[0], pv[1], pv[2], pv[3], pv[4], pv[5], pv[6],
-                    pv[7]);
-        }
-        if (e1 != hipSuccess) return SYZCOV_EHIP;
-        if (const char *e = getenv("SYZCOV_MR_STOP"))
-            if (b >= strtoull(e, nullptr, 0)) return SYZCOV_EINVAL;  // debug: stop before the fault
-        }
-#endif
         // the chunk's first covers (+ covered, unless rebuilt below)
         hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
                            (int)!cover_from_first);
@@ -901,26 +778,8 @@ static int minimize_range_impl(
                            (const unsigned long long *)rec_cnt, rec_cap, (const int32_t *)first_w,
                            pc_span, covered);
     SYZ_LAUNCH_CHECK();
-#ifdef SYZ_MR_DEBUG
-    {
-        uint32_t h[4] = {0, 0, 0, 0};
-        hipError_t e1 = hipStreamSynchronize(s);
-        hipMemcpy(h, A.dbg, 16, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[mr dbg] pass1 done: %s, check %u\n", hipGetErrorString(e1), h[0]);
-        if (e1 != hipSuccess) return SYZCOV_EHIP;
-    }
-#endif
     if (!do_pass2) return 0;
     rc = mr_pass2(A, pc_span, nullptr, nullptr, kept, s);
-#ifdef SYZ_MR_DEBUG
-    {
-        uint32_t h[4] = {0, 0, 0, 0};
-        hipError_t e1 = hipStreamSynchronize(s);
-        hipMemcpy(h, A.dbg, 16, hipMemcpyDeviceToHost);
-        fprintf(stderr, "[mr dbg] pass2 done: %s, check %u value %#llx\n", hipGetErrorString(e1),
-                h[0], (unsigned long long)h[1] | ((unsigned long long)h[2] << 32));
-    }
-#endif
     return rc;
 }
 

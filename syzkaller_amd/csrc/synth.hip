@@ -96,9 +96,35 @@ __global__ __launch_bounds__(SC_THREADS) void stream_copy_kernel(const uint4 *__
         dst[i] = src[i];
 }
 
+// The plain form (one 16-byte element per thread, one pass, default cache
+// policy), the shape of the guide's float4 copy (MI355X_MICROARCH.md, HBM3E
+// measured bandwidth): the bench reports the better of the two forms.
+__global__ __launch_bounds__(256) void flat_copy_kernel(const uint4 *__restrict__ src,
+                                                        uint4 *__restrict__ dst, uint64_t n4) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n4) dst[i] = src[i];
+}
+
 }  // namespace syz
 
 using namespace syz;
+
+extern "C" int syzcov_dev_copy_peak(const void *src, void *dst, size_t nbytes, int form,
+                                    void *stream) {
+    if (!src || !dst || nbytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16 || form < 0 ||
+        form > 1)
+        return SYZCOV_EINVAL;
+    if (nbytes == 0) return 0;
+    const uint64_t n4 = nbytes / 16;
+    if (form == 0)
+        hipLaunchKernelGGL(stream_copy_kernel, dim3(256 * 2), dim3(SC_THREADS), 0,
+                           (hipStream_t)stream, (const uint4 *)src, (uint4 *)dst, n4);
+    else
+        hipLaunchKernelGGL(flat_copy_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, (const uint4 *)src, (uint4 *)dst, n4);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
 
 extern "C" int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes, void *stream) {
     if (!src || !dst || nbytes % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return SYZCOV_EINVAL;
