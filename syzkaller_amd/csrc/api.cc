@@ -47,7 +47,6 @@ uint32_t force_flags() {
     if (strstr(e, "redo")) f |= FORCE_REDO;
     if (strstr(e, "nc_lds")) f |= FORCE_NC_LDS;
     if (strstr(e, "nc_probe")) f |= FORCE_NC_PROBE;
-    if (strstr(e, "nc_gather")) f |= FORCE_NC_GATHER;  // key mode: membership gathered per PC
     return f;
 }
 

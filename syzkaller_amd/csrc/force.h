@@ -4,7 +4,6 @@
 #include <stdint.h>
 
 namespace syz {
-enum : uint32_t { FORCE_CANON3 = 1u, FORCE_REDO = 2u, FORCE_NC_LDS = 4u, FORCE_NC_PROBE = 8u,
-                  FORCE_NC_GATHER = 16u };
+enum : uint32_t { FORCE_CANON3 = 1u, FORCE_REDO = 2u, FORCE_NC_LDS = 4u, FORCE_NC_PROBE = 8u };
 uint32_t force_flags();
 }  // namespace syz

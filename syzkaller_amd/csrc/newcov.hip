@@ -238,7 +238,6 @@ static_assert(SPLIT_NS <= 64, "one sample per lane");
 // become empty sub-runs.  An end outside the index space: stats 1.  Key
 // positions only (pc_index_range): the candidate pass checks every PC's
 // membership in the universe.
-template <uint32_t RS>
 __global__ __launch_bounds__(256) void newcov_split_kernel(
     const uint64_t *__restrict__ rec_off, const uint32_t *__restrict__ pcs,
     const uint32_t *__restrict__ perm, const uint32_t *__restrict__ coff, int ncalls, Index X,
@@ -265,7 +264,7 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
 #pragma unroll
             for (int g = 0; g < SQ_G; g++) {
                 const uint32_t qy = g0 + g;
-                v[g] = qy + 1 < nqry ? (qy + 1) << RS : 0xFFFFFFFFu;
+                v[g] = qy + 1 < nqry ? (qy + 1) << RSH : 0xFFFFFFFFu;
                 const uint32_t c = qy < nqry ? (uint32_t)__popcll(__ballot(l < ns && kx < v[g])) : 0u;
                 if (n <= SPLIT_NS) {
                     lo[g] = c;
@@ -380,12 +379,11 @@ __global__ __launch_bounds__(1024) void range_scan_kernel(const uint32_t *__rest
 
 // Work-item prefix over (call, range) pairs e = c * nr + q: ceil(rows / CHR)
 // items each.
-// qmajor: e = q * ncalls + c (range-major: consecutive items share a range)
 __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restrict__ coff,
                                                          int ncalls, uint32_t nr,
                                                          const uint32_t *__restrict__ Rq,
                                                          uint32_t stride, uint32_t CHR,
-                                                         uint32_t *__restrict__ ipre, int qmajor) {
+                                                         uint32_t *__restrict__ ipre) {
     __shared__ uint32_t tmp[1024 / 64 + 1];
     const uint32_t ne = (uint32_t)ncalls * nr;
     uint32_t carry = 0;
@@ -393,8 +391,7 @@ __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restr
         const uint32_t e = e0 + threadIdx.x;
         uint32_t v = 0;
         if (e < ne) {
-            const uint32_t c = qmajor ? e % (uint32_t)ncalls : e / nr;
-            const uint32_t q = qmajor ? e / (uint32_t)ncalls : e - c * nr;
+            const uint32_t c = e / nr, q = e - c * nr;
             const uint32_t *R = Rq + (uint64_t)q * stride;
             v = (R[coff[c + 1]] - R[coff[c]] + CHR - 1) / CHR;
         }
@@ -426,15 +423,14 @@ __global__ __launch_bounds__(256) void desc_kernel(const uint32_t *__restrict__ 
                                                    uint32_t nr, const uint32_t *__restrict__ Rq,
                                                    uint32_t stride, uint32_t CHR,
                                                    const uint32_t *__restrict__ ipre,
-                                                   uint4 *__restrict__ desc, int qmajor) {
+                                                   uint4 *__restrict__ desc) {
     const uint32_t ne = (uint32_t)ncalls * nr;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
-        const uint32_t c = qmajor ? e % (uint32_t)ncalls : e / nr;
-        const uint32_t q = qmajor ? e / (uint32_t)ncalls : e - c * nr;
+        const uint32_t c = e / nr, q = e - c * nr;
         const uint32_t *R = Rq + (uint64_t)q * stride;
         const uint32_t r0 = R[coff[c]], r1 = R[coff[c + 1]], base = ipre[e];
         for (uint32_t i = 0; r0 + i * CHR < r1; i++)
-            desc[base + i] = make_uint4(e, r0 + i * CHR, min(r0 + (i + 1) * CHR, r1), c << 8 | q);
+            desc[base + i] = make_uint4(e, r0 + i * CHR, min(r0 + (i + 1) * CHR, r1), 0u);
     }
 }
 
@@ -676,162 +672,6 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             gather(s0 + LC_U, pcB);
             issue(s0 + 2 * LC_U, pcA);
             test(s0 + LC_U, pcB);
-        }
-    }
-    if (nc) flush();
-    if (bad && l == 0) stats[0] = 3u;
-    if (nonmem && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
-}
-
-
-// ---------------------------------------------------------------------------
-// Key mode: the candidate pass with the universe's membership table in LDS.
-// The index space is cut into ranges of 2^17 keys; a workgroup holds range
-// q's membership bytes (the universe PC's low kshift bits, 0x7F for a key
-// without one: 128 KB) and one call's (maxCover | flakes) bits over the range
-// (16 KB), so a PC costs two LDS reads and no global gather (the byte gather
-// of newcov_cand_lds_kernel: 132 M random bytes per C5 batch).  Work items
-// (range, call, rows) are range-major and drawn from a counter (stats[2]) by a
-// grid of one workgroup per CU, which restages the 128 KB table only when its
-// range changes and the 16 KB of bits when the call does.
-constexpr uint32_t RSK = 17;
-
-__global__ __launch_bounds__(LC_THREADS, 1) __attribute__((amdgpu_num_sgpr(80))) void newcov_cand_keym_kernel(
-    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
-    uint64_t words_per_call, Index X, const uint8_t *__restrict__ low_of_key,
-    const uint32_t *__restrict__ ipre, uint32_t ne, const uint4 *__restrict__ desc,
-    const uint4 *__restrict__ rows, const uint32_t *__restrict__ qoff, uint2 *__restrict__ clist,
-    uint32_t *__restrict__ stats) {
-    extern __shared__ uint4 s_low4[];  // (1 << RSK) / 16 uint4: membership bytes
-    __shared__ uint32_t s_bits[(1u << RSK) / 32];
-    __shared__ uint2 s_cb[LC_THREADS / 64 * LC_CBW];
-    __shared__ uint32_t s_item;
-    const uint32_t t = threadIdx.x, l = __lane_id(), wv = t >> 6;
-    const uint8_t *s_low = (const uint8_t *)s_low4;
-    const uint32_t nitems = ipre[ne];
-    const __amdgpu_buffer_rsrc_t pr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)pcs, 0, npc * 4u, 0x00020000);
-    const uint32_t ks = X.kshift, lowmask = (1u << ks) - 1u;
-    uint64_t bad = 0, nonmem = 0;
-    uint2 *cb = s_cb + wv * LC_CBW;
-    uint32_t nc = 0;
-    auto flush = [&]() {
-        uint32_t base = 0;
-        if (l == 0) base = atomicAdd(&stats[1], nc);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (l < nc) clist[base + l] = cb[l];
-        nc = 0;
-    };
-    auto emit = [&](bool cand, uint32_t k, uint32_t pc) {
-        const uint64_t m = __ballot(cand);
-        if (m) {
-            const uint32_t n = (uint32_t)__popcll(m);
-            const uint32_t rank = (uint32_t)__popcll(m & ((1ull << l) - 1ull));
-            if (nc + n > LC_CBW) flush();
-            if (n > LC_CBW) {
-                uint32_t base = 0;
-                if (l == 0) base = atomicAdd(&stats[1], n);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (cand) clist[base + rank] = make_uint2(k, pc);
-            } else {
-                if (cand) cb[nc + rank] = make_uint2(k, pc);
-                nc += n;
-            }
-        }
-    };
-    uint32_t cur_q = 0xFFFFFFFFu, cur_c = 0xFFFFFFFFu;
-    for (;;) {
-        if (t == 0) s_item = atomicAdd(&stats[2], 1u);
-        __syncthreads();  // also: every wave is done with the tables of the last item
-        const uint32_t w = s_item;
-        if (w >= nitems) break;
-        const uint4 d = desc[w];
-        const uint32_t c = d.w >> 8, q = d.w & 255u, r0 = d.y, r1 = d.z;
-        if (q != cur_q) {  // the range's membership bytes (the table is padded
-                           // to whole ranges with 0x7F: no universe PC)
-            const uint4 *src = reinterpret_cast<const uint4 *>(low_of_key + ((uint64_t)q << RSK));
-            for (uint32_t j = t; j < ((1u << RSK) >> 4); j += LC_THREADS) s_low4[j] = src[j];
-            cur_q = q;
-            cur_c = 0xFFFFFFFFu;
-        }
-        if (c != cur_c) {  // (maxCover[c] | flakes) over the range
-            const uint64_t wbase = (uint64_t)q << (RSK - 5);
-            const uint32_t nw = (uint32_t)min<uint64_t>((uint64_t)1 << (RSK - 5),
-                                                         words_per_call - wbase);
-            const uint4 *M4 = reinterpret_cast<const uint4 *>(mfl + (uint64_t)c * words_per_call + wbase);
-            uint4 *sb4 = reinterpret_cast<uint4 *>(s_bits);
-            for (uint32_t j = t; j < ((1u << RSK) >> 7); j += LC_THREADS)
-                sb4[j] = 4 * j < nw ? M4[j] : make_uint4(~0u, ~0u, ~0u, ~0u);
-            cur_c = c;
-        }
-        __syncthreads();
-        const uint4 *R = rows + qoff[q];
-        const uint32_t obase = X.kbase + (q << RSK);
-        const uint32_t per = (r1 - r0 + LC_THREADS / 64 - 1) / (LC_THREADS / 64);
-        const uint32_t w0 = min(r1, r0 + wv * per), w1 = min(r1, w0 + per);
-        uint4 my = make_uint4(0, 0, 0, 0);
-        uint32_t nrow = 0, p0v = 0;
-        auto rows64 = [&](uint32_t rb_) {
-            nrow = min(64u, w1 - rb_);
-            const uint4 dsc = R[rb_ + min(l, nrow - 1)];
-            my = l < nrow ? dsc : make_uint4(dsc.x, 0, 0, 0);
-            const bool need = l < nrow && !(my.z >> 18 & 1u);
-            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(pr, need ? (my.x - 1) * 4u : 0xFFFFFFF0u, 0, 0);
-            p0v = need ? v : 0u;
-        };
-        auto issue = [&](uint32_t s0, uint4 *pc) {
-#pragma unroll
-            for (int u = 0; u < LC_U; u++) {
-                const uint32_t i = (s0 + u) & 63;
-                const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
-                const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
-                const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
-                const bool any = s0 + u < nrow && 4 * l + 3 >= lo && 4 * l < hi;
-                pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      pr, any ? l * 16u : 0xFFFFFFF0u, any ? ra * 4u : 0u, 0));
-            }
-        };
-        auto test = [&](uint32_t s0, const uint4 *pc) {
-#pragma unroll
-            for (int u = 0; u < LC_U; u++) {
-                if (s0 + u >= nrow) break;  // wave-uniform
-                const uint32_t i = (s0 + u) & 63;
-                const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
-                const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
-                const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
-                uint32_t o[4], wd[4], mb[4];
-#pragma unroll
-                for (int c2 = 0; c2 < 4; c2++) {  // masked into the range: unconditional reads
-                    o[c2] = ((v[c2] >> ks) - obase) & ((1u << RSK) - 1u);
-                    wd[c2] = s_bits[o[c2] >> 5];
-                    mb[c2] = s_low[o[c2]];
-                }
-                const uint32_t p0 = __builtin_amdgcn_update_dpp(
-                    __builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
-#pragma unroll
-                for (int c2 = 0; c2 < 4; c2++) {
-                    const uint64_t vm = lane_range(lo > (uint32_t)c2 ? (lo - c2 + 3) >> 2 : 0u,
-                                                   hi > (uint32_t)c2 ? (hi - c2 + 3) >> 2 : 0u);
-                    const uint32_t lo1 = first ? lo + 1 : lo;
-                    const uint64_t pm = lane_range(lo1 > (uint32_t)c2 ? (lo1 - c2 + 3) >> 2 : 0u,
-                                                   hi > (uint32_t)c2 ? (hi - c2 + 3) >> 2 : 0u);
-                    bad |= __ballot((c2 ? v[c2 - 1] : p0) > v[c2]) & pm;
-                    nonmem |= __ballot(mb[c2] != (v[c2] & lowmask)) & vm;
-                    const uint64_t cm = __ballot(!((wd[c2] >> (o[c2] & 31)) & 1u)) & vm;
-                    if (cm) emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c2]);
-                }
-            }
-        };
-        uint4 pcA[LC_U], pcB[LC_U];
-        for (uint32_t rb = w0; rb < w1; rb += 64) {
-            rows64(rb);
-            issue(0, pcA);
-            for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * LC_U) {
-                issue(s0 + LC_U, pcB);
-                test(s0, pcA);
-                issue(s0 + 2 * LC_U, pcA);
-                test(s0 + LC_U, pcB);
-            }
         }
     }
     if (nc) flush();
@@ -1221,16 +1061,12 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
             hipStreamSynchronize(st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
         const uint32_t kbase = ends[0] >> ks;
         const uint64_t nkeys = (uint64_t)(ends[1] >> ks) - kbase + 1;
-        // the membership table padded to whole 2^17-key ranges of "no PC"
-        // (newcov_cand_keym_kernel stages whole ranges)
-        const uint64_t lok_bytes = align_up(nkeys, 1ull << RSK);
         if (hipMalloc(&st->pc_of_key, nkeys * 4) != hipSuccess ||
-            hipMalloc(&st->low_of_key, lok_bytes) != hipSuccess) {
+            hipMalloc(&st->low_of_key, nkeys) != hipSuccess) {
             rc = SYZCOV_ENOMEM;
             break;
         }
-        if (hipMemsetAsync(st->low_of_key, 0x7F, lok_bytes, st->s) != hipSuccess ||
-            hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
+        if (hipMemsetAsync(d_n, 0, 4, st->s) != hipSuccess) { rc = SYZCOV_EHIP; break; }
         // (the keymap zero-fills pc_of_key and 0x7F-fills low_of_key first)
         if ((rc = syzcov_dev_universe_keymap(lst, hn, ks, kbase, nkeys, st->pc_of_key,
                                              st->low_of_key, d_n, st->s)))
@@ -1373,18 +1209,11 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                                (uint4 *)st->mfl);
             st->mfl_stale = false;
         }
-        // key mode over <= 32 ranges of 2^17 keys: the membership table in LDS
-        // (newcov_cand_keym_kernel); otherwise 2^19-index ranges, membership
-        // bytes gathered per PC (newcov_cand_lds_kernel)
-        const uint64_t nrk = (st->X.span + (1ull << RSK) - 1) >> RSK;
-        const bool keym = st->X.key_mode && nrk <= NR_MAX && !(force_flags() & FORCE_NC_GATHER);
-        static std::atomic<uint32_t> lds_done[3];
+        static std::atomic<uint32_t> lds_done[2];
         auto kfn = st->X.key_mode ? newcov_cand_lds_kernel<true> : newcov_cand_lds_kernel<false>;
-        int rc = keym ? set_dyn_lds_once((const void *)newcov_cand_keym_kernel, 1 << RSK, lds_done[2])
-                      : set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3),
-                                         lds_done[st->X.key_mode ? 1 : 0]);
+        int rc = set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[st->X.key_mode ? 1 : 0]);
         if (rc) return rc;
-        const uint32_t nr = keym ? (uint32_t)nrk : (uint32_t)nr64, stride = (uint32_t)nrec + 1;
+        const uint32_t nr = (uint32_t)nr64, stride = (uint32_t)nrec + 1;
         uint4 *desc = (uint4 *)((uint8_t *)st->grp + grp_desc_off(st->ncalls));
         uint32_t *nq = (uint32_t *)(ws + Lw.nq), *csum = (uint32_t *)(ws + Lw.csum);
         uint32_t *rq = (uint32_t *)(ws + Lw.rq), *qoff = (uint32_t *)(ws + Lw.qoff);
@@ -1400,52 +1229,32 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
             (nrows + ITEMS_MAX - 1) / ITEMS_MAX);
         // sub-runs of the grouped records (records with a bad call id are not
         // grouped: coff[nc] <= nrec)
-        if (keym)
-            hipLaunchKernelGGL(newcov_split_kernel<RSK>, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0,
-                               s, rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff,
-                               st->ncalls, st->X, nr, stride, nq, bq, stats);
-        else
-            hipLaunchKernelGGL(newcov_split_kernel<RSH>, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0,
-                               s, rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff,
-                               st->ncalls, st->X, nr, stride, nq, bq, stats);
+        hipLaunchKernelGGL(newcov_split_kernel, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0, s,
+                           rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls,
+                           st->X, nr, stride, nq, bq, stats);
         const uint32_t nb = (uint32_t)((nrec + RS_CHUNK - 1) / RS_CHUNK);
         hipLaunchKernelGGL(range_sum_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
                            (const uint64_t *)bq, (uint32_t)nrec, stride, csum);
         hipLaunchKernelGGL(range_scan_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
                            (const uint64_t *)bq, (uint32_t)nrec, stride, (const uint32_t *)csum, rq);
         hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
-                           st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre, (int)keym);
+                           st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre);
         hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(64), 0, s, (const uint32_t *)rq,
                            (uint32_t)nrec, stride, nr, qoff);
         const uint32_t ne = nc * nr;
         hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, s,
                            (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)rq, stride, CHR,
-                           (const uint32_t *)ipre, desc, (int)keym);
+                           (const uint32_t *)ipre, desc);
         hipLaunchKernelGGL(row_fill_kernel, dim3(grid_for((uint64_t)nrec * nr, 256, 16384)),
                            dim3(256), 0, s, (const uint32_t *)nq, (const uint64_t *)bq,
                            (const uint32_t *)rq, (const uint32_t *)perm, (const uint32_t *)coff,
                            st->ncalls, nr, stride, (const uint32_t *)qoff, rows);
         // items <= rows / CHR + non-empty (call, range) pairs; the excess exits
         const uint64_t items = nrows / CHR + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
-        if (keym) {  // one workgroup per CU draws the range-major items
-            int dev = 0, ncu = 256;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                ncu = 256;
-            hipLaunchKernelGGL(newcov_cand_keym_kernel,
-                               dim3((unsigned)std::min<uint64_t>(items, (uint64_t)ncu)),
-                               dim3(LC_THREADS), (size_t)(1u << RSK), s, pcs, (uint32_t)npc,
-                               (const uint32_t *)st->mfl, st->words, st->X,
-                               (const uint8_t *)st->low_of_key, (const uint32_t *)ipre, ne,
-                               (const uint4 *)desc, (const uint4 *)rows, (const uint32_t *)qoff,
-                               clist, stats);
-        } else {
-            hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS),
-                               (size_t)(1u << (RSH - 3)), s, pcs, (uint32_t)npc,
-                               (const uint32_t *)st->mfl, st->words, st->X, nr,
-                               (const uint32_t *)ipre, ne, (const uint4 *)desc, (const uint4 *)rows,
-                               (const uint32_t *)qoff, clist, stats);
-        }
+        hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS), (size_t)(1u << (RSH - 3)), s, pcs,
+                           (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
+                           st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
+                           (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
     } else {
         const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
         hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off,

@@ -93,14 +93,11 @@ def test_new_inputs_vs_sequential():
     cc.close()
 
 
-@pytest.fixture(params=["lds", "probe", "gather"])
+@pytest.fixture(params=["lds", "probe"])
 def newcov_path(request, monkeypatch):
-    """The candidate passes of newcov.hip: LDS-staged key ranges (key mode:
-    the membership table in LDS too), global bitmap probes (the library picks
-    one per batch from its shape), and the LDS pass with per-PC membership
-    gathers (key mode; window mode has no membership)."""
-    env = {"lds": "nc_lds", "probe": "nc_probe", "gather": "nc_lds,nc_gather"}[request.param]
-    monkeypatch.setenv("SYZCOV_FORCE", env)
+    """Both candidate passes of newcov.hip: LDS-staged key ranges and global
+    bitmap probes (the library picks one per batch from its shape)."""
+    monkeypatch.setenv("SYZCOV_FORCE", "nc_" + request.param)
     return request.param
 
 
