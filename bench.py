@@ -416,16 +416,22 @@ def c3_single(args, dev):
 
 
 def dropin_legs(args, dev):
-    """cover.Minimize through the drop-in C-ABI from HOST buffers (what the cgo
-    shim of INTEGRATION.md calls): syzcov_minimize (stateless: stage, a
-    transient window-mode engine over the corpus' PC extent, read back) and
-    syzcov_corpus_minimize_host on a persistent key-mode handle (the manager's
-    form).  PCIe-inclusive; the corpora are the C1 / C2 synthetic ones."""
+    """cover.Minimize through the drop-in C-ABI from HOST buffers, PCIe
+    included, on the C1 / C2 synthetic corpora (raw covers, as a manager
+    holds them):
+      shim       syzcov_minimize with the order Go's own sort.Sort produced (what
+                 the cgo shim of INTEGRATION.md passes; here the library's restated
+                 sort over the raw lengths stands in for it, timed apart): the
+                 cached window-mode engine, one call after a warm-up call
+      handle     syzcov_corpus_minimize_host on a persistent key-mode handle
+                 (the manager's resident form; its own order over canonical lengths)
+      groups     syzcov_minimize_corpus (Manager.minimizeCorpus, manager.go:504-524)
+                 over the same corpus split into 293 call groups (sys.CallCount)."""
     import ctypes as C
     import numpy as np
     import torch
     from syzkaller_amd import _lib
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe
+    from syzkaller_amd.engine import synth_corpus, synth_universe
     L = _lib.lib()
     legs = {}
     for name, n, seed in (("C1", 10_000, SEED_C1), ("C2", args.inputs, SEED)):
@@ -437,10 +443,23 @@ def dropin_legs(args, dev):
         del off, raw, lens
         torch.cuda.empty_cache()
         out = np.empty(n, np.int32)
+        # the shim's order: Go sort.Sort(minInputArray) over len(cov) (cover.go:113)
+        rl = np.diff(h_off).astype(np.int64)
+        order = np.empty(n, np.int32)
+        _lib.check(L.syzcov_sort_order(rl.ctypes.data, n, 0, order.ctypes.data), "sort_order")
+        ts = []
+        for _ in range(2):  # the first call creates the cached engine
+            t0 = time.perf_counter()
+            k = _lib.check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n,
+                                             order.ctypes.data, 0, out.ctypes.data), "minimize")
+            ts.append(time.perf_counter() - t0)
+        kept_shim = out[:k].copy()
         t0 = time.perf_counter()
-        k = _lib.check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n, None, 0,
-                                         out.ctypes.data), "minimize")
-        t1 = time.perf_counter()
+        k0 = _lib.check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n, None, 0,
+                                          out.ctypes.data), "minimize")
+        t_noorder = time.perf_counter() - t0
+        assert k0 == k and np.array_equal(out[:k0], kept_shim)
+        L.syzcov_pool_trim()
         univ = synth_universe(args.log2_space, seed, device=dev).cpu().numpy().view(np.uint32)
         cfg = _lib.CorpusCfg(n_max=n, p_max=total, max_seg_len=max_len,
                              universe=univ.ctypes.data, universe_n=univ.size)
@@ -457,15 +476,33 @@ def dropin_legs(args, dev):
                             "corpus_minimize_host")
             tk.append(time.perf_counter() - ta)
         L.syzcov_corpus_destroy(h.value)
-        legs[name] = {
+        leg = {
             "inputs": n, "raw_pcs": total,
-            "syzcov_minimize_ms": round((t1 - t0) * 1e3, 2), "syzcov_minimize_kept": k,
-            "syzcov_minimize_input_pcs_per_s": total / (t1 - t0),
+            "shim_ms": round(ts[1] * 1e3, 2), "shim_first_call_ms": round(ts[0] * 1e3, 2),
+            "shim_kept": k, "shim_input_pcs_per_s": total / ts[1],
+            "restated_order_in_library_ms": round(t_noorder * 1e3, 2),
             "handle_minimize_host_ms": round(min(tk[1:]) * 1e3, 2),
             "handle_minimize_host_kept": k2, "handle_union": nu.value,
             "handle_minimize_host_input_pcs_per_s": total / min(tk[1:]),
-            "note": "host buffers in and out, PCIe transfers included; syzcov_minimize orders "
-                    "by the raw lengths it is given (Minimize of covers as given)"}
+            "shim_vs_handle": ts[1] / min(tk[1:]),
+            "note": "host buffers in and out, PCIe transfers included; the shim orders by the "
+                    "raw lengths (Minimize of covers as given), the handle by canonical lengths"}
+        # Manager.minimizeCorpus: the corpus in 293 call groups (synthetic call ids)
+        calls = np.empty(n, np.int32)
+        s_ = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        cid = torch.empty(n, dtype=torch.int32, device=dev)
+        _lib.check(L.syzcov_dev_synth_callids(seed, 0, n, 293, C.c_void_p(cid.data_ptr()), s_),
+                   "synth_callids")
+        calls[:] = cid.cpu().numpy()
+        t0 = time.perf_counter()
+        kg = _lib.check(L.syzcov_minimize_corpus(calls.ctypes.data, h_off.ctypes.data,
+                                                 h_pcs.ctypes.data, n, 0, out.ctypes.data),
+                        "minimize_corpus")
+        tg = time.perf_counter() - t0
+        leg.update({"groups": 293, "minimize_corpus_ms": round(tg * 1e3, 2),
+                    "minimize_corpus_kept": kg, "minimize_corpus_input_pcs_per_s": total / tg})
+        L.syzcov_pool_trim()
+        legs[name] = leg
         del h_pcs, h_off
     return legs
 

@@ -22,4 +22,6 @@ for v in base noconf; do
   env $e timeout -k 10 120 python -u tools/kbench.py canon --keys --reps 4 > $o/canon_$v.log 2>&1 || { tail -5 $o/canon_$v.log; exit 1; }
   echo "canon $v: $(tail -2 $o/canon_$v.log | head -1)"
 done
+timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > $o/bench.json 2> $o/bench.err
+rc=$?; cat $o/bench.json; [ $rc -ne 0 ] && tail -20 $o/bench.err; fatal $rc bench
 echo done
