@@ -343,6 +343,12 @@ namespace syz {
 constexpr size_t kEngineMinInputs = 1024;
 int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,
                         const int32_t *order, int32_t *out_idx, int64_t *out_n);
+// Manager.minimizeCorpus with at least this many inputs runs on the corpus
+// engine (per-group Minimize over one rank space, corpus.hip); below it the
+// per-group launches cost more than the dictionary path's batched slabs
+constexpr size_t kGroupEngineMinInputs = 65536;
+int minimize_corpus_via_engine(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                               size_t n, int32_t *out_idx, int64_t *out_n);
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
 int ui_stats_launch(const uint64_t *off, const uint32_t *pcs, uint32_t n, const int32_t *call,
                     uint32_t ncalls, const uint64_t *tab, uint32_t pc_lo, uint32_t nids,
@@ -601,6 +607,12 @@ int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, con
     if (!call || !offsets || !out_idx || n > 0x7FFFFFFF || sort_variant != 0)
         return SYZCOV_EINVAL;
     if (offsets[n] > offsets[0] && !pcs) return SYZCOV_EINVAL;
+    if (n >= kGroupEngineMinInputs && device_count() > 0) {
+        int64_t k = 0;
+        const int rc = minimize_corpus_via_engine(call, offsets, pcs, n, out_idx, &k);
+        if (rc < 0) return rc;
+        if (rc == 1) return k;
+    }
     CtxLease lease;
     Ctx *c = lease.get();
     if (!c) return SYZCOV_ENODEV;

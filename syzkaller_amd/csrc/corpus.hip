@@ -18,6 +18,7 @@
 // Every buffer lives in one device block, carved by a fixed layout, either
 // allocated by the handle or handed in by the caller (torch's caching
 // allocator in Python), so the exchanged buffers can be wrapped as tensors.
+#include <algorithm>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -486,6 +487,31 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
         c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
         c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, 0, 0, 0,
         c.buf<void>(SYZCOV_CORPUS_WS), s);
+}
+
+int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                          const uint32_t *split, const int32_t *order, size_t n_items,
+                          uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+                          const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered,
+                          int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
+                          uint8_t *cand, uint8_t *kept, uint32_t *err_flag,
+                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s);
+
+// Minimize per group of ranks [grp_off[g], grp_off[g+1]) (host offsets), one
+// GPU: Manager.minimizeCorpus's per-call cover.Minimize (manager.go:516-524)
+// over an order that concatenates the groups' own sort.Sort orders.
+static int ph_minimize_groups(Corpus &c, const uint64_t *grp_off, uint32_t ngroups,
+                              hipStream_t s) {
+    if (!c.canon || !c.N || c.shard) return SYZCOV_EINVAL;
+    return minimize_range_groups(
+        c.off, c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN), c.canon, c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT),
+        c.buf<int32_t>(SYZCOV_CORPUS_ORDER), c.n, c.pc_lo, c.span, c.rshift,
+        c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT),
+        c.key_mode ? c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY) : nullptr,
+        c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.buf<int32_t>(SYZCOV_CORPUS_FIRST),
+        c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
+        c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT),
+        (uint32_t *)(scal(c) + SC_ERR), grp_off, ngroups, c.buf<void>(SYZCOV_CORPUS_WS), s);
 }
 
 // Window mode, sharded: the dictionary of the merged covered set and this
@@ -1227,6 +1253,111 @@ static int64_t dropin_run(DropinCache &dc, const uint64_t *offsets, const uint32
                  : SYZCOV_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = SYZCOV_EHIP;
     return rc ? rc : (int64_t)r.n_kept + 1;  // + 1: 0 means "not taken"
+}
+
+int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
+                          uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
+                          hipStream_t s);
+
+// Manager.minimizeCorpus (manager.go:504-524) on the cached engine: the
+// corpus is staged as it is; the groups (inputs of one RpcInput.Call, corpus
+// order inside, :511-516) exist only in the processing order, which
+// concatenates every group's Go sort.Sort order (the segmented restatement,
+// gosort.hip) — so the engine canonicalizes once and runs one Minimize per
+// group over its rank interval (minimize_range_groups).  Kept corpus indices
+// come out grouped by ascending call value, each group in its Minimize order.
+static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uint64_t *offsets,
+                                 const uint32_t *pcs, size_t n, int32_t *out_idx, hipStream_t s) {
+    const uint64_t base = offsets[0], P = offsets[n] - base;
+    std::vector<uint64_t> hoff(n + 1);
+    size_t max_len = 1;
+    for (size_t i = 0; i <= n; i++) {
+        hoff[i] = offsets[i] - base;
+        if (i && hoff[i] < hoff[i - 1]) return SYZCOV_EINVAL;
+        if (i) max_len = std::max<size_t>(max_len, hoff[i] - hoff[i - 1]);
+    }
+    // groups: stable by call value (the reference's append order)
+    std::vector<int32_t> perm(n);
+    for (size_t i = 0; i < n; i++) perm[i] = (int32_t)i;
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](int32_t a, int32_t b) { return call[a] < call[b]; });
+    std::vector<uint64_t> goff;
+    std::vector<int64_t> lens(n);
+    for (size_t i = 0; i < n; i++) {
+        if (i == 0 || call[perm[i]] != call[perm[i - 1]]) goff.push_back(i);
+        lens[i] = (int64_t)(hoff[perm[i] + 1] - hoff[perm[i]]);  // len(cov), duplicates included
+    }
+    goff.push_back(n);
+    const uint32_t G = (uint32_t)goff.size() - 1;
+    const size_t wseg = syzcov_dev_sort_seg_ws_size(n, G);
+    const size_t o_pcs = align_up((n + 1) * 8, 256), o_perm = o_pcs + align_up((P + 1) * 4, 256),
+                 o_goff = o_perm + align_up(n * 4, 256), o_lens = o_goff + align_up((G + 1) * 8, 256),
+                 o_ordg = o_lens + align_up(n * 8, 256), o_ordc = o_ordg + align_up(n * 4, 256),
+                 o_rg = o_ordc + align_up(n * 4, 256), o_mm = o_rg + align_up(n * 4, 256),
+                 o_ws = o_mm + 256, need = o_ws + align_up(wseg, 256);
+    if (need > dc.stage_cap) {
+        if (dc.stage) hipFree(dc.stage);
+        dc.stage = nullptr;
+        dc.stage_cap = 0;
+        if (hipMalloc(&dc.stage, need) != hipSuccess) return 0;
+        dc.stage_cap = need;
+    }
+    uint8_t *st = (uint8_t *)dc.stage;
+    uint64_t *d_off = (uint64_t *)st, *d_goff = (uint64_t *)(st + o_goff);
+    uint32_t *d_pcs = (uint32_t *)(st + o_pcs), *d_mm = (uint32_t *)(st + o_mm);
+    int32_t *d_perm = (int32_t *)(st + o_perm), *d_ordg = (int32_t *)(st + o_ordg),
+            *d_ordc = (int32_t *)(st + o_ordc);
+    SYZ_HIP(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(d_perm, perm.data(), n * 4, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(d_goff, goff.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
+    SYZ_HIP(hipMemcpyAsync(st + o_lens, lens.data(), n * 8, hipMemcpyHostToDevice, s));
+    int rc = minmax_pcs(d_pcs, P, d_mm, s);
+    if (rc) return rc;
+    uint32_t mm[2];
+    SYZ_HIP(hipMemcpyAsync(mm, d_mm, 8, hipMemcpyDeviceToHost, s));
+    SYZ_HIP(hipStreamSynchronize(s));
+    if (nrange_of((uint64_t)mm[1] - mm[0] + 1, kRangeShiftWindow) > 256) return 0;
+    rc = syzcov_dev_sort_order_segmented((const int64_t *)(st + o_lens), d_goff, G, n, 0, d_ordg,
+                                         st + o_ws, wseg, s);
+    if (!rc)
+        rc = minimize_groups_order(d_ordg, d_perm, d_goff, G, (uint32_t)n, d_ordc,
+                                   (uint32_t *)(st + o_rg), s);
+    if (rc) return rc;
+    rc = dropin_handle(dc, n, P, max_len, mm[0], mm[1]);
+    if (rc <= 0) return rc;
+    Corpus &c = *get(dc.h);
+    Use u(&c);
+    rc = ph_canon(c, d_off, d_pcs, n, s);
+    if (!rc) rc = ph_order_given(c, d_ordc, n, s);
+    if (!rc) rc = ph_minimize_groups(c, goff.data(), G, s);
+    if (!rc) rc = ph_finish(c, s);
+    syzcov_corpus_res r{};
+    if (!rc) rc = ph_result(c, &r, s);
+    if (!rc && r.n_kept)
+        rc = hipMemcpyAsync(out_idx, r.kept_idx, (size_t)r.n_kept * 4, hipMemcpyDeviceToHost, s) ==
+                     hipSuccess
+                 ? 0
+                 : SYZCOV_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = SYZCOV_EHIP;
+    return rc ? rc : (int64_t)r.n_kept + 1;
+}
+
+int minimize_corpus_via_engine(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
+                               size_t n, int32_t *out_idx, int64_t *out_n) {
+    if (offsets[n] == offsets[0]) return 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    DropinCache &dc = g_dropin[dev];
+    std::unique_lock<std::mutex> lk(dc.mu, std::try_to_lock);
+    if (!lk.owns_lock()) return 0;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
+    const int64_t k = dropin_run_groups(dc, call, offsets, pcs, n, out_idx, s);
+    hipStreamDestroy(s);
+    if (k <= 0) return (int)k;
+    *out_n = k - 1;
+    return 1;
 }
 
 int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,

@@ -685,7 +685,8 @@ static int minimize_range_impl(
     uint32_t range_shift, const uint64_t *range_tot, uint32_t *covered, int32_t *first_w,
     uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
     size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, const uint8_t *low_of_key,
-    uint32_t *err_flag, void *ws, void *stream) {
+    uint32_t *err_flag, void *ws, void *stream, const uint64_t *grp_off = nullptr,
+    uint32_t ngroups = 0) {
     hipStream_t s = (hipStream_t)stream;
     if (n_items == 0) {
         if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
@@ -723,7 +724,7 @@ static int minimize_range_impl(
 #define SYZ_MR_GROWTH 4
 #endif
     if (first_chunk == 0) first_chunk = SYZ_MR_FIRST;
-    if (growth < 2) growth = SYZ_MR_GROWTH;
+    if (growth < 2) growth = grp_off ? 8 : SYZ_MR_GROWTH;
     // sweep at C2: 2^17 PCs per workgroup 4.03, 2^19 4.00, 2^20 4.40 ms
 #ifndef SYZ_MR_HINT_LOG
 #define SYZ_MR_HINT_LOG 19
@@ -736,43 +737,78 @@ static int minimize_range_impl(
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     // below 2^24 keys (64 MB of first_w) the covered set is rebuilt from first_w
     const bool cover_from_first = pc_span <= (1ull << 24);
-    uint64_t a = 0, step = first_chunk;
-    int par = 0;  // done-mark set of this chunk
-    uint32_t nchunk = 0;
-    while (a < n_items) {
-        const uint64_t b = std::min<uint64_t>(n_items, a + step);
-        // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
-        // P = 16R pieces per slice (fewer, larger pieces in the small chunks,
-        // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2)
-        uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
-        G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
-        const uint64_t P = SYZ_MR_PPS * (uint64_t)nrange;  // pieces per slice
-        G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
-        // dynamic pieces: one workgroup per CU draws them
-        if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
-        A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
-                              (size_t)nchunk * 256);
-        A.npieces = (uint32_t)G;
-        const unsigned grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
-        nchunk++;
-        hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
-                           (uint32_t)b, (uint32_t)P, (int)(a != 0));
-        // the chunk's first covers (+ covered, unless rebuilt below)
-        hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
-                           (int)!cover_from_first);
-        // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
-        // first_w (16 MB at 2^22 keys) instead of an atomicOr per record (C2 key
-        // mode: 5 vs 74-274 us per early chunk)
-        if (cover_from_first && b < n_items)
-            RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
-        par ^= 1;
-        a = b;
-        step *= growth;
+    // pass 1 over the items [a0, a1) in geometric chunks (covered empty at a0)
+    auto run_span = [&](uint64_t a0, uint64_t a1, uint64_t step0) -> int {
+        uint64_t a = a0, step = step0;
+        int par = 0;  // done-mark set of this chunk
+        uint32_t nchunk = 0;
+        while (a < a1) {
+            const uint64_t b = std::min<uint64_t>(a1, a + step);
+            // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
+            // P = 16R pieces per slice (fewer, larger pieces in the small chunks,
+            // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2)
+            uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
+            G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
+            const uint64_t P = SYZ_MR_PPS * (uint64_t)nrange;  // pieces per slice
+            G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
+            // dynamic pieces: one workgroup per CU draws them
+            if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
+            A.pctr = (uint32_t *)((uint8_t *)ws + 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
+                                  (size_t)nchunk * 256);
+            A.npieces = (uint32_t)G;
+            const unsigned grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
+            nchunk++;
+            hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
+                               (uint32_t)b, (uint32_t)P, (int)(a != a0));
+            // the chunk's first covers (+ covered, unless rebuilt below)
+            hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
+                               (int)!cover_from_first);
+            // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
+            // first_w (16 MB at 2^22 keys) instead of an atomicOr per record (C2
+            // key mode: 5 vs 74-274 us per early chunk)
+            if (cover_from_first && b < a1)
+                RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
+            par ^= 1;
+            a = b;
+            step *= growth;
 #ifdef SYZ_MR_MAXCHUNK
-        step = std::min<uint64_t>(step, SYZ_MR_MAXCHUNK);  // tuning sweeps only
+            step = std::min<uint64_t>(step, SYZ_MR_MAXCHUNK);  // tuning sweeps only
 #endif
+        }
+        hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
+        return 0;
+    };
+    if (grp_off) {
+        // Manager.minimizeCorpus (manager.go:504-524): one cover.Minimize per
+        // call group, the groups' processing orders concatenated into one rank
+        // space ([grp_off[g], grp_off[g+1]) is group g).  Each group runs pass 1
+        // from an empty covered set, its own pass 2, and returns first_w to
+        // INT32_MAX at its records, so the next group starts clean.  (Groups
+        // are far shorter than a corpus: first chunk 256, growth 8.)
+        if (!do_pass2 || ngroups == 0 || grp_off[ngroups] != n_items) return SYZCOV_EINVAL;
+        for (uint32_t g = 0; g < ngroups; g++) {
+            const uint64_t a0 = grp_off[g], a1 = grp_off[g + 1];
+            if (a1 < a0 || a1 > n_items) return SYZCOV_EINVAL;
+            if (a1 == a0) continue;
+            if (g) SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters, done marks
+            if (!cover_from_first)
+                SYZ_HIP(hipMemsetAsync(covered, 0, (((uint64_t)nrange << range_shift) + 7) / 8, s));
+            RC_(run_span(a0, a1, 256));
+            hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, A,
+                               (const uint64_t *)nullptr, (const int32_t *)nullptr, kept);
+            hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, A.n_items,
+                               (const int32_t *)A.first_w, (const uint64_t *)nullptr,
+                               (const int32_t *)nullptr, kept);
+            hipLaunchKernelGGL(mr::reset_kernel, dim3(1024), dim3(256), 0, s, A);
+            hipLaunchKernelGGL(mr::ovf_reset_kernel, dim3(2048), dim3(256), 0, s,
+                               (const unsigned long long *)rec_cnt, rec_cap, first_w, pc_span);
+            SYZ_LAUNCH_CHECK();
+        }
+        // covered: no union is asked of a grouped step (left empty)
+        SYZ_HIP(hipMemsetAsync(covered, 0, (((uint64_t)nrange << range_shift) + 7) / 8, s));
+        return 0;
     }
-    hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
+    RC_(run_span(0, n_items, first_chunk));
     if (cover_from_first) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
     // record overflow: the union comes from first_w instead (cover_from_first
     // already rebuilt covered from first_w)
@@ -785,6 +821,22 @@ static int minimize_range_impl(
     rc = mr_pass2(A, pc_span, nullptr, nullptr, kept, s);
     return rc;
 }
+
+// Minimize per call group over one rank space (corpus.hip: the grouped
+// drop-in for Manager.minimizeCorpus); key mode when low_of_key is given.
+namespace syz {
+int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
+                          const uint32_t *split, const int32_t *order, size_t n_items,
+                          uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+                          const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered,
+                          int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
+                          uint8_t *cand, uint8_t *kept, uint32_t *err_flag,
+                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s) {
+    return minimize_range_impl(off, len, pcs, split, order, nullptr, n_items, pc_lo, pc_span,
+                               range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand,
+                               kept, 1, 0, 0, 0, low_of_key, err_flag, ws, s, grp_off, ngroups);
+}
+}  // namespace syz
 
 extern "C" int syzcov_dev_minimize_range(
     const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,

@@ -233,3 +233,66 @@ def test_c5_newcov_stream_fullsize(torch, name, keys):
         hh.update(st.max_cover(c).astype("<u4").tobytes())
     assert hh.hexdigest() == g["max_cover_sha256"]
     st.close()
+
+
+def _c2_host(torch, g):
+    from syzkaller_amd.engine import synth_corpus
+    off, raw, lens, total = synth_corpus(g["n"], g["seed"], mean=g["mean"], sigma=g["sigma"],
+                                         log2_space=g["log2_space"])
+    assert total == g["raw_pcs"]
+    h_off = off.cpu().numpy().astype(np.uint64)
+    h_pcs = raw[:total].cpu().numpy().view(np.uint32).copy()
+    del off, raw
+    torch.cuda.empty_cache()
+    return h_off, h_pcs
+
+
+def test_c2_dropin_raw_covers_digest(torch):
+    """cover.Minimize through the drop-in C-ABI (host buffers) on C2's RAW
+    covers, as the cgo shim calls it: with the caller's own sort.Sort order
+    over len(cov) (here the library's restated order over the raw lengths
+    stands in for Go's) and without an order: the oracle's kept list (C2R,
+    oracle/grouped_full.c with one group)."""
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    g = golden("C2R")
+    h_off, h_pcs = _c2_host(torch, g)
+    n = g["n"]
+    out = np.empty(n, np.int32)
+    rl = np.diff(h_off).astype(np.int64)
+    order = np.empty(n, np.int32)
+    _lib.check(L.syzcov_sort_order(rl.ctypes.data, n, 0, order.ctypes.data), "sort_order")
+    for op in (order, None):
+        k = _lib.check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n,
+                                         None if op is None else op.ctypes.data, 0,
+                                         out.ctypes.data), "minimize")
+        assert k == g["n_kept"]
+        assert out[:16].tolist() == g["kept_head"]
+        assert hashlib.sha256(out[:k].astype("<i4").tobytes()).hexdigest() == g["kept_sha256"]
+    L.syzcov_pool_trim()
+
+
+def test_c2_minimize_corpus_293_groups_digest(torch):
+    """Manager.minimizeCorpus (manager.go:504-524) on C2's raw covers in 293
+    call groups (synthetic call ids) through syzcov_minimize_corpus (the
+    engine's per-group Minimize over one rank space): the oracle's kept
+    corpus indices, groups in ascending call id (C2G, oracle/grouped_full.c)."""
+    import ctypes as C
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    g = golden("C2G")
+    h_off, h_pcs = _c2_host(torch, g)
+    n = g["n"]
+    cid = torch.empty(n, dtype=torch.int32, device="cuda")
+    _lib.check(L.syzcov_dev_synth_callids(g["seed"], 0, n, g["ncalls"], C.c_void_p(cid.data_ptr()),
+                                          C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+               "synth_callids")
+    calls = cid.cpu().numpy().astype(np.int32)
+    out = np.empty(n, np.int32)
+    k = _lib.check(L.syzcov_minimize_corpus(calls.ctypes.data, h_off.ctypes.data,
+                                            h_pcs.ctypes.data, n, 0, out.ctypes.data),
+                   "minimize_corpus")
+    assert k == g["n_kept"]
+    assert out[:16].tolist() == g["kept_head"]
+    assert hashlib.sha256(out[:k].astype("<i4").tobytes()).hexdigest() == g["kept_sha256"]
+    L.syzcov_pool_trim()

@@ -65,6 +65,20 @@ def test_minimize_corpus_synthetic(cover):
     assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
 
 
+def test_minimize_corpus_engine_size(cover):
+    """At >= 65,536 inputs syzcov_minimize_corpus runs on the corpus engine
+    (one Minimize per call group over one rank space): raw covers with
+    duplicates, tie-heavy lengths, groups of very different sizes (one huge,
+    many tiny, a single-input one), against the oracle."""
+    rng = np.random.default_rng(61)
+    n = 70_000
+    covs = [rng.integers(0x81000000, 0x81000000 + 3000, size=int(rng.integers(0, 40))).astype(
+        np.uint32) for _ in range(n)]
+    calls = np.where(rng.random(n) < 0.5, 7, rng.integers(0, 400, size=n)).astype(np.int32)
+    calls[123] = 100_000  # a group of one
+    assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
+
+
 def test_minimize_corpus_manager_mirror():
     from syzkaller_amd.manager import RpcInput, minimize_corpus
     covs = [[1, 2, 3, 4], [5], [1, 2], [3, 4, 5, 6, 7], [5, 6], [3, 7]]

@@ -7,6 +7,10 @@ digests the GPU tests compare the engine against.
   C2  1M inputs    seed 0x5EED0002   (one MI355X; also the world-8 rehearsal)
   C3  10M inputs   seed 0x5EED0003   (the 8-GPU config; 82 GB of raw PCs)
   C5S the same stream over 514 batches (512 history, steady state)
+  C2G Manager.minimizeCorpus over C2's RAW covers in 293 call groups
+      (synthetic call ids; oracle/grouped_full.c): the kept corpus indices
+  C2R cover.Minimize over C2's RAW covers (one group: order by raw lengths,
+      what the drop-in syzcov_minimize computes from host buffers)
   C5  34 batches of 65,536 call records, seed 0x5EED0005, 293 calls: the
       fuzzer's new-coverage check (oracle/newcov_full.c), per-batch is_new
       flags and the final per-call maxCover (the bench's stream: 32 history
@@ -78,6 +82,29 @@ def run(name: str, threads: int) -> dict:
     return out
 
 
+GROUPED = {"C2G": dict(seed=0x5EED0002, n=1_000_000, ncalls=293),
+           "C2R": dict(seed=0x5EED0002, n=1_000_000, ncalls=1)}
+
+
+def run_grouped(name: str) -> dict:
+    g = GROUPED[name]
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    exe = os.path.join(ROOT, "oracle", "build", "grouped_full")
+    with tempfile.TemporaryDirectory() as d:
+        t0 = time.time()
+        out = os.path.join(d, "kept.i32")
+        r = subprocess.run([exe, hex(g["seed"]), str(g["n"]), str(MEAN), str(SIGMA), str(LOG2),
+                            str(g["ncalls"]), out], check=True, capture_output=True, text=True)
+        summary = json.loads(r.stdout)
+        kept = np.fromfile(out, dtype=np.int32)
+        return dict(seed=g["seed"], n=g["n"], ncalls=g["ncalls"], mean=MEAN, sigma=SIGMA,
+                    log2_space=LOG2, raw_pcs=summary["raw_pcs"], n_kept=summary["n_kept"],
+                    kept_sha256=sha(out), kept_head=kept[:16].tolist(),
+                    kept_tail=kept[-16:].tolist(), covers="raw (duplicates count in len)",
+                    groups="orc_synth_callid(seed, i, ncalls), ascending call id",
+                    sort="pdqsort (Go >= 1.19)", oracle_seconds=round(time.time() - t0, 1))
+
+
 def run_c5(threads: int, c: dict = C5) -> dict:
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     exe = os.path.join(ROOT, "oracle", "build", "newcov_full")
@@ -119,6 +146,8 @@ def main():
         nt = int(os.environ.get("ORACLE_THREADS", os.cpu_count() or 8))
         if name in ("C5", "C5S"):
             data[name] = run_c5(nt, C5 if name == "C5" else C5S)
+        elif name in GROUPED:
+            data[name] = run_grouped(name)
         else:
             data[name] = run(name, nt)
         print(json.dumps(data[name]), flush=True)
