@@ -495,19 +495,6 @@ constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
 
-// The 11-bit digit of a key.  SYZ_PROBE_NOCONF (timing probe only, wrong
-// results): a digit whose histogram word is lane-distinct within every 32-lane
-// group, i.e. the same LDS operations without bank conflicts.
-__device__ __forceinline__ uint32_t digit11(uint32_t k, uint32_t sh, uint32_t l) {
-#ifdef SYZ_PROBE_NOCONF
-    const uint32_t x = k >> sh;
-    return ((l & 31u) << 1) | (x & 1u) | (((x >> 1) & 15u) << 6);
-#else
-    (void)l;
-    return (k >> sh) & 2047u;
-#endif
-}
-
 // exclusive scan of the 2048 u16 counts in bin order, in place
 __device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(h);
@@ -541,45 +528,58 @@ __device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
     for (int q = 0; q < 4; q++) h4[4 * l + q] = make_uint4(0, 0, 0, 0);
 }
 
-// count the digit (k >> sh) & 2047 of the real slots (pads: the lane's dummy word)
-template <bool RAW, int NK>
-__device__ __forceinline__ void count16(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
-                                       uint32_t lo, uint32_t hi, uint32_t *h, uint32_t sh) {
+// Gapped key words (the sort's register/LDS form in canon_key_kernel): the
+// 22-bit key's digits 12 bits apart, lo11 | hi11 << 12, the PC's low bits
+// from bit 24.  A real key's 12-bit digit (k >> sh) & 4095 (sh 0 or 12) is its
+// 11-bit digit; a PAD slot's word has digit 2048 + 2l in both passes, whose
+// histogram word KWORDS + l is its lane's private dummy: pads need no
+// per-slot select in the count and scatter loops (they rank on the dummy,
+// which starts each scatter at CAP, so they land past the real keys).
+__device__ __forceinline__ uint32_t gap_key(uint32_t key, uint32_t low) {
+    return (key & 2047u) | ((key >> 11) << 12) | (low << 24);
+}
+__device__ __forceinline__ uint32_t pad_word(uint32_t l) {
+    const uint32_t d = 2048u + 2u * l;
+    return d | (d << 12);
+}
+// the key word of common.h (key | low << SYZ_KEY_BITS) of a gapped word
+__device__ __forceinline__ uint32_t ungap_word(uint32_t g) {
+    return (g & 2047u) | (((g >> 12) & 2047u) << 11) | ((g >> 24) << SYZ_KEY_BITS);
+}
+constexpr uint32_t GAP_KEY_MASK = 2047u | (2047u << 12);
+
+// count / rank+scatter over gapped words: no validity tests (pads carry
+// their lane's dummy digit).  Inactive row quads hold pads too.
+template <int NK>
+__device__ __forceinline__ void count_gap(const uint32_t (&k)[NK], uint32_t nq, uint32_t *h,
+                                          uint32_t sh) {
     constexpr int NQ = NK / 4;
 #pragma unroll
     for (int q = 0; q < NQ; q++)
         if ((uint32_t)q < nq) {
 #pragma unroll
             for (int c = 0; c < 4; c++) {
-                const bool ok = real_slot<RAW, NK>(q * 4 + c, l, lo, hi);
-                const uint32_t d = digit11(k[q * 4 + c], sh, l);
-                atomicAdd(&h[ok ? d >> 1 : KWORDS + l], ok ? hinc(d) : 1u);
+                const uint32_t d = (k[q * 4 + c] >> sh) & 4095u;
+                atomicAdd(&h[d >> 1], hinc(d));
             }
         }
 }
 
-// rank (ds_add_rtn on the u16 half) and scatter; atomics of BQ row quads
-// issued before their stores, as scatter_rows
-template <bool RAW, int NK, int BQ = SYZ_CANON_BQ>
-__device__ __forceinline__ void scatter16(const uint32_t (&k)[NK], uint32_t nq, uint32_t l,
-                                          uint32_t lo, uint32_t hi, uint32_t *buf, uint32_t *h,
-                                          uint32_t sh) {
+template <int NK, int BQ = SYZ_CANON_BQ>
+__device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq, uint32_t *buf,
+                                            uint32_t *h, uint32_t sh) {
     constexpr int NQ = NK / 4;
-    constexpr uint32_t CAP = 64 * NK;
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += BQ) {
         if ((uint32_t)q0 >= nq) continue;
         uint32_t pos[4 * BQ];
-        bool ok[4 * BQ];
 #pragma unroll
-        for (int j = 0; j < 4 * BQ; j++) {  // branch-free, as scatter_rows
-            ok[j] = (uint32_t)(q0 + j / 4) < nq && real_slot<RAW, NK>(q0 * 4 + j, l, lo, hi);
-            const uint32_t d = digit11(k[q0 * 4 + j], sh, l);
-            pos[j] = atomicAdd(&h[ok[j] ? d >> 1 : KWORDS + l], ok[j] ? hinc(d) : 1u) >>
-                     ((d & 1u) << 4);
+        for (int j = 0; j < 4 * BQ; j++) {
+            const uint32_t d = (k[q0 * 4 + j] >> sh) & 4095u;
+            pos[j] = atomicAdd(&h[d >> 1], hinc(d)) >> ((d & 1u) << 4);
         }
 #pragma unroll
-        for (int j = 0; j < 4 * BQ; j++) buf[ok[j] ? pos[j] & 0xFFFFu : CAP + l] = k[q0 * 4 + j];
+        for (int j = 0; j < 4 * BQ; j++) buf[pos[j] & 0xFFFFu] = k[q0 * 4 + j];
     }
 }
 
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                                                                    const uint32_t *count) {
     constexpr int CAP = 64 * NK;
     constexpr int NQ = NK / 4;
-    __shared__ uint32_t s_buf[WPB][CAP + 64];
+    __shared__ uint32_t s_buf[WPB][CAP + NK];  // + the lane's pads (<= NK) past CAP
     __shared__ __attribute__((aligned(16))) uint32_t s_h[WPB][KWORDS + 64];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
@@ -598,6 +598,12 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     const uint32_t span_m1 = (uint32_t)(P.span - 1);
     const uint32_t kmax = (uint32_t)(P.nkeys - 1);
     const bool inplace = P.out == P.raw;
+    const uint32_t pad = pad_word(l);
+    // the previous word of slot 0: the sentinel's key word (cover.go:31,
+    // `last := sent`), gapped; ~0 never equals a gapped word
+    const uint32_t sent_g = P.sent_key == 0xFFFFFFFFu
+                                ? 0xFFFFFFFFu
+                                : gap_key(P.sent_key & SYZ_KEY_MASK, P.sent_key >> SYZ_KEY_BITS);
     uint32_t racc[MAX_RPL];
 #pragma unroll
     for (int q = 0; q < MAX_RPL; q++) racc[q] = 0;
@@ -630,7 +636,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
         const uint32_t nq = (end + 255) >> 8;
-        uint32_t k[NK] = {};  // slots of inactive row quads rank on dummies
+        uint32_t k[NK];  // gapped words; slots outside the segment are pads
+#pragma unroll
+        for (int j = 0; j < NK; j++) k[j] = pad;
         bool oob = false;
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
@@ -643,9 +651,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const bool valid = idx >= head && idx < end;
                     const bool out = vv[c] - P.pc_lo > span_m1;
                     oob |= valid && out;
-                    k[q * 4 + c] = out ? kmax
-                                       : ((vv[c] >> P.kshift) - P.kbase) |
-                                             ((vv[c] & P.lowmask) << KEY_BITS);
+                    const uint32_t g = out ? gap_key(kmax, 0u)
+                                           : gap_key((vv[c] >> P.kshift) - P.kbase, vv[c] & P.lowmask);
+                    k[q * 4 + c] = valid ? g : pad;
                 }
             }
         }
@@ -654,11 +662,20 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         // ---------------------------------------- pass 0: low 11 bits
         hist16_zero<NQ>(h, l);
         wave_sync();
-        count16<true, NK>(k, nq, l, head, end, h, 0);
+        count_gap<NK>(k, nq, h, 0);
         wave_sync();
         hist16_scan(h, l);
+        h[KWORDS + l] = CAP;  // the lane's pads rank from CAP on
         wave_sync();
-        scatter16<true, NK, BQK>(k, nq, l, head, end, buf, h, 0);
+        scatter_gap<NK, BQK>(k, nq, buf, h, 0);
+        wave_sync();
+        // slots [n, 256 nq) are read back by pass 1: pads of the reading lane
+        // (fewer than 260 slots: at most 5 per lane, unrolled)
+#pragma unroll
+        for (uint32_t t = 0; t < 5; t++) {
+            const uint32_t p = (n & ~63u) + l + 64 * t;
+            if (p >= n && p < nq * 256u) buf[p] = pad;
+        }
         wave_sync();
         // ---------------------------- pass 1: high 11 bits, stable (row-major)
 #pragma unroll
@@ -669,11 +686,12 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
             }
         hist16_zero<NQ>(h, l);
         wave_sync();
-        count16<false, NK>(k, nq, l, 0, n, h, KB);
+        count_gap<NK>(k, nq, h, 12);
         wave_sync();
         hist16_scan(h, l);
+        h[KWORDS + l] = CAP;
         wave_sync();
-        scatter16<false, NK, BQK>(k, nq, l, 0, n, buf, h, KB);
+        scatter_gap<NK, BQK>(k, nq, buf, h, 12);
         wave_sync();
         // --------------------------------- order check + unique + write
 #pragma unroll
@@ -683,13 +701,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
         uint32_t bad = P.force_redo;
-#ifdef SYZ_PROBE_NOCONF
-        const uint32_t probe_ok = 0;  // the probe's order is not a sort: never redo
-#else
-        const uint32_t probe_ok = 1;
-#endif
         if (inplace) {  // nothing may be written before the order is known
-            uint32_t carry = P.sent_key;
+            uint32_t carry = sent_g;
 #pragma unroll
             for (int q = 0; q < NQ; q++)
                 if ((uint32_t)q < nq) {
@@ -699,7 +712,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
-                        bad |= probe_ok & (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                        bad |= (uint32_t)((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) &
                                (uint32_t)(e - 1u < n - 1u);
                     }
                 }
@@ -708,7 +721,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = P.sent_key;
+        uint32_t cnt = 0, carry = sent_g;
         uint32_t *outp = P.out + base;
 #pragma unroll
         for (int q = 0; q < NQ; q++)
@@ -719,15 +732,16 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= probe_ok & (uint32_t)((v & KEY_MASK) < (prev & KEY_MASK)) &
+                    bad |= (uint32_t)((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) &
                            (uint32_t)(e - 1u < n - 1u);
                     // whole words: distinct PCs stay distinct even if they share a key
                     const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
                     if (keep) {
-                        outp[pos] = v;  // the key word: the PC is kept exactly
-                        buf[pos] = v & KEY_MASK;
+                        const uint32_t w = ungap_word(v);
+                        outp[pos] = w;  // the key word: the PC is kept exactly
+                        buf[pos] = w & KEY_MASK;
                     }
                     cnt += (uint32_t)__popcll(m);
                 }

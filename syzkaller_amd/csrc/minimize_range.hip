@@ -771,9 +771,6 @@ static int minimize_range_impl(
             par ^= 1;
             a = b;
             step *= growth;
-#ifdef SYZ_MR_MAXCHUNK
-            step = std::min<uint64_t>(step, SYZ_MR_MAXCHUNK);  // tuning sweeps only
-#endif
         }
         hipLaunchKernelGGL(mr::total_kernel, dim3(1), dim3(64), 0, s, A);
         return 0;
