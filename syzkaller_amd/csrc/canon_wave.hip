@@ -529,27 +529,43 @@ __device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
 }
 
 // Gapped key words (the sort's register/LDS form in canon_key_kernel): the
-// 22-bit key's digits 12 bits apart, lo11 | hi11 << 12, the PC's low bits
-// from bit 24.  A real key's 12-bit digit (k >> sh) & 4095 (sh 0 or 12) is its
-// 11-bit digit; a PAD slot's word has digit 2048 + 2l in both passes, whose
-// histogram word KWORDS + l is its lane's private dummy: pads need no
-// per-slot select in the count and scatter loops (they rank on the dummy,
-// which starts each scatter at CAP, so they land past the real keys).
+// 22-bit key's digits 12 bits apart, lo11 | hi11 << 12, and the PC's low bits
+// at bit 26 as in the output word (common.h), so that the output word is one
+// shift and one bit-field insert away (ungap_word).  A real key's 12-bit digit
+// (k >> sh) & 4095 (sh 0 or 12) is its 11-bit digit; a PAD slot's word has
+// digit 2048 + 2l in both passes, whose histogram word KWORDS + l is its
+// lane's private dummy: pads need no per-slot select in the count and scatter
+// loops (they rank on the dummy, which starts each scatter at CAP, so they
+// land past the real keys).
 __device__ __forceinline__ uint32_t gap_key(uint32_t key, uint32_t low) {
-    return (key & 2047u) | ((key >> 11) << 12) | (low << 24);
+    return key + (key & ~2047u) + (low << SYZ_KEY_BITS);  // key < 2^22
 }
 __device__ __forceinline__ uint32_t pad_word(uint32_t l) {
     const uint32_t d = 2048u + 2u * l;
     return d | (d << 12);
 }
-// the key word of common.h (key | low << SYZ_KEY_BITS) of a gapped word
+// the key word of common.h (key | low << SYZ_KEY_BITS) of a gapped word: bits
+// 0-10 and 25-31 stay, bits 12-25 move down by one (bits 23-25 are zero)
 __device__ __forceinline__ uint32_t ungap_word(uint32_t g) {
-    return (g & 2047u) | (((g >> 12) & 2047u) << 11) | ((g >> 24) << SYZ_KEY_BITS);
+    constexpr uint32_t KEEP = 0x7FFu | (0x7Fu << 25);
+    return (g & KEEP) | ((g >> 1) & ~KEEP);  // one v_bfi_b32
 }
 constexpr uint32_t GAP_KEY_MASK = 2047u | (2047u << 12);
+static_assert(SYZ_KEY_BITS == 26, "gapped words keep the low bits in place");
+
+// the histogram word of digit field x (bins 2w, 2w + 1 share word w): one
+// bit-field extract and one shift-add (the compiler rewrites a constant
+// extract as (x << 1) & 0x1FFC plus the base, three operations)
+__device__ __forceinline__ uint32_t *pair_word(uint32_t *h, uint32_t x) {
+    uint32_t w;
+    asm("v_bfe_u32 %0, %1, 1, 11" : "=v"(w) : "v"(x));
+    return &h[w];
+}
 
 // count / rank+scatter over gapped words: no validity tests (pads carry
-// their lane's dummy digit).  Inactive row quads hold pads too.
+// their lane's dummy digit).  Inactive row quads hold pads too.  The bin
+// pair's half is selected by hs = digit << 4: shifts and v_bfe_u32 read only
+// its low 5 bits, (digit & 1) << 4.
 template <int NK>
 __device__ __forceinline__ void count_gap(const uint32_t (&k)[NK], uint32_t nq, uint32_t *h,
                                           uint32_t sh) {
@@ -559,8 +575,8 @@ __device__ __forceinline__ void count_gap(const uint32_t (&k)[NK], uint32_t nq, 
         if ((uint32_t)q < nq) {
 #pragma unroll
             for (int c = 0; c < 4; c++) {
-                const uint32_t d = (k[q * 4 + c] >> sh) & 4095u;
-                atomicAdd(&h[d >> 1], hinc(d));
+                const uint32_t x = k[q * 4 + c] >> sh;
+                atomicAdd(pair_word(h, x), 1u << ((x << 4) & 31u));
             }
         }
 }
@@ -572,14 +588,20 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += BQ) {
         if ((uint32_t)q0 >= nq) continue;
-        uint32_t pos[4 * BQ];
+        uint32_t r[4 * BQ];
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++) {
-            const uint32_t d = (k[q0 * 4 + j] >> sh) & 4095u;
-            pos[j] = atomicAdd(&h[d >> 1], hinc(d)) >> ((d & 1u) << 4);
+            const uint32_t x = k[q0 * 4 + j] >> sh;
+            r[j] = atomicAdd(pair_word(h, x), 1u << ((x << 4) & 31u));
         }
+        // every rank atomic of the batch is in flight before the first result
+        // is used (interleaved, the extracts waited on each atomic in turn)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4 * BQ; j++) buf[pos[j] & 0xFFFFu] = k[q0 * 4 + j];
+        for (int j = 0; j < 4 * BQ; j++) {
+            const uint32_t hs = (k[q0 * 4 + j] >> sh) << 4;
+            buf[__builtin_amdgcn_ubfe(r[j], hs, 16)] = k[q0 * 4 + j];  // offset = hs & 31
+        }
     }
 }
 
@@ -594,7 +616,6 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
     uint32_t *h = s_h[w];
-    const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t span_m1 = (uint32_t)(P.span - 1);
     const uint32_t kmax = (uint32_t)(P.nkeys - 1);
     const bool inplace = P.out == P.raw;
@@ -618,14 +639,14 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         n_n = (uint32_t)(P.off[seg_n + 1] - base_n);
         const uint64_t a0 = base_n & ~3ull;
         const uint32_t end = (uint32_t)(base_n - a0) + n_n;
-        const uint32_t nq = (end + 255) >> 8;
         const uint4 *src = reinterpret_cast<const uint4 *>(P.raw + a0);
+        // every row quad, straight-line (the conversion below is branch-free
+        // and reads them all); chunks past the end re-read chunk 0
 #pragma unroll
-        for (int q = 0; q < NQ; q++)
-            if ((uint32_t)q < nq) {
-                const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-                vn[q] = src[e4 < end ? q * 64 + l : 0];
-            }
+        for (int q = 0; q < NQ; q++) {
+            const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
+            vn[q] = src[e4 < end ? q * 64 + l : 0];
+        }
     };
     uint32_t li = blockIdx.x * WPB + w;
     if (li < nl) issue(li);
@@ -636,29 +657,36 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
         const uint32_t nq = (end + 255) >> 8;
-        uint32_t k[NK];  // gapped words; slots outside the segment are pads
-#pragma unroll
-        for (int j = 0; j < NK; j++) k[j] = pad;
+        // gapped words, branch-free; slots outside the segment are pads
+        // (slot (q, l, c) holds raw index 4 (64 q + l) + c - head)
+        // (a slot is real iff head <= 4 (64 q + l) + c < end: the upper bound
+        // is one signed compare against a uniform value, the lower one only
+        // concerns lane 0's first row quad)
+        uint32_t k[NK];
         bool oob = false;
+        const int l4 = (int)(4u * l);
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
-            if ((uint32_t)q < nq) {
-                const uint32_t e4 = (uint32_t)(q * 64 + l) * 4u;
-                const uint32_t vv[4] = {vn[q].x, vn[q].y, vn[q].z, vn[q].w};
+            const uint32_t vv[4] = {vn[q].x, vn[q].y, vn[q].z, vn[q].w};
 #pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const uint32_t idx = e4 + c;
-                    const bool valid = idx >= head && idx < end;
-                    const bool out = vv[c] - P.pc_lo > span_m1;
-                    oob |= valid && out;
-                    const uint32_t g = out ? gap_key(kmax, 0u)
-                                           : gap_key((vv[c] >> P.kshift) - P.kbase, vv[c] & P.lowmask);
-                    k[q * 4 + c] = valid ? g : pad;
-                }
+            for (int c = 0; c < 4; c++) {
+                bool valid = l4 < (int)end - (256 * q + c);
+                if (q == 0 && c < 3) valid &= l4 + c >= (int)head;
+                const bool out = vv[c] - P.pc_lo > span_m1;
+                oob |= valid & out;
+                // an out-of-window word sorts as the last key (its low bits
+                // are kept: the step fails on SYZCOV_ERR_WINDOW anyway)
+                const uint32_t g = gap_key(out ? kmax : (vv[c] >> P.kshift) - P.kbase,
+                                           vv[c] & P.lowmask);
+                k[q * 4 + c] = valid ? g : pad;
+                // materialised here: sunk into the count loop, the selects kept
+                // every slot's masks alive (SGPR spills through VGPR lanes)
+                asm volatile("" : "+v"(k[q * 4 + c]));
             }
         }
+        // (before the next segment's loads: deferred, the slots' masks stayed alive)
+        if (__builtin_amdgcn_ballot_w64(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
         if (li + nw < nl) issue(li + nw);
-        if (__ballot(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
         // ---------------------------------------- pass 0: low 11 bits
         hist16_zero<NQ>(h, l);
         wave_sync();
@@ -700,7 +728,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
 #pragma unroll
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
-        uint32_t bad = P.force_redo;
+        bool bad = P.force_redo != 0;
         if (inplace) {  // nothing may be written before the order is known
             uint32_t carry = sent_g;
 #pragma unroll
@@ -712,8 +740,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
-                        bad |= (uint32_t)((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) &
-                               (uint32_t)(e - 1u < n - 1u);
+                        bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (e - 1u < n - 1u);
                     }
                 }
             if (__ballot(bad)) {
@@ -732,16 +759,17 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= (uint32_t)((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) &
-                           (uint32_t)(e - 1u < n - 1u);
+                    bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (e - 1u < n - 1u);
                     // whole words: distinct PCs stay distinct even if they share a key
-                    const uint32_t keep = (uint32_t)(e < n) & (uint32_t)(v != prev);
-                    const uint64_t m = __ballot(keep);
-                    const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                    const bool keep = (e < n) & (v != prev);
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
                     if (keep) {
+                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
+                                                       (uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                         const uint32_t w = ungap_word(v);
                         outp[pos] = w;  // the key word: the PC is kept exactly
-                        buf[pos] = w & KEY_MASK;
+                        buf[pos] = w;   // (the split search masks the key)
                     }
                     cnt += (uint32_t)__popcll(m);
                 }
@@ -767,7 +795,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         uint32_t lo2 = 0, hi2 = cnt;
                         while (lo2 < hi2) {
                             const uint32_t mid = (lo2 + hi2) >> 1;
-                            if (buf[mid] < b) lo2 = mid + 1; else hi2 = mid;
+                            if ((buf[mid] & KEY_MASK) < b) lo2 = mid + 1; else hi2 = mid;
                         }
                         s2 = lo2;
                     }

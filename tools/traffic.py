@@ -4,7 +4,10 @@ WRITE_SIZE in separate runs, MI355X_MICROARCH.md 'HBM'):
   bytes_read  = 2 * FETCH_SIZE[KB] * 1024   (gfx950 tallies 128-B requests at 64 B)
   bytes_write = WRITE_SIZE[KB] * 1024
 per step of each phase = sum over the phase's kernels of their per-step totals.
-Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json] [kernel run once per step]"""
+Usage: tools/traffic.py <fetch_dir> <write_dir> [out.json] [kernel run once per step] [last N]
+With "last N", only the dispatches issued from the N-th last dispatch of the
+step kernel on count (the bench's timed steps: e.g. C5's batches after its
+history and warm-up), divided over N steps."""
 import collections
 import csv
 import glob
@@ -19,7 +22,9 @@ PHASES = {
     "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "min_records_kernel",
                  "cover_records_kernel", "first_to_bits_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
-    "newcov": ("newcov_", "hash_clear_kernel"),
+    "newcov": ("newcov_", "hash_clear_kernel", "grp_hist", "grp_scan", "grp_scatter", "nc_zero",
+               "range_sum", "range_scan", "item_scan", "row_offsets", "desc_kernel", "row_fill",
+               "mfl_build", "accept_or"),
     "prio": ("prio_",),
     "order": ("gsort::",),
     "compact": ("compact_", "scan_blocks"),
@@ -31,21 +36,32 @@ PHASES = {
 STEP_KERNEL = "bin_kernel"
 
 
+LAST = 0
+
+
 def per_step(d, counter):
     """Counter total per bench step for each kernel name: a kernel may run
     several times per step (pass1_kernel once per rank chunk), so the total is
     divided by the number of steps, counted as the dispatches of bin_kernel
     (canon bins once per step)."""
-    tot = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
+    rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            k = r["Kernel_Name"]
-            tot[k] += float(r["Counter_Value"])
-            disp[k].add(r["Dispatch_Id"])
-    steps = max([len(v) for k, v in disp.items() if STEP_KERNEL in k] or [1])
+            if r["Counter_Name"] == counter:
+                rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    first = 0
+    if LAST:
+        ids = sorted({i for i, k, _ in rows if STEP_KERNEL in k})
+        if len(ids) < LAST:
+            raise SystemExit(f"{d}: {len(ids)} dispatches of {STEP_KERNEL}, fewer than {LAST}")
+        first = ids[-LAST]
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for i, k, v in rows:
+        if i >= first:
+            tot[k] += v
+            disp[k].add(i)
+    steps = LAST or max([len(v) for k, v in disp.items() if STEP_KERNEL in k] or [1])
     return {k: tot[k] / steps for k in tot}
 
 
@@ -56,10 +72,12 @@ def phase_of(name):
     return None
 
 
-def main(fd, wd, out=None, step_kernel=None):
-    global STEP_KERNEL
+def main(fd, wd, out=None, step_kernel=None, last=None):
+    global STEP_KERNEL, LAST
     if step_kernel:  # the kernel that runs once per step (default: canon's bin_kernel)
         STEP_KERNEL = step_kernel
+    if last:
+        LAST = int(last)
     fetch = per_step(fd, "FETCH_SIZE")
     write = per_step(wd, "WRITE_SIZE")
     res = {}
