@@ -34,8 +34,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
-# this same bench command (tools/profile.sh -> tools/traffic.py), committed per round
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03_traffic.json")
+# this same bench command (tools/profile_r04.sh -> tools/traffic.py), committed per round
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_traffic.json")
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED_C1 = 0x5EED0001  # BASELINE.json configs[0]: the CPU (reference) config
 SEED = 0x5EED0002     # configs[1]: 1M inputs, one GPU
@@ -686,6 +686,12 @@ def bench_newcov(args):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "alg_bytes_per_launch": timed_pcs // args.steps * 4},
     }
+    if os.path.exists(TRAFFIC_JSON) and world == 1:
+        with open(TRAFFIC_JSON) as f:
+            tb = json.load(f).get("newcov", {}).get("bytes")
+        if tb:  # per timed batch of this same command's shape (tools/profile_r04.sh)
+            out["roofline"]["traffic"] = tb
+            out["roofline"]["traffic_source"] = os.path.relpath(TRAFFIC_JSON, ROOT)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, 2000, nrec))
     st.close()
