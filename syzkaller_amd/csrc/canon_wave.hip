@@ -721,6 +721,17 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         wave_sync();
         scatter_gap<NK, BQK>(k, nq, buf, h, 12);
         wave_sync();
+        // slots [n, 256 nq) take the last key: the unique loop drops them as
+        // repeats and the order check passes them, with no per-slot bound test
+        if (n) {
+            const uint32_t last = buf[n - 1];  // (not among the slots written)
+#pragma unroll
+            for (uint32_t t = 0; t < 5; t++) {
+                const uint32_t p = (n & ~63u) + l + 64 * t;
+                if (p >= n && p < nq * 256u) buf[p] = last;
+            }
+            wave_sync();
+        }
         // --------------------------------- order check + unique + write
 #pragma unroll
         for (int q = 0; q < NQ; q++)
@@ -736,11 +747,11 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 if ((uint32_t)q < nq) {
 #pragma unroll
                     for (int c = 0; c < 4; c++) {
-                        const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
                         const uint32_t v = k[q * 4 + c];
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
-                        bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (e - 1u < n - 1u);
+                        // (slot 0's predecessor is the sentinel: no order)
+                        bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (q + c > 0 || l > 0);
                     }
                 }
             if (__ballot(bad)) {
@@ -755,13 +766,12 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
             if ((uint32_t)q < nq) {
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
-                    const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (e - 1u < n - 1u);
+                    bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (q + c > 0 || l > 0);
                     // whole words: distinct PCs stay distinct even if they share a key
-                    const bool keep = (e < n) & (v != prev);
+                    const bool keep = v != prev;
                     const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
                     if (keep) {
                         const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
