@@ -415,6 +415,10 @@ static int ph_order_given(Corpus &c, const int32_t *order, size_t N, hipStream_t
     return 0;
 }
 
+int sort_order_part_dev(const int64_t *lens, size_t n, uint32_t part, uint32_t nparts,
+                        int32_t *order, void *ws, size_t ws_size, uint32_t *err_dev,
+                        hipStream_t s);
+
 // nparts > 1: this shard's part of the order only (syzcov_dev_sort_order_part);
 // the caller MAX all-reduces ORDER[:N] before minimize
 static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s, uint32_t part = 0,
@@ -429,8 +433,10 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s, u
     hipLaunchKernelGGL(corpus_lens_kernel, dim3(grid_for(N, 256, 8192)), dim3(256), 0, s, l32,
                        c.off, (uint64_t)N, lens);
     SYZ_LAUNCH_CHECK();
-    return syzcov_dev_sort_order_part(lens, N, part, nparts, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
-                                      c.buf<void>(SYZCOV_CORPUS_WS), c.ws_size, s);
+    // (an internal sort error fails the step through its flags: no host sync)
+    return sort_order_part_dev(lens, N, part, nparts, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
+                               c.buf<void>(SYZCOV_CORPUS_WS), c.ws_size,
+                               (uint32_t *)(scal(c) + SC_ERR), s);
 }
 
 // Work items: (input, rank).  One GPU: every input, ranks = positions of

@@ -949,8 +949,15 @@ static int read_ctl(uint32_t *h, const uint32_t *ctl, size_t n, uint32_t *pin, h
     return 0;
 }
 
+// The sort's internal error word (ctl[0]) into a step's error flags, on the
+// device: no host turnaround after the finisher (the caller's result()
+// reports it).
+__global__ void sort_err_kernel(const uint32_t *ctl, uint32_t *err) {
+    if (ctl[0]) atomicOr(err, SYZCOV_ERR_ORDER);
+}
+
 static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t part = 0,
-                      uint32_t nparts = 1) {
+                      uint32_t nparts = 1, uint32_t *err_dev = nullptr) {
     PinnedCtl pin;
     bool split = nparts <= 1;  // this part's segments selected (or nothing to split)
     auto split_now = [&](Seg *cur_, uint32_t *ccount_, uint32_t ncur_) {
@@ -1033,6 +1040,12 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t pa
         SYZ_LAUNCH_CHECK();
     }
     if (!h[0] && (h[3] || seeded >= 0)) {
+        if (err_dev) {
+            hipLaunchKernelGGL(sort_err_kernel, dim3(1), dim3(1), 0, s, (const uint32_t *)w.ctl,
+                               err_dev);
+            SYZ_LAUNCH_CHECK();
+            return 0;
+        }
         if (int rc = read_ctl(h, w.ctl, 1, pin.get(), s)) return rc;
     }
     if (h[0]) {
@@ -1043,7 +1056,19 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t pa
 }
 
 static int sort_order_part(const int64_t *lens, size_t n, int sort_variant, uint32_t part,
-                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream);
+                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream,
+                           uint32_t *err_dev = nullptr);
+
+namespace syz {
+// syzcov_dev_sort_order_part with the finisher's error check left on the
+// device (err_dev |= SYZCOV_ERR_ORDER): the corpus handle's order phase
+int sort_order_part_dev(const int64_t *lens, size_t n, uint32_t part, uint32_t nparts,
+                        int32_t *order, void *ws, size_t ws_size, uint32_t *err_dev,
+                        hipStream_t s) {
+    if (nparts == 0 || part >= nparts || !err_dev) return SYZCOV_EINVAL;
+    return sort_order_part(lens, n, 0, part, nparts, order, ws, ws_size, s, err_dev);
+}
+}  // namespace syz
 
 extern "C" int syzcov_dev_sort_order(const int64_t *lens, size_t n, int sort_variant,
                                      int32_t *order, void *ws, size_t ws_size, void *stream) {
@@ -1058,7 +1083,8 @@ extern "C" int syzcov_dev_sort_order_part(const int64_t *lens, size_t n, uint32_
 }
 
 static int sort_order_part(const int64_t *lens, size_t n, int sort_variant, uint32_t part,
-                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream) {
+                           uint32_t nparts, int32_t *order, void *ws, size_t ws_size, void *stream,
+                           uint32_t *err_dev) {
     if (n == 0) return 0;
     if (!lens || !order || n > 0x7FFFFFFF) return SYZCOV_EINVAL;
     if (sort_variant != 0) {
@@ -1075,7 +1101,7 @@ static int sort_order_part(const int64_t *lens, size_t n, int sort_variant, uint
     Ctl c{w.segA, w.ctl + 1, w.ctl + 4, w.small, w.ctl + 3, w.small_cap, w.seg_cap, w.ctl};
     if (n > 1) hipLaunchKernelGGL(seed_kernel, dim3(1), dim3(1), 0, s, (uint32_t)n, c);
     SYZ_LAUNCH_CHECK();
-    if (int rc = run_rounds(w, s, (int64_t)n, part, nparts)) return rc;
+    if (int rc = run_rounds(w, s, (int64_t)n, part, nparts, err_dev)) return rc;
     SYZ_HIP(hipMemcpyAsync(order, w.I, n * 4, hipMemcpyDeviceToDevice, s));
     return 0;
 }
