@@ -207,6 +207,46 @@ def test_engine_key_mode_clustered(torch, force, monkeypatch):
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
 
 
+@pytest.mark.parametrize("in_place", [False, True], ids=["out-of-place", "in-place"])
+def test_engine_key_mode_tiny_segments(torch, in_place):
+    """Covers of 0..9 PCs at every alignment of their first PC (the wave
+    kernel loads 4-PC chunks of a segment: fewer than 4 PCs take the
+    workgroup path, the first and last chunks of longer ones start at the
+    segment's first PC / end at its last), between long covers, with repeats
+    (cover.go:28-40, 104-131)."""
+    from syzkaller_amd.engine import CorpusEngine
+    rng = np.random.default_rng(17)
+    univ = (np.uint64(0x81000000) + 16 * np.arange(1 << 16, dtype=np.uint64)
+            + rng.integers(0, 16, 1 << 16).astype(np.uint64)).astype(np.uint32)
+    covers = []
+    for i in range(400):
+        ln = int(rng.integers(1200, 2600)) if i % 7 == 3 else i % 10
+        c = univ[rng.integers(0, univ.size, size=ln)]
+        if ln > 2 and i % 3 == 0:
+            c[-1] = c[0]  # a repeat
+        covers.append(c.astype(np.uint32))
+    lens = np.array([c.size for c in covers], np.int64)
+    o_off = np.zeros(len(covers) + 1, np.uint64)
+    o_off[1:] = np.cumsum(lens)
+    o_pcs = np.concatenate(covers + [np.zeros(1, np.uint32)])
+    n = len(covers)
+    off = torch.from_numpy(o_off.astype(np.int64)).cuda()
+    raw = torch.from_numpy(o_pcs.view(np.int32)).cuda()
+    eng = CorpusEngine(n, int(lens.sum()) + 1, int(lens.max()), int(univ[0]),
+                       int(univ[-1]) - int(univ[0]) + 1, universe=univ, canon_in_place=in_place)
+    exp_kept, exp_union = _oracle_of(off, raw, n)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs[:int(lens.sum())])
+    res = eng.step(off, raw, n)
+    assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    if not in_place:
+        canon = eng.canonical_pcs(off, n).cpu().numpy().view(np.uint32)
+        for i in range(n):
+            a, b = int(o_off[i]), int(o_off[i]) + int(c_off[i + 1] - c_off[i])
+            assert np.array_equal(canon[a:b], c_pcs[c_off[i]:c_off[i + 1]]), i
+    assert res.kept_idx.cpu().numpy().tolist() == exp_kept
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
+
+
 def _stray(u: np.ndarray, i: int) -> int:
     """A PC next to universe PC u[i] that is not in the universe."""
     us = set(u.tolist())
