@@ -377,8 +377,11 @@ __global__ __launch_bounds__(1024) void range_scan_kernel(const uint32_t *__rest
     if (b == nb - 1 && threadIdx.x == 1023) R[m] = run;
 }
 
-// Work-item prefix over (call, range) pairs e = c * nr + q: ceil(rows / CHR)
-// items each.
+// Work-item prefix over (call, range) pairs in RANGE-major order, p = q *
+// ncalls + c: ceil(rows / CHR) items each.  Items run in that order, so the
+// workgroups resident at any time test PCs of one key range, and the range's
+// slice of the membership table (2^RSH bytes) stays in L2 for their byte
+// gathers (call-major, the gathers spread over the whole table).
 __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restrict__ coff,
                                                          int ncalls, uint32_t nr,
                                                          const uint32_t *__restrict__ Rq,
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(1024) void item_scan_kernel(const uint32_t *__restr
         const uint32_t e = e0 + threadIdx.x;
         uint32_t v = 0;
         if (e < ne) {
-            const uint32_t c = e / nr, q = e - c * nr;
+            const uint32_t q = e / (uint32_t)ncalls, c = e - q * (uint32_t)ncalls;
             const uint32_t *R = Rq + (uint64_t)q * stride;
             v = (R[coff[c + 1]] - R[coff[c]] + CHR - 1) / CHR;
         }
@@ -418,17 +421,18 @@ __global__ void row_offsets_kernel(const uint32_t *__restrict__ Rq, uint32_t m, 
     }
 }
 
-// Work-item descriptors {e, first row, end row}: thread per pair e.
+// Work-item descriptors {e = c * nr + q, first row, end row}: thread per pair,
+// items placed in range-major order (item_scan_kernel).
 __global__ __launch_bounds__(256) void desc_kernel(const uint32_t *__restrict__ coff, int ncalls,
                                                    uint32_t nr, const uint32_t *__restrict__ Rq,
                                                    uint32_t stride, uint32_t CHR,
                                                    const uint32_t *__restrict__ ipre,
                                                    uint4 *__restrict__ desc) {
     const uint32_t ne = (uint32_t)ncalls * nr;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
-        const uint32_t c = e / nr, q = e - c * nr;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ne; p += gridDim.x * blockDim.x) {
+        const uint32_t q = p / (uint32_t)ncalls, c = p - q * (uint32_t)ncalls, e = c * nr + q;
         const uint32_t *R = Rq + (uint64_t)q * stride;
-        const uint32_t r0 = R[coff[c]], r1 = R[coff[c + 1]], base = ipre[e];
+        const uint32_t r0 = R[coff[c]], r1 = R[coff[c + 1]], base = ipre[p];
         for (uint32_t i = 0; r0 + i * CHR < r1; i++)
             desc[base + i] = make_uint4(e, r0 + i * CHR, min(r0 + (i + 1) * CHR, r1), 0u);
     }
