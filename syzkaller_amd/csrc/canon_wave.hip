@@ -656,7 +656,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         const uint32_t n = n_n;
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
-        const uint32_t nq = (end + 255) >> 8;
+        // (an empty segment sorts nothing: with an unaligned start its one row
+        // quad would hold only pads, which the unique loop would keep)
+        const uint32_t nq = n ? (end + 255) >> 8 : 0u;
         // gapped words, branch-free; slots outside the segment are pads
         // (slot (q, l, c) holds raw index 4 (64 q + l) + c - head)
         // (a slot is real iff head <= 4 (64 q + l) + c < end: the upper bound
