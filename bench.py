@@ -88,7 +88,7 @@ def parse():
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a torch.distributed launcher: start N rank
     processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
-    rank r on GPU r), relay rank 0's JSON line and return the first failing
+    rank r on GPU r), relay rank 0's JSON line (everything else on stderr) and return the first failing
     exit code.  This process never touches the GPU (no torch import): every
     rank is a fresh child, never an exec of a GPU-initialised process."""
     import socket
@@ -103,7 +103,7 @@ def launch_ranks(args) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env, stdout=subprocess.PIPE if r == 0 else None,
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
                                       text=True))
     import threading
     out0 = []  # rank 0 prints one line; read on a thread so a failing rank is seen at once
@@ -122,7 +122,10 @@ def launch_ranks(args) -> int:
         if rc == 0 and c != 0:
             rc = c
     reader.join(timeout=10)
-    sys.stdout.write("".join(out0))
+    # only the JSON line goes to stdout: what the ranks' libraries print there
+    # (gloo's "[Gloo] Rank r is connected ..." notes) is relayed to stderr
+    for line in "".join(out0).splitlines(keepends=True):
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
     sys.stdout.flush()
     return rc
 

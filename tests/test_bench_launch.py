@@ -23,8 +23,10 @@ def test_launcher_forms_world():
         r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run"],
                            capture_output=True, text=True, timeout=120, env=_env())
         assert r.returncode == 0, r.stderr[-2000:]
-        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        assert len(lines) == 1, r.stdout
+        # stdout is the one JSON line and nothing else (gloo's connection
+        # notes from every rank go to stderr)
+        lines = r.stdout.splitlines()
+        assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
         d = json.loads(lines[0])
         assert d["n_gpus"] == n and d["rccl_ranks"] == n, d
 
