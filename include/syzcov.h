@@ -82,6 +82,12 @@ uint64_t syzcov_restore_pc(uint32_t pc, uint32_t base);
  * the reference's aliasing, html.go:236). */
 int64_t syzcov_canonicalize(uint32_t *cov, size_t n);
 
+/* The executor's cover_dedup (executor/executor.cc:574-587) of one raw u64
+ * KCOV buffer: sorts cov IN PLACE, keeps the distinct nonzero PCs (the
+ * reference's `last` starts at 0) at the front and returns their count.
+ * n <= 2^31, else SYZCOV_ETOOLONG. */
+int64_t syzcov_cover_dedup64(uint64_t *cov, size_t n);
+
 /* cover.Difference / SymmetricDifference / Union / Intersection
  * (cover/cover.go:42-79, merge core foreach :81-102).  `out` must hold
  * na (Difference), na+nb (SymmetricDifference, Union), min(na,nb)
@@ -547,6 +553,14 @@ int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32
                                 uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
                                 uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
                                 uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+/* cover_dedup (executor/executor.cc:574-587) of nseg raw u64 KCOV buffers
+ * [off[s], off[s+1]) of pcs, IN PLACE: buffer s becomes its sorted distinct
+ * nonzero PCs, new_len[s] of them (UINT32_MAX for a buffer longer than 2^31
+ * or with off[s+1] < off[s], left untouched).  out32 (nullable, sized like
+ * pcs) receives at the same positions each kept PC truncated to u32, as
+ * executor.cc:459-463 writes them.  No workspace. */
+int syzcov_dev_cover_dedup64(uint64_t *pcs, const uint64_t *off, size_t nseg, uint32_t *new_len,
+                             uint32_t *out32, void *stream);
 /* out[i] = the PC of key word words[i] (exact, no table); in place allowed. */
 int syzcov_dev_words_to_pcs(const uint32_t *words, size_t n, uint32_t kshift, uint32_t kbase,
                             uint32_t *out, void *stream);

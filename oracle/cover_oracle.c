@@ -30,6 +30,26 @@ size_t orc_canonicalize(uint32_t *cov, size_t n) {
     return i;
 }
 
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* executor/executor.cc:574-587: std::sort, then skip pc == last with
+ * last = 0 at the start (:578), so zero PCs are dropped too.  (The network
+ * used to sort is irrelevant: equal u64 values are indistinguishable.) */
+size_t orc_cover_dedup64(uint64_t *cov, size_t n) {
+    qsort(cov, n, sizeof(uint64_t), cmp_u64);
+    size_t w = 0;
+    uint64_t last = 0;
+    for (size_t i = 0; i < n; i++) {
+        uint64_t pc = cov[i];
+        if (pc == last) continue;
+        cov[w++] = last = pc;
+    }
+    return w;
+}
+
 /* The four closures passed to foreach (cover/cover.go:42-79). */
 static uint32_t f_apply(int op, uint32_t v0, uint32_t v1) {
     switch (op) {

@@ -27,6 +27,10 @@ extern "C" {
 /* cover/cover.go:28-40 — in place; returns the new length. */
 size_t orc_canonicalize(uint32_t *cov, size_t n);
 
+/* executor/executor.cc:574-587 cover_dedup — in place; returns the new
+ * length (sorted, distinct, nonzero: `last` starts at 0). */
+size_t orc_cover_dedup64(uint64_t *cov, size_t n);
+
 /* cover/cover.go:42-102.  op: 0 Difference, 1 SymmetricDifference, 2 Union,
  * 3 Intersection.  out must hold na+nb.  Returns result length. */
 size_t orc_setop(int op, const uint32_t *a, size_t na, const uint32_t *b, size_t nb,

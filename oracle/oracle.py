@@ -37,6 +37,8 @@ def lib():
         sz = C.c_size_t
         _lib.orc_canonicalize.argtypes = [p, sz]
         _lib.orc_canonicalize.restype = sz
+        _lib.orc_cover_dedup64.argtypes = [p, sz]
+        _lib.orc_cover_dedup64.restype = sz
         _lib.orc_setop.argtypes = [C.c_int, p, sz, p, sz, p]
         _lib.orc_setop.restype = sz
         _lib.orc_sort_min_inputs.argtypes = [p, p, sz, C.c_int]
@@ -74,6 +76,13 @@ def _u32(x) -> np.ndarray:
 def canonicalize(cov) -> np.ndarray:
     a = _u32(cov).copy()
     n = lib().orc_canonicalize(_ptr(a), a.size)
+    return a[:n]
+
+
+def cover_dedup64(buf) -> np.ndarray:
+    """executor.cc:574-587 on one raw u64 KCOV buffer."""
+    a = np.ascontiguousarray(np.asarray(buf, dtype=np.uint64)).copy()
+    n = lib().orc_cover_dedup64(_ptr(a), a.size)
     return a[:n]
 
 

@@ -1,5 +1,6 @@
 """Pure-Python literal restatement of cover/cover.go, Go's sort.Sort and the
-manager's uniqueCover (syz-manager/html.go:213-238), used
+manager's uniqueCover (syz-manager/html.go:213-238) and the executor's
+cover_dedup (executor/executor.cc:574-587), used
 only to cross-check the C oracle on small cases (two independent
 transcriptions of the same published algorithms).  TEST INFRASTRUCTURE ONLY.
 """
@@ -297,6 +298,17 @@ def corpus_stats(calls, covers, call):  # syz-manager/html.go:157-175 (before th
     total_unique = unique_cover(calls, covers, False)
     return [(i, len(cov), len(intersection([int(x) for x in cov], total_unique)))
             for i, (c, cov) in enumerate(zip(calls, covers)) if c == call]
+
+
+def cover_dedup64(cov):  # executor/executor.cc:574-587
+    cov = sorted(int(x) for x in cov)
+    out, last = [], 0
+    for pc in cov:
+        if pc == last:
+            continue
+        out.append(pc)
+        last = pc
+    return out
 
 
 def parse_exec_output(out, call_num, callid_of_num):

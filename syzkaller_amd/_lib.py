@@ -43,6 +43,7 @@ _SIGS = {
     "syzcov_pool_trim": (C.c_int, []),
     "syzcov_restore_pc": (u64, [u32, u32]),
     "syzcov_canonicalize": (i64, [p_, sz]),
+    "syzcov_cover_dedup64": (i64, [p_, sz]),
     "syzcov_difference": (i64, [p_, sz, p_, sz, p_]),
     "syzcov_symmetric_difference": (i64, [p_, sz, p_, sz, p_]),
     "syzcov_union": (i64, [p_, sz, p_, sz, p_]),
@@ -110,6 +111,7 @@ _SIGS = {
     "syzcov_dev_canon_split_keys": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, u32, u64,
                                               u32, p_, p_, p_, p_, sz, p_]),
     "syzcov_dev_words_to_pcs": (C.c_int, [p_, sz, u32, u32, p_, p_]),
+    "syzcov_dev_cover_dedup64": (C.c_int, [p_, p_, sz, p_, p_, p_]),
     "syzcov_dev_minimize_range_keys": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_, p_, p_,
                                                  p_, p_, u64, p_, p_, p_, C.c_int, p_, p_, p_]),
     "syzcov_dev_minimize_range_keys_pass2": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_,

@@ -286,6 +286,32 @@ int64_t syzcov_canonicalize(uint32_t *cov, size_t n) {
     return nl;
 }
 
+int64_t syzcov_cover_dedup64(uint64_t *cov, size_t n) {
+    if (n == 0) return 0;
+    if (!cov) return SYZCOV_EINVAL;
+    if (n > ((size_t)1 << 31)) return SYZCOV_ETOOLONG;
+    CtxLease lease;
+    Ctx *c = lease.get();
+    if (!c) return SYZCOV_ENODEV;
+    Plan p;
+    size_t i_off = p.add(2 * 8), i_pcs = p.add(n * 8), i_len = p.add(4);
+    std::vector<uint8_t *> b;
+    RC(reserve(c, p, b));
+    uint64_t hoff[2] = {0, n};
+    CK(hipMemcpyAsync(b[i_off], hoff, 16, hipMemcpyHostToDevice, c->s));
+    CK(hipMemcpyAsync(b[i_pcs], cov, n * 8, hipMemcpyHostToDevice, c->s));
+    RC(syzcov_dev_cover_dedup64((uint64_t *)b[i_pcs], (uint64_t *)b[i_off], 1,
+                                (uint32_t *)b[i_len], nullptr, c->s));
+    uint32_t nl = 0;
+    CK(hipMemcpyAsync(&nl, b[i_len], 4, hipMemcpyDeviceToHost, c->s));
+    CK(hipStreamSynchronize(c->s));
+    if (nl) {
+        CK(hipMemcpyAsync(cov, b[i_pcs], (size_t)nl * 8, hipMemcpyDeviceToHost, c->s));
+        CK(hipStreamSynchronize(c->s));
+    }
+    return nl;
+}
+
 static int64_t setop(int op, const uint32_t *a, size_t na, const uint32_t *b_, size_t nb,
                      uint32_t *out) {
     if ((na && !a) || (nb && !b_) || !out) return SYZCOV_EINVAL;

@@ -133,6 +133,15 @@ class CoverState:
         return is_new[:nrec]
 
 
+def cover_dedup(cov) -> np.ndarray:
+    """The executor's cover_dedup (executor/executor.cc:574-587) of one raw
+    u64 KCOV buffer on the GPU: the sorted distinct nonzero PCs.  Batches of
+    device-resident buffers: syzcov_dev_cover_dedup64."""
+    a = np.ascontiguousarray(np.asarray(cov, dtype=np.uint64)).copy()
+    n = check(lib().syzcov_cover_dedup64(_ptr(a), a.size), "cover_dedup") if a.size else 0
+    return a[:n]
+
+
 def parse_exec_output(out: bytes, call_num, callid_of_num):
     """Executor output of one program (ipc/ipc.go:225-291) -> (errnos,
     records) where records = (callid[], call_index[], off[], pcs[]) are the

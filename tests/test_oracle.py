@@ -271,3 +271,25 @@ def test_newcov_full_vs_list_oracle(tmp_path):
         assert 0 < exp.sum() < nrec
     assert mn.tolist() == [len(m) for m in mc]
     assert np.array_equal(mcp, np.concatenate([np.asarray(m, np.uint32) for m in mc]))
+
+
+def test_cover_dedup_restatement():
+    """executor.cc:574-587 (no reference test covers cover_dedup, and
+    executor.cc does not build on its own: parity unpinned; the two
+    restatements and numpy's unique agree, including its zero rule)."""
+    kat = [([], []), ([0], []), ([0, 0], []), ([7], [7]), ([0, 0, 5, 3, 5], [3, 5]),
+           ([2**64 - 1, 0, 1, 2**64 - 1], [1, 2**64 - 1]),
+           ([0xffffffff81000010, 0xffffffff81000000, 0xffffffff81000010],
+            [0xffffffff81000000, 0xffffffff81000010])]
+    for buf, want in kat:
+        assert orc.cover_dedup64(buf).tolist() == want
+        assert pyref.cover_dedup64(buf) == want
+    rng = np.random.default_rng(11)
+    for n in (1, 2, 17, 300, 5000):
+        for hi in (4, 1 << 20, None):
+            buf = (rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + 1 if hi is None
+                   else rng.integers(0, hi, n).astype(np.uint64))
+            got = orc.cover_dedup64(buf)
+            u = np.unique(buf)
+            assert np.array_equal(got, u[u != 0])
+            assert got.tolist() == pyref.cover_dedup64(buf.tolist())

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Kernel micro-bench on the C2 corpus: times one engine phase at a time.
-    python tools/kbench.py canon|minimize|step|order [--keys] [--inputs N] [--reps R]"""
+    python tools/kbench.py canon|minimize|step|order|dedup [--keys] [--inputs N] [--reps R]
+dedup: the executor's cover_dedup (executor.cc:574-587) over N raw u64 KCOV
+buffers made of the C2 generator's raw PCs (high half 0xffffffff), in place,
+with the u32 output words; the buffers are restored outside the events."""
 import argparse
 import os
 import sys
@@ -43,6 +46,32 @@ def main():
             e.record()
             torch.cuda.synchronize()
             print(f"order: {s.elapsed_time(e):.3f} ms  n={n}", flush=True)
+        return
+    if a.what == "dedup":
+        import ctypes as C
+        from syzkaller_amd._lib import check, lib
+        off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
+                                             log2_space=a.log2_space)
+        src = raw[:total].to(torch.int64) | (-(1 << 32))  # 0xffffffff_xxxxxxxx
+        buf = torch.empty_like(src)
+        o32 = torch.empty(total, dtype=torch.int32, device="cuda")
+        nl = torch.empty(n, dtype=torch.int32, device="cuda")
+        del raw
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        for r in range(a.reps + 1):
+            buf.copy_(src)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            check(lib().syzcov_dev_cover_dedup64(P(buf), P(off), n, P(nl), P(o32), st), "dedup")
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e)
+            kept = int(nl.to(torch.int64).sum().item())
+            if r:
+                print(f"dedup: {ms:.3f} ms  raw {total} u64 PCs in {n} buffers, kept {kept}  "
+                      f"{total / ms / 1e6:.2f} G PCs/s  {(8 * total + 12 * kept) / ms / 1e6:.1f} GB/s "
+                      f"(8 B read per PC + 12 B written per kept PC)", flush=True)
         return
     lo, span = synth_window(a.log2_space)
     off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
