@@ -397,7 +397,7 @@ def c3_single(args, dev):
     del univ, lens
     eng.step(off, raw, n)  # warmup
     torch.cuda.synchronize()
-    steps = 3
+    steps = 10  # ~0.9 s: the strong-scaling anchor wants more than a 3-step sample
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(eng.PHASES) + 1)]
           for _ in range(steps)]
     t0 = time.perf_counter()
@@ -410,6 +410,8 @@ def c3_single(args, dev):
           for i, p in enumerate(eng.PHASES)}
     out = {"workload": f"C3: {n} inputs on one GPU (seed {SEED_C3:#x}), out-of-place canon",
            "ms_per_step": dt * 1e3, "value": total / dt, "unit": "input-PCs/s", "steps": steps,
+           "step_ms_min_max": [round(min(e[0].elapsed_time(e[-1]) for e in ev), 3),
+                               round(max(e[0].elapsed_time(e[-1]) for e in ev), 3)],
            "raw_pcs": total, "phases_ms": ph,
            "results": {"kept": res.n_kept, "union": res.n_union}}
     eng.close()
