@@ -19,6 +19,9 @@ ALGORITHMIC bytes.
 
 --workload prio: config C4 (CalculatePriorities, 1M programs x 1170 calls,
 i8 MFMA AᵀA) — a separate line with an MFMA roofline.
+--workload newcov: config C5 (the fuzzer's streaming new-coverage check).
+--workload dedup: the executor's cover_dedup (executor.cc:574-587) of raw u64
+KCOV buffers (--records buffers per batch, the C2 length distribution).
 """
 from __future__ import annotations
 
@@ -43,6 +46,7 @@ SEED_C3 = 0x5EED0003  # configs[2]: 10M inputs over the GPUs of one node
 C3_INPUTS = 10_000_000
 SEED_PRIO = 0x5EED0004
 SEED_NEWCOV = 0x5EED0005
+SEED_DEDUP = 0x5EED0006
 FLAKE_INPUT = 1 << 40  # synthetic input index the C5 flakes set is drawn as
 
 
@@ -51,7 +55,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["corpus", "prio", "newcov"], default="corpus")
+    ap.add_argument("--workload", choices=["corpus", "prio", "newcov", "dedup"], default="corpus")
     ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
     ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
     ap.add_argument("--history", type=int, default=512,
@@ -703,6 +707,94 @@ def bench_newcov(args):
     return rank, world, out
 
 
+def cpu_baseline_dedup(bufs) -> dict:
+    """Oracle cover_dedup (executor.cc:574-587 restated in C: qsort + the
+    `last` loop) over a sample of the same buffers, 1 thread."""
+    from oracle import oracle as orc
+    orc.lib()
+    t0 = time.perf_counter()
+    npc = 0
+    for b in bufs:
+        orc.cover_dedup64(b)
+        npc += b.size
+    dt = time.perf_counter() - t0
+    return {"value": npc / dt, "unit": "raw-PCs/s", "cores": 1, "kind": "port",
+            "sample": f"{len(bufs)} buffers ({npc} raw u64 PCs) of the timed batch, "
+                      f"oracle/ C restatement of executor/executor.cc:574-587 (qsort), 1 thread"}
+
+
+def bench_dedup(args):
+    """The executor's cover_dedup (executor/executor.cc:574-587) on the GPU:
+    batches of raw u64 KCOV buffers (the C2 generator's raw PCs as x86-64
+    kernel addresses 0xffffffff_xxxxxxxx, lengths ~ N(mean, sigma)) deduped in
+    place, with the u32 words executor.cc:459-463 writes.  Every step is a
+    FRESH batch (W + K batches generated into HBM up front)."""
+    import ctypes as C
+    import torch
+    world, rank, dev = init_dist()
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import synth_corpus
+    L = _lib.lib()
+    s = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    nbuf, nb = args.records, args.warmup + args.steps
+    batches = []
+    for b in range(nb):
+        off, raw, _, total = synth_corpus(nbuf, SEED_DEDUP, first=(rank * nb + b) * nbuf,
+                                          mean=args.mean, sigma=args.sigma,
+                                          log2_space=args.log2_space, device=dev)
+        pcs = raw[:total].to(torch.int64) | (-(1 << 32))
+        del raw
+        batches.append((off, pcs, total))
+    o32 = torch.empty(max(b[2] for b in batches), dtype=torch.int32, device=dev)
+    nl = torch.empty(nb, nbuf, dtype=torch.int32, device=dev)
+    ns = min(nbuf, 20000)  # the CPU baseline's sample: the last batch's first buffers
+    soff = batches[-1][0][:ns + 1].cpu().numpy()
+    spcs = batches[-1][1][:int(soff[-1])].cpu().numpy().view("uint64")
+    sample = [spcs[soff[i]:soff[i + 1]].copy() for i in range(ns)]
+    torch.cuda.synchronize()
+    it = [0]
+
+    def run_step(ev):
+        b = it[0]
+        off, pcs, _ = batches[b]
+        if ev is not None:
+            ev[0].record()
+        _lib.check(L.syzcov_dev_cover_dedup64(P(pcs), P(off), nbuf, P(nl[b]), P(o32), s()),
+                   "dev_cover_dedup64")
+        if ev is not None:
+            ev[1].record()
+        it[0] += 1
+    dt, phl = timed(run_step, 1, args, world, dev)
+    kept = nl[args.warmup:].to(torch.int64).sum(1).cpu().tolist()
+    if nl[args.warmup:].min().item() < 0:  # a wide/malformed mark left behind
+        raise RuntimeError("dedup: a buffer was left unprocessed")
+    raw_t = sum(b[2] for b in batches[args.warmup:])
+    alg = (8 * raw_t + 12 * sum(kept)) / args.steps  # read u64 + write u64 and the u32 word
+    achieved = alg / (phl[0] * 1e-3) / 1e9
+    out = {
+        "metric": "raw KCOV PCs deduped/sec (executor cover_dedup, executor.cc:574-587)",
+        "value": raw_t * world / dt, "unit": "raw-PCs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic raw KCOV buffers (C2 lengths, x86-64 kernel addresses), fresh batch "
+                "every step",
+        "config": {"workload": f"cover_dedup: {nbuf} raw u64 KCOV buffers per batch",
+                   "buffers_per_batch": nbuf, "raw_pcs_per_batch": raw_t // args.steps,
+                   "len_mean": args.mean, "len_sigma": args.sigma,
+                   "parallelism": f"shard-by-buffer x{world}"},
+        "phases_ms": {"dedup": round(phl[0], 4)},
+        "results": {"kept_per_batch": kept},
+        "roofline": {"bound": "hbm", "kernel": "dedup (narrow<4,8,16> + wide)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": alg},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_dedup(sample)
+    return rank, world, out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -711,7 +803,8 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} ranks",
               file=sys.stderr)
-    fn = {"prio": bench_prio, "newcov": bench_newcov}.get(args.workload, bench_corpus)
+    fn = {"prio": bench_prio, "newcov": bench_newcov, "dedup": bench_dedup}.get(args.workload,
+                                                                             bench_corpus)
     rank, world, out = (bench_dry if args.dry_run else fn)(args)
     if world > 1:
         import torch.distributed as dist

@@ -415,8 +415,10 @@ __device__ __forceinline__ void walk(Shared<K, E> &sh, uint32_t t, uint64_t nseg
     }
 }
 
+// (occupancy: E = 16 at 128 VGPRs and E = 8 at 96 run 4 and 5 waves per SIMD
+// without spills; E = 4 spills below its 136)
 template <int E>
-__global__ __launch_bounds__(NT) void narrow_kernel(uint64_t *pcs, const uint64_t *off,
+__global__ __launch_bounds__(NT, E == 16 ? 4 : E == 8 ? 5 : 1) void narrow_kernel(uint64_t *pcs, const uint64_t *off,
                                                     uint64_t nseg, uint32_t *new_len,
                                                     uint32_t *out32) {
     __shared__ Shared<uint32_t, E> sh;
