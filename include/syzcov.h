@@ -561,6 +561,20 @@ int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32
  * executor.cc:459-463 writes them.  No workspace. */
 int syzcov_dev_cover_dedup64(uint64_t *pcs, const uint64_t *off, size_t nseg, uint32_t *new_len,
                              uint32_t *out32, void *stream);
+/* Executor KCOV buffers straight into the new-coverage check:
+ * syzcov_dev_cover_dedup64 of the nbuf buffers [off[b], off[b+1]) of pcs64
+ * (in place; off[0] = 0, off[nbuf] = total), then each buffer's kept PCs
+ * truncated to u32 (executor.cc:459-463) packed into a CSR of records:
+ * rec_off[0..nbuf] (u64, rec_off[0] = 0) and rec_pcs (room for `total`
+ * words) -- what syzcov_state_newcov_dev takes, with no host round trip.  A
+ * malformed buffer contributes an empty record and sets *err |= 1 (device
+ * u32, nullable).  (Records are sorted when a buffer's PCs share their high
+ * 32 bits, as a kernel's do; newcov rejects an unsorted one.)
+ * ws: syzcov_dev_cover_ingest64_ws_size(nbuf, total). */
+size_t syzcov_dev_cover_ingest64_ws_size(size_t nbuf, uint64_t total);
+int syzcov_dev_cover_ingest64(uint64_t *pcs64, const uint64_t *off, size_t nbuf, uint64_t total,
+                              uint64_t *rec_off, uint32_t *rec_pcs, uint32_t *err, void *ws,
+                              size_t ws_size, void *stream);
 /* out[i] = the PC of key word words[i] (exact, no table); in place allowed. */
 int syzcov_dev_words_to_pcs(const uint32_t *words, size_t n, uint32_t kshift, uint32_t kbase,
                             uint32_t *out, void *stream);

@@ -112,6 +112,8 @@ _SIGS = {
                                               u32, p_, p_, p_, p_, sz, p_]),
     "syzcov_dev_words_to_pcs": (C.c_int, [p_, sz, u32, u32, p_, p_]),
     "syzcov_dev_cover_dedup64": (C.c_int, [p_, p_, sz, p_, p_, p_]),
+    "syzcov_dev_cover_ingest64_ws_size": (sz, [sz, u64]),
+    "syzcov_dev_cover_ingest64": (C.c_int, [p_, p_, sz, u64, p_, p_, p_, p_, sz, p_]),
     "syzcov_dev_minimize_range_keys": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_, p_, p_,
                                                  p_, p_, u64, p_, p_, p_, C.c_int, p_, p_, p_]),
     "syzcov_dev_minimize_range_keys_pass2": (C.c_int, [p_, p_, p_, p_, p_, p_, sz, u64, u32, p_,

@@ -484,6 +484,93 @@ __global__ __launch_bounds__(NT) void wide_kernel(uint64_t *pcs, const uint64_t 
         });
 }
 
+// ---------------------------------------------------------------------
+// Executor buffers straight into the new-coverage check: the
+// deduped buffers' u32 words packed into a CSR of records.
+constexpr uint32_t IB = 1024;  // buffers per scan block
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+    const uint32_t l = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(v, d, 64);
+        if ((int)l >= d) v += y;
+    }
+    return v;
+}
+
+// exclusive scan over IB threads (u64); *total = the block's sum
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *tmp, uint64_t *total) {
+    const uint32_t w = threadIdx.x >> 6, l = __lane_id();
+    const uint64_t inc = wave_incl_scan64(v);
+    if (l == 63) tmp[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const uint64_t x = l < IB / 64 ? tmp[l] : 0ull;
+        const uint64_t xi = wave_incl_scan64(x);
+        if (l < IB / 64) tmp[l] = xi - x;
+        if (l == IB / 64 - 1) tmp[IB / 64] = xi;
+    }
+    __syncthreads();
+    const uint64_t r = tmp[w] + inc - v;
+    *total = tmp[IB / 64];
+    __syncthreads();
+    return r;
+}
+
+// a malformed buffer (new_len UINT32_MAX) contributes no record PCs
+__device__ __forceinline__ uint64_t rec_len(const uint32_t *nl, uint64_t b, uint64_t nbuf) {
+    return b < nbuf && nl[b] != UINT32_MAX ? nl[b] : 0u;
+}
+
+__global__ __launch_bounds__(IB) void ingest_bsum_kernel(const uint32_t *nl, uint64_t nbuf,
+                                                         uint64_t *bsum) {
+    __shared__ uint64_t tmp[IB / 64 + 1];
+    uint64_t total;
+    block_excl_scan64(rec_len(nl, (uint64_t)blockIdx.x * IB + threadIdx.x, nbuf), tmp, &total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(IB) void ingest_bscan_kernel(uint64_t *bsum, uint64_t nblk) {
+    __shared__ uint64_t tmp[IB / 64 + 1];
+    uint64_t carry = 0;
+    for (uint64_t c = 0; c < nblk; c += IB) {
+        const uint64_t i = c + threadIdx.x;
+        uint64_t total;
+        const uint64_t p = block_excl_scan64(i < nblk ? bsum[i] : 0ull, tmp, &total);
+        if (i < nblk) bsum[i] = carry + p;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(IB) void ingest_off_kernel(const uint32_t *nl, uint64_t nbuf,
+                                                        const uint64_t *bsum, uint64_t *rec_off,
+                                                        uint32_t *err) {
+    __shared__ uint64_t tmp[IB / 64 + 1];
+    const uint64_t b = (uint64_t)blockIdx.x * IB + threadIdx.x;
+    const uint64_t len = rec_len(nl, b, nbuf);
+    uint64_t total;
+    const uint64_t p = bsum[blockIdx.x] + block_excl_scan64(len, tmp, &total);
+    if (b < nbuf) {
+        rec_off[b] = p;
+        if (nl[b] == UINT32_MAX && err) atomicOr(err, 1u);
+    }
+    if (b == nbuf - 1) rec_off[nbuf] = p + len;
+}
+
+// record b's words from their buffer slot to their CSR slot
+__global__ __launch_bounds__(NT) void ingest_copy_kernel(const uint32_t *words, const uint64_t *off,
+                                                         const uint32_t *nl, uint64_t nbuf,
+                                                         const uint64_t *rec_off,
+                                                         uint32_t *rec_pcs) {
+    for (uint64_t b = blockIdx.x; b < nbuf; b += gridDim.x) {
+        const uint64_t len = rec_len(nl, b, nbuf);
+        const uint32_t *src = words + off[b];
+        uint32_t *dst = rec_pcs + rec_off[b];
+        for (uint64_t i = threadIdx.x; i < len; i += NT) dst[i] = src[i];
+    }
+}
+
 }  // namespace dd
 }  // namespace syz
 
@@ -505,6 +592,41 @@ extern "C" int syzcov_dev_cover_dedup64(uint64_t *pcs, const uint64_t *off, size
                        (uint64_t)nseg, new_len, out32);
     hipLaunchKernelGGL(dd::wide_kernel, dim3(grid), dim3(dd::NT), 0, s, pcs, off, (uint64_t)nseg,
                        new_len, out32);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+static size_t ingest_part(size_t n) { return (n + 255) / 256 * 256; }
+
+extern "C" size_t syzcov_dev_cover_ingest64_ws_size(size_t nbuf, uint64_t total) {
+    const size_t nblk = (nbuf + dd::IB - 1) / dd::IB;
+    return ingest_part(nbuf * 4) + ingest_part(total * 4) + ingest_part(nblk * 8);
+}
+
+// executor.cc:574-587 + :459-463 over nbuf raw KCOV buffers, the
+// kept words packed into the records syzcov_state_newcov_dev takes
+extern "C" int syzcov_dev_cover_ingest64(uint64_t *pcs64, const uint64_t *off, size_t nbuf,
+                                         uint64_t total, uint64_t *rec_off, uint32_t *rec_pcs,
+                                         uint32_t *err, void *ws, size_t ws_size, void *stream) {
+    if (nbuf == 0) return 0;
+    if (!pcs64 || !off || !rec_off || !rec_pcs || !ws ||
+        ws_size < syzcov_dev_cover_ingest64_ws_size(nbuf, total))
+        return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    uint8_t *w = (uint8_t *)ws;
+    uint32_t *nl = (uint32_t *)w;
+    uint32_t *words = (uint32_t *)(w + ingest_part(nbuf * 4));
+    uint64_t *bsum = (uint64_t *)(w + ingest_part(nbuf * 4) + ingest_part(total * 4));
+    if (int rc = syzcov_dev_cover_dedup64(pcs64, off, nbuf, nl, words, stream)) return rc;
+    const uint64_t nblk = (nbuf + dd::IB - 1) / dd::IB;
+    hipLaunchKernelGGL(dd::ingest_bsum_kernel, dim3(nblk), dim3(dd::IB), 0, s, nl, (uint64_t)nbuf,
+                       bsum);
+    hipLaunchKernelGGL(dd::ingest_bscan_kernel, dim3(1), dim3(dd::IB), 0, s, bsum, nblk);
+    hipLaunchKernelGGL(dd::ingest_off_kernel, dim3(nblk), dim3(dd::IB), 0, s, nl, (uint64_t)nbuf,
+                       bsum, rec_off, err);
+    const unsigned grid = nbuf < 8192 ? (unsigned)nbuf : 8192u;
+    hipLaunchKernelGGL(dd::ingest_copy_kernel, dim3(grid), dim3(dd::NT), 0, s, words, off, nl,
+                       (uint64_t)nbuf, rec_off, rec_pcs);
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -120,3 +120,87 @@ def test_host_cover_dedup():
         for kind in ("kernel", "wide", "dense"):
             b = _buf(rng, n, kind)
             assert np.array_equal(cover_dedup(b), orc.cover_dedup64(b)), (n, kind)
+
+
+def test_ingest_into_newcov():
+    """raw u64 KCOV buffers -> cover_dedup -> u32 words packed as
+    records (syzcov_dev_cover_ingest64) -> the fuzzer's new-coverage check
+    (syzcov_state_newcov_dev), all on the device, against the oracle's
+    cover_dedup + newcov_batch (fuzzer.go:456-480) over the same buffers."""
+    import torch
+    from syzkaller_amd._lib import check, lib
+    from syzkaller_amd.engine import _p, _stream
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(21)
+    ncalls, lo, span = 17, 0x81000000, 1 << 16
+    lens = [int(x) for x in rng.integers(0, 3000, 600)] + [0, 1, 5000, 9000, 4096]
+    bufs = [np.uint64(0xffffffff00000000 + lo) + rng.integers(0, span, n).astype(np.uint64)
+            for n in lens]
+    for b in bufs[::7]:  # a few zero PCs (dropped by cover_dedup)
+        if b.size:
+            b[0] = 0
+    callids = rng.integers(0, ncalls, len(lens)).astype(np.int32)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(np.asarray(lens, np.uint64), out=off[1:])
+    total = int(off[-1])
+    L = lib()
+    d_pcs = torch.from_numpy(np.concatenate(bufs).view(np.int64).copy()).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_roff = torch.zeros(len(lens) + 1, dtype=torch.int64, device="cuda")
+    d_rpcs = torch.zeros(total, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    wsz = L.syzcov_dev_cover_ingest64_ws_size(len(lens), total)
+    ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+    check(L.syzcov_dev_cover_ingest64(_p(d_pcs), _p(d_off), len(lens), total, _p(d_roff),
+                                      _p(d_rpcs), _p(d_err), _p(ws), wsz, _stream()),
+          "dev_cover_ingest64")
+    recs = [(orc.cover_dedup64(b) & np.uint64(0xFFFFFFFF)).astype(np.uint32) for b in bufs]
+    roff = d_roff.cpu().numpy().view(np.uint64)
+    rpcs = d_rpcs.cpu().numpy().view(np.uint32)
+    assert int(d_err.item()) == 0
+    assert roff.tolist() == np.concatenate([[0], np.cumsum([r.size for r in recs])]).tolist()
+    for k, r in enumerate(recs):
+        assert np.array_equal(rpcs[int(roff[k]):int(roff[k + 1])], r), k
+    # the same records through the device new-coverage check, twice (the
+    # second batch sees the first's maxCover)
+    st = CoverState(ncalls, lo, span)
+    exp_mc = [[] for _ in range(ncalls)]
+    d_cid = torch.from_numpy(callids).cuda()
+    npc = int(roff[-1])
+    nwsz = L.syzcov_state_newcov_ws_size(len(lens), npc)
+    nws = torch.empty(nwsz, dtype=torch.uint8, device="cuda")
+    for rep in range(2):
+        flags = torch.zeros(len(lens), dtype=torch.uint8, device="cuda")
+        stats = torch.zeros(2, dtype=torch.int32, device="cuda")
+        check(L.syzcov_state_newcov_dev(st.h, _p(d_cid), _p(d_roff), _p(d_rpcs), len(lens), npc,
+                                        _p(flags), _p(stats), _p(nws), nwsz, _stream()),
+              "state_newcov_dev")
+        exp, exp_mc = orc.newcov_batch(exp_mc, [], callids, recs)
+        assert int(stats[0].item()) == 0
+        assert np.array_equal(flags.cpu().numpy(), exp), rep
+        assert (rep == 0) == bool(exp.any())
+    for c in range(ncalls):
+        assert np.array_equal(st.max_cover(c), exp_mc[c]), c
+    st.close()
+
+
+def test_ingest_flags_malformed_buffer():
+    import torch
+    from syzkaller_amd._lib import check, lib
+    from syzkaller_amd.engine import _p, _stream
+    # buffer 0 = [0, 6), buffer 1 runs backwards (6 -> 2), buffer 2 is empty
+    off = np.array([0, 6, 2, 2], np.uint64)
+    pcs = np.array([9, 3, 3, 7, 1, 2, 5, 5], np.uint64)
+    L = lib()
+    d_pcs = torch.from_numpy(pcs.view(np.int64).copy()).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_roff = torch.full((4,), -1, dtype=torch.int64, device="cuda")
+    d_rpcs = torch.zeros(8, dtype=torch.int32, device="cuda")
+    d_err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    wsz = L.syzcov_dev_cover_ingest64_ws_size(3, 8)
+    ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+    check(L.syzcov_dev_cover_ingest64(_p(d_pcs), _p(d_off), 3, 8, _p(d_roff), _p(d_rpcs),
+                                      _p(d_err), _p(ws), wsz, _stream()), "dev_cover_ingest64")
+    assert int(d_err.item()) == 1
+    assert d_roff.cpu().tolist() == [0, 5, 5, 5]
+    assert d_rpcs.cpu().numpy()[:5].tolist() == [1, 2, 3, 7, 9]
