@@ -62,6 +62,10 @@ struct CoverState {
     bool mfl_stale = true;
     uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
     uint8_t *low_of_key = nullptr;  // key mode: membership table (pc_index)
+    // key mode with kshift <= 4: the same table as nibbles over whole ranges
+    // of 2^RSH keys (8 keys per word), staged half a range at a time in LDS by
+    // the candidate pass's separate membership pass (newcov.hip)
+    uint32_t *nib = nullptr;
     // LDS-staged candidate pass: per-call record counts | offsets | cursors |
     // work-item prefix over (call, range) | work-item descriptors; one batch
     // at a time per state

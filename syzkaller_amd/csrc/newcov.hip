@@ -502,7 +502,11 @@ __device__ __forceinline__ uint64_t lane_range(uint32_t a, uint32_t b) {
 #ifndef SYZ_NC_KEY_WPE
 #define SYZ_NC_KEY_WPE 4  // key mode: 128 VGPRs (the deferred membership bytes) at one workgroup per CU: 0.97 vs 1.41 ms per C5 batch at 8
 #endif
-template <bool KEY>
+// SEP (key mode, kshift <= 4): no per-PC membership gathers here; the
+// separate pass (newcov_memb_kernel) checks every PC from LDS, and this pass
+// checks its candidates only (the keys of maxCover | flakes all hold a
+// universe PC, so a PC whose key has none is always a candidate).
+template <bool KEY, bool SEP>
 __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__((amdgpu_num_sgpr(72))) void newcov_cand_lds_kernel(
     const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
     uint64_t words_per_call, Index X, uint32_t nr, const uint32_t *__restrict__ ipre, uint32_t ne,
@@ -605,7 +609,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
     // next step: C5 1.23 ms per batch)
     uint32_t mb[LC_U * 4];
     auto gather = [&](uint32_t s0, const uint4 *pc) {
-        if (!KEY) return;
+        if (!KEY || SEP) return;
 #pragma unroll
         for (int u = 0; u < LC_U; u++) {
             const uint32_t i = (s0 + u) & 63;
@@ -652,9 +656,16 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
                 const uint64_t pm = lane_range(lo1 > (uint32_t)c ? (lo1 - c + 3) >> 2 : 0u,
                                                hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
                 bad |= __ballot((c ? v[c - 1] : p0) > v[c]) & pm;
-                if (KEY) nonmem |= __ballot(mb[u * 4 + c] != (v[c] & lowmask)) & vm;
+                if (KEY && !SEP) nonmem |= __ballot(mb[u * 4 + c] != (v[c] & lowmask)) & vm;
                 const uint64_t cm = __ballot(!((wd[c] >> (o[c] & 31)) & 1u)) & vm;
-                if (cm) emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);  // rare
+                if (cm) {  // rare
+                    if (KEY && SEP) {  // the candidates' membership, one byte each
+                        const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
+                            lr, (cm >> l) & 1u ? (v[c] >> ks) - obase + (q << RSH) : 0xFFFFFFF0u, 0, 0);
+                        nonmem |= __ballot(mc != (v[c] & lowmask)) & cm;
+                    }
+                    emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);
+                }
             }
         }
     };
@@ -689,6 +700,116 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
     if (nc) flush();
     if (bad && l == 0) stats[0] = 3u;
     if (nonmem && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
+}
+
+// ---------------------------------------------------------------------------
+// Separate membership pass (key mode, kshift <= 4): every PC of the row
+// streams against the universe's low bits, staged as nibbles in LDS half a
+// range (2^(RSH-1) keys, 128 KB) at a time.  Workgroup (g, h) takes the g-th
+// of MB_G equal slices of the whole row stream (ranges in order; the coverage
+// is skewed, 40% of the PCs in range 0, so slicing by range left most CUs
+// idle: 0.89 ms) and checks their PCs of half h of each range it crosses,
+// restaging the table per range: the rows are read once per half, 2 x 4 B per
+// PC, instead of one L2 byte request per PC in the candidate pass (those
+// requests bound it: 0.92 vs 0.44 ms per C5 batch without them).  A PC whose
+// key holds no universe PC is a candidate (its maxCover | flakes bit is
+// clear) and checked there exactly.
+constexpr int MB_THREADS = 1024;
+constexpr uint32_t MB_G = 256;  // row slices per half (a multiple of 8)
+constexpr int MB_U = 4;         // rows per wave step (two steps in flight)
+
+__global__ void nib_build_kernel(const uint8_t *__restrict__ low_of_key, uint64_t nkeys,
+                                 uint64_t nwords, uint32_t *__restrict__ nib) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint64_t k = w * 8 + j;
+            x |= (k < nkeys ? low_of_key[k] & 15u : 0u) << (4 * j);
+        }
+        nib[w] = x;
+    }
+}
+
+__global__ __launch_bounds__(MB_THREADS) void newcov_memb_kernel(
+    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ nib, Index X,
+    uint32_t nr, const uint4 *__restrict__ rows, const uint32_t *__restrict__ qoff,
+    uint32_t *__restrict__ stats) {
+    extern __shared__ uint4 s_nb4[];  // 2^(RSH-1) nibbles
+    constexpr uint32_t HW = 1u << (RSH - 4);  // words per half range
+    // workgroups i and i + 8 share an XCD (round-robin dispatch): the two
+    // halves of a slice run there together and the second read of the rows
+    // hits that XCD's L2
+    const uint32_t i16 = blockIdx.x & 15u;
+    const uint32_t g = (blockIdx.x >> 4) * 8 + (i16 & 7u), h = i16 >> 3;
+    const uint32_t t = threadIdx.x, l = __lane_id(), wv = t >> 6;
+    const uint32_t *s_nb = (const uint32_t *)s_nb4;
+    const uint32_t rt = qoff[nr];
+    uint32_t a = (uint32_t)((uint64_t)rt * g / MB_G);
+    const uint32_t b = (uint32_t)((uint64_t)rt * (g + 1) / MB_G);
+    uint32_t q = 0;
+    while (q + 1 < nr && qoff[q + 1] <= a) q++;
+    const uint32_t ks = X.kshift, lowmask = (1u << ks) - 1u;
+    const __amdgpu_buffer_rsrc_t pr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)pcs, 0, npc * 4u, 0x00020000);
+    bool bad = false;
+    for (; a < b; q++) {
+        const uint32_t e = min(b, qoff[q + 1]);
+        if (a >= e) continue;
+        // this range's half of the table (the previous one's readers are done)
+        __syncthreads();
+        const uint4 *src = (const uint4 *)(nib + ((uint64_t)q << (RSH - 3)) + (uint64_t)h * HW);
+#pragma unroll
+        for (uint32_t i = 0; i < HW / 4 / MB_THREADS; i++)
+            s_nb4[t + i * MB_THREADS] = src[t + i * MB_THREADS];
+        __syncthreads();
+        const uint32_t hb = X.kbase + (q << RSH) + (h << (RSH - 1));  // the half's first key
+        // two steps of MB_U rows in flight per wave: the next step's loads are
+        // issued before this step is tested (rows past e load nothing)
+        constexpr uint32_t STEP = (MB_THREADS / 64) * MB_U;
+        uint4 pa[MB_U], pb[MB_U];
+        uint32_t la[MB_U], ha[MB_U], lb[MB_U], hbb[MB_U];
+        auto load = [&](uint32_t r0, uint4 (&pc)[MB_U], uint32_t (&lo)[MB_U],
+                        uint32_t (&hi)[MB_U]) {
+#pragma unroll
+            for (int u = 0; u < MB_U; u++) {
+                const bool row = r0 + u < e;  // wave-uniform
+                const uint4 d = rows[row ? r0 + u : a];
+                lo[u] = row ? d.z & 511u : 0u;
+                hi[u] = row ? (d.z >> 9) & 511u : 0u;
+                const bool any = 4 * l + 3 >= lo[u] && 4 * l < hi[u];
+                pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      pr, any ? l * 16u : 0xFFFFFFF0u,
+                                                      any ? d.x * 4u : 0u, 0));
+            }
+        };
+        auto check = [&](const uint4 (&pc)[MB_U], const uint32_t (&lo)[MB_U],
+                         const uint32_t (&hi)[MB_U]) {
+#pragma unroll
+            for (int u = 0; u < MB_U; u++) {
+                const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint32_t el = 4 * l + c;
+                    const uint32_t rel = (v[c] >> ks) - hb;
+                    const bool in = el >= lo[u] && el < hi[u] && rel < (1u << (RSH - 1));
+                    const uint32_t nb = (s_nb[(rel >> 3) & (HW - 1)] >> ((rel & 7) * 4)) & 15u;
+                    bad |= in & (nb != (v[c] & lowmask));
+                }
+            }
+        };
+        uint32_t r0 = a + wv * MB_U;
+        load(r0, pa, la, ha);
+        for (; r0 < e; r0 += 2 * STEP) {
+            load(r0 + STEP, pb, lb, hbb);
+            check(pa, la, ha);
+            load(r0 + 2 * STEP, pa, la, ha);
+            check(pb, lb, hbb);
+        }
+        a = e;
+    }
+    if (__ballot(bad) && l == 0) stats[0] = 1u;  // not in the universe: the batch is rejected
 }
 
 // ---------------------------------------------------------------------------
@@ -946,6 +1067,7 @@ extern "C" int syzcov_state_destroy(syzcov_cover_state h) {
     if (st->mfl) hipFree(st->mfl);
     if (st->pc_of_key) hipFree(st->pc_of_key);
     if (st->low_of_key) hipFree(st->low_of_key);
+    if (st->nib) hipFree(st->nib);
     if (st->grp) hipFree(st->grp);
     if (st->scratch) hipFree(st->scratch);
     if (st->ev_state) hipEventDestroy(st->ev_state);
@@ -1032,8 +1154,10 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
     }
     if (st->pc_of_key) hipFree(st->pc_of_key);
     if (st->low_of_key) hipFree(st->low_of_key);
+    if (st->nib) hipFree(st->nib);
     st->pc_of_key = nullptr;
     st->low_of_key = nullptr;
+    st->nib = nullptr;
     st->X = Index{0, st->pc_lo, 0, 0, st->pc_span, nullptr};  // back to window mode
     if (n == 0) return alloc_maps(st);
     // the sorted unique universe on the device: window bits -> list
@@ -1091,6 +1215,16 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
             rc = SYZCOV_EINVAL;
             break;
         }
+        if (ks <= 4) {  // the separate membership pass's nibbles, whole ranges
+            const uint64_t nwords = ((nkeys + (1ull << RSH) - 1) >> RSH) << (RSH - 3);
+            if (hipMalloc(&st->nib, nwords * 4) != hipSuccess) {
+                st->nib = nullptr;
+                rc = SYZCOV_ENOMEM;
+                break;
+            }
+            hipLaunchKernelGGL(nib_build_kernel, dim3(grid_for(nwords, 256, 8192)), dim3(256), 0,
+                               st->s, (const uint8_t *)st->low_of_key, nkeys, nwords, st->nib);
+        }
         st->X = Index{1, st->pc_lo, ks, kbase, nkeys, st->low_of_key};
         rc = alloc_maps(st);
     } while (0);
@@ -1102,8 +1236,10 @@ extern "C" int syzcov_state_set_universe(syzcov_cover_state h, const uint32_t *p
     if (rc) {
         if (st->pc_of_key) hipFree(st->pc_of_key);
         if (st->low_of_key) hipFree(st->low_of_key);
+        if (st->nib) hipFree(st->nib);
         st->pc_of_key = nullptr;
         st->low_of_key = nullptr;
+        st->nib = nullptr;
         st->X = Index{0, st->pc_lo, 0, 0, st->pc_span, nullptr};
         alloc_maps(st);
     }
@@ -1221,10 +1357,16 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                                (uint4 *)st->mfl);
             st->mfl_stale = false;
         }
-        static std::atomic<uint32_t> lds_done[2];
-        auto kfn = st->X.key_mode ? newcov_cand_lds_kernel<true> : newcov_cand_lds_kernel<false>;
-        int rc = set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[st->X.key_mode ? 1 : 0]);
+        static std::atomic<uint32_t> lds_done[3], memb_done;
+        const bool sep = st->X.key_mode && st->nib;
+        const int kv = !st->X.key_mode ? 0 : sep ? 2 : 1;
+        auto kfn = kv == 0 ? newcov_cand_lds_kernel<false, false>
+                   : kv == 1 ? newcov_cand_lds_kernel<true, false>
+                             : newcov_cand_lds_kernel<true, true>;
+        int rc = set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[kv]);
         if (rc) return rc;
+        if (sep && (rc = set_dyn_lds_once((const void *)newcov_memb_kernel, 1 << (RSH - 2), memb_done)))
+            return rc;
         const uint32_t nr = (uint32_t)nr64, stride = (uint32_t)nrec + 1;
         uint4 *desc = (uint4 *)((uint8_t *)st->grp + grp_desc_off(st->ncalls));
         uint32_t *nq = (uint32_t *)(ws + Lw.nq), *csum = (uint32_t *)(ws + Lw.csum);
@@ -1267,6 +1409,11 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                            (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
                            st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
                            (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
+        if (sep)
+            hipLaunchKernelGGL(newcov_memb_kernel, dim3(MB_G * 2), dim3(MB_THREADS),
+                               (size_t)(1u << (RSH - 2)), s, pcs, (uint32_t)npc,
+                               (const uint32_t *)st->nib, st->X, nr, (const uint4 *)rows,
+                               (const uint32_t *)qoff, stats);
     } else {
         const unsigned gx = (grid_for(nrec, NC_WPB, 4096) + 7) & ~7u;  // a multiple of the 8 XCDs
         hipLaunchKernelGGL(newcov_cand_kernel, dim3(gx), dim3(NC_THREADS), 0, s, callid, rec_off,

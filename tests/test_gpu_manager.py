@@ -307,6 +307,41 @@ def test_newcov_key_mode(spacing, newcov_path):
     st.close()
 
 
+@pytest.mark.parametrize("kshift_lows", [16, 64])
+def test_newcov_covered_key_wrong_low_bits(newcov_path, kshift_lows):
+    """A PC that shares its key with a universe PC already in maxCover (so its
+    bitmap bit is SET: not a candidate) but has other low bits is not in the
+    universe: the batch is rejected whole.  kshift 4 takes the separate
+    nibble membership pass of the LDS candidate path, kshift 6 the per-PC
+    byte gathers; the probe path checks every PC itself."""
+    from syzkaller_amd import SyzcovError
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(43 + kshift_lows)
+    lo, n = 0x81000000, 1 << 15
+    univ = (lo + kshift_lows * np.arange(n) + rng.integers(0, kshift_lows, n)).astype(np.uint32)
+    st = CoverState(4, lo, kshift_lows * n)
+    st.set_universe(univ)
+    # big enough batches that the LDS path is chosen on its own as well
+    recs = [np.sort(rng.choice(univ, 1500, replace=False)) for _ in range(400)]
+    cids = (np.arange(400) % 4).astype(np.int32)
+    exp, mc = orc.newcov_batch([[] for _ in range(4)], [], cids, recs)
+    assert np.array_equal(st.new_coverage(cids, recs), exp)
+    before = [st.max_cover(c) for c in range(4)]
+    covered = int(mc[1][len(mc[1]) // 2])  # in call 1's maxCover
+    stray = (covered & ~(kshift_lows - 1)) | ((covered + 1) & (kshift_lows - 1))
+    assert stray not in set(univ.tolist())
+    bad = [np.sort(np.concatenate([r[r != covered], [stray]])).astype(np.uint32)
+           for r in recs[:400]]
+    bad = [r if k == 1 else recs[k] for k, r in enumerate(bad)]  # one stray PC in record 1
+    with pytest.raises(SyzcovError):
+        st.new_coverage(cids, bad)
+    for c in range(4):
+        assert np.array_equal(st.max_cover(c), before[c])
+    # the same batch without the stray PC changes nothing either (all covered)
+    assert not st.new_coverage(cids, recs).any()
+    st.close()
+
+
 def test_newcov_universe_of_call_sites(newcov_path):
     """A universe registered as the call SITES of __sanitizer_cov_trace_pc
     (objdump's addresses) while KCOV reports return addresses (site + 5 on
