@@ -765,47 +765,53 @@ __global__ __launch_bounds__(MB_THREADS) void newcov_memb_kernel(
             s_nb4[t + i * MB_THREADS] = src[t + i * MB_THREADS];
         __syncthreads();
         const uint32_t hb = X.kbase + (q << RSH) + (h << (RSH - 1));  // the half's first key
-        // two steps of MB_U rows in flight per wave: the next step's loads are
-        // issued before this step is tested (rows past e load nothing)
-        constexpr uint32_t STEP = (MB_THREADS / 64) * MB_U;
-        uint4 pa[MB_U], pb[MB_U];
-        uint32_t la[MB_U], ha[MB_U], lb[MB_U], hbb[MB_U];
-        auto load = [&](uint32_t r0, uint4 (&pc)[MB_U], uint32_t (&lo)[MB_U],
-                        uint32_t (&hi)[MB_U]) {
+        // each wave takes 64 consecutive rows at a time, their descriptors
+        // one per lane (a single vector load, read back with readlane), and
+        // streams them MB_U rows per step, the next step's loads issued before
+        // this step is tested (rows past the block load nothing)
+        for (uint32_t rb = a + wv * 64; rb < e; rb += (MB_THREADS / 64) * 64) {
+            const uint32_t nrow = min(64u, e - rb);
+            const uint4 dsc = rows[rb + min(l, nrow - 1)];
+            uint4 pa[MB_U], pb[MB_U];
+            auto load = [&](uint32_t s0, uint4 (&pc)[MB_U]) {
 #pragma unroll
-            for (int u = 0; u < MB_U; u++) {
-                const bool row = r0 + u < e;  // wave-uniform
-                const uint4 d = rows[row ? r0 + u : a];
-                lo[u] = row ? d.z & 511u : 0u;
-                hi[u] = row ? (d.z >> 9) & 511u : 0u;
-                const bool any = 4 * l + 3 >= lo[u] && 4 * l < hi[u];
-                pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      pr, any ? l * 16u : 0xFFFFFFF0u,
-                                                      any ? d.x * 4u : 0u, 0));
-            }
-        };
-        auto check = [&](const uint4 (&pc)[MB_U], const uint32_t (&lo)[MB_U],
-                         const uint32_t (&hi)[MB_U]) {
-#pragma unroll
-            for (int u = 0; u < MB_U; u++) {
-                const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
-#pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    const uint32_t el = 4 * l + c;
-                    const uint32_t rel = (v[c] >> ks) - hb;
-                    const bool in = el >= lo[u] && el < hi[u] && rel < (1u << (RSH - 1));
-                    const uint32_t nb = (s_nb[(rel >> 3) & (HW - 1)] >> ((rel & 7) * 4)) & 15u;
-                    bad |= in & (nb != (v[c] & lowmask));
+                for (int u = 0; u < MB_U; u++) {
+                    const uint32_t i = (s0 + u) & 63;
+                    const uint32_t st = __builtin_amdgcn_readlane(dsc.x, i);
+                    const uint32_t z = __builtin_amdgcn_readlane(dsc.z, i);
+                    const bool row = s0 + u < nrow;  // wave-uniform
+                    const uint32_t lo = z & 511u, hi = row ? (z >> 9) & 511u : 0u;
+                    const bool any = 4 * l + 3 >= lo && 4 * l < hi;
+                    pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          pr, any ? l * 16u : 0xFFFFFFF0u,
+                                                          any ? st * 4u : 0u, 0));
                 }
+            };
+            auto check = [&](uint32_t s0, const uint4 (&pc)[MB_U]) {
+#pragma unroll
+                for (int u = 0; u < MB_U; u++) {
+                    const uint32_t i = (s0 + u) & 63;
+                    const uint32_t z = __builtin_amdgcn_readlane(dsc.z, i);
+                    const bool row = s0 + u < nrow;
+                    const uint32_t lo = z & 511u, hi = row ? (z >> 9) & 511u : 0u;
+                    const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const uint32_t el = 4 * l + c;
+                        const uint32_t rel = (v[c] >> ks) - hb;
+                        const bool in = el >= lo && el < hi && rel < (1u << (RSH - 1));
+                        const uint32_t nb = (s_nb[(rel >> 3) & (HW - 1)] >> ((rel & 7) * 4)) & 15u;
+                        bad |= in & (nb != (v[c] & lowmask));
+                    }
+                }
+            };
+            load(0, pa);
+            for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * MB_U) {
+                load(s0 + MB_U, pb);
+                check(s0, pa);
+                load(s0 + 2 * MB_U, pa);
+                check(s0 + MB_U, pb);
             }
-        };
-        uint32_t r0 = a + wv * MB_U;
-        load(r0, pa, la, ha);
-        for (; r0 < e; r0 += 2 * STEP) {
-            load(r0 + STEP, pb, lb, hbb);
-            check(pa, la, ha);
-            load(r0 + 2 * STEP, pa, la, ha);
-            check(pb, lb, hbb);
         }
         a = e;
     }
