@@ -46,8 +46,12 @@ def test_no_oracle_in_product():
     assert os.path.exists(os.path.join(root, "oracle", "oracle.h"))
 
 
-def test_gfx950_code_object_present():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
-                          _lib.LIB_PATH], capture_output=True, text=True)
+def test_gfx950_code_object_present(tmp_path):
+    # (--offloading writes the extracted code objects next to its input: a copy
+    # in a scratch directory keeps them out of the package)
+    import shutil
+    lib = shutil.copy(_lib.LIB_PATH, tmp_path / "libsyzcov.so")
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     txt = out.stdout + out.stderr
     assert "gfx950" in txt
