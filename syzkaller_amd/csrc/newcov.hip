@@ -1311,7 +1311,12 @@ static int forced_path() {
     return (f & FORCE_NC_LDS) ? 1 : (f & FORCE_NC_PROBE) ? 2 : 0;
 }
 // work items of the LDS pass per batch (64 rows at least per item)
-constexpr uint32_t NC_ITEMS = 1024;
+// work items per batch: 512 / 1024 / 2048 / 4096 measured 0.642-0.646 /
+// 0.671-0.675 / 0.644-0.649 / 0.70 ms per steady-state C5 batch
+#ifndef SYZ_NC_ITEMS
+#define SYZ_NC_ITEMS 512
+#endif
+constexpr uint32_t NC_ITEMS = SYZ_NC_ITEMS;
 
 static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *rec_off,
                          const uint32_t *pcs, size_t nrec, uint64_t npc, uint8_t *is_new,
