@@ -715,7 +715,12 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
 // key holds no universe PC is a candidate (its maxCover | flakes bit is
 // clear) and checked there exactly.
 constexpr int MB_THREADS = 1024;
-constexpr uint32_t MB_G = 256;  // row slices per half (a multiple of 8)
+// (128 / 256 / 384 / 512 slices: 0.645-0.647 / 0.644-0.648 / 0.661 / 0.649-0.650
+// ms per steady-state C5 batch)
+#ifndef SYZ_NC_MB_G
+#define SYZ_NC_MB_G 256
+#endif
+constexpr uint32_t MB_G = SYZ_NC_MB_G;  // row slices per half (a multiple of 8)
 constexpr int MB_U = 4;         // rows per wave step (two steps in flight)
 
 __global__ void nib_build_kernel(const uint8_t *__restrict__ low_of_key, uint64_t nkeys,
