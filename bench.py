@@ -2,10 +2,12 @@
 """Benchmarks of the syzkaller coverage hot path on MI355X.
 
 Default (the driver's headline line): input-PCs processed/sec for
-Canonicalize + Minimize + maxCover Union (BASELINE.json metric).  N=1 runs
-config C2 (1M inputs, one GPU); N>1 runs config C3 (10M global inputs sharded
-by input over the ranks, RCCL merges; total work fixed, so "strong" scaling
-across N >= 2); --global-inputs overrides the corpus size.
+Canonicalize + Minimize + maxCover Union (BASELINE.json metric) over config C3
+(10M inputs, the config the target is quoted on) at EVERY N: the whole corpus
+on one GPU at N=1, sharded by input over the ranks at N>1 (RCCL merges; total
+work fixed, so "strong" scaling and one config.workload string for the whole
+1 -> 8 curve); --global-inputs overrides the corpus size.  N=1 adds config C2
+(1M inputs, one GPU) as the `c2` sub-record.
 
 One step = one pass of the hot path over one synthetic corpus already
 resident in HBM (raw KCOV lists, CSR):
@@ -37,13 +39,24 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
-# this same bench command (tools/profile_r04.sh -> tools/traffic.py), committed per round
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r04_traffic.json")
+# this same bench command (tools/profile.sh -> tools/traffic.py), committed per round:
+# {"C3": {phase: ...}, "C2": ..., "newcov": ..., "dedup": ...}
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05_traffic.json")
+
+
+def traffic_of(workload: str, phase: str):
+    """(bytes per launch, source) of a phase of a workload, or (None, None)."""
+    if not os.path.exists(TRAFFIC_JSON):
+        return None, None
+    with open(TRAFFIC_JSON) as f:
+        b = json.load(f).get(workload, {}).get(phase, {}).get("bytes")
+    return b, (f"{os.path.relpath(TRAFFIC_JSON, ROOT)}[{workload}][{phase}]" if b else None)
 I8_PEAK_TOPS = 5000.0      # dense i8 MFMA = 2x bf16 (~2.5 PF dense): MI355X_MICROARCH.md
 SEED_C1 = 0x5EED0001  # BASELINE.json configs[0]: the CPU (reference) config
 SEED = 0x5EED0002     # configs[1]: 1M inputs, one GPU
 SEED_C3 = 0x5EED0003  # configs[2]: 10M inputs over the GPUs of one node
 C3_INPUTS = 10_000_000
+C2_INPUTS = 1_000_000
 SEED_PRIO = 0x5EED0004
 SEED_NEWCOV = 0x5EED0005
 SEED_DEDUP = 0x5EED0006
@@ -63,10 +76,10 @@ def parse():
                          "maxCover near saturation, a long-running fuzzer; 32: the early, "
                          "candidate-heavy regime)")
     ap.add_argument("--inputs", type=int, default=1_000_000,
-                    help="inputs (programs) per GPU at N=1 (config C2)")
+                    help="prio: programs per GPU; dedup/newcov: see --records")
     ap.add_argument("--global-inputs", type=int, default=None,
-                    help="corpus inputs over all ranks, sharded by input (default at N>1: "
-                         "config C3's 10M inputs, seed 0x5EED0003)")
+                    help="corpus inputs over all ranks, sharded by input (default: config "
+                         "C3's 10M inputs, seed 0x5EED0003, at every N)")
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=None)
     ap.add_argument("--mean", type=int, default=2048)
     ap.add_argument("--sigma", type=int, default=512)
@@ -76,8 +89,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--prio-dense", action="store_true",
                     help="prio: contract over all C keys instead of the active positional keys")
-    ap.add_argument("--no-c3", action="store_true",
-                    help="N=1: skip the C3-on-one-GPU sub-record (the strong-scaling anchor)")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="N=1: skip the C2 sub-record (1M inputs, BASELINE configs[1])")
     ap.add_argument("--no-dropin", action="store_true",
                     help="N=1: skip the drop-in legs (cover.Minimize from host buffers)")
     ap.add_argument("--no-universe", action="store_true",
@@ -145,7 +158,10 @@ def bench_dry(args):
         t = __import__("torch").ones(1)
         dist.all_reduce(t)
         assert int(t.item()) == world
+    glob = args.global_inputs or C3_INPUTS
     out = {"metric": "dry run (no workload)", "value": None, "n_gpus": world,
+           "config": {"workload": corpus_workload(glob)[2], "global_inputs": glob,
+                      "parallelism": f"shard-by-input x{world}"},
            "rccl_ranks": dist.get_world_size() if world > 1 else 1,
            "backend": dist.get_backend() if world > 1 else None}
     return rank, world, out
@@ -176,7 +192,9 @@ def cpu_baseline(args):
                    f"+ Union fold {t3 - t2:.2f}s, 1 thread, oracle/ C restatement of "
                    f"cover/cover.go (Go toolchain absent)"),
         "phases_s": {"canonicalize": t1 - t0, "minimize": t2 - t1, "union_fold": t3 - t2},
+        # cover.Minimize (its sort.Sort included, cover.go:113) + the Union fold
         "minimize_canonical_pcs_per_s": canon_pcs / (t2 - t1),
+        "minimize_union_canonical_pcs_per_s": canon_pcs / (t3 - t1),
         "union_fold_canonical_pcs_per_s": canon_pcs / (t3 - t2),
         "results": {"kept": int(len(kept)), "union": int(union.size)},
         "host": platform.processor() or platform.machine(),
@@ -282,26 +300,32 @@ def timed(run_step, nphase, args, world, dev):
     return dt, ph
 
 
-def bench_corpus(args):
-    import torch
-    world, rank, dev = init_dist()
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
-    # N=1: config C2 (1M inputs); N>1: config C3 (10M global inputs, sharded
-    # by input: rank r holds [r*n, (r+1)*n)), unless --global-inputs says otherwise
-    glob = args.global_inputs
-    if glob is None and world > 1:
-        glob = C3_INPUTS
-    if glob is None:
-        n, seed, cname = args.inputs, SEED, "C2"
+def corpus_workload(glob: int) -> tuple[str, int, str]:
+    """(config name, seed, config.workload) of a corpus of `glob` inputs over
+    all ranks: the same string at every N, so the driver's 1 -> 8 curve joins
+    like with like (the sharding is in config.parallelism)."""
+    if glob == C3_INPUTS:
+        cname, seed = "C3", SEED_C3
+    elif glob == C2_INPUTS:
+        cname, seed = "C2", SEED
     else:
-        n = -(-glob // world)
-        seed, cname = (SEED_C3, "C3") if glob == C3_INPUTS else (SEED, "custom")
-    if args.seed is not None:
-        seed = args.seed
+        cname, seed = "custom", SEED
+    return cname, seed, f"{cname}: Canonicalize + Minimize + maxCover union, {glob} inputs"
+
+
+def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key):
+    """K timed steps of the corpus pipeline over `glob` inputs (rank r holds
+    [r*n, (r+1)*n)), generated into HBM, canonicalized out of place; returns
+    the measured part of a line (phases, roofline of the dominant phase and of
+    Minimize, results)."""
+    import torch
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n = -(-glob // world)
     lo, span = synth_window(args.log2_space)
     off, raw, lens, total = synth_corpus(n, seed, first=rank * n, mean=args.mean,
                                          sigma=args.sigma, log2_space=args.log2_space, device=dev)
     max_len = int(lens.max().item())
+    del lens
     # the PC universe (allCoverPCs, syz-manager/cover.go:57-69) is registered once,
     # outside the timed steps, like the resident maxCover
     univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev)
@@ -313,115 +337,100 @@ def bench_corpus(args):
     del univ
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
-    dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), args,
-                    world, dev)
+    a = argparse.Namespace(steps=steps, warmup=warmup)
+    dt, phl = timed(lambda ev: eng.step(off, raw, n, sync=False, ev=ev), len(phases), a, world,
+                    dev)
     ph = dict(zip(phases, phl))
     res = eng.result()
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
-    value = total * world * args.steps / dt
     # algorithmic bytes per launch: canon reads raw + writes the
     # canonical list; minimize reads the canonical list once
     alg = eng.alg_bytes(total, canon_pcs)
     dom = max(alg, key=lambda p: ph[p])
     achieved = alg[dom] / (ph[dom] * 1e-3) / 1e9
-    traffic, tj = None, {}
-    if os.path.exists(TRAFFIC_JSON) and world == 1:
-        with open(TRAFFIC_JSON) as f:
-            tj = json.load(f)
-        traffic = tj.get(dom, {}).get("bytes")
+    traffic, tsrc = traffic_of(traffic_key, dom) if world == 1 else (None, None)
+    mz = alg["minimize"] / (ph["minimize"] * 1e-3) / 1e9
     out = {
-        "metric": "input-PCs processed/sec for Canonicalize+Minimize+Union (maxCover merge)",
-        "value": value, "unit": "input-PCs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak" if glob is None else "strong",
-        "vs_baseline": None,
-        "dtype": "u32", "data": "synthetic (counter-based generator, SURVEY §8d)",
-        "config": {"workload": f"{cname}: Canonicalize + Minimize + maxCover union, "
-                               f"{n * world} inputs" + (f" sharded over {world} GPUs"
-                                                        if world > 1 else ""),
-                   "seed": seed, "inputs_per_gpu": n, "global_inputs": n * world,
-                   "raw_pcs_per_gpu": total,
-                   "canonical_pcs_per_gpu": canon_pcs, "pc_space": 1 << args.log2_space,
-                   "len_mean": args.mean, "len_sigma": args.sigma,
-                   "keys": (f"dense keys of the registered PC universe: (pc >> {eng.kshift}) - "
-                            f"{eng.kbase:#x}, {eng.span} keys" if eng.key_mode
-                            else f"window offsets pc - {lo:#x}, {span} keys"),
-                   "parallelism": f"shard-by-input x{world}"},
+        "value": total * world * steps / dt, "ms_per_step": dt / steps * 1e3,
+        "inputs_per_gpu": n, "raw_pcs_per_gpu": total, "canonical_pcs_per_gpu": canon_pcs,
+        "keys": (f"dense keys of the registered PC universe: (pc >> {eng.kshift}) - "
+                 f"{eng.kbase:#x}, {eng.span} keys" if eng.key_mode
+                 else f"window offsets pc - {lo:#x}, {span} keys"),
         "phases_ms": {k: round(v, 4) for k, v in ph.items()},
         "results": {"kept": res.n_kept, "union": res.n_union, "max_cover": res.max_cover,
                     "n_ids": res.n_ids},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None,
+                     "traffic_source": tsrc,
                      "alg_bytes_per_launch": alg[dom]},
         # the Minimize phase's own roofline (the metric's Minimize + Union part)
         "minimize_roofline": {
-            "achieved": alg["minimize"] / (ph["minimize"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": alg["minimize"] / (ph["minimize"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "traffic": tj.get("minimize", {}).get("bytes"),
+            "achieved": mz, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": mz / HBM_PEAK_GBS,
+            "traffic": traffic_of(traffic_key, "minimize")[0] if world == 1 else None,
             "alg_bytes_per_launch": alg["minimize"]},
-        "minimize_union_pcs_per_s": canon_pcs * world / ((ph["minimize"] + ph.get("exchange", 0.0)
+        # cover.Minimize's own work (cover.go:104-131): Go's sort.Sort order, the
+        # first-cover passes, the kept list; + the union (maxCover merge)
+        "minimize_union_pcs_per_s": canon_pcs * world / ((ph["order"] + ph["minimize"]
+                                                          + ph.get("exchange", 0.0)
                                                           + ph["finish"]) * 1e-3),
     }
+    eng.close()
+    del eng, off, raw
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_corpus(args):
+    """The headline: config C3 (10M inputs, seed 0x5EED0003) at EVERY N — the
+    whole corpus on one GPU at N=1, sharded by input over the ranks at N>1
+    (total work fixed: strong scaling).  N=1 adds config C2 (1M inputs, the
+    one-GPU config of BASELINE.json) as the `c2` sub-record, the drop-in legs
+    and the CPU baseline."""
+    world, rank, dev = init_dist()
+    glob = args.global_inputs or C3_INPUTS
+    cname, seed, workload = corpus_workload(glob)
+    if args.seed is not None:
+        seed = args.seed
+    m = corpus_run(args, world, rank, dev, glob, seed, args.steps, args.warmup, cname)
+    out = {
+        "metric": "input-PCs processed/sec for Canonicalize+Minimize+Union (maxCover merge)",
+        "value": m.pop("value"), "unit": "input-PCs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": m.pop("ms_per_step"),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic (counter-based generator, SURVEY §8d)",
+        "config": {"workload": workload, "seed": seed, "global_inputs": glob,
+                   "inputs_per_gpu": m.pop("inputs_per_gpu"),
+                   "raw_pcs_per_gpu": m.pop("raw_pcs_per_gpu"),
+                   "canonical_pcs_per_gpu": m.pop("canonical_pcs_per_gpu"),
+                   "pc_space": 1 << args.log2_space, "len_mean": args.mean,
+                   "len_sigma": args.sigma, "keys": m.pop("keys"),
+                   "canon": "out of place",
+                   "parallelism": f"shard-by-input x{world}"},
+    }
+    out.update(m)
     if world == 1:
         rates = stream_peak(dev)
         pk = max(rates.values())
         out["roofline"]["peak_measured"] = pk
         out["roofline"]["peak_measured_forms"] = rates
         out["roofline"]["peak_guide_float4_copy"] = 6290.0  # MI355X_MICROARCH.md:36
-        out["roofline"]["frac_of_measured"] = achieved / pk
-    if world == 1 and glob is None:
-        eng.close()
-        del eng, off, raw
-        torch.cuda.empty_cache()
-        if not args.no_c3:
-            out["c3_single_gpu"] = c3_single(args, dev)
+        out["roofline"]["frac_of_measured"] = out["roofline"]["achieved"] / pk
+        if not args.no_c2 and glob != C2_INPUTS:
+            c2 = corpus_run(args, 1, 0, dev, C2_INPUTS, SEED, max(args.steps, 10), args.warmup,
+                            "C2")
+            c2["workload"] = corpus_workload(C2_INPUTS)[2] + " (one GPU, BASELINE configs[1])"
+            c2["seed"] = SEED
+            out["c2"] = c2
         if not args.no_dropin:
             out["dropin"] = dropin_legs(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         cb = out["cpu_baseline"] = cpu_baseline(args)
-        out["vs_cpu"] = value / cb["value"]
+        out["vs_cpu"] = out["value"] / cb["value"]
+        # like with like: both rates count Go's sort.Sort order, the Minimize
+        # passes and the union over canonical PCs
         out["vs_cpu_minimize_union"] = (out["minimize_union_pcs_per_s"]
-                                        / cb["minimize_canonical_pcs_per_s"])
+                                        / cb["minimize_union_canonical_pcs_per_s"])
     return rank, world, out
-
-
-def c3_single(args, dev):
-    """C3 (10M inputs, seed 0x5EED0003, 20.5 G raw PCs = 82 GB) on ONE GPU,
-    canonicalized out of place (82 + 81 GB): the same-workload anchor of the
-    driver's 1 -> 8 GPU strong-scaling curve (N > 1 runs C3 sharded)."""
-    import torch
-    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
-    n = C3_INPUTS
-    lo, span = synth_window(args.log2_space)
-    off, raw, lens, total = synth_corpus(n, SEED_C3, mean=args.mean, sigma=args.sigma,
-                                         log2_space=args.log2_space, device=dev)
-    univ = None if args.no_universe else synth_universe(args.log2_space, SEED_C3, device=dev)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, device=dev, universe=univ)
-    del univ, lens
-    eng.step(off, raw, n)  # warmup
-    torch.cuda.synchronize()
-    steps = 10  # ~0.9 s: the strong-scaling anchor wants more than a 3-step sample
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(eng.PHASES) + 1)]
-          for _ in range(steps)]
-    t0 = time.perf_counter()
-    for k in range(steps):
-        eng.step(off, raw, n, sync=False, ev=ev[k])
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    res = eng.result()
-    ph = {p: round(sum(e[i].elapsed_time(e[i + 1]) for e in ev) / steps, 3)
-          for i, p in enumerate(eng.PHASES)}
-    out = {"workload": f"C3: {n} inputs on one GPU (seed {SEED_C3:#x}), out-of-place canon",
-           "ms_per_step": dt * 1e3, "value": total / dt, "unit": "input-PCs/s", "steps": steps,
-           "step_ms_min_max": [round(min(e[0].elapsed_time(e[-1]) for e in ev), 3),
-                               round(max(e[0].elapsed_time(e[-1]) for e in ev), 3)],
-           "raw_pcs": total, "phases_ms": ph,
-           "results": {"kept": res.n_kept, "union": res.n_union}}
-    eng.close()
-    del eng, off, raw
-    torch.cuda.empty_cache()
-    return out
 
 
 def dropin_legs(args, dev):
@@ -443,7 +452,7 @@ def dropin_legs(args, dev):
     from syzkaller_amd.engine import synth_corpus, synth_universe
     L = _lib.lib()
     legs = {}
-    for name, n, seed in (("C1", 10_000, SEED_C1), ("C2", args.inputs, SEED)):
+    for name, n, seed in (("C1", 10_000, SEED_C1), ("C2", C2_INPUTS, SEED)):
         off, raw, lens, total = synth_corpus(n, seed, mean=args.mean, sigma=args.sigma,
                                              log2_space=args.log2_space, device=dev)
         h_off = off.cpu().numpy().astype(np.uint64)
@@ -695,12 +704,9 @@ def bench_newcov(args):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "alg_bytes_per_launch": timed_pcs // args.steps * 4},
     }
-    if os.path.exists(TRAFFIC_JSON) and world == 1:
-        with open(TRAFFIC_JSON) as f:
-            tb = json.load(f).get("newcov", {}).get("bytes")
-        if tb:  # per timed batch of this same command's shape (tools/profile_r04.sh)
-            out["roofline"]["traffic"] = tb
-            out["roofline"]["traffic_source"] = os.path.relpath(TRAFFIC_JSON, ROOT)
+    if world == 1 and args.history == 512:  # per timed batch of this command's shape
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_of("newcov",
+                                                                                   "newcov")
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, 2000, nrec))
     st.close()
@@ -790,6 +796,8 @@ def bench_dedup(args):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "alg_bytes_per_launch": alg},
     }
+    if world == 1:  # per timed batch of this command's shape
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_of("dedup", "dedup")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_dedup(sample)
     return rank, world, out

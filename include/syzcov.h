@@ -328,10 +328,11 @@ int64_t syzcov_parse_exec_output(const uint8_t *out, size_t out_len, size_t ncal
  *   key mode:    MIN all-reduce FIRST (int32 x span) -> pass2
  *   window mode: all-gather + OR COVERED (bitmap_op) -> n_ids = dense_first
  *                -> MIN all-reduce FIRST_DENSE[:n_ids] -> pass2
- *   -> MAX all-reduce KEPT[:N + 1] (u8): pass2 puts this shard's SYZCOV_ERR_*
- *      flags in KEPT[N] and finish ORs the merged byte into the step's flags,
- *      so every rank fails a step any shard flagged (its aliased first covers
- *      went into the MIN merge)
+ *   -> MAX all-reduce KEPT[:N + 4] (u8): pass2 puts this shard's SYZCOV_ERR_*
+ *      flags in KEPT[N..N+3], one byte per flag bit (so the MAX is the OR of
+ *      each bit), and finish ORs them into the step's flags, so every rank
+ *      fails a step any shard flagged, with the same flags (its aliased first
+ *      covers went into the MIN merge)
  *   -> finish -> result.
  * A step abandoned between minimize(do_pass2 = 0) and pass2 is cleaned up by
  * the next canon (FIRST refilled).  canon_in_place: the canonical key words
@@ -368,8 +369,12 @@ typedef struct syzcov_corpus_res {
     const int32_t *kept_idx;   /* device: kept input indices, processing order */
     const uint32_t *union_pcs; /* device: the sorted union */
     uint32_t fallback;   /* 1: the step saw a PC outside the key space (err_flags says
-                            which) and was recomputed in window mode; results exact */
-    uint32_t reserved_;
+                            which) and was recomputed in window mode; kept list and
+                            union exact */
+    uint32_t max_cover_missed; /* fallback: union PCs the resident maxCover cannot
+                            represent (key mode: not the universe PC of their key;
+                            window mode: outside the window) and so did not take; the
+                            reference's maxCover would hold them (0: maxCover exact) */
 } syzcov_corpus_res;
 /* buffers of the layout (syzcov_corpus_buffer: byte offset in the block, size) */
 enum {
@@ -383,7 +388,7 @@ enum {
     SYZCOV_CORPUS_FIRST,       /* i32 [span] first-cover ranks (INT32_MAX between steps) */
     SYZCOV_CORPUS_REC,         /* u64 [rec_cap] first-cover records */
     SYZCOV_CORPUS_CAND,        /* u8  [n_max + 1] */
-    SYZCOV_CORPUS_KEPT,        /* u8  [n_global + 1] kept flag per global rank */
+    SYZCOV_CORPUS_KEPT,        /* u8  [n_global + 4] kept flag per global rank, + 4 error-flag bytes */
     SYZCOV_CORPUS_LENS,        /* i64 [n_global + 1] */
     SYZCOV_CORPUS_ORDER,       /* i32 [n_global + 1] Go's processing order */
     SYZCOV_CORPUS_KEPT_IDX,    /* i32 [n_global + 1] kept inputs, processing order */

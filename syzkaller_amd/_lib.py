@@ -220,7 +220,7 @@ class CorpusRes(C.Structure):
     """syzcov_corpus_res."""
     _fields_ = [("err_flags", u32), ("n_ids", u32), ("n_kept", u32), ("n_union", u32),
                 ("max_cover", u64), ("records", u64), ("kept_idx", p_), ("union_pcs", p_),
-                ("fallback", u32), ("reserved_", u32)]
+                ("fallback", u32), ("max_cover_missed", u32)]
 
 
 # enum of syzcov_corpus_buffer (include/syzcov.h)

@@ -73,14 +73,19 @@ __global__ void corpus_clear_bit_kernel(uint32_t *covered, uint32_t bit) {
     covered[bit >> 5] &= ~(1u << (bit & 31));
 }
 
-// sharded: this shard's error flags ride in the spare kept byte through the
-// kept MAX all-reduce; finish ORs the merged byte back (every rank fails a step
-// any shard flagged: its aliased first covers went into the MIN merge)
+// sharded: this shard's error flags ride in the spare kept bytes through the
+// kept MAX all-reduce, ONE BYTE PER FLAG BIT (kept[N + b] = bit b), so the
+// MAX of each byte is the OR of that bit over the shards; finish ORs them back
+// (every rank fails a step any shard flagged, with the same flags: its aliased
+// first covers went into the MIN merge)
+constexpr uint32_t kErrBytes = 4;  // SYZCOV_ERR_WINDOW .. SYZCOV_ERR_ORDER
 __global__ void corpus_err_to_kept_kernel(const uint32_t *err, uint8_t *kept_n) {
-    *kept_n = (uint8_t)(*err > 255u ? 255u : *err);
+    for (uint32_t b = 0; b < kErrBytes; b++) kept_n[b] = (uint8_t)((*err >> b) & 1u);
 }
 __global__ void corpus_err_from_kept_kernel(uint32_t *err, const uint8_t *kept_n) {
-    *err |= *kept_n;
+    uint32_t e = 0;
+    for (uint32_t b = 0; b < kErrBytes; b++) e |= (kept_n[b] ? 1u : 0u) << b;
+    *err |= e;
 }
 
 // maxCover |= covered, unless the step saw a PC outside the key space (its
@@ -107,19 +112,29 @@ __global__ __launch_bounds__(256) void corpus_merge_kernel(uint32_t *__restrict_
 __global__ void corpus_merge_pcs_kernel(const uint32_t *__restrict__ pcs, uint32_t n,
                                         const uint32_t *__restrict__ pc_of_key, uint32_t kshift,
                                         uint32_t kbase, uint32_t lo, uint64_t span,
-                                        uint32_t *__restrict__ maxc) {
+                                        uint32_t *__restrict__ maxc,
+                                        unsigned long long *missed) {
+    uint32_t miss = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t pc = pcs[i];
         uint64_t b;
         if (pc_of_key) {
             b = (uint64_t)(pc >> kshift) - kbase;
-            if ((pc >> kshift) < kbase || b >= span || pc_of_key[b] != pc) continue;
+            if ((pc >> kshift) < kbase || b >= span || pc_of_key[b] != pc) {
+                miss++;
+                continue;
+            }
         } else {
             b = (uint64_t)pc - lo;
-            if (pc < lo || b >= span) continue;
+            if (pc < lo || b >= span) {
+                miss++;
+                continue;
+            }
         }
         atomicOr(&maxc[b >> 5], 1u << (b & 31));
     }
+    for (int d = 32; d >= 1; d >>= 1) miss += __shfl_xor(miss, d, 64);
+    if (__lane_id() == 0 && miss) atomicAdd(missed, (unsigned long long)miss);
 }
 
 __global__ __launch_bounds__(256) void corpus_popcount_kernel(const uint32_t *__restrict__ w,
@@ -163,6 +178,7 @@ struct Corpus {
     const uint32_t *raw_in = nullptr;  // the step's raw PCs when canon is out of place
     bool allow_fallback = true;     // a PC outside the key space: window-mode recompute
     bool order_given = false;       // the step's order came from the caller (ORDER)
+    bool order_lens_given = false;  // ... or was sorted over the caller's lengths
     uint32_t *fb_union = nullptr;   // a fallback union larger than UNION (grow-only)
     size_t fb_union_cap = 0;
     bool fb_union_used = false;     // this step's union lives in fb_union
@@ -214,7 +230,7 @@ static int64_t plan(Corpus &c) {
     sz[SYZCOV_CORPUS_FIRST] = c.span * 4;
     sz[SYZCOV_CORPUS_REC] = g.rec_cap * 8;
     sz[SYZCOV_CORPUS_CAND] = n + 1;
-    sz[SYZCOV_CORPUS_KEPT] = N + 1;
+    sz[SYZCOV_CORPUS_KEPT] = N + kErrBytes;
     sz[SYZCOV_CORPUS_LENS] = (N + 1) * 8;
     sz[SYZCOV_CORPUS_ORDER] = (N + 1) * 4;
     sz[SYZCOV_CORPUS_KEPT_IDX] = (N + 1) * 4;
@@ -344,9 +360,10 @@ static Corpus *get(syzcov_corpus h) { return reinterpret_cast<Corpus *>(h); }
 
 // Scalars (u64 words of SCAL): 0 err flags (u32), 1 n_ids (u32), 2 n_kept
 // (u32), 3 n_union (u32), 4 |maxCover| (u64), 5 / 6 local ranks / items
-// (u32), 7 record count (u64).
+// (u32), 7 record count (u64), 10 fallback min/max PC (2 x u32), 11 fallback
+// union PCs maxCover cannot represent (u64).
 enum { SC_ERR = 0, SC_NIDS = 1, SC_NKEPT = 2, SC_NUNION = 3, SC_MAXCOV = 4, SC_CR = 5,
-       SC_CI = 6, SC_REC = 7 };
+       SC_CI = 6, SC_REC = 7, SC_MM = 10, SC_MISSED = 11 };
 
 // SCAL[0] bit: the step was recomputed by corpus_fallback (results valid)
 constexpr uint32_t kErrRecomputed = 1u << 31;
@@ -408,6 +425,7 @@ static int ph_order_given(Corpus &c, const int32_t *order, size_t N, hipStream_t
     int rc = order_begin(c, c.shard, N, s);
     if (rc) return rc;
     c.order_given = true;
+    c.order_lens_given = false;
     hipLaunchKernelGGL(corpus_order_copy_kernel, dim3(grid_for(N, 256, 8192)), dim3(256), 0, s,
                        order, (uint64_t)N, c.buf<int32_t>(SYZCOV_CORPUS_ORDER),
                        (uint32_t *)(scal(c) + SC_ERR));
@@ -426,6 +444,7 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s, u
     int rc = order_begin(c, lens32 != nullptr, N, s);
     if (rc) return rc;
     c.order_given = false;
+    c.order_lens_given = lens32 != nullptr && !c.shard;
     int64_t *lens = c.buf<int64_t>(SYZCOV_CORPUS_LENS);
     const uint32_t *l32 = lens32 ? (const uint32_t *)lens32
                                  : (c.cfg.order_by ? nullptr
@@ -640,14 +659,17 @@ int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *mm, hipStream_t s);
 // buffers; maxCover takes the union's PCs it can represent.  `order`: the
 // step's own order when the caller gave it, else canonical / raw lengths as cfg.
 static int corpus_fallback(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
-    const int32_t *order = c.order_given ? c.buf<int32_t>(SYZCOV_CORPUS_ORDER) : nullptr;
+    // the caller's order, or the order the step computed over the caller's
+    // lengths (Go's sort over them, exact): either way the step's ORDER
+    const int32_t *order =
+        c.order_given || c.order_lens_given ? c.buf<int32_t>(SYZCOV_CORPUS_ORDER) : nullptr;
     if (c.shard || !c.raw_in || !c.off || !c.n || !c.allow_fallback) return 1;
     uint64_t ends[2];
     SYZ_HIP(hipMemcpyAsync(&ends[0], c.off, 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipMemcpyAsync(&ends[1], c.off + c.n, 8, hipMemcpyDeviceToHost, s));
     SYZ_HIP(hipStreamSynchronize(s));
     if (ends[1] <= ends[0]) return 1;
-    uint32_t *mm = (uint32_t *)(scal(c) + 10);  // spare scalar words
+    uint32_t *mm = (uint32_t *)(scal(c) + SC_MM);
     int rc = minmax_pcs(c.raw_in + ends[0], ends[1] - ends[0], mm, s);
     if (rc) return rc;
     uint32_t hm[2];
@@ -700,19 +722,23 @@ static int corpus_fallback(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
         if (!rc) {  // maxCover |= the union's representable PCs
             uint64_t *sc = scal(c);
             uint32_t *maxc = c.buf<uint32_t>(SYZCOV_CORPUS_MAX_COVER);
+            SYZ_HIP(hipMemsetAsync(sc + SC_MISSED, 0, 8, s));
             if (rw.n_union)
                 hipLaunchKernelGGL(corpus_merge_pcs_kernel, dim3(grid_for(rw.n_union, 256, 1024)),
                                    dim3(256), 0, s, (const uint32_t *)un, rw.n_union,
                                    c.key_mode ? c.buf<uint32_t>(SYZCOV_CORPUS_PC_OF_KEY) : nullptr,
-                                   c.kshift, c.kbase, c.pc_lo, c.span, maxc);
+                                   c.kshift, c.kbase, c.pc_lo, c.span, maxc,
+                                   (unsigned long long *)(sc + SC_MISSED));
             SYZ_HIP(hipMemsetAsync(sc + SC_MAXCOV, 0, 8, s));
             hipLaunchKernelGGL(corpus_popcount_kernel, dim3(grid_for(c.nwords, 256, 1024)),
                                dim3(256), 0, s, (const uint32_t *)maxc, (uint64_t)c.nwords,
                                (unsigned long long *)(sc + SC_MAXCOV));
             SYZ_LAUNCH_CHECK();
-            uint64_t mc = 0;
+            uint64_t mc = 0, missed = 0;
             SYZ_HIP(hipMemcpyAsync(&mc, sc + SC_MAXCOV, 8, hipMemcpyDeviceToHost, s));
+            SYZ_HIP(hipMemcpyAsync(&missed, sc + SC_MISSED, 8, hipMemcpyDeviceToHost, s));
             SYZ_HIP(hipStreamSynchronize(s));
+            r->max_cover_missed = (uint32_t)std::min<uint64_t>(missed, 0xFFFFFFFFu);
             r->n_ids = rw.n_ids;
             r->n_kept = rw.n_kept;
             r->n_union = rw.n_union;
@@ -753,9 +779,11 @@ static int ph_result(Corpus &c, syzcov_corpus_res *r, hipStream_t s) {
     r->kept_idx = c.buf<int32_t>(SYZCOV_CORPUS_KEPT_IDX);
     r->union_pcs = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);
     r->fallback = 0;
+    r->max_cover_missed = 0;
     if (err & kErrRecomputed) {  // corpus_fallback already ran for this step
         r->err_flags = err & ~kErrRecomputed;
         r->fallback = 1;
+        r->max_cover_missed = (uint32_t)std::min<uint64_t>(h[SC_MISSED], 0xFFFFFFFFu);
         if (c.fb_union_used) r->union_pcs = c.fb_union;
         return 0;
     }
@@ -1176,6 +1204,9 @@ static int dropin_handle(DropinCache &dc, size_t n, uint64_t P, size_t max_len, 
     if (nrange_of(nhi - nlo + 1, kRangeShiftWindow) > 256) {
         nlo = lo & ~((1ull << kRangeShiftWindow) - 1);
         nhi = hi;
+        // aligning lo down can add a 257th range to an extent just under
+        // 2^28 PCs: then the exact extent (which the caller checked fits)
+        if (nrange_of(nhi - nlo + 1, kRangeShiftWindow) > 256) nlo = lo;
     }
     nhi = std::min<uint64_t>(0xFFFFFFFFull, nhi);
     syzcov_corpus_cfg cfg{};
@@ -1194,9 +1225,9 @@ static int dropin_handle(DropinCache &dc, size_t n, uint64_t P, size_t max_len, 
         cfg.p_max = P;
         rc = syzcov_corpus_create(&cfg, nullptr, 0, &dc.h);
     }
-    if (rc) {
+    if (rc) {  // short of memory or a window the engine cannot take: the dictionary path
         dc.h = 0;
-        return rc == SYZCOV_ENOMEM ? 0 : rc;
+        return rc == SYZCOV_ENOMEM || rc == SYZCOV_ERANGE ? 0 : rc;
     }
     dc.n_cap = cfg.n_max;
     dc.p_cap = cfg.p_max;

@@ -170,11 +170,12 @@ class ShardedEngine(CorpusEngine):
             n_ids = check(L.syzcov_corpus_dense_first(h, s), "corpus_dense_first")
             merge_first(self.first_dense[:n_ids])                   # RCCL int32 MIN
         check(L.syzcov_corpus_pass2(h, s), "corpus_pass2")          # kept against the global first
-        # RCCL uint8 MAX of kept flags by global rank; kept[N] carries the
-        # shard's error flags (pass 2 wrote them, finish ORs the merged byte
-        # back: a shard that saw a non-universe PC fed its aliased first covers
-        # into the MIN merge, so every rank fails the step)
-        merge_kept(self.kept[:N + 1])
+        # RCCL uint8 MAX of kept flags by global rank; kept[N..N+3] carry the
+        # shard's error flags, one byte per flag bit (pass 2 wrote them, finish
+        # ORs the merged bytes back: a shard that saw a non-universe PC fed its
+        # aliased first covers into the MIN merge, so every rank fails the step
+        # with the same flags)
+        merge_kept(self.kept[:N + 4])
         mark_ev()
         self.finish()
         mark_ev()

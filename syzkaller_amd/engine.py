@@ -55,6 +55,7 @@ class StepResult:
     max_cover: int              # |maxCover| after the merge
     fallback: bool = False      # a PC outside the key space: recomputed in window mode
     err_flags: int = 0          # SYZCOV_ERR_* bits the step saw (with fallback: why)
+    max_cover_missed: int = 0   # fallback: union PCs maxCover cannot represent (not taken)
 
 
 _DT = {"CANON": torch.int32, "NEW_LEN": torch.int32, "SPLIT": torch.int32,
@@ -198,6 +199,7 @@ class CorpusEngine:
         rc = self.L.syzcov_corpus_result(self.h, C.byref(r), _stream())
         if rc < 0:
             msg = self.L.syzcov_last_error().decode(errors="replace")
+            msg += f" [err_flags {r.err_flags:#x}]"
             if r.err_flags & SYZCOV_ERR_UNIVERSE:
                 msg += (" (key mode would alias it with a universe PC; keys.hip; the window-mode "
                         "recompute needs the raw PCs: canon in place or sharded cannot)")
@@ -211,7 +213,8 @@ class CorpusEngine:
                                                 _stream()), "dev_stream_copy")
             union = union[:r.n_union]
         return StepResult(self.kept_idx[:r.n_kept], r.n_kept, union, r.n_union,
-                          r.n_ids, r.max_cover, bool(r.fallback), r.err_flags)
+                          r.n_ids, r.max_cover, bool(r.fallback), r.err_flags,
+                          r.max_cover_missed)
 
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """The canonical covers as PCs, in the CSR slots of `off` (key mode:

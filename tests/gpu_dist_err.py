@@ -2,7 +2,9 @@
 two key-mode ranks share cuda:0 (gloo collectives staged through the host).
 (1) Rank 1's shard holds one PC that is not in the universe: its aliased
 first covers go into the MIN merge, so EVERY rank's step must fail, not only
-rank 1's (the error byte rides in KEPT[N] through the kept MAX merge).
+rank 1's (the error bits ride in KEPT[N..N+3] through the kept MAX merge,
+one byte per bit); rank 0's out-of-extent PC adds SYZCOV_ERR_WINDOW, and every
+rank must report both flags.
 (2) A step abandoned after pass 1 (no exchange, no pass 2) leaves its first
 ranks in FIRST: the next step must still give the clean results.
 Each rank prints OK."""
@@ -42,11 +44,15 @@ def worker(rank, world, port):
         stray = next(int(uh[t]) + d for t in range(i, uh.size) for d in (1, 2, 3, 5)
                      if int(uh[t]) + d not in us)
         raw[j] = np.int32(np.uint32(stray))
+    # ... and a PC outside the universe's extent on rank 0 (SYZCOV_ERR_WINDOW):
+    # every rank must see both flags, OR-merged (one kept byte per flag bit)
+    if rank == 0:
+        raw[int(off[n // 3].item()) + 1] = np.int32(np.uint32(int(uh[-1]) + (1 << 12)))
     try:
         eng.step(off, raw, n)
         raise AssertionError(f"rank {rank}: a shard's non-universe PC did not fail the step")
     except RuntimeError as e:
-        assert "universe" in str(e), (rank, str(e))
+        assert "[err_flags 0x5]" in str(e), (rank, str(e))  # WINDOW | UNIVERSE on every rank
     # (2) abandon a step after pass 1, then a full step on the clean corpus
     off, raw, lens, total = corpus()
     eng.canonicalize(off, raw, n)

@@ -48,3 +48,32 @@ def test_failing_ranks_end_the_run():
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_same_workload_at_every_n(monkeypatch):
+    """The driver builds its 1 -> 8 curve from `value` at each N: the N=1 line
+    must name the same workload (C3, 10M inputs) as the N>1 lines."""
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    def fake_run(args, world, rank, dev, glob, seed, steps, warmup, key):
+        seen.update(glob=glob, seed=seed, key=key)
+        return {"value": 1.0, "ms_per_step": 1.0, "inputs_per_gpu": glob, "raw_pcs_per_gpu": 0,
+                "canonical_pcs_per_gpu": 0, "keys": "", "phases_ms": {},
+                "roofline": {"achieved": 1.0}, "minimize_union_pcs_per_s": 1.0}
+    monkeypatch.setattr(bench, "init_dist", lambda: (1, 0, None))
+    monkeypatch.setattr(bench, "corpus_run", fake_run)
+    monkeypatch.setattr(bench, "stream_peak", lambda dev: {"flat_float4": 1.0})
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--no-c2", "--no-dropin", "--no-cpu"])
+    _, _, one = bench.bench_corpus(bench.parse())
+    assert seen == {"glob": bench.C3_INPUTS, "seed": bench.SEED_C3, "key": "C3"}
+    lines = {}
+    for n in (1, 2):
+        r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run"],
+                           capture_output=True, text=True, timeout=120, env=_env())
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[n] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert one["config"]["workload"] == lines[1]["config"]["workload"] \
+        == lines[2]["config"]["workload"], (one["config"], lines)
+    assert one["config"]["workload"].startswith("C3: ") and one["scaling"] == "strong"

@@ -219,3 +219,23 @@ def test_corpus_handle_errors(L):
             assert k1 == k0 and kept1.tolist() == kept0.tolist()
         finally:
             L.syzcov_corpus_destroy(h)
+
+
+def test_dropin_minimize_unaligned_wide_extent(L):
+    """cover.Minimize through the drop-in on >= 1024 inputs (the cached-engine
+    route) whose PC extent is just under 2^28 PCs and starts off a 2^20-PC
+    boundary: aligning the window down would need 257 ranges, so the engine
+    takes the exact extent (or the dictionary path) and the call never fails."""
+    rng = np.random.default_rng(9)
+    lo = 0x10000000 + (1 << 19) + 5
+    hi = lo + (1 << 28) - (1 << 19) - 1
+    n = 1100
+    lens = rng.integers(1, 300, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    pcs = rng.integers(lo, hi + 1, int(off[-1]), dtype=np.uint64).astype(np.uint32)
+    pcs[0], pcs[-1] = lo, hi  # the extent's two ends
+    out = np.empty(n, np.int32)
+    k = L.syzcov_minimize(off.ctypes.data, pcs.ctypes.data, n, None, 0, out.ctypes.data)
+    assert k >= 0, L.syzcov_last_error()
+    assert out[:k].tolist() == list(orc.minimize_csr(off, pcs))

@@ -297,6 +297,7 @@ def test_engine_key_mode_nonuniverse(torch, force, in_place, monkeypatch):
         assert res.kept_idx.cpu().numpy().tolist() == exp_kept, where
         assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union), where
         assert res.max_cover == mc0  # the stray PC has no key of its own
+        assert res.max_cover_missed == 1  # ... and maxCover says it did not take it
         res2 = eng.result()  # a second read returns the recomputed step
         assert res2.fallback and res2.n_kept == res.n_kept
         res3 = eng.step(off, raw, n)  # and the next step recomputes again
@@ -326,6 +327,7 @@ def test_engine_key_mode_fallback_outside_extent(torch):
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
     univ_in_union = np.intersect1d(exp_union, uh).size
     assert res.max_cover == univ_in_union
+    assert res.max_cover_missed == exp_union.size - univ_in_union == 3
     # host form, canon in place inside the handle, with a caller order
     L = _lib.lib()
     h_off = off.cpu().numpy().astype(np.uint64)
@@ -351,6 +353,40 @@ def test_engine_key_mode_fallback_outside_extent(torch):
     L.syzcov_corpus_destroy(h.value)
     assert out[:k].tolist() == exp_p
     assert np.array_equal(un[:nu.value], exp_union)
+
+
+def test_engine_key_mode_fallback_keeps_caller_lens_order(torch):
+    """A step ordered by CALLER lengths (syzcov_corpus_order with lens) whose
+    corpus holds a non-universe PC: the window-mode recompute must process the
+    inputs in the order sorted over those lengths, not the handle's own."""
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 1200, 15, 0x5EED0002
+    u = synth_universe(log2, seed)
+    uh = u.cpu().numpy().view(np.uint32)
+    lo, span = synth_window(log2)
+    off, raw, lens, total = synth_corpus(n, seed, mean=700, sigma=300, log2_space=log2)
+    j = int(off[500].item()) + 2
+    raw[j] = np.int32(np.uint32(_stray(uh, int(np.searchsorted(uh, int(raw[j].item()) & 0xFFFFFFFF)))))
+    # caller lengths unrelated to the covers: Go's sort over them decides the order
+    clens = np.random.default_rng(11).integers(1, 50, n).astype(np.int32)
+    order = orc.sort_order(clens.astype(np.int64))
+    o_off = off.cpu().numpy().astype(np.uint64)
+    o_pcs = raw[:total].cpu().numpy().view(np.uint32)
+    c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
+    seen, exp = set(), []
+    for i in order:
+        cov = c_pcs[c_off[i]:c_off[i + 1]]
+        if any(int(p) not in seen for p in cov):
+            exp.append(int(i))
+        seen.update(int(p) for p in cov)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u)
+    eng.canonicalize(off, raw, n)
+    eng.sort_order(torch.from_numpy(clens).cuda(), n)
+    eng.minimize(True)
+    eng.finish()
+    res = eng.result()
+    assert res.fallback and res.err_flags & 4
+    assert res.kept_idx.cpu().numpy().tolist() == exp
 
 
 def test_engine_key_mode_gap_key(torch):

@@ -1,0 +1,69 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench lines (run on the GPU box from the repo root):
+#   corpus C3 (the headline) and C2 (the sub-record): kernel trace + stats, and
+#     FETCH_SIZE / WRITE_SIZE passes over one step -> per-phase HBM bytes
+#   canon wave counters (tools/kbench.py step --keys, one C2 step)
+#   newcov C5 (steady state) and dedup: trace + stats, FETCH / WRITE of the
+#     timed batches only;  prio C4: trace + stats
+#   -> OUT/traffic.json {"C3": phases, "C2": phases, "newcov": ..., "dedup": ...}
+# Counters are never combined with tracing; each pass is its own run within the
+# per-block limits (MI355X_MICROARCH.md, HBM / rocprofv3).
+#   usage: tools/profile.sh OUT [parts: corpus canon newcov dedup prio]
+set -o pipefail
+export TMPDIR=/tmp
+o=${1:-gpurun_out/prof}; shift
+parts=${*:-corpus canon newcov dedup prio}
+mkdir -p $o
+B="python3 bench.py --no-cpu --no-c2 --no-dropin"
+has() { case " $parts " in *" $1 "*) return 0;; esac; return 1; }
+pmc_pair() {  # name, step kernel ("" = bin_kernel), last-N ("" = all steps), bench args...
+  local name=$1 sk=$2 last=$3; shift 3
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/${name}_fetch -o run -- "$@" > $o/${name}_f.log 2>&1 || { tail -5 $o/${name}_f.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/${name}_write -o run -- "$@" > $o/${name}_w.log 2>&1 || { tail -5 $o/${name}_w.log; exit 1; }
+  python3 tools/traffic.py $o/${name}_fetch $o/${name}_write $o/traffic_${name}.json $sk $last > /dev/null && cat $o/traffic_${name}.json
+}
+trace() {  # name, bench args...
+  local name=$1; shift
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $o/${name}_trace -o run -- "$@" > $o/${name}_trace.log 2>&1 || { tail -20 $o/${name}_trace.log; exit 1; }
+  python3 tools/trace_summary.py $o/${name}_trace > $o/${name}_summary.txt && head -16 $o/${name}_summary.txt
+}
+if has corpus; then
+  trace C3 $B --steps 5 --warmup 2
+  pmc_pair C3 "" "" $B --steps 1 --warmup 0
+  trace C2 $B --global-inputs 1000000 --steps 10 --warmup 2
+  pmc_pair C2 "" "" $B --global-inputs 1000000 --steps 1 --warmup 0
+fi
+if has canon; then
+  i=0
+  for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" \
+             "SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_COUNT"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d $o/pmc$i -o run -- python3 tools/kbench.py step --keys --reps 1 > $o/pmc$i.log 2>&1 || { tail -3 $o/pmc$i.log; echo "pmc pass $i failed"; exit 1; }
+  done
+  python3 tools/pmc_summary.py $o > $o/pmc_summary.txt 2>&1; grep -A18 "canon_key_kernel<32" $o/pmc_summary.txt | head -20
+fi
+if has newcov; then
+  N="$B --workload newcov --steps 10 --warmup 3"
+  trace newcov $N
+  pmc_pair newcov newcov_own_kernel 10 $N
+fi
+if has dedup; then
+  D="$B --workload dedup --steps 10 --warmup 3"
+  trace dedup $D
+  pmc_pair dedup "narrow_kernel<4>" 10 $D
+fi
+if has prio; then
+  trace prio $B --workload prio --steps 10 --warmup 3
+fi
+python3 - $o <<'PY'
+import glob, json, os, sys
+o = sys.argv[1]
+out = {}
+for f in sorted(glob.glob(os.path.join(o, "traffic_*.json"))):
+    out[os.path.basename(f)[8:-5]] = json.load(open(f))
+out["_source"] = ("rocprofv3 --pmc FETCH_SIZE (x2, MI355X_MICROARCH.md) / WRITE_SIZE passes over "
+                  "bench.py (C3 / C2: one step; newcov / dedup: the 10 timed batches), "
+                  "tools/profile.sh -> tools/traffic.py")
+json.dump(out, open(os.path.join(o, "traffic.json"), "w"), indent=1, sort_keys=True)
+PY
+echo profile_done

@@ -26,6 +26,7 @@ PHASES = {
                "range_sum", "range_scan", "item_scan", "row_offsets", "desc_kernel", "row_fill",
                "mfl_build", "accept_or"),
     "prio": ("prio_",),
+    "dedup": ("narrow_kernel", "wide_kernel"),
     "order": ("gsort::",),
     "compact": ("compact_", "scan_blocks"),
     "union": ("dict_",),
