@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--no-universe", action="store_true",
                     help="window offsets instead of the dense keys of the registered PC "
                          "universe (keys.hip), for the corpus engine and newcov's maxCover")
+    ap.add_argument("--canon-layout", type=int, default=0, choices=[0, 1],
+                    help="canonical lists: 0 CSR slots, 1 line-aligned sub-runs "
+                         "(syzcov_corpus_cfg.canon_layout)")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group, run no workload (a check of "
                          "the --gpus N launcher; runs on a host without a GPU)")
@@ -331,9 +334,11 @@ def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key):
     univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev)
     if world > 1:
         from syzkaller_amd.dist import ShardedEngine
-        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev, universe=univ)
+        eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev, universe=univ,
+                            canon_layout=args.canon_layout)
     else:
-        eng = CorpusEngine(n, total, max_len, lo, span, device=dev, universe=univ)
+        eng = CorpusEngine(n, total, max_len, lo, span, device=dev, universe=univ,
+                           canon_layout=args.canon_layout)
     del univ
     torch.cuda.synchronize()
     phases = list(eng.PHASES)
@@ -353,6 +358,7 @@ def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key):
     out = {
         "value": total * world * steps / dt, "ms_per_step": dt / steps * 1e3,
         "inputs_per_gpu": n, "raw_pcs_per_gpu": total, "canonical_pcs_per_gpu": canon_pcs,
+        "aligned": bool(eng.canon_align_k),
         "keys": (f"dense keys of the registered PC universe: (pc >> {eng.kshift}) - "
                  f"{eng.kbase:#x}, {eng.span} keys" if eng.key_mode
                  else f"window offsets pc - {lo:#x}, {span} keys"),
@@ -404,7 +410,8 @@ def bench_corpus(args):
                    "canonical_pcs_per_gpu": m.pop("canonical_pcs_per_gpu"),
                    "pc_space": 1 << args.log2_space, "len_mean": args.mean,
                    "len_sigma": args.sigma, "keys": m.pop("keys"),
-                   "canon": "out of place",
+                   "canon": "out of place" + (", line-aligned sub-runs" if m.pop("aligned")
+                                              else ", CSR slots"),
                    "parallelism": f"shard-by-input x{world}"},
     }
     out.update(m)

@@ -351,6 +351,10 @@ typedef struct syzcov_corpus_cfg {
     int canon_in_place;  /* canonical lists overwrite the raw ones (max_seg_len <= 16384) */
     int order_by;        /* 0: canonical lengths; 1: raw lengths (Minimize of covers as given) */
     uint64_t rec_cap;    /* first-cover records (0 = default) */
+    int canon_layout;    /* 0: the canonical lists in the raw lists' CSR slots; 1 (out of
+                            place over > 1 range): line-aligned, every input's range
+                            sub-run on its own 128-B lines, so Minimize reads each line
+                            once (CANON holds p_max + 31 (nrange + 1) n_max + 32 words) */
 } syzcov_corpus_cfg;
 typedef struct syzcov_corpus_info_t {
     uint32_t key_mode, kshift, kbase, pc_lo; /* key(pc) = (pc >> kshift) - kbase */
@@ -359,6 +363,9 @@ typedef struct syzcov_corpus_info_t {
     uint64_t win_span, nrange, nwords, n_global, union_cap, rec_cap;
     void *mem;
     uint64_t mem_size;
+    uint64_t canon_align_k; /* 0: CANON in CSR slots; else the line-aligned layout's
+                               ak = 31 (nrange + 1): input i at align32(off[i] + ak i),
+                               range j's sub-run at + align32(split[i][j-1] + 31 j) */
 } syzcov_corpus_info_t;
 typedef struct syzcov_corpus_res {
     uint32_t err_flags;  /* SYZCOV_ERR_* bits of the step */
@@ -412,6 +419,10 @@ int syzcov_corpus_create(const syzcov_corpus_cfg *cfg, void *mem, size_t mem_siz
 int syzcov_corpus_destroy(syzcov_corpus h);
 int syzcov_corpus_info(syzcov_corpus h, syzcov_corpus_info_t *out);
 int syzcov_corpus_buffer(syzcov_corpus h, int which, uint64_t *offset, uint64_t *bytes);
+/* The step's canonical lists (key words in key mode) copied into the raw
+ * lists' CSR slots: out[off[i] .. off[i] + new_len[i]) (device, p_max words),
+ * whichever layout CANON holds (info.canon_align_k). */
+int syzcov_corpus_canonical(syzcov_corpus h, uint32_t *out, void *stream);
 /* Phases (device pointers, asynchronous on `stream`).  raw is written when
  * canon_in_place. */
 int syzcov_corpus_canon(syzcov_corpus h, const uint64_t *off, uint32_t *raw, size_t n,
@@ -558,6 +569,21 @@ int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *raw, uint32
                                 uint64_t pc_span, uint32_t kshift, uint32_t kbase, uint64_t nkeys,
                                 uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
                                 uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+/* Either of the two above (key mode iff key_out) writing the LINE-ALIGNED
+ * layout: every (input, range) sub-run starts on its own 128-byte line, so a
+ * Minimize pass that reads range j of an input in one workgroup and range j + 1
+ * in another never fetches a line twice.  With ak = 31 (nrange + 1), input i's
+ * words start at align32(off[i] + ak i) and range j's sub-run at
+ * + align32(split[i][j-1] + 31 j) (split[i][-1] = 0); out holds
+ * syzcov_dev_canon_aligned_words(p, nseg, nrange) words.  split is required;
+ * out must not alias raw.  Read it back with syzcov_dev_minimize_range_aligned. */
+int syzcov_dev_canon_split_aligned(const uint64_t *off, const uint32_t *raw, uint32_t *out,
+                                   uint32_t *new_len, size_t nseg, size_t max_seg_len,
+                                   uint32_t pc_lo, uint64_t pc_span, uint32_t kshift,
+                                   uint32_t kbase, uint64_t nkeys, int key_out,
+                                   uint32_t range_shift, uint32_t *split, uint64_t *range_tot,
+                                   uint32_t *err_flag, void *ws, size_t ws_size, void *stream);
+uint64_t syzcov_dev_canon_aligned_words(uint64_t p_max, uint64_t nseg, uint64_t nrange);
 /* cover_dedup (executor/executor.cc:574-587) of nseg raw u64 KCOV buffers
  * [off[s], off[s+1]) of pcs, IN PLACE: buffer s becomes its sorted distinct
  * nonzero PCs, new_len[s] of them (UINT32_MAX for a buffer longer than 2^31
@@ -643,6 +669,29 @@ int syzcov_dev_minimize_range_keys_pass2(const uint64_t *off, const uint32_t *le
                                          int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
                                          uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
                                          void *ws, void *stream);
+/* syzcov_dev_minimize_range(_keys) over canonical lists in the line-aligned
+ * layout of syzcov_dev_canon_split_aligned (key mode iff low_of_key: pc_lo = 0,
+ * pc_span = the key count, err_flag as in _keys); default chunking. */
+int syzcov_dev_minimize_range_aligned(const uint64_t *off, const uint32_t *pcs,
+                                      const uint32_t *split, const int32_t *order,
+                                      const int32_t *ranks, size_t n_items, uint32_t pc_lo,
+                                      uint64_t pc_span, uint32_t range_shift,
+                                      const uint64_t *range_tot, const uint8_t *low_of_key,
+                                      uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                                      uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand,
+                                      uint8_t *kept, int do_pass2, uint32_t *err_flag, void *ws,
+                                      void *stream);
+/* Its sharded pass 2 (key_mode: tab and first_dense NULL, as _keys_pass2;
+ * window mode: as syzcov_dev_minimize_range_pass2). */
+int syzcov_dev_minimize_range_aligned_pass2(const uint64_t *off, const uint32_t *pcs,
+                                            const uint32_t *split, const int32_t *order,
+                                            const int32_t *ranks, size_t n_items, uint32_t pc_lo,
+                                            uint64_t pc_span, uint32_t range_shift,
+                                            const uint64_t *range_tot, int key_mode,
+                                            uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                                            uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand,
+                                            const uint64_t *tab, const int32_t *first_dense,
+                                            uint8_t *kept, void *ws, void *stream);
 /* Sharded runs: call syzcov_dev_minimize_range with do_pass2 = 0 (first_w then
  * holds this shard's first ranks and covered its union), merge the shards'
  * covered bitmaps (OR) into the dictionary `tab` (syzcov_dev_dict_build_bits),

@@ -81,6 +81,16 @@ _SIGS = {
     "syzcov_corpus_destroy": (C.c_int, [u64]),
     "syzcov_corpus_info": (C.c_int, [u64, p_]),
     "syzcov_corpus_buffer": (C.c_int, [u64, C.c_int, p_, p_]),
+    "syzcov_corpus_canonical": (C.c_int, [u64, p_, p_]),
+    "syzcov_dev_canon_split_aligned": (C.c_int, [p_, p_, p_, p_, sz, sz, u32, u64, u32, u32, u64,
+                                                 C.c_int, u32, p_, p_, p_, p_, sz, p_]),
+    "syzcov_dev_canon_aligned_words": (u64, [u64, u64, u64]),
+    "syzcov_dev_minimize_range_aligned": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, u64, u32, p_, p_,
+                                                    p_, p_, p_, u64, p_, p_, p_, C.c_int, p_, p_,
+                                                    p_]),
+    "syzcov_dev_minimize_range_aligned_pass2": (C.c_int, [p_, p_, p_, p_, p_, sz, u32, u64, u32,
+                                                          p_, C.c_int, p_, p_, p_, u64, p_, p_, p_,
+                                                          p_, p_, p_, p_]),
     "syzcov_corpus_canon": (C.c_int, [u64, p_, p_, sz, p_]),
     "syzcov_corpus_order": (C.c_int, [u64, p_, sz, p_]),
     "syzcov_corpus_order_given": (C.c_int, [u64, p_, sz, p_]),
@@ -205,7 +215,7 @@ class CorpusCfg(C.Structure):
     _fields_ = [("n_max", sz), ("n_global", sz), ("rank", sz), ("p_max", u64),
                 ("max_seg_len", sz), ("pc_lo", u32), ("pc_span", u64), ("universe", p_),
                 ("universe_n", sz), ("canon_in_place", C.c_int), ("order_by", C.c_int),
-                ("rec_cap", u64)]
+                ("rec_cap", u64), ("canon_layout", C.c_int)]
 
 
 class CorpusInfo(C.Structure):
@@ -213,7 +223,7 @@ class CorpusInfo(C.Structure):
     _fields_ = [("key_mode", u32), ("kshift", u32), ("kbase", u32), ("pc_lo", u32),
                 ("span", u64), ("win_lo", u32), ("sent_key", u32), ("win_span", u64),
                 ("nrange", u64), ("nwords", u64), ("n_global", u64), ("union_cap", u64),
-                ("rec_cap", u64), ("mem", p_), ("mem_size", u64)]
+                ("rec_cap", u64), ("mem", p_), ("mem_size", u64), ("canon_align_k", u64)]
 
 
 class CorpusRes(C.Structure):

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(THREADS) void canon_class_kernel(
     const uint64_t *__restrict__ off, const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
     uint32_t *__restrict__ new_len, const uint32_t *__restrict__ list,
     const uint32_t *__restrict__ count, uint8_t *__restrict__ pres, uint32_t pc_lo,
-    uint64_t pc_span, uint32_t *__restrict__ err) {
+    uint64_t pc_span, uint32_t *__restrict__ err, uint32_t ak = 0) {
     constexpr int CAP = THREADS * ITEMS;
     __shared__ uint32_t sm[CAP];
     __shared__ uint32_t scan_tmp[THREADS / 64 + 1];
@@ -158,9 +158,12 @@ __global__ __launch_bounds__(THREADS) void canon_class_kernel(
         for (int i = 0; i < ITEMS; i++)
             if (keepmask & (1u << i)) sm[pos++] = v[i];
         __syncthreads();
+        // (ak: contiguous at the input's line-aligned base, common.h; the
+        // caller spreads the ranges' sub-runs apart once their splits are known)
+        uint32_t *o = out + aligned_base(base, seg, ak);
         for (uint32_t k = t; k < total; k += THREADS) {
             const uint32_t pc = sm[k];
-            out[base + k] = pc;
+            o[k] = pc;
             if (pres) mark_pc(pres, pc, pc_lo, pc_span, err);
         }
         if (t == 0) new_len[seg] = total;
@@ -252,12 +255,12 @@ __global__ __launch_bounds__(256) void large_unique_kernel(
     const uint64_t *__restrict__ off, const uint32_t *__restrict__ list, uint32_t nlarge,
     const uint64_t *__restrict__ scratch_off, const uint32_t *__restrict__ sorted,
     uint32_t *__restrict__ out, uint32_t *__restrict__ new_len, uint8_t *__restrict__ pres,
-    uint32_t pc_lo, uint64_t pc_span, uint32_t *__restrict__ err) {
+    uint32_t pc_lo, uint64_t pc_span, uint32_t *__restrict__ err, uint32_t ak) {
     __shared__ uint32_t scan_tmp[256 / 64 + 1];
     for (uint32_t li = blockIdx.x; li < nlarge; li += gridDim.x) {
         const uint32_t seg = list[li];
-        const uint64_t base = off[seg];
-        const uint64_t n = off[seg + 1] - base;
+        const uint64_t base = aligned_base(off[seg], seg, ak);
+        const uint64_t n = off[seg + 1] - off[seg];
         const uint32_t *s = sorted + scratch_off[li];
         uint64_t wpos = 0;
         for (uint64_t cb = 0; cb < n; cb += 256) {
@@ -308,7 +311,7 @@ extern "C" size_t syzcov_dev_canon_ws_size(size_t nseg, size_t max_seg_len) {
 namespace syz {
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
-                     uint64_t pc_span, uint32_t *err, hipStream_t s);
+                     uint64_t pc_span, uint32_t *err, hipStream_t s, uint32_t ak = 0);
 }
 
 extern "C" int syzcov_dev_canonicalize(const uint64_t *off, const uint32_t *in, uint32_t *out,
@@ -375,16 +378,16 @@ namespace syz {
 // for segments too long for a wave and for any segment whose wave sort failed
 // its order check.  Longer listed segments are skipped (large path).
 int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
-                    const uint32_t *list, const uint32_t *count, hipStream_t s) {
+                    const uint32_t *list, const uint32_t *count, hipStream_t s, uint32_t ak) {
     hipLaunchKernelGGL((canon_class_kernel<1024, 16>), dim3(256), dim3(1024), 0, s, off, in, out,
-                       new_len, list, count, nullptr, 0u, (uint64_t)0, nullptr);
+                       new_len, list, count, nullptr, 0u, (uint64_t)0, nullptr, ak);
     SYZ_LAUNCH_CHECK();
     return 0;
 }
 
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
-                     uint64_t pc_span, uint32_t *err, hipStream_t s) {
+                     uint64_t pc_span, uint32_t *err, hipStream_t s, uint32_t ak) {
     // host copies of the large-segment list and lengths (small)
     uint32_t *hlist = (uint32_t *)malloc(nlarge * sizeof(uint32_t));
     if (!hlist) return SYZCOV_ENOMEM;
@@ -451,7 +454,7 @@ int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uin
         }
         hipLaunchKernelGGL(large_unique_kernel, dim3(std::min<uint32_t>(nlarge, 1024)), dim3(256),
                            0, s, off, dlist, nlarge, dsoff, src, out, new_len, pres, pc_lo,
-                           pc_span, err);
+                           pc_span, err, ak);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             rc = SYZCOV_EHIP;
         hipFree(dcount);

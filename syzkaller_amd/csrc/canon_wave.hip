@@ -37,10 +37,10 @@
 namespace syz {
 
 int canon_list_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
-                    const uint32_t *list, const uint32_t *count, hipStream_t s);
+                    const uint32_t *list, const uint32_t *count, hipStream_t s, uint32_t ak);
 int canon_large_path(const uint64_t *off, const uint32_t *in, uint32_t *out, uint32_t *new_len,
                      const uint32_t *dlist, uint32_t nlarge, uint8_t *pres, uint32_t pc_lo,
-                     uint64_t pc_span, uint32_t *err, hipStream_t s);
+                     uint64_t pc_span, uint32_t *err, hipStream_t s, uint32_t ak);
 
 #ifndef SYZ_CANON_W32
 #define SYZ_CANON_W32 3
@@ -179,7 +179,31 @@ struct Params {
     uint32_t *big_list, *big_cnt;    // n > WAVE_MAX (listed by bin_kernel)
     uint32_t *err;
     uint32_t force_redo;             // SYZCOV_FORCE=redo: every segment takes the redo path
+    uint32_t ak;                     // line-aligned sub-runs (common.h SYZ_ALIGN_K), 0 = CSR slots
 };
+
+// Line-aligned writes (common.h): the output position of the kept word at
+// canonical index pos is pos + delta, delta = aligned_sub(s, j, ak) - s for the
+// range j the word falls in (s = the index of j's first word).  Words arrive in
+// sorted order, a row of 64 at a time; a lane whose word is the first of its
+// range (`start`) derives the delta, and it holds until the next start (at
+// most R per segment, so the uniform loop over a row's starts is short).
+__device__ __forceinline__ uint32_t aligned_delta(uint64_t start_mask, uint32_t pos, uint32_t rng,
+                                                  uint32_t ak, uint32_t l, uint32_t &dcar) {
+    uint32_t delta = dcar;
+    if (start_mask) {  // wave-uniform
+        const uint32_t dl = aligned_sub(pos, rng, ak) - pos;
+        uint64_t rem = start_mask;
+        while (rem) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(rem);
+            rem &= rem - 1;
+            const uint32_t db = __builtin_amdgcn_readlane(dl, b);
+            if (l >= b) delta = db;
+            dcar = db;
+        }
+    }
+    return delta;
+}
 
 // Wave-aggregated binning of segments into capacity classes (one atomic per
 // wave and class): lists[c][..] = segments with cls_lo[c] <= n <= cls_hi[c].
@@ -395,8 +419,8 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = P.sent_key;
-        uint32_t *outp = P.out + base;
+        uint32_t cnt = 0, carry = P.sent_key, dcar = 0;
+        uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
@@ -413,11 +437,21 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                         (uint32_t)(e < n) & (uint32_t)(v != prev) & (uint32_t)(v <= span_m1);
                     const uint64_t m = __ballot(keep);
                     const uint32_t pos = cnt + (uint32_t)__popcll(m & lt);
+                    // key mode: the PC's key word (common.h); the key map is
+                    // monotone, so sorted unique PCs give sorted words
+                    const uint32_t wo = P.key_out ? key_word(v + P.pc_lo, P.kshift, P.kbase)
+                                                  : v + P.pc_lo;
+                    uint32_t delta = 0;
+                    if (P.ak) {  // uniform: the range of each word (keys or offsets)
+                        const uint32_t rv = (P.key_out ? wo & SYZ_KEY_MASK : v) >> P.rshift;
+                        const uint32_t rp = (P.key_out ? key_word(prev + P.pc_lo, P.kshift, P.kbase)
+                                                             & SYZ_KEY_MASK
+                                                       : prev) >> P.rshift;
+                        const uint64_t sm = __ballot(keep && (pos == 0 || rv != rp));
+                        delta = aligned_delta(sm, pos, rv, P.ak, l, dcar);
+                    }
                     if (keep) {
-                        // key mode: the PC's key word (common.h); the key map
-                        // is monotone, so sorted unique PCs give sorted words
-                        outp[pos] = P.key_out ? key_word(v + P.pc_lo, P.kshift, P.kbase)
-                                              : v + P.pc_lo;
+                        outp[pos + delta] = wo;
                         buf[pos] = v;
                     }
                     cnt += (uint32_t)__popcll(m);
@@ -761,8 +795,11 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = sent_g;
-        uint32_t *outp = P.out + base;
+        uint32_t cnt = 0, carry = sent_g, dcar = 0;
+        uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
+        // gapped key bits of the range index: a word starts a range iff they
+        // differ from its predecessor's (or it is the first kept word)
+        const uint32_t rmask = GAP_KEY_MASK & ~((2u << P.rshift) - 1u);
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
@@ -775,13 +812,19 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     // whole words: distinct PCs stay distinct even if they share a key
                     const bool keep = v != prev;
                     const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+                    const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
+                                                   (uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    const uint32_t w = ungap_word(v);
+                    uint32_t delta = 0;
+                    if (P.ak) {  // uniform
+                        const uint64_t sm = __builtin_amdgcn_ballot_w64(
+                            keep && (pos == 0 || ((v ^ prev) & rmask) != 0));
+                        delta = aligned_delta(sm, pos, (w & KEY_MASK) >> P.rshift, P.ak, l, dcar);
+                    }
                     if (keep) {
-                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
-                                                       (uint32_t)(m >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        const uint32_t w = ungap_word(v);
-                        outp[pos] = w;  // the key word: the PC is kept exactly
-                        buf[pos] = w;   // (the split search masks the key)
+                        outp[pos + delta] = w;  // the key word: the PC is kept exactly
+                        buf[pos] = w;           // (the split search masks the key)
                     }
                     cnt += (uint32_t)__popcll(m);
                 }
@@ -840,7 +883,7 @@ __global__ __launch_bounds__(64) void split_list_kernel(Params P, const uint32_t
     for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
         const uint32_t seg = list[li];
         if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
-        const uint32_t *c = P.out + P.off[seg];
+        const uint32_t *c = P.out + aligned_base(P.off[seg], seg, P.ak);  // contiguous still
         const uint32_t cnt = P.new_len[seg];
         uint32_t carry = 0;
         for (uint32_t jb = 0; jb < P.nrange; jb += 64) {
@@ -878,7 +921,7 @@ __global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_
     for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
         const uint32_t seg = list[li];
         if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
-        uint32_t *c = P.out + P.off[seg];
+        uint32_t *c = P.out + aligned_base(P.off[seg], seg, P.ak);
         const uint32_t cnt = P.new_len[seg];
         bool bad = false;
         for (uint32_t i = __lane_id(); i < cnt; i += 64) {
@@ -891,6 +934,37 @@ __global__ __launch_bounds__(64) void keyify_list_kernel(Params P, const uint32_
             if (__lane_id() == 0) {
                 atomicOr(P.err, SYZCOV_ERR_WINDOW);
                 P.new_len[seg] = 0;
+            }
+        }
+    }
+}
+
+// The workgroup paths write a segment contiguously at its line-aligned base;
+// once its split points are known its range sub-runs move up to their aligned
+// starts (common.h), in place: every word moves to an equal or higher index,
+// so the ranges go last to first and each range's words top chunk first, the
+// whole chunk read before any of it is written (a workgroup per segment).
+__global__ __launch_bounds__(256) void spread_list_kernel(Params P, const uint32_t *list,
+                                                          const uint32_t *count, int big_only) {
+    const uint32_t nl = *count;
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint32_t seg = list[li];
+        if (big_only && P.off[seg + 1] - P.off[seg] <= WAVE_MAX) continue;
+        uint32_t *c = P.out + aligned_base(P.off[seg], seg, P.ak);
+        const uint32_t *sp = P.split + (uint64_t)seg * P.nrange;
+        for (int j = (int)P.nrange - 1; j > 0; j--) {
+            const uint32_t s0 = sp[j - 1], s1 = sp[j];
+            const uint32_t d = aligned_sub(s0, (uint32_t)j, P.ak) - s0;
+            if (s1 == s0 || d == 0) continue;
+            for (uint32_t top = s1; top > s0;) {
+                const uint32_t lo = top - s0 > blockDim.x ? top - blockDim.x : s0;
+                const uint32_t i = lo + threadIdx.x;
+                uint32_t v = 0;
+                if (i < top) v = c[i];
+                __syncthreads();
+                if (i < top) c[i + d] = v;
+                __syncthreads();
+                top = lo;
             }
         }
     }
@@ -969,7 +1043,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
                             int key_out, uint32_t range_shift,
                             uint32_t *split,
                             uint64_t *range_tot, uint32_t *err_flag, void *ws, size_t ws_size,
-                            void *stream) {
+                            void *stream, int aligned = 0) {
     if (nseg == 0) return 0;
     if (!off || !raw || !out || !new_len || !err_flag || !ws) return SYZCOV_EINVAL;
     if (pc_span == 0 || pc_span > (1ull << 32) || (uint64_t)pc_lo + pc_span > (1ull << 32))
@@ -988,6 +1062,8 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     if (range_shift > 20) return SYZCOV_EINVAL;
     const uint64_t nrange = (nkeys + (1ull << range_shift) - 1) >> range_shift;
     if (split && nrange > (uint64_t)cw::MAX_RPL * 64) return SYZCOV_ERANGE;
+    // the line-aligned layout needs the split points and its own buffer
+    if (aligned && (!split || out == raw)) return SYZCOV_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     uint8_t *w = (uint8_t *)ws;
     uint32_t *cnts = (uint32_t *)w;  // [0] redo, [1] big, [2..] classes
@@ -1032,6 +1108,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     const int key2 =
         (key_out && nkeys <= (1ull << 22) && !(force & FORCE_CANON3)) ? SYZ_CANON_KEY2 : 0;
     P.force_redo = (force & FORCE_REDO) ? 1u : 0u;
+    P.ak = aligned ? SYZ_ALIGN_K((uint32_t)nrange) : 0u;
     cw::Params PK = P;  // the key kernel's unique loop compares (key | low bits) words
     PK.sent_key = so < pc_span ? ((0xFFFFFFFFu >> kshift) - kbase) | (P.lowmask << cw::KEY_BITS)
                                : 0xFFFFFFFFu;  // a word's key is < 2^25: never equal
@@ -1083,14 +1160,17 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
         if (split)
             hipLaunchKernelGGL(cw::split_list_kernel, dim3(grid), dim3(64), 0, s, P, list, cnt,
                                big_only);
+        if (P.ak)
+            hipLaunchKernelGGL(cw::spread_list_kernel, dim3(grid), dim3(256), 0, s, P, list, cnt,
+                               big_only);
     };
     // segments whose wave sort failed the order check (not expected on gfx950)
-    int rc = canon_list_path(off, raw, out, new_len, redo, cnts, s);
+    int rc = canon_list_path(off, raw, out, new_len, redo, cnts, s, P.ak);
     if (rc) return rc;
     finish_list(redo, cnts, 0, 64);
     if (max_seg_len > cw::WAVE_MAX) {
         if (max_seg_len <= 16384) {
-            rc = canon_list_path(off, raw, out, new_len, big, cnts + 1, s);
+            rc = canon_list_path(off, raw, out, new_len, big, cnts + 1, s, P.ak);
             if (rc) return rc;
         } else {
             uint32_t nbig = 0;
@@ -1099,7 +1179,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
             if (nbig) {
                 // the window is checked by keyify_list_kernel
                 rc = canon_large_path(off, raw, out, new_len, big, nbig, nullptr, pc_lo,
-                                      pc_span, err_flag, s);
+                                      pc_span, err_flag, s, P.ak);
                 if (rc) return rc;
             }
         }
@@ -1129,4 +1209,23 @@ extern "C" int syzcov_dev_canon_split_keys(const uint64_t *off, const uint32_t *
     return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span, kshift,
                             kbase, nkeys, 1, range_shift, split, range_tot, err_flag, ws, ws_size,
                             stream);
+}
+
+extern "C" int syzcov_dev_canon_split_aligned(const uint64_t *off, const uint32_t *raw,
+                                              uint32_t *out, uint32_t *new_len, size_t nseg,
+                                              size_t max_seg_len, uint32_t pc_lo,
+                                              uint64_t pc_span, uint32_t kshift, uint32_t kbase,
+                                              uint64_t nkeys, int key_out, uint32_t range_shift,
+                                              uint32_t *split, uint64_t *range_tot,
+                                              uint32_t *err_flag, void *ws, size_t ws_size,
+                                              void *stream) {
+    return canon_split_impl(off, raw, out, new_len, nseg, max_seg_len, pc_lo, pc_span,
+                            key_out ? kshift : 0, key_out ? kbase : pc_lo,
+                            key_out ? nkeys : pc_span, key_out ? 1 : 0, range_shift, split,
+                            range_tot, err_flag, ws, ws_size, stream, 1);
+}
+
+extern "C" uint64_t syzcov_dev_canon_aligned_words(uint64_t p_max, uint64_t nseg,
+                                                   uint64_t nrange) {
+    return aligned_words(p_max, nseg, SYZ_ALIGN_K((uint32_t)nrange));
 }

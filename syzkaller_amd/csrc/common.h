@@ -129,6 +129,28 @@ __host__ __device__ __forceinline__ uint32_t key_word(uint32_t pc, uint32_t kshi
     return ((pc >> kshift) - kbase) | ((pc & ((1u << kshift) - 1u)) << SYZ_KEY_BITS);
 }
 
+// Line-aligned canonical layout: every (input, range) sub-run
+// of the canonical lists starts on its own 128-byte line, so Minimize's pass 1
+// (minimize_range.hip), which reads range j of an input in a different
+// workgroup than range j + 1, never fetches a line twice.  With R ranges and
+// ak = SYZ_ALIGN_K(R) = 31 (R + 1):
+//   input i's words start at   aligned_base(off[i], i, ak) = align32(off[i] + ak i)
+//   range j's sub-run at       + aligned_sub(s_{j-1}, j)   = align32(s_{j-1} + 31 j)
+// (s_j = split[i][j], s_{-1} = 0).  Sub-run j ends at or below s_j + 31 (j + 1),
+// so sub-runs never overlap, and input i ends below aligned_base of i + 1:
+// the buffer holds p + ak n + 32 words for n inputs of p raw PCs.  ak = 0 is
+// the plain CSR layout (input i at off[i], sub-run j at s_{j-1}).
+__host__ __device__ constexpr uint32_t SYZ_ALIGN_K(uint32_t nrange) { return 31u * (nrange + 1u); }
+__host__ __device__ __forceinline__ uint64_t aligned_base(uint64_t off_i, uint64_t i, uint32_t ak) {
+    return ak ? (off_i + (uint64_t)ak * i + 31u) & ~31ull : off_i;
+}
+__host__ __device__ __forceinline__ uint32_t aligned_sub(uint32_t s_prev, uint32_t j, uint32_t ak) {
+    return ak ? (s_prev + 31u * j + 31u) & ~31u : s_prev;
+}
+static inline uint64_t aligned_words(uint64_t p, uint64_t n, uint32_t ak) {
+    return ak ? p + (uint64_t)ak * n + 32 : p;
+}
+
 // 64-bit splitmix (synthetic generator; identical to oracle/synth_oracle.c).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;

@@ -164,6 +164,7 @@ struct Corpus {
     uint64_t span = 0;
     uint32_t sent_key = 0xFFFFFFFFu;  // index of PC 0xFFFFFFFF in that window, or none
     uint32_t rshift = kRangeShiftWindow, nrange = 1;
+    uint32_t ak = 0;        // line-aligned canonical layout: SYZ_ALIGN_K(nrange), 0 = CSR slots
     uint64_t nwords = 0, n_global = 0, union_cap = 0;
     int world = 1;
     bool shard = false;  // the sharded protocol (cfg.n_global given, even at world 1)
@@ -220,7 +221,7 @@ static int64_t plan(Corpus &c) {
     const size_t n = g.n_max, N = c.n_global;
     size_t *sz = c.sizes;
     for (int b = 0; b < SYZCOV_CORPUS_NBUF; b++) sz[b] = 0;
-    sz[SYZCOV_CORPUS_CANON] = g.canon_in_place ? 0 : (g.p_max + 1) * 4;
+    sz[SYZCOV_CORPUS_CANON] = g.canon_in_place ? 0 : (aligned_words(g.p_max, n, c.ak) + 1) * 4;
     sz[SYZCOV_CORPUS_NEW_LEN] = (n + 1) * 4;
     sz[SYZCOV_CORPUS_SPLIT] = c.nrange > 1 ? n * c.nrange * 4 : 0;
     sz[SYZCOV_CORPUS_RANGE_TOT] = c.nrange * 8;
@@ -314,6 +315,12 @@ static int setup(Corpus &c, const syzcov_corpus_cfg *cfg) {
         set_error("PC window too wide for the range engine (> 256 ranges of 2^20)");
         return SYZCOV_ERANGE;
     }
+    // canon_layout 1, out of place over more than one range: every (input,
+    // range) sub-run on its own 128-B lines (common.h).  Not the default: at
+    // C3 it cut Minimize from 22.4 to 20.0 ms but its writes took canon from
+    // 62.7 to 71.1 ms (C2: 2.85 -> 2.76 and 6.62 -> 7.44).
+    if (g.canon_layout < 0 || g.canon_layout > 1) return SYZCOV_EINVAL;
+    c.ak = !g.canon_in_place && c.nrange > 1 && g.canon_layout == 1 ? SYZ_ALIGN_K(c.nrange) : 0;
     c.nwords = (c.span + 31) / 32;
     if (g.rec_cap == 0)
         g.rec_cap = std::max<uint64_t>(1ull << 22, std::min<uint64_t>(g.p_max, 1ull << 26));
@@ -370,6 +377,8 @@ constexpr uint32_t kErrRecomputed = 1u << 31;
 
 static uint64_t *scal(const Corpus &c) { return c.buf<uint64_t>(SYZCOV_CORPUS_SCAL); }
 static bool sharded(const Corpus &c) { return c.shard; }
+// the canonical lists in the line-aligned layout (common.h): out of place, R > 1
+static bool aligned(const Corpus &c) { return c.ak != 0; }
 
 // --------------------------------------------------------------- phases
 static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hipStream_t s) {
@@ -396,6 +405,11 @@ static int ph_canon(Corpus &c, const uint64_t *off, uint32_t *raw, size_t n, hip
     uint32_t *nl = c.buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN);
     uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
     void *ws = c.buf<void>(SYZCOV_CORPUS_WS);
+    if (aligned(c))  // line-aligned sub-runs for Minimize's pass 1 (common.h)
+        return syzcov_dev_canon_split_aligned(off, raw, c.canon, nl, n, c.cfg.max_seg_len,
+                                              c.win_lo, c.win_span, c.kshift, c.kbase, c.span,
+                                              c.key_mode, c.rshift, split, rt, (uint32_t *)sc, ws,
+                                              c.ws_size, s);
     if (c.key_mode)
         return syzcov_dev_canon_split_keys(off, raw, c.canon, nl, n, c.cfg.max_seg_len, c.win_lo,
                                            c.win_span, c.kshift, c.kbase, c.span, c.rshift, split,
@@ -498,6 +512,14 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
     const uint32_t *split = c.buf<uint32_t>(SYZCOV_CORPUS_SPLIT);
     const uint64_t *rt = c.buf<uint64_t>(SYZCOV_CORPUS_RANGE_TOT);
     if (!do_pass2) c.pass2_pending = true;
+    if (aligned(c))
+        return syzcov_dev_minimize_range_aligned(
+            c.off, c.canon, split, items, ranks, c.n, c.pc_lo, c.span, c.rshift, rt,
+            c.key_mode ? c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY) : nullptr,
+            c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.buf<int32_t>(SYZCOV_CORPUS_FIRST),
+            c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
+            c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2,
+            (uint32_t *)(scal(c) + SC_ERR), c.buf<void>(SYZCOV_CORPUS_WS), s);
     if (c.key_mode)
         return syzcov_dev_minimize_range_keys(
             c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
@@ -520,7 +542,8 @@ int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32
                           const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered,
                           int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
                           uint8_t *cand, uint8_t *kept, uint32_t *err_flag,
-                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s);
+                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s,
+                          int aligned);
 
 // Minimize per group of ranks [grp_off[g], grp_off[g+1]) (host offsets), one
 // GPU: Manager.minimizeCorpus's per-call cover.Minimize (manager.go:516-524)
@@ -536,7 +559,8 @@ static int ph_minimize_groups(Corpus &c, const uint64_t *grp_off, uint32_t ngrou
         c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.buf<int32_t>(SYZCOV_CORPUS_FIRST),
         c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
         c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT),
-        (uint32_t *)(scal(c) + SC_ERR), grp_off, ngroups, c.buf<void>(SYZCOV_CORPUS_WS), s);
+        (uint32_t *)(scal(c) + SC_ERR), grp_off, ngroups, c.buf<void>(SYZCOV_CORPUS_WS), s,
+        aligned(c));
 }
 
 // Window mode, sharded: the dictionary of the merged covered set and this
@@ -578,7 +602,14 @@ static int ph_pass2(Corpus &c, hipStream_t s) {
     uint32_t *cov = c.buf<uint32_t>(SYZCOV_CORPUS_COVERED);
     uint64_t *rec = c.buf<uint64_t>(SYZCOV_CORPUS_REC);
     uint8_t *cand = c.buf<uint8_t>(SYZCOV_CORPUS_CAND), *kept = c.buf<uint8_t>(SYZCOV_CORPUS_KEPT);
-    int rc = c.key_mode
+    int rc = aligned(c)
+                 ? syzcov_dev_minimize_range_aligned_pass2(
+                       c.off, c.canon, split, items, ranks, c.n, c.pc_lo, c.span, c.rshift, rt,
+                       c.key_mode, cov, first, rec, c.cfg.rec_cap, scal(c) + SC_REC, cand,
+                       c.key_mode ? nullptr : c.buf<uint64_t>(SYZCOV_CORPUS_TAB),
+                       c.key_mode ? nullptr : c.buf<int32_t>(SYZCOV_CORPUS_FIRST_DENSE), kept,
+                       c.buf<void>(SYZCOV_CORPUS_WS), s)
+             : c.key_mode
                  ? syzcov_dev_minimize_range_keys_pass2(
                        c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt, cov,
                        first, rec, c.cfg.rec_cap, scal(c) + SC_REC, cand, kept,
@@ -1019,6 +1050,42 @@ int syzcov_corpus_info(syzcov_corpus h, syzcov_corpus_info_t *out) {
     out->sent_key = c->sent_key;
     out->mem = c->mem;
     out->mem_size = c->mem_size;
+    out->canon_align_k = c->ak;
+    return 0;
+}
+
+// The step's canonical lists in the raw lists' CSR slots (out[off[i] ..
+// off[i] + new_len[i])), from whichever layout CANON holds: one wave per
+// input copies its sub-runs range by range.
+__global__ __launch_bounds__(256) void corpus_unalign_kernel(const uint64_t *__restrict__ off,
+                                                             const uint32_t *__restrict__ canon,
+                                                             const uint32_t *__restrict__ split,
+                                                             const uint32_t *__restrict__ nl,
+                                                             uint64_t n, uint32_t nrange,
+                                                             uint32_t ak,
+                                                             uint32_t *__restrict__ out) {
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; i < n; i += nw) {
+        const uint64_t ib = aligned_base(off[i], i, ak);
+        uint32_t s0 = 0;
+        for (uint32_t j = 0; j < nrange; j++) {
+            const uint32_t s1 = (split && nrange > 1) ? split[i * nrange + j] : nl[i];
+            const uint64_t a = ib + aligned_sub(s0, j, ak);
+            for (uint32_t q = __lane_id(); q < s1 - s0; q += 64) out[off[i] + s0 + q] = canon[a + q];
+            s0 = s1;
+        }
+    }
+}
+
+int syzcov_corpus_canonical(syzcov_corpus h, uint32_t *out, void *stream) {
+    Corpus *c = get(h);
+    if (!c || !out || !c->canon || !c->off || !c->n) return SYZCOV_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(corpus_unalign_kernel, dim3(grid_for(c->n, 4, 8192)), dim3(256), 0, s, c->off,
+                       (const uint32_t *)c->canon, c->buf<uint32_t>(SYZCOV_CORPUS_SPLIT),
+                       c->buf<uint32_t>(SYZCOV_CORPUS_NEW_LEN), (uint64_t)c->n, c->nrange, c->ak,
+                       out);
+    SYZ_LAUNCH_CHECK();
     return 0;
 }
 

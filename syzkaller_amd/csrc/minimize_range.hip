@@ -100,6 +100,7 @@ struct Args {
     uint32_t keymask;          // SYZ_KEY_MASK in key mode, ~0 otherwise
     const uint8_t *low_of_key; // [nrange << rshift] bytes, 0x7F past the keys
     uint32_t *err;             // SYZCOV_ERR_UNIVERSE
+    uint32_t ak;               // line-aligned sub-runs (common.h), 0: CSR slots
 };
 
 
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
         if (threadIdx.x < rows) {
             const uint32_t seg = (uint32_t)A.order[t0 + threadIdx.x];
             s_seg[threadIdx.x] = seg;
-            base_r[t0 + threadIdx.x] = A.off[seg];
+            base_r[t0 + threadIdx.x] = aligned_base(A.off[seg], seg, A.ak);
         }
         __syncthreads();
         if (!A.split) {  // one range: the column is the canonical length
@@ -309,7 +310,8 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         uint64_t a0 = 0;
         const int32_t rk = d_rk;
         if (item < w1) {
-            const uint64_t st = d_base + d_s0;
+            // line-aligned: the sub-run owns its lines and starts on one (head 0)
+            const uint64_t st = d_base + aligned_sub(d_s0, rho, A.ak);
             m = d_s1 - d_s0;
             a0 = st & ~3ull;
             const uint32_t head = (uint32_t)(st - a0);
@@ -532,10 +534,15 @@ __global__ void ovf_pass2_kernel(Args A, uint32_t n_items, const int32_t *first_
         if (!A.cand[j]) continue;
         const int32_t rank = A.ranks ? A.ranks[j] : (int32_t)j;
         const uint64_t o = A.base_r[j];
-        const uint32_t n = A.split_t[(uint64_t)(A.nrange - 1) * A.n_items + j];
         bool hit = false;
-        for (uint32_t q = threadIdx.x; q < n; q += blockDim.x)
-            hit |= first_of(first_w, tab, first_d, (A.pcs[o + q] & A.keymask) - A.pc_lo) == rank;
+        uint32_t s0 = 0;
+        for (uint32_t rho = 0; rho < A.nrange; rho++) {  // the item's sub-runs
+            const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + j];
+            const uint64_t a = o + aligned_sub(s0, rho, A.ak);
+            for (uint32_t q = threadIdx.x; q < s1 - s0; q += blockDim.x)
+                hit |= first_of(first_w, tab, first_d, (A.pcs[a + q] & A.keymask) - A.pc_lo) == rank;
+            s0 = s1;
+        }
         if (__syncthreads_or(hit) && threadIdx.x == 0) kept[rank] = 1;
     }
 }
@@ -652,6 +659,7 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.keymask = 0xFFFFFFFFu;
     A.low_of_key = nullptr;
     A.err = nullptr;
+    A.ak = 0;
     return 0;
 }
 
@@ -686,7 +694,7 @@ static int minimize_range_impl(
     uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
     size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, const uint8_t *low_of_key,
     uint32_t *err_flag, void *ws, void *stream, const uint64_t *grp_off = nullptr,
-    uint32_t ngroups = 0) {
+    uint32_t ngroups = 0, int aligned = 0) {
     hipStream_t s = (hipStream_t)stream;
     if (n_items == 0) {
         if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
@@ -697,6 +705,10 @@ static int minimize_range_impl(
     int rc = mr_args(A, off, len, pcs, split, order, ranks, n_items, pc_lo, pc_span, range_shift,
                      range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
     if (rc) return rc;
+    if (aligned) {  // line-aligned sub-runs (common.h) need the split points
+        if (!split) return SYZCOV_EINVAL;
+        A.ak = SYZ_ALIGN_K(A.nrange);
+    }
     const bool keym = low_of_key != nullptr;
     if (keym) {  // key words over <= 2^25 keys, 2^rshift table bytes in LDS
         if (!err_flag || pc_lo != 0 || range_shift > 17 || pc_span > (1ull << 25))
@@ -828,12 +840,45 @@ int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32
                           const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered,
                           int32_t *first_w, uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt,
                           uint8_t *cand, uint8_t *kept, uint32_t *err_flag,
-                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s) {
+                          const uint64_t *grp_off, uint32_t ngroups, void *ws, hipStream_t s,
+                          int aligned) {
     return minimize_range_impl(off, len, pcs, split, order, nullptr, n_items, pc_lo, pc_span,
                                range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand,
-                               kept, 1, 0, 0, 0, low_of_key, err_flag, ws, s, grp_off, ngroups);
+                               kept, 1, 0, 0, 0, low_of_key, err_flag, ws, s, grp_off, ngroups,
+                               aligned);
 }
 }  // namespace syz
+
+// The line-aligned layout of syzcov_dev_canon_split_aligned (common.h): key
+// mode iff low_of_key (then pc_lo = 0, pc_span = the key count, err_flag).
+extern "C" int syzcov_dev_minimize_range_aligned(
+    const uint64_t *off, const uint32_t *pcs, const uint32_t *split, const int32_t *order,
+    const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+    const uint64_t *range_tot, const uint8_t *low_of_key, uint32_t *covered, int32_t *first_w,
+    uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
+    int do_pass2, uint32_t *err_flag, void *ws, void *stream) {
+    return minimize_range_impl(off, nullptr, pcs, split, order, ranks, n_items, pc_lo, pc_span,
+                               range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt,
+                               cand, kept, do_pass2, 0, 0, 0, low_of_key, err_flag, ws, stream,
+                               nullptr, 0, 1);
+}
+
+extern "C" int syzcov_dev_minimize_range_aligned_pass2(
+    const uint64_t *off, const uint32_t *pcs, const uint32_t *split, const int32_t *order,
+    const int32_t *ranks, size_t n_items, uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,
+    const uint64_t *range_tot, int key_mode, uint32_t *covered, int32_t *first_w, uint64_t *rec,
+    uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, const uint64_t *tab,
+    const int32_t *first_dense, uint8_t *kept, void *ws, void *stream) {
+    if (n_items == 0) return 0;
+    if (!kept || !split || (tab && !first_dense)) return SYZCOV_EINVAL;
+    mr::Args A;
+    int rc = mr_args(A, off, nullptr, pcs, split, order, ranks, n_items, pc_lo, pc_span,
+                     range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand, ws);
+    if (rc) return rc;
+    A.ak = SYZ_ALIGN_K(A.nrange);
+    if (key_mode) A.keymask = SYZ_KEY_MASK;  // the overflow fallback reads the words
+    return mr_pass2(A, pc_span, tab, first_dense, kept, (hipStream_t)stream);
+}
 
 extern "C" int syzcov_dev_minimize_range(
     const uint64_t *off, const uint32_t *len, const uint32_t *pcs, const uint32_t *split,

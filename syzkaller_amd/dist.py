@@ -123,10 +123,10 @@ class ShardedEngine(CorpusEngine):
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  rank: int, world: int, device="cuda", universe=None, canon_in_place=False,
-                 split_order: bool = True):
+                 split_order: bool = True, canon_layout: int = 0):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
                          n_global=n * world, rank=rank, universe=universe,
-                         canon_in_place=canon_in_place)
+                         canon_in_place=canon_in_place, canon_layout=canon_layout)
         self.rank, self.world, self.n_local = rank, world, n
         # the ranks split the Go order's late rounds and finisher (each finishes
         # the segments starting in its block), merged by an int32 MAX all-reduce

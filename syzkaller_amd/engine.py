@@ -82,7 +82,8 @@ class CorpusEngine:
 
     def __init__(self, n_max: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  device="cuda", n_global: int | None = None, rank: int = 0, rec_cap: int = 0,
-                 canon_in_place: bool = False, universe=None, order_by: int = 0):
+                 canon_in_place: bool = False, universe=None, order_by: int = 0,
+                 canon_layout: int = 0):
         L = lib()
         dev = torch.device(device)
         if dev.index is None:
@@ -100,7 +101,8 @@ class CorpusEngine:
                         max_seg_len=max_seg_len, pc_lo=pc_lo, pc_span=pc_span,
                         universe=None if self._univ is None else self._univ.ctypes.data,
                         universe_n=0 if self._univ is None else self._univ.size,
-                        canon_in_place=int(canon_in_place), order_by=order_by, rec_cap=rec_cap)
+                        canon_in_place=int(canon_in_place), order_by=order_by, rec_cap=rec_cap,
+                        canon_layout=canon_layout)
         size = check(L.syzcov_corpus_mem_size(C.byref(cfg)), "corpus_mem_size")
         with torch.cuda.device(dev):
             self.mem = torch.empty(size, dtype=torch.uint8, device=dev)
@@ -117,6 +119,7 @@ class CorpusEngine:
         self.win_lo, self.win_span = info.win_lo, info.win_span
         self.nrange, self.nwords = info.nrange, info.nwords
         self.rec_cap = info.rec_cap
+        self.canon_align_k = info.canon_align_k  # 0: CANON in CSR slots
         self.sent_key = None if info.sent_key == 0xFFFFFFFF else info.sent_key
         for name in CORPUS_BUFS:
             setattr(self, name.lower(), self._view(name))
@@ -219,10 +222,15 @@ class CorpusEngine:
     def canonical_pcs(self, off: torch.Tensor, n: int) -> torch.Tensor:
         """The canonical covers as PCs, in the CSR slots of `off` (key mode:
         decoded from the key words canon wrote there)."""
+        lists = self.canon
+        if self.canon_align_k:  # line-aligned layout: back into the CSR slots
+            lists = torch.zeros(int(off[n].item()) + 1, dtype=torch.int32, device=self.dev)
+            check(self.L.syzcov_corpus_canonical(self.h, _p(lists), _stream()),
+                  "corpus_canonical")
         if not self.key_mode:
-            return self.canon
-        out = torch.empty_like(self.canon)
-        check(self.L.syzcov_dev_words_to_pcs(_p(self.canon), int(off[n].item()), self.kshift,
+            return lists
+        out = torch.empty_like(lists)
+        check(self.L.syzcov_dev_words_to_pcs(_p(lists), int(off[n].item()), self.kshift,
                                              self.kbase, _p(out), _stream()), "dev_words_to_pcs")
         return out
 

@@ -60,6 +60,7 @@ def test_same_workload_at_every_n(monkeypatch):
     def fake_run(args, world, rank, dev, glob, seed, steps, warmup, key):
         seen.update(glob=glob, seed=seed, key=key)
         return {"value": 1.0, "ms_per_step": 1.0, "inputs_per_gpu": glob, "raw_pcs_per_gpu": 0,
+                "aligned": True,
                 "canonical_pcs_per_gpu": 0, "keys": "", "phases_ms": {},
                 "roofline": {"achieved": 1.0}, "minimize_union_pcs_per_s": 1.0}
     monkeypatch.setattr(bench, "init_dist", lambda: (1, 0, None))

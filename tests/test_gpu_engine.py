@@ -29,14 +29,20 @@ def test_synth_matches_cpu_twin(torch):
         assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
 
 
+@pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
                                                (500, 9000, 6000, 20)])
-def test_engine_step_vs_oracle(torch, n, mean, sigma, log2):
+def test_engine_step_vs_oracle(torch, n, mean, sigma, log2, layout):
+    """Window mode against the oracle, canonical lists in CSR slots or in the
+    line-aligned layout (every (input, range) sub-run on its own lines); the
+    500-input case holds inputs past the wave kernels (> 8189 and > 16384
+    PCs: the workgroup paths, whose output is spread to the aligned starts)."""
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_window
     seed = 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
     lo, span = synth_window(log2)
-    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, canon_layout=layout)
+    assert bool(eng.canon_align_k) == (layout == 1 and eng.nrange > 1)
     res = eng.step(off, raw, n)
     # oracle
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)

@@ -42,15 +42,18 @@ def test_keymap_roundtrip(torch):
         universe_keymap(np.array([5, 3], np.uint32), "cuda")
 
 
+@pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
-                                               (500, 9000, 6000, 20), (2000, 600, 300, 17)])
-def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2):
+                                               (500, 9000, 6000, 20), (2000, 600, 300, 17),
+                                               (3000, 1500, 900, 19)])
+def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2, layout):
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     seed = 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
     lo, span = synth_window(log2)
     eng = CorpusEngine(n, total, int(lens.max().item()), lo, span,
-                       universe=synth_universe(log2, seed))
+                       universe=synth_universe(log2, seed), canon_layout=layout)
+    assert bool(eng.canon_align_k) == (layout == 1 and eng.nrange > 1)
     assert eng.key_mode and eng.span == 1 << log2 and eng.kshift == 4
     res = eng.step(off, raw, n)
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=mean, sigma=sigma, log2_space=log2)
@@ -419,22 +422,32 @@ def test_engine_key_mode_gap_key(torch):
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
 
 
+@pytest.mark.parametrize("force", ["redo", "canon3"])
+@pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
 @pytest.mark.parametrize("keys", [True, False], ids=["key-mode", "window-mode"])
-def test_engine_forced_redo_vs_oracle(torch, keys, monkeypatch):
+def test_engine_forced_redo_vs_oracle(torch, keys, layout, force, monkeypatch):
     """The canon wave sort checks its own order and sends a failing segment to
     the workgroup sort (canon.hip).  Forcing every segment down that path
-    (SYZCOV_FORCE=redo) must give the oracle's results."""
-    monkeypatch.setenv("SYZCOV_FORCE", "redo")
+    (SYZCOV_FORCE=redo; in the line-aligned layout its contiguous output is
+    then spread to the sub-runs' aligned starts), or key mode down the 3-pass
+    wave sort (canon3), must give the oracle's results."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     n, log2, seed = 3000, 18, 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=2048, sigma=900, log2_space=log2)
     lo, span = synth_window(log2)
     eng = CorpusEngine(n, total, int(lens.max().item()), lo, span,
-                       universe=synth_universe(log2, seed) if keys else None)
+                       universe=synth_universe(log2, seed) if keys else None,
+                       canon_layout=layout)
     res = eng.step(off, raw, n)
     o_off, o_pcs = orc.synth_corpus(seed, n, mean=2048, sigma=900, log2_space=log2)
     c_off, c_pcs = orc.canonicalize_csr(o_off, o_pcs)
     assert np.array_equal(eng.new_len[:n].cpu().numpy(), np.diff(c_off).astype(np.int32))
+    canon = eng.canonical_pcs(off, n).cpu().numpy().view(np.uint32)
+    offs = off.cpu().numpy()
+    for i in range(0, n, 37):
+        assert np.array_equal(canon[offs[i]:offs[i] + int(c_off[i + 1] - c_off[i])],
+                              c_pcs[c_off[i]:c_off[i + 1]])
     assert res.kept_idx.cpu().numpy().tolist() == list(orc.minimize_csr(c_off, c_pcs))
     assert np.array_equal(res.union.cpu().numpy().view(np.uint32), orc.union_fold_csr(c_off, c_pcs))
 
