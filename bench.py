@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--no-universe", action="store_true",
                     help="window offsets instead of the dense keys of the registered PC "
                          "universe (keys.hip), for the corpus engine and newcov's maxCover")
+    ap.add_argument("--x86", action="store_true",
+                    help="corpus: the x86-like PC universe (neighbours 5..11 bytes apart, kshift 2) "
+                         "instead of one PC per 16-byte slot; config name gets an X")
     ap.add_argument("--canon-layout", type=int, default=0, choices=[0, 1],
                     help="canonical lists: 0 CSR slots, 1 line-aligned sub-runs "
                          "(syzcov_corpus_cfg.canon_layout)")
@@ -316,22 +319,23 @@ def corpus_workload(glob: int) -> tuple[str, int, str]:
     return cname, seed, f"{cname}: Canonicalize + Minimize + maxCover union, {glob} inputs"
 
 
-def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key):
+def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key, x86=False):
     """K timed steps of the corpus pipeline over `glob` inputs (rank r holds
     [r*n, (r+1)*n)), generated into HBM, canonicalized out of place; returns
     the measured part of a line (phases, roofline of the dominant phase and of
-    Minimize, results)."""
+    Minimize, results).  x86: the x86-like PC universe (kshift 2)."""
     import torch
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     n = -(-glob // world)
-    lo, span = synth_window(args.log2_space)
+    lo, span = synth_window(args.log2_space, x86=x86)
     off, raw, lens, total = synth_corpus(n, seed, first=rank * n, mean=args.mean,
-                                         sigma=args.sigma, log2_space=args.log2_space, device=dev)
+                                         sigma=args.sigma, log2_space=args.log2_space, device=dev,
+                                         x86=x86)
     max_len = int(lens.max().item())
     del lens
     # the PC universe (allCoverPCs, syz-manager/cover.go:57-69) is registered once,
     # outside the timed steps, like the resident maxCover
-    univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev)
+    univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev, x86=x86)
     if world > 1:
         from syzkaller_amd.dist import ShardedEngine
         eng = ShardedEngine(n, total, max_len, lo, span, rank, world, device=dev, universe=univ,
@@ -395,9 +399,13 @@ def bench_corpus(args):
     world, rank, dev = init_dist()
     glob = args.global_inputs or C3_INPUTS
     cname, seed, workload = corpus_workload(glob)
+    if args.x86:
+        cname += "X"
+        workload = workload.replace(":", "X (x86-like PC universe):", 1)
     if args.seed is not None:
         seed = args.seed
-    m = corpus_run(args, world, rank, dev, glob, seed, args.steps, args.warmup, cname)
+    m = corpus_run(args, world, rank, dev, glob, seed, args.steps, args.warmup, cname,
+                   x86=args.x86)
     out = {
         "metric": "input-PCs processed/sec for Canonicalize+Minimize+Union (maxCover merge)",
         "value": m.pop("value"), "unit": "input-PCs/s", "n_gpus": world, "steps": args.steps,
@@ -422,12 +430,21 @@ def bench_corpus(args):
         out["roofline"]["peak_measured_forms"] = rates
         out["roofline"]["peak_guide_float4_copy"] = 6290.0  # MI355X_MICROARCH.md:36
         out["roofline"]["frac_of_measured"] = out["roofline"]["achieved"] / pk
-        if not args.no_c2 and glob != C2_INPUTS:
+        if not args.no_c2 and (glob != C2_INPUTS or args.x86):
             c2 = corpus_run(args, 1, 0, dev, C2_INPUTS, SEED, max(args.steps, 10), args.warmup,
                             "C2")
             c2["workload"] = corpus_workload(C2_INPUTS)[2] + " (one GPU, BASELINE configs[1])"
             c2["seed"] = SEED
             out["c2"] = c2
+        if not args.no_c2 and not (glob == C2_INPUTS and args.x86):
+            # C2 over an x86-like universe (PCs 5..11 bytes apart, kshift 2,
+            # 2^23 keys): the canon's 3-pass sort and 64 Minimize ranges
+            cx = corpus_run(args, 1, 0, dev, C2_INPUTS, SEED, max(args.steps, 10), args.warmup,
+                            "C2X", x86=True)
+            cx["workload"] = ("C2X: C2 over the x86-like PC universe (neighbours 5..11 bytes "
+                              "apart, kshift 2)")
+            cx["seed"] = SEED
+            out["c2x"] = cx
         if not args.no_dropin:
             out["dropin"] = dropin_legs(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:

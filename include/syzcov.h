@@ -743,17 +743,23 @@ int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, uint64_t nby
                           uint64_t *popcount_out, void *stream);
 
 /* Synthetic corpus (integer-exact): lengths for inputs
- * [first, first+n), then PCs into CSR. */
+ * [first, first+n), then PCs into CSR.  mode bit 0: uniform key draws (else
+ * k = 2^S u^3); bit 1: the x86-like universe (neighbouring PCs 5..11 bytes
+ * apart: U[k] = 0x81000000 + 8k + (h(k) & 3), kshift 2), else one PC per
+ * 16-byte slot (U[k] = 0x81000000 + 16k + (h(k) & 15), kshift 4). */
 int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean, uint32_t sigma,
                           uint32_t *lens, void *stream);
 int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
-                         uint32_t log2_space, int uniform, uint32_t *pcs, void *stream);
+                         uint32_t log2_space, int mode, uint32_t *pcs, void *stream);
 /* C5's synthetic call records: out[i] = CallID of record first + i, uniform
  * over [0, ncalls) (counter-based: oracle/synth_oracle.c regenerates it). */
 int syzcov_dev_synth_callids(uint64_t seed, uint64_t first, size_t n, uint32_t ncalls,
                              int32_t *out, void *stream);
-/* The synthetic PC universe U[k], k < 2^log2_space (sorted). */
+/* The synthetic PC universe U[k], k < 2^log2_space (sorted);
+ * _mode: bit 1 of syzcov_dev_synth_pcs's mode selects the x86-like one. */
 int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out, void *stream);
+int syzcov_dev_synth_universe_mode(uint64_t seed, uint32_t log2_space, int mode, uint32_t *out,
+                                   void *stream);
 /* dst <- src, 16-byte aligned, nbytes % 16 == 0: the streaming-copy kernel
  * whose rate the bench reports as the measured HBM peak. */
 int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes, void *stream);

@@ -68,12 +68,13 @@ static size_t canon_radix(uint32_t *a, uint32_t *tmp, size_t n) {
 typedef struct {
     uint64_t seed;
     uint32_t mean, sigma, log2;
+    int mode; /* synth mode: bit 1 = the x86-like universe */
 } cfg_t;
 
 /* canonical cover of synthetic input `i` into out (capacity 65535); returns length */
 static size_t gen_canon(const cfg_t *c, uint64_t i, uint32_t *out, uint32_t *tmp) {
     uint32_t L = orc_synth_len(c->seed, i, c->mean, c->sigma);
-    orc_synth_input(c->seed, i, L, c->log2, 0, out);
+    orc_synth_input(c->seed, i, L, c->log2, c->mode, out);
     return canon_radix(out, tmp, L);
 }
 
@@ -134,11 +135,11 @@ static int write_file(const char *dir, const char *name, const void *data, size_
 }
 
 int main(int argc, char **argv) {
-    if (argc != 8) {
-        fprintf(stderr, "usage: %s SEED N MEAN SIGMA LOG2 THREADS OUTDIR\n", argv[0]);
+    if (argc != 8 && argc != 9) {
+        fprintf(stderr, "usage: %s SEED N MEAN SIGMA LOG2 THREADS OUTDIR [MODE]\n", argv[0]);
         return 2;
     }
-    cfg_t c = {strtoull(argv[1], 0, 0), 0, 0, 0};
+    cfg_t c = {strtoull(argv[1], 0, 0), 0, 0, 0, argc == 9 ? atoi(argv[8]) : 0};
     const uint64_t n = strtoull(argv[2], 0, 0);
     c.mean = (uint32_t)strtoul(argv[3], 0, 0);
     c.sigma = (uint32_t)strtoul(argv[4], 0, 0);
@@ -151,7 +152,7 @@ int main(int argc, char **argv) {
         uint32_t *a = malloc(65536 * 4), *b = malloc(65536 * 4), *t = malloc(65536 * 4);
         for (uint64_t i = 0; i < 64 && i < n; i++) {
             uint32_t L = orc_synth_len(c.seed, i, c.mean, c.sigma);
-            orc_synth_input(c.seed, i, L, c.log2, 0, a);
+            orc_synth_input(c.seed, i, L, c.log2, c.mode, a);
             memcpy(b, a, (size_t)L * 4);
             size_t k1 = canon_radix(a, t, L), k2 = orc_canonicalize(b, L);
             if (k1 != k2 || memcmp(a, b, k1 * 4)) {

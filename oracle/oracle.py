@@ -60,6 +60,8 @@ def lib():
                                          C.c_int, p]
         _lib.orc_synth_universe.argtypes = [C.c_uint64, C.c_uint32]
         _lib.orc_synth_universe.restype = C.c_uint32
+        _lib.orc_synth_universe_mode.argtypes = [C.c_uint64, C.c_uint32, C.c_int]
+        _lib.orc_synth_universe_mode.restype = C.c_uint32
         _lib.orc_synth_callid.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
         _lib.orc_synth_callid.restype = C.c_int32
     return _lib
@@ -288,10 +290,18 @@ def synth_lens(seed: int, n: int, mean: int = 2048, sigma: int = 512, first: int
     return np.array([f(seed, first + i, mean, sigma) for i in range(n)], dtype=np.uint32)
 
 
-def synth_input(seed: int, i: int, length: int, log2_space: int = 22, uniform: bool = False):
+def synth_input(seed: int, i: int, length: int, log2_space: int = 22, uniform: bool = False,
+                x86: bool = False):
     out = np.empty(max(int(length), 1), dtype=np.uint32)
-    lib().orc_synth_input(seed, i, int(length), log2_space, int(uniform), _ptr(out))
+    lib().orc_synth_input(seed, i, int(length), log2_space, int(uniform) | (2 if x86 else 0),
+                          _ptr(out))
     return out[:length]
+
+
+def synth_universe(seed: int, log2_space: int = 22, x86: bool = False) -> np.ndarray:
+    """The generator's PC universe U[k], k < 2^log2_space (sorted)."""
+    f = lib().orc_synth_universe_mode
+    return np.array([f(seed, k, 2 if x86 else 0) for k in range(1 << log2_space)], np.uint32)
 
 
 def synth_callids(seed: int, n: int, ncalls: int, first: int = 0) -> np.ndarray:
@@ -301,7 +311,7 @@ def synth_callids(seed: int, n: int, ncalls: int, first: int = 0) -> np.ndarray:
 
 
 def synth_corpus(seed: int, n: int, mean: int = 2048, sigma: int = 512, log2_space: int = 22,
-                 uniform: bool = False, first: int = 0):
+                 uniform: bool = False, first: int = 0, x86: bool = False):
     """Raw (non-canonical) corpus in CSR form: (offsets u64[n+1], pcs u32)."""
     lens = synth_lens(seed, n, mean, sigma, first)
     off = np.zeros(n + 1, dtype=np.uint64)
@@ -310,7 +320,7 @@ def synth_corpus(seed: int, n: int, mean: int = 2048, sigma: int = 512, log2_spa
     f = lib().orc_synth_input
     base = pcs.ctypes.data
     for i in range(n):
-        f(seed, first + i, int(lens[i]), log2_space, int(uniform),
+        f(seed, first + i, int(lens[i]), log2_space, int(uniform) | (2 if x86 else 0),
           C.c_void_p(base + 4 * int(off[i])))
     return off, pcs
 

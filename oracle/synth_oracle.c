@@ -8,6 +8,7 @@
  *   draw      k    = floor(2^S * u^3), u = x / 2^32, x = 32 hash bits  -> (x^3) >> (96 - S)
  *                    (every key < 2^S is reachable; S <= 32)
  *             (uniform variant: k = top S hash bits)
+ *   x86 universe (mode bit 1): U[k] = 0x81000000 + 8k + (h(k) & 3), neighbours 5..11 B apart
  * TEST INFRASTRUCTURE ONLY.
  */
 #include "oracle.h"
@@ -19,10 +20,13 @@ static uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-uint32_t orc_synth_universe(uint64_t seed, uint32_t k) {
+uint32_t orc_synth_universe_mode(uint64_t seed, uint32_t k, int mode) {
     uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)k);
+    if (mode & 2) return 0x81000000u + 8u * k + (uint32_t)(h & 3u); /* x86-like gaps 5..11 */
     return 0x81000000u + 16u * k + (uint32_t)(h & 15u);
 }
+
+uint32_t orc_synth_universe(uint64_t seed, uint32_t k) { return orc_synth_universe_mode(seed, k, 0); }
 
 uint32_t orc_synth_len(uint64_t seed, uint64_t input, uint32_t mean, uint32_t sigma) {
     uint64_t base = splitmix64(seed ^ splitmix64(input ^ 0x5851F42D4C957F2Dull));
@@ -40,8 +44,10 @@ uint32_t orc_synth_len(uint64_t seed, uint64_t input, uint32_t mean, uint32_t si
     return (uint32_t)L;
 }
 
+/* mode bit 0: uniform draws; bit 1: the x86-like universe */
 void orc_synth_input(uint64_t seed, uint64_t input, uint32_t len, uint32_t log2_space,
-                     int uniform, uint32_t *out) {
+                     int mode, uint32_t *out) {
+    const int uniform = mode & 1;
     uint64_t base = splitmix64(seed ^ splitmix64(input + 0x632BE59BD9B4E019ull));
     for (uint32_t j = 0; j < len; j++) {
         uint64_t h = splitmix64(base + (uint64_t)(j + 1) * 0x9E3779B97F4A7C15ull);
@@ -52,7 +58,7 @@ void orc_synth_input(uint64_t seed, uint64_t input, uint32_t len, uint32_t log2_
             uint64_t x = h >> 32; /* 32 bits; x^3 < 2^96 */
             k = (uint32_t)((uint64_t)(((unsigned __int128)(x * x) * x) >> 64) >> (32 - log2_space));
         }
-        out[j] = orc_synth_universe(seed, k);
+        out[j] = orc_synth_universe_mode(seed, k, mode);
     }
 }
 

@@ -148,6 +148,7 @@ _SIGS = {
     "syzcov_dev_synth_lens": (C.c_int, [u64, u64, sz, u32, u32, p_, p_]),
     "syzcov_dev_synth_pcs": (C.c_int, [u64, u64, sz, p_, u32, C.c_int, p_, p_]),
     "syzcov_dev_synth_universe": (C.c_int, [u64, u32, p_, p_]),
+    "syzcov_dev_synth_universe_mode": (C.c_int, [u64, u32, C.c_int, p_, p_]),
     "syzcov_dev_synth_callids": (C.c_int, [u64, u64, sz, u32, p_, p_]),
     "syzcov_dev_stream_copy": (C.c_int, [p_, p_, sz, p_]),
     "syzcov_dev_copy_peak": (C.c_int, [p_, p_, sz, C.c_int, p_]),

@@ -6,9 +6,14 @@
 
 namespace syz {
 
-__device__ __forceinline__ uint32_t synth_universe(uint64_t seed, uint32_t k) {
+// SYNTH_X86 (mode bit 1): an x86-like universe, neighbouring KCOV return
+// addresses 5..11 bytes apart (8k + 0..3), so kshift 2 and about 2 keys per PC;
+// otherwise one PC per 16-byte slot (kshift 4, a key per PC).
+constexpr int SYNTH_UNIFORM = 1, SYNTH_X86 = 2;
+__device__ __forceinline__ uint32_t synth_universe(uint64_t seed, uint32_t k, int mode = 0) {
     const uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)k);
-    return 0x81000000u + 16u * k + (uint32_t)(h & 15u);
+    return (mode & SYNTH_X86) ? 0x81000000u + 8u * k + (uint32_t)(h & 3u)
+                              : 0x81000000u + 16u * k + (uint32_t)(h & 15u);
 }
 
 __global__ void synth_lens_kernel(uint64_t seed, uint64_t first, uint64_t n, uint32_t mean,
@@ -33,14 +38,14 @@ __global__ void synth_lens_kernel(uint64_t seed, uint64_t first, uint64_t n, uin
 
 __global__ void synth_pcs_kernel(uint64_t seed, uint64_t first, uint64_t n,
                                  const uint64_t *__restrict__ off, uint32_t log2_space,
-                                 int uniform, uint32_t *__restrict__ pcs) {
+                                 int mode, uint32_t *__restrict__ pcs) {
     for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint64_t base = splitmix64(seed ^ splitmix64((first + i) + 0x632BE59BD9B4E019ull));
         const uint64_t b = off[i], len = off[i + 1] - b;
         for (uint64_t j = threadIdx.x; j < len; j += blockDim.x) {
             const uint64_t h = splitmix64(base + (j + 1) * 0x9E3779B97F4A7C15ull);
             uint32_t k;
-            if (uniform) {
+            if (mode & SYNTH_UNIFORM) {
                 k = (uint32_t)(h >> (64 - log2_space));
             } else {
                 // u = x / 2^32 (32 hash bits: every one of the 2^S keys is
@@ -49,7 +54,7 @@ __global__ void synth_pcs_kernel(uint64_t seed, uint64_t first, uint64_t n,
                 const uint64_t x = h >> 32;
                 k = (uint32_t)(__umul64hi(x * x, x) >> (32 - log2_space));
             }
-            pcs[b + j] = synth_universe(seed, k);
+            pcs[b + j] = synth_universe(seed, k, mode);
         }
     }
 }
@@ -64,9 +69,10 @@ __global__ void synth_callids_kernel(uint64_t seed, uint64_t first, uint64_t n, 
     }
 }
 
-__global__ void synth_universe_kernel(uint64_t seed, uint32_t n, uint32_t *__restrict__ out) {
+__global__ void synth_universe_kernel(uint64_t seed, uint32_t n, int mode,
+                                      uint32_t *__restrict__ out) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
-        out[k] = synth_universe(seed, k);
+        out[k] = synth_universe(seed, k, mode);
 }
 
 // Streaming copy, 16 B per lane: the measured HBM peak the bench reports
@@ -135,14 +141,19 @@ extern "C" int syzcov_dev_stream_copy(const void *src, void *dst, size_t nbytes,
     return 0;
 }
 
-extern "C" int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out,
-                                         void *stream) {
-    if (!out || log2_space < 1 || log2_space > 26) return SYZCOV_EINVAL;
+extern "C" int syzcov_dev_synth_universe_mode(uint64_t seed, uint32_t log2_space, int mode,
+                                              uint32_t *out, void *stream) {
+    if (!out || log2_space < 1 || log2_space > 26 || mode < 0 || mode > 3) return SYZCOV_EINVAL;
     const uint32_t n = 1u << log2_space;
     hipLaunchKernelGGL(synth_universe_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
-                       (hipStream_t)stream, seed, n, out);
+                       (hipStream_t)stream, seed, n, mode, out);
     SYZ_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int syzcov_dev_synth_universe(uint64_t seed, uint32_t log2_space, uint32_t *out,
+                                         void *stream) {
+    return syzcov_dev_synth_universe_mode(seed, log2_space, 0, out, stream);
 }
 
 extern "C" int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean,
@@ -156,12 +167,13 @@ extern "C" int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, ui
 }
 
 extern "C" int syzcov_dev_synth_pcs(uint64_t seed, uint64_t first, size_t n, const uint64_t *off,
-                                    uint32_t log2_space, int uniform, uint32_t *pcs,
+                                    uint32_t log2_space, int mode, uint32_t *pcs,
                                     void *stream) {
     if (n == 0) return 0;
-    if (!off || !pcs || log2_space < 1 || log2_space > 26) return SYZCOV_EINVAL;
+    if (!off || !pcs || log2_space < 1 || log2_space > 26 || mode < 0 || mode > 3)
+        return SYZCOV_EINVAL;
     hipLaunchKernelGGL(synth_pcs_kernel, dim3(grid_for(n, 1, 16384)), dim3(256), 0,
-                       (hipStream_t)stream, seed, first, (uint64_t)n, off, log2_space, uniform,
+                       (hipStream_t)stream, seed, first, (uint64_t)n, off, log2_space, mode,
                        pcs);
     SYZ_LAUNCH_CHECK();
     return 0;

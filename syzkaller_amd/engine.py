@@ -325,9 +325,11 @@ class PrioEngine:
 
 
 def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int = 512,
-                 log2_space: int = 22, uniform: bool = False, device="cuda"):
+                 log2_space: int = 22, uniform: bool = False, device="cuda", x86: bool = False):
     """Generate a raw synthetic corpus directly in HBM (counter-based, so the
-    CPU twin in oracle/ reproduces it bit-for-bit)."""
+    CPU twin in oracle/ reproduces it bit-for-bit).  x86: PCs of the x86-like
+    universe (neighbours 5..11 bytes apart, kshift 2), else one per 16-byte
+    slot."""
     L = lib()
     dev = torch.device(device)
     lens = torch.empty(n, dtype=torch.int32, device=dev)
@@ -337,8 +339,8 @@ def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int
     torch.cumsum(lens.to(torch.int64), 0, out=off[1:])
     total = int(off[-1].item())
     pcs = torch.empty(total + 1, dtype=torch.int32, device=dev)
-    check(L.syzcov_dev_synth_pcs(seed, first, n, _p(off), log2_space, int(uniform), _p(pcs), s),
-          "synth_pcs")
+    check(L.syzcov_dev_synth_pcs(seed, first, n, _p(off), log2_space,
+                                 int(uniform) | (2 if x86 else 0), _p(pcs), s), "synth_pcs")
     return off, pcs, lens, total
 
 
@@ -419,13 +421,15 @@ def universe_keymap(universe, dev):
     return ks, kbase, nkeys, pc_of_key, low_of_key, int(uh[0]), int(uh[-1])
 
 
-def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda") -> torch.Tensor:
+def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda",
+                   x86: bool = False) -> torch.Tensor:
     """The synthetic generator's PC universe U[k], k < 2^log2_space (sorted;
-    it depends on the corpus seed)."""
+    it depends on the corpus seed; x86: the 5..11-byte-gap universe)."""
     u = torch.empty(1 << log2_space, dtype=torch.int32, device=device)
-    check(lib().syzcov_dev_synth_universe(seed, log2_space, _p(u), _stream()), "synth_universe")
+    check(lib().syzcov_dev_synth_universe_mode(seed, log2_space, 2 if x86 else 0, _p(u),
+                                               _stream()), "synth_universe")
     return u
 
 
-def synth_window(log2_space: int = 22):
-    return SYNTH_PC_LO, 16 << log2_space
+def synth_window(log2_space: int = 22, x86: bool = False):
+    return SYNTH_PC_LO, (8 if x86 else 16) << log2_space

@@ -3,6 +3,7 @@ oracle's digests (tests/golden/fullsize_digests.json, written by
 tools/gen_golden_fullsize.py from oracle/fullsize.c).
 
   C2  1M inputs, one GPU                      kept / union / order / lens digests
+  C2X C2 over the x86-like universe (kshift 2, 2^23 keys), both canon layouts
   C3  10M inputs (82 GB raw), one GPU         kept / union / order / lens digests
   C3  canonical lengths in 1M chunks + the 10M Go sort order on the device
   C2  world-8 sharded rehearsal on one GPU    kept / union / order digests
@@ -42,17 +43,18 @@ def torch():
     return t
 
 
-def _engine_vs_digest(torch, name, inplace, keys=True):
+def _engine_vs_digest(torch, name, inplace, keys=True, layout=0):
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     g = golden(name)
     n = g["n"]
+    x86 = bool(g.get("synth_mode", 0) & 2)
     off, raw, lens, total = synth_corpus(n, g["seed"], mean=g["mean"], sigma=g["sigma"],
-                                         log2_space=g["log2_space"])
+                                         log2_space=g["log2_space"], x86=x86)
     assert total == g["raw_pcs"]
-    lo, span = synth_window(g["log2_space"])
-    univ = synth_universe(g["log2_space"], g["seed"]) if keys else None
+    lo, span = synth_window(g["log2_space"], x86=x86)
+    univ = synth_universe(g["log2_space"], g["seed"], x86=x86) if keys else None
     eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, canon_in_place=inplace,
-                       universe=univ)
+                       universe=univ, canon_layout=layout)
     assert eng.key_mode == keys
     res = eng.step(off, raw, n)
     assert int(eng.new_len[:n].to(torch.int64).sum().item()) == g["canonical_pcs"]
@@ -76,6 +78,15 @@ def test_c2_fullsize_digest(torch, keys):
     g = golden("C2")
     res = eng.step(off, raw, g["n"])
     assert sha(res.kept_idx) == g["kept_sha256"] and sha(res.union) == g["union_sha256"]
+
+
+@pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
+def test_c2x_fullsize_digest(torch, layout):
+    """C2 over the x86-like universe (PCs 5..11 bytes apart): kshift 2, 2^23
+    dense keys (the 3-pass canon sort, 64 Minimize ranges) against the
+    oracle's C2X digests, canonical lists in both layouts."""
+    eng, off, raw = _engine_vs_digest(torch, "C2X", inplace=False, layout=layout)
+    assert eng.kshift == 2 and eng.span == (1 << 23) - 1 and eng.nrange == 64
 
 
 def test_c3_fullsize_digest(torch):

@@ -6,6 +6,7 @@ digests the GPU tests compare the engine against.
   C1  10k inputs   seed 0x5EED0001   (CPU-only config)
   C2  1M inputs    seed 0x5EED0002   (one MI355X; also the world-8 rehearsal)
   C3  10M inputs   seed 0x5EED0003   (the 8-GPU config; 82 GB of raw PCs)
+  C2X C2 over the x86-like universe (PCs 5..11 bytes apart: kshift 2, 2^23 keys)
   C5S the same stream over 514 batches (512 history, steady state)
   C2G Manager.minimizeCorpus over C2's RAW covers in 293 call groups
       (synthetic call ids; oracle/grouped_full.c): the kept corpus indices
@@ -41,6 +42,9 @@ CONFIGS = {
     "C1": dict(seed=0x5EED0001, n=10_000),
     "C2": dict(seed=0x5EED0002, n=1_000_000),
     "C3": dict(seed=0x5EED0003, n=10_000_000),
+    # C2 over the x86-like universe: 2^22 PCs 5..11 bytes apart, so kshift 2
+    # and 2^23 keys (synth mode bit 1)
+    "C2X": dict(seed=0x5EED0002, n=1_000_000, mode=2),
 }
 MEAN, SIGMA, LOG2 = 2048, 512, 22
 C5 = dict(seed=0x5EED0005, records=65536, batches=34, ncalls=293)
@@ -65,11 +69,13 @@ def run(name: str, threads: int) -> dict:
     with tempfile.TemporaryDirectory() as d:
         t0 = time.time()
         r = subprocess.run([exe, hex(cfg["seed"]), str(cfg["n"]), str(MEAN), str(SIGMA), str(LOG2),
-                            str(threads), d], check=True, capture_output=True, text=True)
+                            str(threads), d, str(cfg.get("mode", 0))], check=True,
+                           capture_output=True, text=True)
         summary = json.loads(r.stdout)
         kept = np.fromfile(os.path.join(d, "kept.i32"), dtype=np.int32)
         union = np.fromfile(os.path.join(d, "union.u32"), dtype=np.uint32)
         out = dict(seed=cfg["seed"], n=cfg["n"], mean=MEAN, sigma=SIGMA, log2_space=LOG2,
+                   synth_mode=cfg.get("mode", 0),
                    raw_pcs=summary["raw_pcs"], canonical_pcs=summary["canonical_pcs"],
                    n_kept=summary["n_kept"], kept_sha256=sha(os.path.join(d, "kept.i32")),
                    kept_head=kept[:16].tolist(), kept_tail=kept[-16:].tolist(),

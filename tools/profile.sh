@@ -32,6 +32,8 @@ if has corpus; then
   pmc_pair C3 "" "" $B --steps 1 --warmup 0
   trace C2 $B --global-inputs 1000000 --steps 10 --warmup 2
   pmc_pair C2 "" "" $B --global-inputs 1000000 --steps 1 --warmup 0
+  trace C2X $B --global-inputs 1000000 --x86 --steps 10 --warmup 2
+  pmc_pair C2X "" "" $B --global-inputs 1000000 --x86 --steps 1 --warmup 0
 fi
 if has canon; then
   i=0
