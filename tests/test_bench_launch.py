@@ -57,7 +57,7 @@ def test_same_workload_at_every_n(monkeypatch):
     import bench
     seen = {}
 
-    def fake_run(args, world, rank, dev, glob, seed, steps, warmup, key):
+    def fake_run(args, world, rank, dev, glob, seed, steps, warmup, key, x86=False):
         seen.update(glob=glob, seed=seed, key=key)
         return {"value": 1.0, "ms_per_step": 1.0, "inputs_per_gpu": glob, "raw_pcs_per_gpu": 0,
                 "aligned": True,
