@@ -447,6 +447,7 @@ def bench_corpus(args):
             out["c2x"] = cx
         if not args.no_dropin:
             out["dropin"] = dropin_legs(args, dev)
+            out["dropin"]["pairwise"] = pairwise_leg()
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         cb = out["cpu_baseline"] = cpu_baseline(args)
         out["vs_cpu"] = out["value"] / cb["value"]
@@ -547,6 +548,67 @@ def dropin_legs(args, dev):
         legs[name] = leg
         del h_pcs, h_off
     return legs
+
+
+def pairwise_leg(reps: int = 2000, nthreads: int = 32) -> dict:
+    """The drop-in per-call set ops on the fuzzer's list sizes: cover.Difference
+    and cover.Union (cover/cover.go:42-79) of two ~2k-PC canonical lists, as
+    syz-fuzzer calls Difference twice per executed call (fuzzer.go:465-466),
+    through syzcov_difference / syzcov_union (one device round trip each) from
+    1 thread and from `nthreads` concurrent threads, beside the oracle's merge
+    (C, 1 thread: Go's foreach loop)."""
+    import ctypes as C
+    import threading
+    import numpy as np
+    from oracle import oracle as orc
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(17)
+    pool = 0x81000000 + 16 * np.arange(1 << 16, dtype=np.uint32)
+    a = np.sort(rng.choice(pool, 2048, replace=False)).astype(np.uint32)
+    b = np.sort(np.concatenate([a[rng.random(a.size) < 0.95],
+                                rng.choice(pool, 100, replace=False)])).astype(np.uint32)
+    b = np.unique(b)
+    out = {}
+    for name, fn in (("difference", L.syzcov_difference), ("union", L.syzcov_union)):
+        def calls(k, o):
+            for _ in range(k):
+                fn(a.ctypes.data, a.size, b.ctypes.data, b.size, o.ctypes.data)
+        o = np.empty(a.size + b.size, np.uint32)
+        calls(50, o)  # the first call creates the context pool
+        t0 = time.perf_counter()
+        calls(reps, o)
+        t1 = time.perf_counter()
+        per = max(1, reps // nthreads)
+        outs = [np.empty(a.size + b.size, np.uint32) for _ in range(nthreads)]
+        th = [threading.Thread(target=calls, args=(per, outs[i])) for i in range(nthreads)]
+        t2 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        t3 = time.perf_counter()
+        # the oracle's merge (C: Go's foreach loop) on the same buffers, called
+        # like the library (pointers, preallocated output)
+        op = orc.DIFFERENCE if name == "difference" else orc.UNION
+        ol, co = orc.lib(), np.empty(a.size + b.size + 1, np.uint32)
+        ol.orc_setop(op, a.ctypes.data, a.size, b.ctypes.data, b.size, co.ctypes.data)
+        t4 = time.perf_counter()
+        for _ in range(reps):
+            ol.orc_setop(op, a.ctypes.data, a.size, b.ctypes.data, b.size, co.ctypes.data)
+        t5 = time.perf_counter()
+        out[name] = {"us_per_call_1_thread": round((t1 - t0) / reps * 1e6, 2),
+                     f"us_per_call_{nthreads}_threads": round((t3 - t2) / (per * nthreads) * 1e6, 2),
+                     "calls_per_s_1_thread": reps / (t1 - t0),
+                     f"calls_per_s_{nthreads}_threads": per * nthreads / (t3 - t2),
+                     "cpu_oracle_us_per_call": round((t5 - t4) / reps * 1e6, 2)}
+    L.syzcov_pool_trim()
+    out["lists"] = f"|a| = {a.size}, |b| = {b.size} canonical PCs (95% of a plus 100 others)"
+    out["note"] = ("one GPU round trip per call (2 H2D copies, a kernel, a D2H copy, a sync); "
+                   "both timings include the ctypes call (~1 us). The "
+                   "fuzzer's per-call checks belong on syzcov_newcov_batch / syzcov_state_triage "
+                   "(INTEGRATION.md)")
+    return out
 
 
 def bench_prio(args):
