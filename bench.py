@@ -97,7 +97,7 @@ def parse():
                     help="window offsets instead of the dense keys of the registered PC "
                          "universe (keys.hip), for the corpus engine and newcov's maxCover")
     ap.add_argument("--x86", action="store_true",
-                    help="corpus: the x86-like PC universe (neighbours 5..11 bytes apart, kshift 2) "
+                    help="corpus: the x86-like PC universe (neighbours 5..14 bytes apart, kshift 2) "
                          "instead of one PC per 16-byte slot; config name gets an X")
     ap.add_argument("--canon-layout", type=int, default=0, choices=[0, 1],
                     help="canonical lists: 0 CSR slots, 1 line-aligned sub-runs "
@@ -437,11 +437,11 @@ def bench_corpus(args):
             c2["seed"] = SEED
             out["c2"] = c2
         if not args.no_c2 and not (glob == C2_INPUTS and args.x86):
-            # C2 over an x86-like universe (PCs 5..11 bytes apart, kshift 2,
+            # C2 over an x86-like universe (PCs 5..14 bytes apart, kshift 2,
             # 2^23 keys): the canon's 3-pass sort and 64 Minimize ranges
             cx = corpus_run(args, 1, 0, dev, C2_INPUTS, SEED, max(args.steps, 10), args.warmup,
                             "C2X", x86=True)
-            cx["workload"] = ("C2X: C2 over the x86-like PC universe (neighbours 5..11 bytes "
+            cx["workload"] = ("C2X: C2 over the x86-like PC universe (neighbours 5..14 bytes "
                               "apart, kshift 2)")
             cx["seed"] = SEED
             out["c2x"] = cx

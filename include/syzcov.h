@@ -744,8 +744,9 @@ int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, uint64_t nby
 
 /* Synthetic corpus (integer-exact): lengths for inputs
  * [first, first+n), then PCs into CSR.  mode bit 0: uniform key draws (else
- * k = 2^S u^3); bit 1: the x86-like universe (neighbouring PCs 5..11 bytes
- * apart: U[k] = 0x81000000 + 8k + (h(k) & 3), kshift 2), else one PC per
+ * k = 2^S u^3); bit 1: the x86-like universe (neighbouring PCs 5..14 bytes
+ * apart: pairs per 16-byte block, U[2m] = 0x81000000 + 16m + a, U[2m+1] = U[2m] + 5 + b,
+ * kshift 2), else one PC per
  * 16-byte slot (U[k] = 0x81000000 + 16k + (h(k) & 15), kshift 4). */
 int syzcov_dev_synth_lens(uint64_t seed, uint64_t first, size_t n, uint32_t mean, uint32_t sigma,
                           uint32_t *lens, void *stream);

@@ -86,7 +86,7 @@ void orc_build_choice_table(const float *prios, const uint8_t *enabled, int C, i
 /* Synthetic corpus generator (integer-exact variant; see
  * syzkaller_amd/csrc/synth.hip for the device twin). */
 uint32_t orc_synth_len(uint64_t seed, uint64_t input, uint32_t mean, uint32_t sigma);
-/* mode bit 0: uniform key draws; bit 1: the x86-like universe (5..11-byte gaps) */
+/* mode bit 0: uniform key draws; bit 1: the x86-like universe (5..14-byte gaps) */
 void orc_synth_input(uint64_t seed, uint64_t input, uint32_t len, uint32_t log2_space,
                      int mode, uint32_t *out);
 uint32_t orc_synth_universe(uint64_t seed, uint32_t k);

@@ -8,7 +8,8 @@
  *   draw      k    = floor(2^S * u^3), u = x / 2^32, x = 32 hash bits  -> (x^3) >> (96 - S)
  *                    (every key < 2^S is reachable; S <= 32)
  *             (uniform variant: k = top S hash bits)
- *   x86 universe (mode bit 1): U[k] = 0x81000000 + 8k + (h(k) & 3), neighbours 5..11 B apart
+ *   x86 universe (mode bit 1): U[2m] = 0x81000000 + 16m + a, U[2m+1] = U[2m] + 5 + b,
+ *                (a, b) = 2-bit fields of h(m): neighbours 5..14 B apart, kshift 2
  * TEST INFRASTRUCTURE ONLY.
  */
 #include "oracle.h"
@@ -21,8 +22,12 @@ static uint64_t splitmix64(uint64_t x) {
 }
 
 uint32_t orc_synth_universe_mode(uint64_t seed, uint32_t k, int mode) {
+    if (mode & 2) { /* x86-like: pairs per 16-byte block, gaps 5..14 */
+        uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)(k >> 1));
+        return 0x81000000u + 16u * (k >> 1) + (uint32_t)(h & 3u) +
+               (k & 1u) * (5u + (uint32_t)((h >> 2) & 3u));
+    }
     uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)k);
-    if (mode & 2) return 0x81000000u + 8u * k + (uint32_t)(h & 3u); /* x86-like gaps 5..11 */
     return 0x81000000u + 16u * k + (uint32_t)(h & 15u);
 }
 

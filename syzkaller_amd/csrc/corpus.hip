@@ -1380,11 +1380,28 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
         if (i && hoff[i] < hoff[i - 1]) return SYZCOV_EINVAL;
         if (i) max_len = std::max<size_t>(max_len, hoff[i] - hoff[i - 1]);
     }
-    // groups: stable by call value (the reference's append order)
+    // groups: stable by call value (the reference's append order); a counting
+    // sort over the calls' value range (sys.CallCount values in practice), a
+    // stable comparison sort only for a sparse one
     std::vector<int32_t> perm(n);
-    for (size_t i = 0; i < n; i++) perm[i] = (int32_t)i;
-    std::stable_sort(perm.begin(), perm.end(),
-                     [&](int32_t a, int32_t b) { return call[a] < call[b]; });
+    {
+        int32_t cmin = INT32_MAX, cmax = INT32_MIN;
+        for (size_t i = 0; i < n; i++) {
+            cmin = std::min(cmin, call[i]);
+            cmax = std::max(cmax, call[i]);
+        }
+        const uint64_t span = (uint64_t)((int64_t)cmax - cmin) + 1;
+        if (span <= std::max<uint64_t>(1u << 16, 4 * (uint64_t)n)) {
+            std::vector<uint32_t> cnt(span + 1, 0);
+            for (size_t i = 0; i < n; i++) cnt[(uint64_t)((int64_t)call[i] - cmin) + 1]++;
+            for (uint64_t v = 0; v < span; v++) cnt[v + 1] += cnt[v];
+            for (size_t i = 0; i < n; i++) perm[cnt[(uint64_t)((int64_t)call[i] - cmin)]++] = (int32_t)i;
+        } else {
+            for (size_t i = 0; i < n; i++) perm[i] = (int32_t)i;
+            std::stable_sort(perm.begin(), perm.end(),
+                             [&](int32_t a, int32_t b) { return call[a] < call[b]; });
+        }
+    }
     std::vector<uint64_t> goff;
     std::vector<int64_t> lens(n);
     for (size_t i = 0; i < n; i++) {

@@ -7,13 +7,19 @@
 namespace syz {
 
 // SYNTH_X86 (mode bit 1): an x86-like universe, neighbouring KCOV return
-// addresses 5..11 bytes apart (8k + 0..3), so kshift 2 and about 2 keys per PC;
-// otherwise one PC per 16-byte slot (kshift 4, a key per PC).
+// addresses 5..14 bytes apart: PCs in pairs per 16-byte block, the first at
+// 16m + a, the second 5 + b bytes later (a, b < 4, hashed per pair), so some
+// pairs share an 8-byte block: kshift 2 and 2 keys per PC.  Otherwise one PC
+// per 16-byte slot (kshift 4, a key per PC).
 constexpr int SYNTH_UNIFORM = 1, SYNTH_X86 = 2;
 __device__ __forceinline__ uint32_t synth_universe(uint64_t seed, uint32_t k, int mode = 0) {
+    if (mode & SYNTH_X86) {
+        const uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)(k >> 1));
+        return 0x81000000u + 16u * (k >> 1) + (uint32_t)(h & 3u) +
+               (k & 1u) * (5u + (uint32_t)((h >> 2) & 3u));
+    }
     const uint64_t h = splitmix64(seed ^ 0xA0761D6478BD642Full ^ (uint64_t)k);
-    return (mode & SYNTH_X86) ? 0x81000000u + 8u * k + (uint32_t)(h & 3u)
-                              : 0x81000000u + 16u * k + (uint32_t)(h & 15u);
+    return 0x81000000u + 16u * k + (uint32_t)(h & 15u);
 }
 
 __global__ void synth_lens_kernel(uint64_t seed, uint64_t first, uint64_t n, uint32_t mean,

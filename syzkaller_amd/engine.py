@@ -328,7 +328,7 @@ def synth_corpus(n: int, seed: int, first: int = 0, mean: int = 2048, sigma: int
                  log2_space: int = 22, uniform: bool = False, device="cuda", x86: bool = False):
     """Generate a raw synthetic corpus directly in HBM (counter-based, so the
     CPU twin in oracle/ reproduces it bit-for-bit).  x86: PCs of the x86-like
-    universe (neighbours 5..11 bytes apart, kshift 2), else one per 16-byte
+    universe (neighbours 5..14 bytes apart, kshift 2), else one per 16-byte
     slot."""
     L = lib()
     dev = torch.device(device)
@@ -424,7 +424,7 @@ def universe_keymap(universe, dev):
 def synth_universe(log2_space: int = 22, seed: int = 0x5EED0002, device="cuda",
                    x86: bool = False) -> torch.Tensor:
     """The synthetic generator's PC universe U[k], k < 2^log2_space (sorted;
-    it depends on the corpus seed; x86: the 5..11-byte-gap universe)."""
+    it depends on the corpus seed; x86: the 5..14-byte-gap universe)."""
     u = torch.empty(1 << log2_space, dtype=torch.int32, device=device)
     check(lib().syzcov_dev_synth_universe_mode(seed, log2_space, 2 if x86 else 0, _p(u),
                                                _stream()), "synth_universe")

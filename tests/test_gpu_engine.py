@@ -21,12 +21,16 @@ def _to_np_u32(t):
 
 
 def test_synth_matches_cpu_twin(torch):
-    from syzkaller_amd.engine import synth_corpus
-    for uniform in (False, True):
-        off, pcs, lens, total = synth_corpus(300, 0x5EED0001, first=1000, uniform=uniform)
-        o_off, o_pcs = orc.synth_corpus(0x5EED0001, 300, first=1000, uniform=uniform)
+    from syzkaller_amd.engine import synth_corpus, synth_universe
+    for uniform, x86 in ((False, False), (True, False), (False, True), (True, True)):
+        off, pcs, lens, total = synth_corpus(300, 0x5EED0001, first=1000, uniform=uniform,
+                                             x86=x86)
+        o_off, o_pcs = orc.synth_corpus(0x5EED0001, 300, first=1000, uniform=uniform, x86=x86)
         assert np.array_equal(off.cpu().numpy().astype(np.uint64), o_off)
         assert np.array_equal(_to_np_u32(pcs)[:total], o_pcs[:total])
+    for x86 in (False, True):
+        assert np.array_equal(_to_np_u32(synth_universe(14, 0x5EED0001, x86=x86)),
+                              orc.synth_universe(0x5EED0001, 14, x86=x86))
 
 
 @pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])

@@ -82,7 +82,7 @@ def test_c2_fullsize_digest(torch, keys):
 
 @pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
 def test_c2x_fullsize_digest(torch, layout):
-    """C2 over the x86-like universe (PCs 5..11 bytes apart): kshift 2, 2^23
+    """C2 over the x86-like universe (PCs 5..14 bytes apart): kshift 2, 2^23
     dense keys (the 3-pass canon sort, 64 Minimize ranges) against the
     oracle's C2X digests, canonical lists in both layouts."""
     eng, off, raw = _engine_vs_digest(torch, "C2X", inplace=False, layout=layout)

@@ -6,7 +6,7 @@ digests the GPU tests compare the engine against.
   C1  10k inputs   seed 0x5EED0001   (CPU-only config)
   C2  1M inputs    seed 0x5EED0002   (one MI355X; also the world-8 rehearsal)
   C3  10M inputs   seed 0x5EED0003   (the 8-GPU config; 82 GB of raw PCs)
-  C2X C2 over the x86-like universe (PCs 5..11 bytes apart: kshift 2, 2^23 keys)
+  C2X C2 over the x86-like universe (PCs 5..14 bytes apart: kshift 2, 2^23 keys)
   C5S the same stream over 514 batches (512 history, steady state)
   C2G Manager.minimizeCorpus over C2's RAW covers in 293 call groups
       (synthetic call ids; oracle/grouped_full.c): the kept corpus indices
@@ -42,7 +42,7 @@ CONFIGS = {
     "C1": dict(seed=0x5EED0001, n=10_000),
     "C2": dict(seed=0x5EED0002, n=1_000_000),
     "C3": dict(seed=0x5EED0003, n=10_000_000),
-    # C2 over the x86-like universe: 2^22 PCs 5..11 bytes apart, so kshift 2
+    # C2 over the x86-like universe: 2^22 PCs 5..14 bytes apart, so kshift 2
     # and 2^23 keys (synth mode bit 1)
     "C2X": dict(seed=0x5EED0002, n=1_000_000, mode=2),
 }

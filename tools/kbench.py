@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Kernel micro-bench on the C2 corpus: times one engine phase at a time.
-    python tools/kbench.py canon|minimize|step|order|dedup [--keys] [--inputs N] [--reps R]
+    python tools/kbench.py canon|minimize|step|order|dedup|groups [--keys] [--inputs N] [--reps R]
+groups: syzcov_minimize_corpus (293 call groups) and syzcov_minimize from host
+buffers of the C2 corpus, wall time per call.
 dedup: the executor's cover_dedup (executor.cc:574-587) over N raw u64 KCOV
 buffers made of the C2 generator's raw PCs (high half 0xffffffff), in place,
 with the u32 output words; the buffers are restored outside the events."""
@@ -46,6 +48,35 @@ def main():
             e.record()
             torch.cuda.synchronize()
             print(f"order: {s.elapsed_time(e):.3f} ms  n={n}", flush=True)
+        return
+    if a.what == "groups":  # Manager.minimizeCorpus drop-in from host buffers (C2 + call ids)
+        import ctypes as C
+        import numpy as np
+        from syzkaller_amd._lib import check, lib
+        L = lib()
+        off, raw, lens, total = synth_corpus(n, 0x5EED0002, mean=a.mean, sigma=a.sigma,
+                                             log2_space=a.log2_space)
+        h_off = off.cpu().numpy().astype(np.uint64)
+        h_pcs = raw[:total].cpu().numpy().view(np.uint32)
+        cid = torch.empty(n, dtype=torch.int32, device="cuda")
+        check(L.syzcov_dev_synth_callids(0x5EED0002, 0, n, 293, C.c_void_p(cid.data_ptr()),
+                                         C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "synth_callids")
+        calls = cid.cpu().numpy()
+        del off, raw, lens, cid
+        torch.cuda.empty_cache()
+        out = np.empty(n, np.int32)
+        for r in range(a.reps + 1):
+            t0 = time.perf_counter()
+            k = check(L.syzcov_minimize_corpus(calls.ctypes.data, h_off.ctypes.data,
+                                               h_pcs.ctypes.data, n, 0, out.ctypes.data),
+                      "minimize_corpus")
+            t1 = time.perf_counter()
+            k1 = check(L.syzcov_minimize(h_off.ctypes.data, h_pcs.ctypes.data, n, None, 0,
+                                         out.ctypes.data), "minimize")
+            t2 = time.perf_counter()
+            print(f"groups: minimize_corpus {1e3 * (t1 - t0):.1f} ms (kept {k}), "
+                  f"minimize {1e3 * (t2 - t1):.1f} ms (kept {k1})", flush=True)
         return
     if a.what == "dedup":
         import ctypes as C
