@@ -456,6 +456,255 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
     if (KEYM && __ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
 }
 
+// Key mode pass 1 (the corpus engine's path), the chunk stream above with
+// fewer vector operations per PC (pass 1 measured VALU-bound: ~18 VALU
+// instructions per PC per lane, 57% of wave cycles waiting, at C2):
+//  - 32-byte lane chunks (two 16-byte loads), so the per-chunk item lookup
+//    (marks, DPP prefix max, descriptor reads) is paid once per 8 PCs;
+//  - the staged byte is low | UNcovered << 7 (bit 7 set for a key no earlier
+//    chunk covered), so "covered and a universe PC" is one compare of the
+//    byte with the word's low bits: the byte index is the word & (2^17 - 1)
+//    (key - range base, the low bits above bit 25 masked off), and the common
+//    case (every PC covered and valid) costs an and, a shift, a compare and the
+//    element's bounds test;
+//  - anything else (uncovered: a record; covered but not the universe PC:
+//    SYZCOV_ERR_UNIVERSE) is sorted out on a rare, wave-uniform slow path.
+// A record's membership is checked there too (its byte's low 7 bits).
+template <int UG>
+__global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a, uint32_t b,
+                                                             uint32_t P, int load_cov) {
+    constexpr uint32_t CW = 8;  // words per lane chunk
+    // one dynamic block, the range's table at LDS address 0 so that a
+    // table read is ds_read_u8 of (word & mask) with no base add; then
+    // (KEYS_LDS_EXTRA bytes) the wave descriptors and the piece plan
+    extern __shared__ uint32_t s_cov[];
+    auto *s_a0 = reinterpret_cast<uint64_t(*)[64]>(
+        reinterpret_cast<uint8_t *>(s_cov) + ((size_t)1 << 17));   // 32-byte aligned base
+    auto *s_he = reinterpret_cast<uint32_t(*)[64]>(s_a0 + NWAVE);  // (end << 3) | head
+    auto *s_ex = s_he + NWAVE;                                     // first chunk of the item
+    auto *s_rk = reinterpret_cast<int32_t(*)[64]>(s_ex + NWAVE);
+    auto *s_own = reinterpret_cast<uint32_t(*)[64]>(s_rk + NWAVE); // item + 1 per chunk
+    uint32_t *s_plan = reinterpret_cast<uint32_t *>(s_own + NWAVE);
+    uint32_t &s_next = s_plan[MAX_R + 1];
+    const uint32_t G = A.npieces;
+    s_own[threadIdx.x >> 6][__lane_id()] = 0u;
+    plan_pieces(A, G, P, s_plan);
+    const uint32_t region = blockIdx.x % NCTR;
+    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
+    unsigned long long *const rrec = A.rec + region * A.cap_k;
+    const uint8_t *const s_cov8 = reinterpret_cast<const uint8_t *>(s_cov);
+    const uint32_t bmask = (1u << A.rshift) - 1u;
+    uint32_t cur_rho = 0xFFFFFFFFu;
+    uint32_t nonmem = 0;
+    for (;;) {
+    if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+    __syncthreads();
+    uint32_t g = s_next;
+    __syncthreads();
+    if (g >= G) break;
+    {
+        const uint32_t S = G / P;  // range-major: g = position * S + slice
+        g = (g % S) * P + g / S;
+    }
+    uint32_t rho, i0, i1;
+    if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
+    if (rho != cur_rho) {  // table bytes | UNcovered << 7, 16 keys per uint4
+        uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
+        const uint32_t nq = (1u << A.rshift) >> 4;
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
+        const uint32_t *cw = A.covered + ((uint64_t)rho << A.rshift) / 32;
+        auto spread = [](uint32_t x) {  // bit i -> bit 8i + 7
+            return ((x & 1u) << 7) | ((x & 2u) << 14) | ((x & 4u) << 21) | ((x & 8u) << 28);
+        };
+        for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
+            uint4 t = t4[q];
+            const uint32_t ub =
+                load_cov ? ~(cw[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu : 0xFFFFu;
+            t.x |= spread(ub);
+            t.y |= spread(ub >> 4);
+            t.z |= spread(ub >> 8);
+            t.w |= spread(ub >> 12);
+            s4[q] = t;
+        }
+        cur_rho = rho;
+        __syncthreads();
+    }
+    const uint32_t l = __lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+    const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+    uint32_t d_s0 = 0, d_s1 = 0;
+    uint64_t d_base = 0;
+    int32_t d_rk = 0;
+    auto load_desc = [&](uint32_t ib_) {
+        const uint32_t item = ib_ + l;
+        d_s0 = d_s1 = 0;
+        d_base = 0;
+        d_rk = 0;
+        if (item < w1) {
+            d_rk = A.ranks ? A.ranks[item] : (int32_t)item;
+            d_s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            d_s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            d_base = A.base_r[item];
+        }
+    };
+    if (w0 < w1) load_desc(w0);
+    for (uint32_t ib = w0; ib < w1; ib += 64) {
+        const uint32_t item = ib + l;
+        uint32_t m = 0, nch = 0, he = 0;
+        uint64_t a0 = 0;
+        const int32_t rk = d_rk;
+        if (item < w1) {
+            const uint64_t st = d_base + aligned_sub(d_s0, rho, A.ak);
+            m = d_s1 - d_s0;
+            a0 = st & ~7ull;
+            const uint32_t head = (uint32_t)(st - a0);
+            he = ((head + m) << 3) | head;
+            nch = m ? (head + m + CW - 1) / CW : 0u;
+        }
+        if (ib + 64 < w1) load_desc(ib + 64);
+        const uint32_t incl = wave_incl_scan(nch);
+        const uint32_t ex_l = incl - nch;
+        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        s_a0[w][l] = a0;
+        s_he[w][l] = he;
+        s_ex[w][l] = ex_l;
+        s_rk[w][l] = rk;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t sj = 0;
+        uint4 v0[UG], v1[UG];
+        uint32_t cj[UG], co[UG], hv[UG];
+        auto issue = [&](uint32_t c0, uint4 (&d0)[UG], uint4 (&d1)[UG], uint32_t (&dj)[UG],
+                         uint32_t (&dc)[UG], uint32_t (&dh)[UG]) {
+            uint32_t jj[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t cb = c0 + u * 64;
+                const uint32_t c = cb + l;
+                if (ex_l - cb < 64u) atomicMax(&s_own[w][ex_l - cb], l + 1u);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mk = s_own[w][l];
+                s_own[w][l] = 0u;
+                const uint32_t pm = wave_incl_max(mk);
+                const uint32_t j = pm ? max(sj, pm - 1u) : sj;
+                sj = __builtin_amdgcn_readlane(j, 63);
+                jj[u] = j;
+                dj[u] = c < tot ? j : 64u;
+            }
+            uint64_t ba[UG];
+            uint32_t bx[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                ba[u] = s_a0[w][jj[u]];
+                bx[u] = s_ex[w][jj[u]];
+                dh[u] = s_he[w][jj[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t c = c0 + u * 64 + l;
+                dc[u] = dj[u] < 64 ? c - bx[u] : 0u;  // past the end: chunk 0, never tested
+                const uint4 *p = reinterpret_cast<const uint4 *>(A.pcs + ba[u]) + 2 * dc[u];
+                d0[u] = p[0];
+                // the second half only if it holds words of the sub-run (no
+                // read further past a sub-run's end than a 16-byte chunk's)
+                d1[u] = p[dc[u] * CW + 4 < (dh[u] >> 3) ? 1 : 0];
+            }
+        };
+        issue(0, v0, v1, cj, co, hv);
+        for (uint32_t c0 = 0; c0 < tot; c0 += 64 * UG) {
+            uint4 n0[UG], n1[UG];
+            uint32_t nj[UG], nc[UG], nh[UG];
+            issue(c0 + 64 * UG, n0, n1, nj, nc, nh);
+            const uint32_t bm = issue_fence(bmask);
+            uint32_t wd[UG * CW], tb[UG * CW];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t vv[CW] = {v0[u].x, v0[u].y, v0[u].z, v0[u].w,
+                                         v1[u].x, v1[u].y, v1[u].z, v1[u].w};
+#pragma unroll
+                for (int k = 0; k < (int)CW; k++) {
+                    wd[u * CW + k] = vv[k];
+                    tb[u * CW + k] = s_cov8[vv[k] & bm];
+                }
+            }
+            // element k of a lane's chunk is in its sub-run iff lo <= k < hi
+            int lo[UG];
+            uint32_t span[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                lo[u] = (int)(hv[u] & 7u) - (int)(co[u] * CW);
+                const int hi = cj[u] < 64 ? (int)(hv[u] >> 3) - (int)(co[u] * CW) : lo[u];
+                span[u] = (uint32_t)(hi - lo[u]);
+            }
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < UG; u++)
+#pragma unroll
+                for (int k = 0; k < (int)CW; k++)
+                    any |= ((uint32_t)(k - lo[u]) < span[u]) &
+                           (tb[u * CW + k] != (wd[u * CW + k] >> SYZ_KEY_BITS));
+            if (__ballot(any)) {  // rare once the early chunks are done
+                uint32_t um = 0;  // records: uncovered elements
+#pragma unroll
+                for (int u = 0; u < UG; u++)
+#pragma unroll
+                    for (int k = 0; k < (int)CW; k++) {
+                        const uint32_t t = tb[u * CW + k], lw = wd[u * CW + k] >> SYZ_KEY_BITS;
+                        const uint32_t in = (uint32_t)((uint32_t)(k - lo[u]) < span[u]) &
+                                            (uint32_t)(t != lw);
+                        nonmem |= in & (uint32_t)((t & 0x7Fu) != lw);
+                        um |= (in & (t >> 7)) << (u * CW + k);
+                    }
+                if (__ballot(um != 0)) {
+                    const uint32_t cnt = (uint32_t)__popc(um);
+                    const uint32_t inc2 = wave_incl_scan(cnt);
+                    const uint32_t t2 = __shfl(inc2, 63, 64);
+                    unsigned long long basei = 0;
+                    if (l == 0) basei = atomicAdd(rctr, (unsigned long long)t2);
+                    uint64_t slot = __shfl(basei, 0, 64) + (inc2 - cnt);
+                    if (um) {
+#pragma unroll
+                        for (int u = 0; u < UG; u++) {
+                            if (!((um >> (u * CW)) & 0xFFu)) continue;
+                            const int32_t rki = s_rk[w][cj[u]];
+                            A.cand[ib + cj[u]] = 1;
+#pragma unroll
+                            for (int k = 0; k < (int)CW; k++)
+                                if ((um >> (u * CW + k)) & 1u) {
+                                    const uint32_t wo = wd[u * CW + k] & SYZ_KEY_MASK;
+                                    if (slot < A.cap_k)
+                                        rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
+                                    else  // no room: its min cannot wait
+                                        atomicMin(&A.first_w[wo], rki);
+                                    slot++;
+                                }
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                v0[u] = n0[u];
+                v1[u] = n1[u];
+                cj[u] = nj[u];
+                co[u] = nc[u];
+                hv[u] = nh[u];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    }
+    if (__ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
+}
+
+// dynamic LDS of pass1_keys_kernel past its 2^17-byte table
+constexpr size_t KEYS_LDS_EXTRA =
+    NWAVE * 64 * (8 + 4 * 4) + (MAX_R + 2) * 4;
+
 // Region loops: block b serves region b % NCTR (the grid is a multiple of
 // NCTR), records [lo_k, min(ctr_k, cap_k)) of it.
 #define SYZ_FOR_RECORDS(A, LO, i, r)                                                          \
@@ -726,9 +975,24 @@ static int minimize_range_impl(
                        (uint64_t *)A.base_r, (uint32_t *)A.split_t);
     const size_t lds = ((size_t)1 << range_shift) / (keym ? 1 : 8);
     using K = void (*)(mr::Args, uint32_t, uint32_t, uint32_t, int);
+#ifndef SYZ_MR_KEYS_UG
+#define SYZ_MR_KEYS_UG 2
+#endif
+#ifndef SYZ_MR_OLD_KEYS
+    const K k1 = keym ? mr::pass1_keys_kernel<SYZ_MR_KEYS_UG> : mr::pass1_stream_kernel<2, false>;
+#else
     const K k1 = keym ? mr::pass1_stream_kernel<2, true> : mr::pass1_stream_kernel<2, false>;
+#endif
     static std::atomic<uint32_t> attr_set[2];
-    if ((rc = set_dyn_lds_once((const void *)k1, 128 * 1024, attr_set[keym ? 1 : 0]))) return rc;
+#ifndef SYZ_MR_OLD_KEYS
+    // (the table at LDS 0 holds 2^range_shift <= 2^17 bytes, the rest past 2^17)
+    const size_t lds1 = keym ? ((size_t)1 << 17) + mr::KEYS_LDS_EXTRA : lds;
+#else
+    const size_t lds1 = lds;
+#endif
+    if ((rc = set_dyn_lds_once((const void *)k1, (uint32_t)std::max<size_t>(lds1, 128 * 1024),
+                               attr_set[keym ? 1 : 0])))
+        return rc;
 #ifndef SYZ_MR_FIRST
 #define SYZ_MR_FIRST 64
 #endif
@@ -770,7 +1034,7 @@ static int minimize_range_impl(
             A.npieces = (uint32_t)G;
             const unsigned grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
             nchunk++;
-            hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds, s, A, (uint32_t)a,
+            hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds1, s, A, (uint32_t)a,
                                (uint32_t)b, (uint32_t)P, (int)(a != a0));
             // the chunk's first covers (+ covered, unless rebuilt below)
             hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
