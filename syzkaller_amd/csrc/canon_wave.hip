@@ -109,6 +109,9 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
 #ifndef SYZ_CANON_BQ
 #define SYZ_CANON_BQ 2
 #endif
+#ifndef SYZ_CANON_BQ_AL
+#define SYZ_CANON_BQ_AL SYZ_CANON_BQ
+#endif
 // Only REAL keys take part: slots outside the segment (the aligned head, the
 // tail of the last row quad) are skipped rather than ranked as maximal pads,
 // which would all hit ONE histogram address (serialised same-address LDS
@@ -639,7 +642,7 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
     }
 }
 
-template <int NK, int MINW, int BQK = SYZ_CANON_BQ>
+template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, const uint32_t *list,
                                                                    const uint32_t *count) {
     constexpr int CAP = 64 * NK;
@@ -795,11 +798,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = sent_g, dcar = 0;
+        uint32_t cnt = 0, carry = sent_g;
         uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
-        // gapped key bits of the range index: a word starts a range iff they
-        // differ from its predecessor's (or it is the first kept word)
-        const uint32_t rmask = GAP_KEY_MASK & ~((2u << P.rshift) - 1u);
+        constexpr bool direct = !ALIGNED;  // line-aligned: written from buf below
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
@@ -812,19 +813,14 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     // whole words: distinct PCs stay distinct even if they share a key
                     const bool keep = v != prev;
                     const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
-                    const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
-                                                   (uint32_t)(m >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    const uint32_t w = ungap_word(v);
-                    uint32_t delta = 0;
-                    if (P.ak) {  // uniform
-                        const uint64_t sm = __builtin_amdgcn_ballot_w64(
-                            keep && (pos == 0 || ((v ^ prev) & rmask) != 0));
-                        delta = aligned_delta(sm, pos, (w & KEY_MASK) >> P.rshift, P.ak, l, dcar);
-                    }
                     if (keep) {
-                        outp[pos + delta] = w;  // the key word: the PC is kept exactly
-                        buf[pos] = w;           // (the split search masks the key)
+                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
+                                                       (uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const uint32_t w = ungap_word(v);
+                        // the key word: the PC is kept exactly (line-aligned: from buf below)
+                        if (direct) outp[pos] = w;
+                        buf[pos] = w;  // (the split search masks the key)
                     }
                     cnt += (uint32_t)__popcll(m);
                 }
@@ -855,11 +851,25 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         s2 = lo2;
                     }
                     const uint32_t prev_s = __shfl_up(s2, 1, 64);
-                    const uint32_t c2 = s2 - (l == 0 ? carry2 : prev_s);
+                    const uint32_t sprev = l == 0 ? carry2 : prev_s;  // keys below range j
+                    const uint32_t c2 = s2 - sprev;
                     carry2 = __shfl(s2, 63, 64);
                     if (j < P.nrange) {
                         sp[j] = s2;
                         racc[q] += c2;
+                        // line-aligned: range j's words move up by this much (the
+                        // histogram is free once the sort is done)
+                        if (!direct) h[j] = aligned_sub(sprev, j, P.ak) - sprev;
+                    }
+                }
+            }
+            if (!direct) {  // the sorted words from buf to their aligned sub-runs
+                wave_sync();
+                for (uint32_t p0 = 0; p0 < cnt; p0 += 64) {
+                    const uint32_t p = p0 + l;
+                    if (p < cnt) {
+                        const uint32_t w = buf[p];
+                        outp[p + h[(w & KEY_MASK) >> P.rshift]] = w;
                     }
                 }
             }
@@ -996,7 +1006,7 @@ static unsigned resident_grid(uint64_t nseg) {
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, cap));
 }
 
-template <int NK, int MW>
+template <int NK, int MW, bool AL>
 static unsigned resident_grid_key(uint64_t nseg) {
     static unsigned cap = 0;
     if (!cap) {
@@ -1006,8 +1016,8 @@ static unsigned resident_grid_key(uint64_t nseg) {
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess) ncu = pr.multiProcessorCount;
         }
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void *>(cw::canon_key_kernel<NK, MW>), 64 * cw::WPB,
-                0) != hipSuccess || nb < 1)
+                &nb, reinterpret_cast<const void *>(cw::canon_key_kernel<NK, MW, AL>),
+                64 * cw::WPB, 0) != hipSuccess || nb < 1)
             nb = 1;
         cap = (unsigned)(nb * ncu);
     }
@@ -1017,8 +1027,14 @@ static unsigned resident_grid_key(uint64_t nseg) {
 template <int NK, int MW>
 static void launch_key_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
                              uint64_t nseg, hipStream_t s) {
-    hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW>), dim3(resident_grid_key<NK, MW>(nseg)),
-                       dim3(64 * cw::WPB), 0, s, P, lc, cnt);
+    if (P.ak)  // line-aligned sub-runs: a separate build of the kernel (no per-word branch)
+        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, true>),
+                           dim3(resident_grid_key<NK, MW, true>(nseg)), dim3(64 * cw::WPB), 0, s,
+                           P, lc, cnt);
+    else
+        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, false>),
+                           dim3(resident_grid_key<NK, MW, false>(nseg)), dim3(64 * cw::WPB), 0,
+                           s, P, lc, cnt);
 }
 
 extern "C" size_t syzcov_dev_canon_split_ws_size(size_t nseg) {
