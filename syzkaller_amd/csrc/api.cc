@@ -47,6 +47,7 @@ uint32_t force_flags() {
     if (strstr(e, "redo")) f |= FORCE_REDO;
     if (strstr(e, "nc_lds")) f |= FORCE_NC_LDS;
     if (strstr(e, "nc_probe")) f |= FORCE_NC_PROBE;
+    if (strstr(e, "group_chunks")) f |= FORCE_GROUP_CHUNKS;
     return f;
 }
 

@@ -1362,6 +1362,9 @@ static int64_t dropin_run(DropinCache &dc, const uint64_t *offsets, const uint32
 int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
                           uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
                           hipStream_t s);
+static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, const uint64_t *d_off,
+                          uint32_t *d_pcs, const int32_t *d_ordc, const uint64_t *d_goff,
+                          uint32_t lo, uint32_t hi, int32_t *out_idx, hipStream_t s);
 
 // Manager.minimizeCorpus (manager.go:504-524) on the cached engine: the
 // corpus is staged as it is; the groups (inputs of one RpcInput.Call, corpus
@@ -1370,6 +1373,15 @@ int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint6
 // gosort.hip) — so the engine canonicalizes once and runs one Minimize per
 // group over its rank interval (minimize_range_groups).  Kept corpus indices
 // come out grouped by ascending call value, each group in its Minimize order.
+int universe_shift_dev(const uint32_t *u, uint32_t n, uint32_t *d_ks, hipStream_t s);
+size_t minimize_groups_lds_ws_size(size_t n_items, uint64_t nkeys, uint32_t range_shift);
+int minimize_groups_lds(const uint64_t *off, const uint32_t *words, const uint32_t *split,
+                        const int32_t *order, size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                        const uint64_t *goff_dev, uint32_t ngroups, uint8_t *kept, void *ws,
+                        hipStream_t s);
+constexpr uint32_t kGroupLdsMaxItems = 1u << 16;  // minimize_range.hip GM_MAX_ITEMS
+constexpr uint32_t kGroupLdsShift = 15;           // keys per LDS piece: 2^15 ranks
+
 static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uint64_t *offsets,
                                  const uint32_t *pcs, size_t n, int32_t *out_idx, hipStream_t s) {
     const uint64_t base = offsets[0], P = offsets[n] - base;
@@ -1445,6 +1457,14 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
         rc = minimize_groups_order(d_ordg, d_perm, d_goff, G, (uint32_t)n, d_ordc,
                                    (uint32_t *)(st + o_rg), s);
     if (rc) return rc;
+    uint64_t gmax = 0;
+    for (uint32_t g = 0; g < G; g++) gmax = std::max<uint64_t>(gmax, goff[g + 1] - goff[g]);
+    if (gmax <= kGroupLdsMaxItems && !(force_flags() & FORCE_GROUP_CHUNKS)) {
+        const int64_t k = groups_lds(n, P, max_len, G, d_off, d_pcs, d_ordc, d_goff, mm[0], mm[1],
+                                     out_idx, s);
+        if (k != 0) return k;  // taken (or failed); 0: the per-group engine below
+        SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
+    }
     rc = dropin_handle(dc, n, P, max_len, mm[0], mm[1]);
     if (rc <= 0) return rc;
     Corpus &c = *get(dc.h);
@@ -1462,6 +1482,114 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
                  : SYZCOV_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = SYZCOV_EHIP;
     return rc ? rc : (int64_t)r.n_kept + 1;
+}
+
+
+// Manager.minimizeCorpus with every group small (<= 2^16 inputs, as a
+// corpus of ~10^5-10^6 inputs over a few thousand syscalls has): the corpus
+// is staged (d_off, d_pcs raw), grouped and ordered (d_ordc: rank -> input,
+// d_goff: the groups' rank intervals).  The union of the corpus (a window-
+// mode step on a transient handle, canon out of place) is its own PC
+// universe: its kshift makes the keys (pc >> kshift) - kbase collision-free
+// on every corpus PC, so key words need no membership check.  The raw lists
+// are canonicalized into key words over ranges of 2^15 keys and every (group,
+// range) piece takes its first covers in LDS (group_min_kernel): no chunks,
+// no records, no per-group launches.  Returns kept + 1 (0: not taken).
+static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, const uint64_t *d_off,
+                          uint32_t *d_pcs, const int32_t *d_ordc, const uint64_t *d_goff,
+                          uint32_t lo, uint32_t hi, int32_t *out_idx, hipStream_t s) {
+    syzcov_corpus_cfg cfg{};
+    cfg.n_max = n;
+    cfg.p_max = P;
+    cfg.max_seg_len = max_len;
+    cfg.pc_lo = lo;
+    cfg.pc_span = (uint64_t)hi - lo + 1;
+    cfg.order_by = 1;
+    syzcov_corpus h = 0;
+    int rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
+    if (rc) return rc == SYZCOV_ENOMEM || rc == SYZCOV_ERANGE ? 0 : rc;
+    Corpus &c = *get(h);
+    int64_t ret = 0;
+    void *scratch = nullptr;
+    do {
+        // (1) the corpus union: one window-mode Minimize (its own order)
+        rc = ph_canon(c, d_off, d_pcs, n, s);
+        if (!rc) rc = ph_order(c, nullptr, n, s);
+        if (!rc) rc = ph_minimize(c, 1, s);
+        if (!rc) rc = ph_finish(c, s);
+        syzcov_corpus_res r{};
+        if (!rc) rc = ph_result(c, &r, s);
+        if (rc) break;
+        // the union drops PC 0xFFFFFFFF (cover.go:97); the universe keeps it
+        const uint32_t nu = r.n_union + (hi == 0xFFFFFFFFu ? 1u : 0u);
+        if (nu == 0) { rc = SYZCOV_EHIP; break; }
+        uint32_t *univ = c.buf<uint32_t>(SYZCOV_CORPUS_UNION);  // sized span + 1 >= nu
+        if (r.union_pcs != univ) break;  // (no side buffer in window mode: not taken)
+        if (hi == 0xFFFFFFFFu) {
+            const uint32_t sent = 0xFFFFFFFFu;
+            SYZ_HIP(hipMemcpyAsync(univ + r.n_union, &sent, 4, hipMemcpyHostToDevice, s));
+        }
+        uint32_t *d_ks = (uint32_t *)(scal(c) + SC_MM);
+        if ((rc = universe_shift_dev(univ, nu, d_ks, s))) break;
+        uint32_t ks = 0, ends[2];
+        SYZ_HIP(hipMemcpyAsync(&ks, d_ks, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipMemcpyAsync(&ends[0], univ, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipMemcpyAsync(&ends[1], univ + nu - 1, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+        ks = std::min<uint32_t>(ks, SYZCOV_KSHIFT_MAX);
+        const uint32_t kbase = ends[0] >> ks;
+        const uint64_t nkeys = (uint64_t)(ends[1] >> ks) - kbase + 1;
+        if (nkeys > (1ull << 25)) break;  // key words: keys < 2^25
+        // (2) key words over ranges of 2^15 keys (out of place: CANON)
+        const uint64_t R = (nkeys + (1ull << kGroupLdsShift) - 1) >> kGroupLdsShift;
+        if (R > 256) break;  // minimize_range.hip MAX_R: not taken
+        const size_t o_nl = 0, o_split = align_up((n + 1) * 4, 256),
+                     o_rt = o_split + align_up(n * R * 4, 256), o_err = o_rt + align_up(R * 8, 256),
+                     o_kept = o_err + 256, o_out = o_kept + align_up(n, 256),
+                     o_cnt = o_out + align_up(n * 4, 256), o_ws = o_cnt + 256,
+                     ws_sz = std::max({syzcov_dev_canon_split_ws_size(n),
+                                       minimize_groups_lds_ws_size(n, nkeys, kGroupLdsShift),
+                                       syzcov_dev_compact_ws_size(n)}),
+                     need = o_ws + align_up(ws_sz, 256);
+        if (hipMalloc(&scratch, need) != hipSuccess) {
+            scratch = nullptr;
+            break;  // short of memory: not taken
+        }
+        uint8_t *sc8 = (uint8_t *)scratch;
+        uint32_t *nl = (uint32_t *)(sc8 + o_nl), *split = (uint32_t *)(sc8 + o_split);
+        uint32_t *err = (uint32_t *)(sc8 + o_err);
+        uint8_t *kept = sc8 + o_kept;
+        int32_t *d_out = (int32_t *)(sc8 + o_out);
+        uint32_t *d_cnt = (uint32_t *)(sc8 + o_cnt);
+        SYZ_HIP(hipMemsetAsync(sc8 + o_rt, 0, R * 8 + 256, s));  // range totals, err
+        uint32_t *words = c.buf<uint32_t>(SYZCOV_CORPUS_CANON);
+        rc = syzcov_dev_canon_split_keys(d_off, d_pcs, words, nl, n, max_len, ends[0],
+                                         (uint64_t)ends[1] - ends[0] + 1, ks, kbase, nkeys,
+                                         kGroupLdsShift, split, (uint64_t *)(sc8 + o_rt), err,
+                                         sc8 + o_ws, ws_sz, s);
+        // (3) first covers per (group, range) in LDS; kept by rank
+        if (!rc)
+            rc = minimize_groups_lds(d_off, words, split, d_ordc, n, nkeys, kGroupLdsShift, d_goff,
+                                     G, kept, sc8 + o_ws, s);
+        if (!rc) rc = syzcov_dev_compact_kept(kept, d_ordc, n, d_out, d_cnt, sc8 + o_ws, s);
+        if (rc) break;
+        uint32_t hk[2];
+        SYZ_HIP(hipMemcpyAsync(&hk[0], d_cnt, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipMemcpyAsync(&hk[1], err, 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+        if (hk[1]) {  // every corpus PC is in its own union: cannot happen
+            set_error("grouped minimize: canonicalize flags %#x", hk[1]);
+            rc = SYZCOV_EHIP;
+            break;
+        }
+        if (hk[0]) SYZ_HIP(hipMemcpyAsync(out_idx, d_out, (size_t)hk[0] * 4, hipMemcpyDeviceToHost, s));
+        SYZ_HIP(hipStreamSynchronize(s));
+        ret = (int64_t)hk[0] + 1;
+    } while (0);
+    hipStreamSynchronize(s);
+    if (scratch) hipFree(scratch);
+    syzcov_corpus_destroy(h);
+    return rc ? rc : ret;
 }
 
 int minimize_corpus_via_engine(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,

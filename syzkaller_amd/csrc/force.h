@@ -4,6 +4,12 @@
 #include <stdint.h>
 
 namespace syz {
-enum : uint32_t { FORCE_CANON3 = 1u, FORCE_REDO = 2u, FORCE_NC_LDS = 4u, FORCE_NC_PROBE = 8u };
+enum : uint32_t {
+    FORCE_CANON3 = 1u,
+    FORCE_REDO = 2u,
+    FORCE_NC_LDS = 4u,
+    FORCE_NC_PROBE = 8u,
+    FORCE_GROUP_CHUNKS = 16u,  // minimizeCorpus: the per-group chunked engine for small groups too
+};
 uint32_t force_flags();
 }  // namespace syz

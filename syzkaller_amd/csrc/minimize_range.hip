@@ -701,6 +701,125 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     if (__ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
 }
 
+// Manager.minimizeCorpus (syz-manager/manager.go:504-524) when every call
+// group is small: per group, exact first covers in LDS, with no chunks and
+// no records.  Piece (g, rho): a workgroup streams the range-rho sub-runs of
+// every item of group g (ranks [goff[g], goff[g+1]) of the grouped order,
+// key words of ranges of 2^rshift <= 2^15 keys) and takes ds_min(first[key -
+// rho base], local rank) in a 128 KB table; every entry holding a rank is
+// the first cover of its key in the group, so that rank is kept (cover.go:
+// 114-129 keeps an input iff it holds a PC no earlier input of its Minimize
+// call holds).  Ranks are flagged in an LDS bitmap first (an item is the
+// first cover of many keys), then written out once per piece.  The stream is
+// pass1_keys_kernel's (32-byte lane chunks, marks + DPP for the item of a
+// chunk).
+constexpr uint32_t GM_TAB = 1u << 15;           // keys per piece (int32 ranks)
+constexpr uint32_t GM_MAX_ITEMS = 1u << 16;     // items per group on this path
+struct GmArgs {
+    const uint32_t *words;      // key words (common.h), CSR slots
+    const uint64_t *base_r;     // [items] off[order[j]] (prep_kernel)
+    const uint32_t *split_t;    // [nrange][items] split[order[j]][rho]
+    const uint64_t *goff;       // [ngroups + 1] rank intervals of the groups
+    uint32_t n_items, ngroups, nrange, rshift;
+    uint32_t *pctr;             // next piece
+    uint8_t *kept;              // [n_items] by rank
+};
+
+__global__ __launch_bounds__(THREADS) void group_min_kernel(GmArgs A) {
+    constexpr uint32_t CW = 8;
+    extern __shared__ uint32_t s_tab[];  // GM_TAB ranks at LDS 0, then:
+    auto *s_a0 = reinterpret_cast<uint64_t(*)[64]>(s_tab + GM_TAB);
+    auto *s_he = reinterpret_cast<uint32_t(*)[64]>(s_a0 + NWAVE);
+    auto *s_ex = s_he + NWAVE;
+    auto *s_own = s_ex + NWAVE;
+    uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_own + NWAVE);  // GM_MAX_ITEMS bits
+    uint32_t &s_next = s_bits[GM_MAX_ITEMS / 32];
+    const uint32_t l = __lane_id();
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    s_own[w][l] = 0u;
+    const uint32_t npieces = A.ngroups * A.nrange;
+    const uint32_t kmask = (1u << A.rshift) - 1u;
+    for (;;) {
+        if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+        __syncthreads();
+        const uint32_t p = s_next;
+        __syncthreads();
+        if (p >= npieces) break;
+        const uint32_t g = p / A.nrange, rho = p - g * A.nrange;
+        const uint32_t i0 = (uint32_t)A.goff[g], i1 = (uint32_t)A.goff[g + 1];
+        if (i1 <= i0) continue;
+        for (uint32_t q = threadIdx.x; q < GM_TAB / 4; q += THREADS)
+            reinterpret_cast<uint4 *>(s_tab)[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t q = threadIdx.x; q < (i1 - i0 + 31) / 32; q += THREADS) s_bits[q] = 0u;
+        __syncthreads();
+        const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+        const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+        for (uint32_t ib = w0; ib < w1; ib += 64) {
+            const uint32_t item = ib + l;
+            uint32_t nch = 0, he = 0;
+            uint64_t a0 = 0;
+            if (item < w1) {
+                const uint32_t s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+                const uint32_t s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+                const uint64_t st = A.base_r[item] + s0;
+                const uint32_t m = s1 - s0;
+                a0 = st & ~7ull;
+                const uint32_t head = (uint32_t)(st - a0);
+                he = ((head + m) << 3) | head;
+                nch = m ? (head + m + CW - 1) / CW : 0u;
+            }
+            const uint32_t incl = wave_incl_scan(nch);
+            const uint32_t ex_l = incl - nch;
+            const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+            s_a0[w][l] = a0;
+            s_he[w][l] = he;
+            s_ex[w][l] = ex_l;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t sj = 0;
+            for (uint32_t c0 = 0; c0 < tot; c0 += 64) {
+                const uint32_t c = c0 + l;
+                if (ex_l - c0 < 64u) atomicMax(&s_own[w][ex_l - c0], l + 1u);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mk = s_own[w][l];
+                s_own[w][l] = 0u;
+                const uint32_t pm = wave_incl_max(mk);
+                const uint32_t j = pm ? max(sj, pm - 1u) : sj;
+                sj = __builtin_amdgcn_readlane(j, 63);
+                if (c < tot) {
+                    const uint64_t ba = s_a0[w][j];
+                    const uint32_t hv = s_he[w][j];
+                    const uint32_t co = c - s_ex[w][j];
+                    const uint4 *ptr = reinterpret_cast<const uint4 *>(A.words + ba) + 2 * co;
+                    const uint4 v0 = ptr[0];
+                    const uint4 v1 = ptr[co * CW + 4 < (hv >> 3) ? 1 : 0];
+                    const uint32_t vv[CW] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                    const int lo = (int)(hv & 7u) - (int)(co * CW);
+                    const uint32_t span = (uint32_t)((int)(hv >> 3) - (int)(co * CW) - lo);
+                    const uint32_t rank = ib + j - i0;  // local rank in the group
+#pragma unroll
+                    for (int k = 0; k < (int)CW; k++)
+                        if ((uint32_t)(k - lo) < span) atomicMin(&s_tab[vv[k] & kmask], rank);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        // first covers -> their ranks' bits -> kept bytes
+        for (uint32_t q = threadIdx.x; q < GM_TAB; q += THREADS) {
+            const uint32_t r = s_tab[q];
+            if (r != ~0u) atomicOr(&s_bits[r >> 5], 1u << (r & 31));
+        }
+        __syncthreads();
+        for (uint32_t r = threadIdx.x; r < i1 - i0; r += THREADS)
+            if ((s_bits[r >> 5] >> (r & 31)) & 1u) A.kept[i0 + r] = 1;
+        __syncthreads();
+    }
+}
+constexpr size_t GM_LDS = GM_TAB * 4 + NWAVE * 64 * (8 + 3 * 4) + GM_MAX_ITEMS / 8 + 16;
+
 // dynamic LDS of pass1_keys_kernel past its 2^17-byte table
 constexpr size_t KEYS_LDS_EXTRA =
     NWAVE * 64 * (8 + 4 * 4) + (MAX_R + 2) * 4;
@@ -1110,6 +1229,51 @@ int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32
                                range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt, cand,
                                kept, 1, 0, 0, 0, low_of_key, err_flag, ws, s, grp_off, ngroups,
                                aligned);
+}
+}  // namespace syz
+
+// Manager.minimizeCorpus over small groups (group_min_kernel): key words of
+// ranges of 2^range_shift <= 2^15 keys (split [n][nrange]), the grouped order
+// (rank -> input), the groups' rank intervals on the device.  kept by rank.
+namespace syz {
+size_t minimize_groups_lds_ws_size(size_t n_items, uint64_t nkeys, uint32_t range_shift) {
+    return 256 + align_up(n_items * 8, 256) + align_up(mr_nrange(nkeys, range_shift) * n_items * 4, 256);
+}
+
+int minimize_groups_lds(const uint64_t *off, const uint32_t *words, const uint32_t *split,
+                        const int32_t *order, size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                        const uint64_t *goff_dev, uint32_t ngroups, uint8_t *kept, void *ws,
+                        hipStream_t s) {
+    if (n_items == 0 || ngroups == 0) return 0;
+    if (!off || !words || !split || !order || !goff_dev || !kept || !ws || range_shift > 15 ||
+        n_items > 0x7FFFFFFF)
+        return SYZCOV_EINVAL;
+    const uint64_t nrange = mr_nrange(nkeys, range_shift);
+    if (nrange > (uint64_t)mr::MAX_R || nrange * ngroups > 0xFFFFFFFFull) return SYZCOV_ERANGE;
+    mr::Args A{};
+    A.off = off;
+    A.split = split;
+    A.order = order;
+    A.n_items = (uint32_t)n_items;
+    A.nrange = (uint32_t)nrange;
+    uint32_t *pctr = (uint32_t *)ws;
+    uint64_t *base_r = (uint64_t *)((uint8_t *)ws + 256);
+    uint32_t *split_t = (uint32_t *)((uint8_t *)base_r + align_up(n_items * 8, 256));
+    SYZ_HIP(hipMemsetAsync(pctr, 0, 4, s));
+    SYZ_HIP(hipMemsetAsync(kept, 0, n_items, s));
+    static std::atomic<uint32_t> prep_attr{0}, gm_attr{0};
+    int rc = set_dyn_lds_once((const void *)mr::prep_kernel, 80 * 1024, prep_attr);
+    if (!rc) rc = set_dyn_lds_once((const void *)mr::group_min_kernel, (int)mr::GM_LDS, gm_attr);
+    if (rc) return rc;
+    hipLaunchKernelGGL(mr::prep_kernel, dim3(grid_for(n_items, 64, 8192)), dim3(256),
+                       64 * (nrange + 1) * sizeof(uint32_t), s, A, base_r, split_t);
+    mr::GmArgs G{words, base_r, split_t, goff_dev, (uint32_t)n_items, ngroups, (uint32_t)nrange,
+                 range_shift, pctr, kept};
+    hipLaunchKernelGGL(mr::group_min_kernel, dim3((unsigned)std::min<uint64_t>(nrange * ngroups,
+                                                                              (uint64_t)dev_cus())),
+                       dim3(mr::THREADS), mr::GM_LDS, s, G);
+    SYZ_LAUNCH_CHECK();
+    return 0;
 }
 }  // namespace syz
 

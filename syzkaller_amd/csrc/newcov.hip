@@ -955,6 +955,18 @@ __global__ void universe_shift_kernel(const uint32_t *__restrict__ u, uint32_t n
     if (__lane_id() == 0) atomicMin(out, m);
 }
 
+// kshift of a sorted unique PC list on the device (*d_ks = min over
+// neighbours of the highest differing bit; 31 for a single PC): the host
+// caps it at SYZCOV_KSHIFT_MAX (corpus.hip's grouped drop-in)
+int universe_shift_dev(const uint32_t *u, uint32_t n, uint32_t *d_ks, hipStream_t s) {
+    SYZ_HIP(hipMemsetD32Async((hipDeviceptr_t)d_ks, 31, 1, s));
+    if (n > 1)
+        hipLaunchKernelGGL(universe_shift_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, s, u,
+                           n, d_ks);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
 // addInput (fuzzer.go:372-373): an accepted input's whole cover (flakes
 // included, the sentinel excluded) joins corpusCover and maxCover.  One wave
 // per record; nothing on a rejected batch.

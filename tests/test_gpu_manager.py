@@ -79,6 +79,36 @@ def test_minimize_corpus_engine_size(cover):
     assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
 
 
+@pytest.mark.parametrize("force", ["", "group_chunks"])
+@pytest.mark.parametrize("universe", ["dense", "x86", "sentinel", "wide"])
+def test_minimize_corpus_grouped_paths(cover, monkeypatch, force, universe):
+    """Both grouped Minimize paths of syzcov_minimize_corpus at engine size:
+    the LDS path (every group <= 2^16 inputs: per-(group, key range) first
+    covers over the corpus union's keys) and the per-group chunked engine
+    (SYZCOV_FORCE=group_chunks).  Universes: a dense window, x86-like PC pairs
+    (kshift 2), PC 0xFFFFFFFF in some covers (cover.go:97 drops it from
+    Minimize's sets), and 32-bit-wide PCs (too many keys: the LDS path
+    declines and the chunked engine runs)."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
+    rng = np.random.default_rng(62)
+    n = 66_000
+    lo = 0x81000000
+    if universe == "x86":
+        pool = np.array([orc.lib().orc_synth_universe_mode(0x5EED0007, k, 2) for k in range(1 << 13)],
+                        np.uint32)
+    elif universe == "wide":
+        pool = np.unique(rng.integers(0, 1 << 32, size=20000, dtype=np.uint64)).astype(np.uint32)
+    else:
+        pool = np.arange(lo, lo + 5000, dtype=np.uint32)
+    covs = [rng.choice(pool, size=int(rng.integers(0, 40))) for _ in range(n)]
+    if universe in ("sentinel", "wide"):
+        for i in rng.integers(0, n, size=300):
+            covs[i] = np.append(covs[i], np.uint32(0xFFFFFFFF))
+    calls = rng.integers(0, 300, size=n).astype(np.int32)
+    calls[:2000] = 9
+    assert cover.MinimizeCorpus(calls, covs) == orc.minimize_corpus(calls, covs)
+
+
 def test_minimize_corpus_manager_mirror():
     from syzkaller_amd.manager import RpcInput, minimize_corpus
     covs = [[1, 2, 3, 4], [5], [1, 2], [3, 4, 5, 6, 7], [5, 6], [3, 7]]
