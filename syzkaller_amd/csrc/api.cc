@@ -48,6 +48,7 @@ uint32_t force_flags() {
     if (strstr(e, "nc_lds")) f |= FORCE_NC_LDS;
     if (strstr(e, "nc_probe")) f |= FORCE_NC_PROBE;
     if (strstr(e, "group_chunks")) f |= FORCE_GROUP_CHUNKS;
+    if (strstr(e, "nc_sep")) f |= FORCE_NC_SEP;
     return f;
 }
 

@@ -10,6 +10,7 @@ enum : uint32_t {
     FORCE_NC_LDS = 4u,
     FORCE_NC_PROBE = 8u,
     FORCE_GROUP_CHUNKS = 16u,  // minimizeCorpus: the per-group chunked engine for small groups too
+    FORCE_NC_SEP = 32u,        // newcov key mode: candidate pass + separate membership pass
 };
 uint32_t force_flags();
 }  // namespace syz

@@ -241,7 +241,7 @@ static_assert(SPLIT_NS <= 64, "one sample per lane");
 __global__ __launch_bounds__(256) void newcov_split_kernel(
     const uint64_t *__restrict__ rec_off, const uint32_t *__restrict__ pcs,
     const uint32_t *__restrict__ perm, const uint32_t *__restrict__ coff, int ncalls, Index X,
-    uint32_t nr, uint32_t stride, uint32_t *__restrict__ nq, uint64_t *__restrict__ Bq,
+    uint32_t nr, uint32_t rsh, uint32_t stride, uint32_t *__restrict__ nq, uint64_t *__restrict__ Bq,
     uint32_t *__restrict__ stats) {
     const uint32_t l = __lane_id(), ng = coff[ncalls];
     for (uint32_t j = blockIdx.x * 4 + (threadIdx.x >> 6); j < ng; j += gridDim.x * 4) {
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void newcov_split_kernel(
 #pragma unroll
             for (int g = 0; g < SQ_G; g++) {
                 const uint32_t qy = g0 + g;
-                v[g] = qy + 1 < nqry ? (qy + 1) << RSH : 0xFFFFFFFFu;
+                v[g] = qy + 1 < nqry ? (qy + 1) << rsh : 0xFFFFFFFFu;
                 const uint32_t c = qy < nqry ? (uint32_t)__popcll(__ballot(l < ns && kx < v[g])) : 0u;
                 if (n <= SPLIT_NS) {
                     lo[g] = c;
@@ -542,8 +542,8 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
     const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(
         (void *)X.low_of_key, 0, KEY ? (int)X.span : 0, 0x00020000);
     const uint32_t lowmask = (1u << ks) - 1u;
-    uint64_t bad = 0;  // lanes that saw a PC below its predecessor
-    uint64_t nonmem = 0;  // lanes that saw a PC outside the universe
+    uint32_t badv = 0;  // this lane saw a PC below its predecessor
+    uint32_t nonv = 0;  // this lane saw a PC outside the universe
     uint4 my = make_uint4(0, 0, 0, 0);
     uint32_t nrow = 0, p0v = 0;
     uint2 *cb = s_cb + wv * LC_CBW;
@@ -625,6 +625,8 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             }
         }
     };
+    // per-lane flags over a row's four components, one ballot per row
+    // (a ballot and two lane masks per component made the test SALU-bound)
     auto test = [&](uint32_t s0, const uint4 *pc) {
 #pragma unroll
         for (int u = 0; u < LC_U; u++) {
@@ -632,6 +634,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             const uint32_t i = (s0 + u) & 63;
             const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
+            const uint32_t lo1 = lo + first, n = hi - lo, n1 = hi - lo1;
             const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
             // bitmap words of the four components (the word index is masked
             // into the staged range, so reads are unconditional and in flight
@@ -646,25 +649,28 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             // for lane 0 the PC before the row
             const uint32_t p0 =
                 __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
+            uint32_t cand = 0;
 #pragma unroll
             for (int c = 0; c < 4; c++) {
-                // lanes whose element 4l + c is valid / has a predecessor in the
-                // sub-run to compare with (scalar masks)
-                const uint64_t vm = lane_range(lo > (uint32_t)c ? (lo - c + 3) >> 2 : 0u,
-                                               hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
-                const uint32_t lo1 = first ? lo + 1 : lo;
-                const uint64_t pm = lane_range(lo1 > (uint32_t)c ? (lo1 - c + 3) >> 2 : 0u,
-                                               hi > (uint32_t)c ? (hi - c + 3) >> 2 : 0u);
-                bad |= __ballot((c ? v[c - 1] : p0) > v[c]) & pm;
-                if (KEY && !SEP) nonmem |= __ballot(mb[u * 4 + c] != (v[c] & lowmask)) & vm;
-                const uint64_t cm = __ballot(!((wd[c] >> (o[c] & 31)) & 1u)) & vm;
-                if (cm) {  // rare
+                // element 4l + c is valid / has a predecessor in the sub-run
+                const uint32_t el = 4 * l + c;
+                const bool valid = el - lo < n, pv = el - lo1 < n1;
+                badv |= (uint32_t)(pv & ((c ? v[c - 1] : p0) > v[c]));
+                if (KEY && !SEP) nonv |= (uint32_t)(valid & (mb[u * 4 + c] != (v[c] & lowmask)));
+                cand |= (uint32_t)(valid & !((wd[c] >> (o[c] & 31)) & 1u)) << c;
+            }
+            if (__ballot(cand != 0)) {  // rare
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint64_t cm = __ballot((cand >> c) & 1u);
+                    if (!cm) continue;
+                    const bool mine = (cm >> l) & 1u;
                     if (KEY && SEP) {  // the candidates' membership, one byte each
                         const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
-                            lr, (cm >> l) & 1u ? (v[c] >> ks) - obase + (q << RSH) : 0xFFFFFFF0u, 0, 0);
-                        nonmem |= __ballot(mc != (v[c] & lowmask)) & cm;
+                            lr, mine ? (v[c] >> ks) - obase + (q << RSH) : 0xFFFFFFF0u, 0, 0);
+                        nonv |= (uint32_t)(mine & (mc != (v[c] & lowmask)));
                     }
-                    emit((cm >> l) & 1u, __builtin_amdgcn_readlane(my.y, i), v[c]);
+                    emit(mine, __builtin_amdgcn_readlane(my.y, i), v[c]);
                 }
             }
         }
@@ -698,8 +704,291 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
         }
     }
     if (nc) flush();
-    if (bad && l == 0) stats[0] = 3u;
-    if (nonmem && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
+    if (__ballot(badv) && l == 0) stats[0] = 3u;
+    if (__ballot(nonv) && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
+}
+
+// ---------------------------------------------------------------------------
+// Fused candidate + membership pass (key mode, kshift <= 4): every PC of the
+// batch is read once.  Ranges of 2^RSF = 2^18 keys: a workgroup holds the
+// range's universe low bits as nibbles (128 KB, nib_build_kernel) and one
+// call's maxCover | flakes bits over the range (32 KB) — the whole 160 KB of
+// LDS — and tests each PC of its rows against both:
+//   covered, nibble == the PC's low bits   nothing (the common case)
+//   covered, nibble != low bits            not a universe PC: batch rejected
+//   uncovered                              candidate; its membership is
+//                                          checked exactly from low_of_key
+// (a key of maxCover | flakes always holds a universe PC, so a PC on a key
+// with none is uncovered and goes the exact way).
+// Persistent slices: workgroup g takes the g-th of G equal slices of the row
+// stream (range-major, calls in order inside a range: row_fill_kernel), so
+// its rows are a run of SEGMENTS (call c, range q).  It restages the nibbles
+// when the range changes (once or twice per slice) and the call's bits per
+// segment; the next segment's bits are loaded into registers while the
+// current one streams, so a segment switch is two barriers and a 32 KB LDS
+// store (a workgroup per (call, range) item paid its launch, staging and
+// first loads in series per item: 0.49 ms per C5 batch).  With no LDS left, a
+// wave buffers up to 64 candidates in registers (lane j holds the j-th),
+// appended by a full-wave ds_permute that is a bijection (candidate lanes to
+// the free slots after the buffered ones, the others to the rest).
+constexpr uint32_t RSF = 18;
+constexpr size_t FUSED_LDS = ((size_t)1 << (RSF - 1)) + ((size_t)1 << (RSF - 3));  // 160 KB
+constexpr uint32_t FG_MAX = 4096;  // slices
+
+// Segment starts in the row stream, flat s = q * nc + c:
+// segb[q * (nc + 1) + c] = qoff[q] + Rq[q][coff[c]] (c <= nc), and for each
+// slice g the segment holding its first row (the last s starting at or before
+// it).  One workgroup.
+__global__ __launch_bounds__(1024) void fused_seg_kernel(const uint32_t *__restrict__ coff,
+                                                         int ncalls, uint32_t nr,
+                                                         const uint32_t *__restrict__ Rq,
+                                                         uint32_t stride,
+                                                         const uint32_t *__restrict__ qoff,
+                                                         uint32_t G, uint32_t *__restrict__ segb,
+                                                         uint32_t *__restrict__ wg_seg) {
+    const uint32_t nc = (uint32_t)ncalls, n = nr * (nc + 1);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t q = i / (nc + 1), c = i - q * (nc + 1);
+        segb[i] = qoff[q] + Rq[(uint64_t)q * stride + coff[c]];
+    }
+    __syncthreads();
+    const uint32_t rt = qoff[nr], ns = nr * nc;
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
+        const uint32_t a = (uint32_t)((uint64_t)rt * g / G);
+        uint32_t lo = 0, hi = ns;  // largest s with start(s) <= a (start(0) = 0)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1, q = mid / nc;
+            if (segb[q * (nc + 1) + (mid - q * nc)] <= a) lo = mid; else hi = mid;
+        }
+        wg_seg[g] = lo;
+    }
+}
+
+__global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
+    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
+    uint64_t words_per_call, const uint32_t *__restrict__ nib, uint64_t nib_words, Index X,
+    uint32_t nr, int ncalls, const uint32_t *__restrict__ segb,
+    const uint32_t *__restrict__ wg_seg, const uint4 *__restrict__ rows,
+    const uint32_t *__restrict__ qoff, uint2 *__restrict__ clist, uint32_t *__restrict__ stats) {
+    extern __shared__ uint4 s_f4[];  // nibbles [0, 128 KB), then the call's bits
+    constexpr uint32_t NBW = 1u << (RSF - 3), MBW = 1u << (RSF - 5);  // words
+    constexpr int SVM = MBW / 4 / LC_THREADS, SVN = NBW / 4 / LC_THREADS;
+    const uint32_t *s_nb = (const uint32_t *)s_f4;
+    const uint32_t *s_m = s_nb + NBW;
+    const uint32_t t = threadIdx.x, l = __lane_id(), wv = t >> 6;
+    const uint32_t nc = (uint32_t)ncalls, ns = nr * nc;
+    const uint32_t rt = qoff[nr];
+    const uint32_t a = (uint32_t)((uint64_t)rt * blockIdx.x / gridDim.x);
+    const uint32_t b = (uint32_t)((uint64_t)rt * (blockIdx.x + 1) / gridDim.x);
+    if (a >= b) return;
+    const __amdgpu_buffer_rsrc_t pr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)pcs, 0, npc * 4u, 0x00020000);
+    const uint32_t ks = X.kshift, lowmask = (1u << ks) - 1u;
+    const __amdgpu_buffer_rsrc_t lr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)X.low_of_key, 0, (int)X.span, 0x00020000);
+    // segment s clipped to the slice (empty if it lies outside)
+    auto seg = [&](uint32_t s, uint32_t &q, uint32_t &c, uint32_t &lo, uint32_t &hi) {
+        q = s / nc;
+        c = s - q * nc;
+        const uint32_t *sb = segb + q * (nc + 1) + c;
+        lo = max(sb[0], a);
+        hi = min(sb[1], b);
+    };
+    auto load_bits = [&](uint32_t q, uint32_t c, uint4 (&sm)[SVM]) {
+        const uint64_t mb = (uint64_t)q * MBW;
+        const uint32_t nvm = (uint32_t)(min<uint64_t>(MBW, words_per_call - mb) >> 2);
+        const uint4 *M4 = (const uint4 *)(mfl + (uint64_t)c * words_per_call + mb);
+#pragma unroll
+        for (int i = 0; i < SVM; i++) {
+            const uint32_t j = t + i * LC_THREADS;
+            sm[i] = j < nvm ? M4[j] : make_uint4(~0u, ~0u, ~0u, ~0u);  // past the keys: covered
+        }
+    };
+    auto store_bits = [&](const uint4 (&sm)[SVM]) {
+#pragma unroll
+        for (int i = 0; i < SVM; i++) s_f4[NBW / 4 + t + i * LC_THREADS] = sm[i];
+    };
+    auto stage_nib = [&](uint32_t q) {  // (a short last range reads its real words only)
+        const uint64_t nbb = (uint64_t)q * NBW;
+        const uint32_t nvn = (uint32_t)(min<uint64_t>(NBW, nib_words - nbb) >> 2);
+        const uint4 *N4 = (const uint4 *)(nib + nbb);
+        uint4 sn[SVN];
+#pragma unroll
+        for (int i = 0; i < SVN; i++) {
+            const uint32_t j = t + i * LC_THREADS;
+            sn[i] = j < nvn ? N4[j] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < SVN; i++) s_f4[t + i * LC_THREADS] = sn[i];
+    };
+    uint4 my = make_uint4(0, 0, 0, 0);
+    uint32_t nrow = 0, p0v = 0, obase = 0, w1 = 0;
+    uint32_t cbk = 0, cbp = 0, ncb = 0;  // candidate buffer: lane j < ncb holds the j-th
+    auto flush = [&]() {
+        uint32_t base = 0;
+        if (l == 0) base = atomicAdd(&stats[1], ncb);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (l < ncb) clist[base + l] = make_uint2(cbk, cbp);
+        ncb = 0;
+    };
+    auto emit = [&](uint64_t m, uint32_t k, uint32_t pc) {
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (ncb + n > 64) flush();
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const bool cand = (m >> l) & 1u;
+        const uint32_t dst = cand ? ncb + rank : (ncb + n + (l - rank)) & 63u;
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)k);
+        const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)pc);
+        const bool in = l - ncb < n;
+        cbk = in ? pk : cbk;
+        cbp = in ? pp : cbp;
+        ncb += n;
+    };
+    auto rows64 = [&](uint32_t rb_) {
+        nrow = min(64u, w1 - rb_);
+        const uint4 dsc = rows[rb_ + min(l, nrow - 1)];
+        my = l < nrow ? dsc : make_uint4(dsc.x, 0, 0, 0);
+        const bool need = l < nrow && !(my.z >> 18 & 1u);
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(pr, need ? (my.x - 1) * 4u : 0xFFFFFFF0u, 0, 0);
+        p0v = need ? v : 0u;
+    };
+    auto issue = [&](uint32_t s0, uint4 *pc) {
+#pragma unroll
+        for (int u = 0; u < LC_U; u++) {
+            const uint32_t i = (s0 + u) & 63;
+            const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
+            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
+            const bool any = s0 + u < nrow && 4 * l + 3 >= lo && 4 * l < hi;
+            pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  pr, any ? l * 16u : 0xFFFFFFF0u, any ? ra * 4u : 0u,
+                                                  SYZ_NC_PC_AUX));
+        }
+    };
+    // per-lane flags over the row's four components, one ballot per row
+    // (ballots and lane masks per component made the test SALU-bound)
+    uint32_t badv = 0, nonv = 0;
+    auto test = [&](uint32_t s0, const uint4 *pc) {
+#pragma unroll
+        for (int u = 0; u < LC_U; u++) {
+            if (s0 + u >= nrow) break;  // wave-uniform
+            const uint32_t i = (s0 + u) & 63;
+            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
+            const uint32_t lo1 = lo + first, n = hi - lo, n1 = hi - lo1;  // (hi > lo)
+            const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
+            uint32_t o[4], wd[4], nw[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                o[c] = (v[c] >> ks) - obase;
+                wd[c] = s_m[(o[c] >> 5) & (MBW - 1)];
+                nw[c] = s_nb[(o[c] >> 3) & (NBW - 1)];
+            }
+            const uint32_t p0 =
+                __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
+            uint32_t cand = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint32_t el = 4 * l + c;
+                const bool valid = el - lo < n, pv = el - lo1 < n1;
+                badv |= (uint32_t)(pv & ((c ? v[c - 1] : p0) > v[c]));
+                const bool cov = (wd[c] >> (o[c] & 31)) & 1u;
+                const uint32_t nb = (nw[c] >> ((o[c] & 7u) * 4u)) & 15u;
+                nonv |= (uint32_t)(valid & cov & (nb != (v[c] & lowmask)));
+                cand |= (uint32_t)(valid & !cov) << c;
+            }
+            if (__ballot(cand != 0)) {  // rare in steady state
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const uint64_t cm = __ballot((cand >> c) & 1u);
+                    if (!cm) continue;
+                    // the candidates' membership, one byte each
+                    const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
+                        lr, (cm >> l) & 1u ? (v[c] >> ks) - X.kbase : 0xFFFFFFF0u, 0, 0);
+                    nonv |= (uint32_t)(((cm >> l) & 1u) & (mc != (v[c] & lowmask)));
+                    emit(cm, __builtin_amdgcn_readlane(my.y, i), v[c]);
+                }
+            }
+        }
+    };
+    // a wave's share of segment rows [lo_, hi_): an even split over the waves
+    uint32_t w0 = 0;
+    auto share = [&](uint32_t lo_, uint32_t hi_) {
+        const uint32_t per = (hi_ - lo_ + LC_THREADS / 64 - 1) / (LC_THREADS / 64);
+        w0 = min(hi_, lo_ + wv * per);
+        w1 = min(hi_, w0 + per);
+    };
+    uint4 pcA[LC_U], pcB[LC_U];
+    uint32_t s = wg_seg[blockIdx.x], q, c, lo, hi;
+    seg(s, q, c, lo, hi);
+    share(lo, hi);
+    if (w0 < w1) {  // the first rows' loads, in flight with the staging
+        rows64(w0);
+        issue(0, pcA);
+    }
+    {
+        uint4 sm[SVM];
+        load_bits(q, c, sm);
+        stage_nib(q);
+        store_bits(sm);
+    }
+    uint32_t cur_q = q;
+    __syncthreads();
+    for (;;) {
+        // the next segment of the slice (calls with no rows in a range are
+        // skipped); its bits load while this one streams
+        uint32_t s2 = s + 1, q2 = 0, c2 = 0, lo2 = 0, hi2 = 0;
+        bool more = false;
+        for (; s2 < ns; s2++) {
+            seg(s2, q2, c2, lo2, hi2);
+            if (lo2 >= b) break;
+            if (hi2 > lo2) {
+                more = true;
+                break;
+            }
+        }
+        uint4 sm[SVM];
+        if (more) load_bits(q2, c2, sm);
+        obase = X.kbase + (q << RSF);
+        // this wave's rows of the segment; the first 64's descriptors and first
+        // step were issued before the segment's barrier
+        for (uint32_t rb = w0; rb < w1; rb += 64) {
+            if (rb != w0) {
+                rows64(rb);
+                issue(0, pcA);
+            }
+            for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * LC_U) {
+                issue(s0 + LC_U, pcB);
+                test(s0, pcA);
+                issue(s0 + 2 * LC_U, pcA);
+                test(s0 + LC_U, pcB);
+            }
+        }
+        if (more) {  // the next segment's first loads, before the barrier
+            share(lo2, hi2);
+            if (w0 < w1) {
+                rows64(w0);
+                issue(0, pcA);
+            }
+        }
+        __syncthreads();
+        if (!more) break;
+        if (q2 != cur_q) {
+            stage_nib(q2);
+            cur_q = q2;
+        }
+        store_bits(sm);
+        __syncthreads();
+        s = s2;
+        q = q2;
+        c = c2;
+        lo = lo2;
+        hi = hi2;
+    }
+    if (ncb) flush();
+    if (__ballot(badv) && l == 0) stats[0] = 3u;
+    if (__ballot(nonv) && l == 0) stats[0] = 1u;  // not in the universe: rejected like a PC out of range
 }
 
 // ---------------------------------------------------------------------------
@@ -1323,6 +1612,13 @@ extern "C" size_t syzcov_state_newcov_ws_size(size_t nrec, uint64_t npc) {
 // pays when the bitmap bytes staged (about nr x calls x 64 KB) stay well
 // under the PCs streamed; otherwise (sparse calls, huge windows) every PC
 // probes the bitmap in global memory.  SYZCOV_FORCE=nc_lds|nc_probe forces one.
+static int dev_cus() {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n = 256;
+    return n > 0 ? n : 256;
+}
 static int forced_path() {
     const uint32_t f = force_flags();
     return (f & FORCE_NC_LDS) ? 1 : (f & FORCE_NC_PROBE) ? 2 : 0;
@@ -1364,9 +1660,15 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                        dim3((unsigned)((nrec + GS_THREADS * GS_PER - 1) / (GS_THREADS * GS_PER))),
                        dim3(GS_THREADS), nc <= GRP_MAX_CALLS ? (size_t)nc * 4 : 0, s, callid,
                        (uint32_t)nrec, st->ncalls, cur, perm);
-    const uint64_t nr64 = (st->X.span + (1ull << RSH) - 1) >> RSH;
+    // key mode with the universe's nibbles: the fused pass over 2^18-key ranges
+    // (SYZCOV_FORCE=nc_sep: the candidate pass, then the separate membership pass)
+    const uint32_t ff = force_flags();
+    const bool fused = st->X.key_mode && st->nib && !(ff & FORCE_NC_SEP) &&
+                       ((st->X.span + (1ull << RSF) - 1) >> RSF) <= NR_MAX;
+    const uint32_t rsh = fused ? RSF : RSH;
+    const uint64_t nr64 = (st->X.span + (1ull << rsh) - 1) >> rsh;
     const int forced = forced_path();
-    const uint64_t range_bytes = std::min<uint64_t>(st->words * 4, 1u << (RSH - 3));
+    const uint64_t range_bytes = std::min<uint64_t>(st->words * 4, 1u << (rsh - 3));
     const bool lds = nr64 <= NR_MAX && npc < (1ull << 30) &&  // buffer offsets: 4 GB of PCs
                      (forced == 1 ||
                       (forced == 0 && 2 * nr64 * (uint64_t)nc * range_bytes <= npc * 4));
@@ -1385,13 +1687,14 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                                (uint4 *)st->mfl);
             st->mfl_stale = false;
         }
-        static std::atomic<uint32_t> lds_done[3], memb_done;
-        const bool sep = st->X.key_mode && st->nib;
+        static std::atomic<uint32_t> lds_done[3], memb_done, fused_done;
+        const bool sep = st->X.key_mode && st->nib && !fused;
         const int kv = !st->X.key_mode ? 0 : sep ? 2 : 1;
         auto kfn = kv == 0 ? newcov_cand_lds_kernel<false, false>
                    : kv == 1 ? newcov_cand_lds_kernel<true, false>
                              : newcov_cand_lds_kernel<true, true>;
-        int rc = set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[kv]);
+        int rc = fused ? set_dyn_lds_once((const void *)newcov_fused_kernel, (int)FUSED_LDS, fused_done)
+                       : set_dyn_lds_once((const void *)kfn, 1 << (RSH - 3), lds_done[kv]);
         if (rc) return rc;
         if (sep && (rc = set_dyn_lds_once((const void *)newcov_memb_kernel, 1 << (RSH - 2), memb_done)))
             return rc;
@@ -1413,30 +1716,47 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         // grouped: coff[nc] <= nrec)
         hipLaunchKernelGGL(newcov_split_kernel, dim3(grid_for(nrec, 4, 16384)), dim3(256), 0, s,
                            rec_off, pcs, (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls,
-                           st->X, nr, stride, nq, bq, stats);
+                           st->X, nr, rsh, stride, nq, bq, stats);
         const uint32_t nb = (uint32_t)((nrec + RS_CHUNK - 1) / RS_CHUNK);
         hipLaunchKernelGGL(range_sum_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
                            (const uint64_t *)bq, (uint32_t)nrec, stride, csum);
         hipLaunchKernelGGL(range_scan_kernel, dim3(nb, nr), dim3(1024), 0, s, (const uint32_t *)nq,
                            (const uint64_t *)bq, (uint32_t)nrec, stride, (const uint32_t *)csum, rq);
-        hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
-                           st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre);
+        if (!fused)
+            hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
+                               st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre);
         hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(64), 0, s, (const uint32_t *)rq,
                            (uint32_t)nrec, stride, nr, qoff);
         const uint32_t ne = nc * nr;
-        hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, s,
-                           (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)rq, stride, CHR,
-                           (const uint32_t *)ipre, desc);
+        if (!fused)
+            hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, s,
+                               (const uint32_t *)coff, st->ncalls, nr, (const uint32_t *)rq, stride,
+                               CHR, (const uint32_t *)ipre, desc);
         hipLaunchKernelGGL(row_fill_kernel, dim3(grid_for((uint64_t)nrec * nr, 256, 16384)),
                            dim3(256), 0, s, (const uint32_t *)nq, (const uint64_t *)bq,
                            (const uint32_t *)rq, (const uint32_t *)perm, (const uint32_t *)coff,
                            st->ncalls, nr, stride, (const uint32_t *)qoff, rows);
         // items <= rows / CHR + non-empty (call, range) pairs; the excess exits
         const uint64_t items = nrows / CHR + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
-        hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS), (size_t)(1u << (RSH - 3)), s, pcs,
-                           (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
-                           st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
-                           (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
+        if (fused) {
+            const uint64_t nib_words = ((st->X.span + (1ull << RSH) - 1) >> RSH) << (RSH - 3);
+            // the segment table in the item descriptors' space (unused here)
+            uint32_t *segb = (uint32_t *)desc, *wg_seg = segb + nr * (nc + 1);
+            const uint32_t fused_g = (uint32_t)std::min<int>(dev_cus(), (int)FG_MAX);
+            hipLaunchKernelGGL(fused_seg_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
+                               st->ncalls, nr, (const uint32_t *)rq, stride, (const uint32_t *)qoff,
+                               fused_g, segb, wg_seg);
+            hipLaunchKernelGGL(newcov_fused_kernel, dim3(fused_g), dim3(LC_THREADS), FUSED_LDS, s,
+                               pcs, (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
+                               (const uint32_t *)st->nib, nib_words, st->X, nr, st->ncalls,
+                               (const uint32_t *)segb, (const uint32_t *)wg_seg,
+                               (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
+        } else {
+            hipLaunchKernelGGL(kfn, dim3((unsigned)items), dim3(LC_THREADS), (size_t)(1u << (RSH - 3)), s, pcs,
+                               (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
+                               st->X, nr, (const uint32_t *)ipre, ne, (const uint4 *)desc,
+                               (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
+        }
         if (sep)
             hipLaunchKernelGGL(newcov_memb_kernel, dim3(MB_G * 2), dim3(MB_THREADS),
                                (size_t)(1u << (RSH - 2)), s, pcs, (uint32_t)npc,

@@ -137,11 +137,14 @@ def test_new_inputs_vs_sequential():
     cc.close()
 
 
-@pytest.fixture(params=["lds", "probe"])
+@pytest.fixture(params=["lds", "sep", "probe"])
 def newcov_path(request, monkeypatch):
-    """Both candidate passes of newcov.hip: LDS-staged key ranges and global
-    bitmap probes (the library picks one per batch from its shape)."""
-    monkeypatch.setenv("SYZCOV_FORCE", "nc_" + request.param)
+    """Every candidate pass of newcov.hip: LDS-staged key ranges (in key mode
+    with kshift <= 4 one fused pass, membership from LDS nibbles; "sep": the
+    candidate pass, then the separate membership pass) and global bitmap
+    probes (the library picks one per batch from its shape)."""
+    monkeypatch.setenv("SYZCOV_FORCE", {"lds": "nc_lds", "sep": "nc_lds,nc_sep",
+                                        "probe": "nc_probe"}[request.param])
     return request.param
 
 

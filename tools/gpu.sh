@@ -9,10 +9,11 @@
 #   bench            the driver's line: bench.py --gpus 1 (STEPS, WARMUP)
 #   newcov | newcov_early | dedup | prio    the other workloads' lines
 #   probe:NAME:ENV:ARGS   one bench line (no CPU baseline) with ENV set and
-#                    ARGS appended (e.g. probe:v1:SYZCOV_LIB=$PWD/syzkaller_amd/variants/v1.so:--no-c2)
+#                    ARGS appended, commas for spaces (e.g.
+#                    probe:v1:SYZCOV_LIB=$PWD/syzkaller_amd/variants/v1.so:--workload,newcov)
 #   trace:ARGS       rocprofv3 kernel trace + stats of bench.py ARGS
 #   kbench:ARGS      tools/kbench.py ARGS (kernel micro-bench)
-#   profile          tools/profile.sh OUTDIR/prof (rocprofv3 stats + PMC passes)
+#   profile          tools/profile.sh OUTDIR/prof $PARTS (rocprofv3 stats + PMC passes)
 set -o pipefail
 export TMPDIR=/tmp
 o=${1:?usage: tools/gpu.sh OUTDIR STEP...}; shift
@@ -59,6 +60,7 @@ for step in "$@"; do
     ;;
   probe:*)
     spec=${step#probe:}; name=${spec%%:*}; rest=${spec#*:}; envs=${rest%%:*}; args=${rest#*:}
+    args=${args//,/ }  # commas separate the appended arguments
     env $(eval echo $envs) timeout -k 10 400 python -u bench.py --no-cpu --no-dropin \
         --steps ${STEPS:-10} --warmup 3 $args > $o/$name.json 2> $o/$name.err
     rc=$?; [ $rc -ne 0 ] && { tail -15 $o/$name.err; fatal $rc $name $o/$name.err; exit 1; }
@@ -75,7 +77,9 @@ for step in "$@"; do
     rc=$?; tail -20 $o/kbench.log; [ $rc -ne 0 ] && { fatal $rc kbench $o/kbench.log; exit 1; }
     ;;
   profile)
-    timeout -k 10 ${PTIME:-900} bash tools/profile.sh $o/prof || exit 1
+    timeout -k 10 ${PTIME:-900} bash tools/profile.sh $o/prof $PARTS || exit 1
+    # the raw per-dispatch CSVs stay on the box (gpurun copies back <= 64 MiB)
+    find $o/prof \( -name '*kernel_trace.csv' -o -name '*counter_collection.csv' \) -delete
     ;;
   *) echo "unknown step $step"; exit 2;;
   esac

@@ -8,11 +8,11 @@
 #   -> OUT/traffic.json {"C3": phases, "C2": phases, "newcov": ..., "dedup": ...}
 # Counters are never combined with tracing; each pass is its own run within the
 # per-block limits (MI355X_MICROARCH.md, HBM / rocprofv3).
-#   usage: tools/profile.sh OUT [parts: corpus canon newcov dedup prio]
+#   usage: tools/profile.sh OUT [parts: corpus canon newcov newcov_early dedup prio]
 set -o pipefail
 export TMPDIR=/tmp
 o=${1:-gpurun_out/prof}; shift
-parts=${*:-corpus canon newcov dedup prio}
+parts=${*:-corpus canon newcov newcov_early dedup prio}
 mkdir -p $o
 B="python3 bench.py --no-cpu --no-c2 --no-dropin"
 has() { case " $parts " in *" $1 "*) return 0;; esac; return 1; }
@@ -47,11 +47,19 @@ fi
 if has newcov; then
   N="$B --workload newcov --steps 10 --warmup 3"
   trace newcov $N
+  python3 tools/trace_last.py $o/newcov_trace newcov_own_kernel 10 > $o/newcov_timed_summary.txt && head -14 $o/newcov_timed_summary.txt
   pmc_pair newcov newcov_own_kernel 10 $N
+fi
+if has newcov_early; then  # the early regime: 32 history batches, every record still new
+  E="$B --workload newcov --history 32 --steps 10 --warmup 3"
+  trace newcov_early $E
+  python3 tools/trace_last.py $o/newcov_early_trace newcov_own_kernel 10 > $o/newcov_early_timed_summary.txt && head -14 $o/newcov_early_timed_summary.txt
+  pmc_pair newcov_early newcov_own_kernel 10 $E
 fi
 if has dedup; then
   D="$B --workload dedup --steps 10 --warmup 3"
   trace dedup $D
+  python3 tools/trace_last.py $o/dedup_trace "narrow_kernel<4>" 10 > $o/dedup_timed_summary.txt
   pmc_pair dedup "narrow_kernel<4>" 10 $D
 fi
 if has prio; then

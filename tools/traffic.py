@@ -19,7 +19,8 @@ PHASES = {
     "canon": ("bin_kernel", "canon_wave_kernel", "canon_key_kernel", "canon_class_kernel",
               "split_list_kernel",
               "keyify_list_kernel", "large_"),
-    "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "min_records_kernel",
+    "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "pass1_keys_kernel",
+                 "min_records_kernel", "group_min_kernel",
                  "cover_records_kernel", "first_to_bits_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
     "newcov": ("newcov_", "hash_clear_kernel", "grp_hist", "grp_scan", "grp_scatter", "nc_zero",
