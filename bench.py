@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["corpus", "prio", "newcov", "dedup"], default="corpus")
     ap.add_argument("--records", type=int, default=65536, help="newcov: call records per batch")
+    ap.add_argument("--no-early", action="store_true",
+                    help="newcov: skip the early-regime sub-record (32 history batches)")
     ap.add_argument("--ncalls", type=int, default=293, help="newcov: CallIDs (sys.CallID)")
     ap.add_argument("--history", type=int, default=512,
                     help="newcov: batches streamed through the check before the bench (512: "
@@ -690,14 +692,13 @@ def cpu_baseline_newcov(args, nrec: int, nhist: int = 16384):
                       f"1 thread"}
 
 
-def bench_newcov(args):
-    """C5: streaming new-coverage check (syz-fuzzer execute, fuzzer.go:456-480)
-    of batches of call records against the resident per-CallID maxCover and
-    the global flakes set.  Every step is a FRESH batch (W + K distinct batches
-    are generated into HBM up front), so maxCover evolves as in a fuzzer."""
+def newcov_run(args, history, world, rank, dev):
+    """One C5 measurement: `history` batches streamed through the check, then
+    W + K fresh timed batches.  Returns (seconds, phase ms, timed PCs, candidates
+    per batch, new records per batch, new records during the history)."""
     import ctypes as C
+    import numpy as np
     import torch
-    world, rank, dev = init_dist()
     from syzkaller_amd import _lib
     from syzkaller_amd.engine import synth_corpus, synth_records, synth_window
     from syzkaller_amd.fuzzer import CoverState
@@ -710,11 +711,10 @@ def bench_newcov(args):
     def make_batch(b):
         # batch b of rank r's stream: records (r * (history + nb) + b) * nrec + k
         # (history batches first): the stream oracle/newcov_full.c restates
-        first = (rank * (args.history + nb) + b) * nrec
+        first = (rank * (history + nb) + b) * nrec
         return synth_records(nrec, SEED_NEWCOV, first, args.ncalls, mean=args.mean,
                              sigma=args.sigma, log2_space=args.log2_space, device=dev)
 
-    import numpy as np
     st = CoverState(args.ncalls, lo, span)
     if not args.no_universe:  # per-call bitmaps over the 2^22 dense keys
         univ = torch.empty(1 << args.log2_space, dtype=torch.int32, device=dev)
@@ -727,9 +727,9 @@ def bench_newcov(args):
                                 sigma=1, log2_space=args.log2_space, device=dev)
     st.set_flakes(np.unique(fp[:int(fo[1].item())].cpu().numpy().view(np.uint32)))
     # a fuzzer that has been running: `history` batches streamed through the
-    # same check before the bench (maxCover near saturation, as in steady state)
+    # same check before the bench (maxCover near saturation after 512)
     hist_new = 0
-    for h in range(args.history):
+    for h in range(history):
         cid, roff, pcs, npc = make_batch(h)
         wsz = L.syzcov_state_newcov_ws_size(nrec, npc)
         ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
@@ -738,13 +738,12 @@ def bench_newcov(args):
                                              None, P(ws), wsz, s()), "state_newcov_dev")
         hist_new += int(flags.sum().item())
         del ws, pcs
-    batches = [make_batch(args.history + b) for b in range(nb)]
+    batches = [make_batch(history + b) for b in range(nb)]
     max_npc = max(b[3] for b in batches)
     wsz = L.syzcov_state_newcov_ws_size(nrec, max_npc)
     ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
-    is_new = torch.zeros(nrec, dtype=torch.uint8, device=dev)
+    is_new = torch.zeros(nb, nrec, dtype=torch.uint8, device=dev)  # counted after the timing
     stats = torch.zeros(nb, 2, dtype=torch.int32, device=dev)
-    nnew = torch.zeros(nb, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     it = [0]
 
@@ -753,17 +752,33 @@ def bench_newcov(args):
         cid, roff, pcs, npc = batches[b]
         if ev is not None:
             ev[0].record()
-        _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc, P(is_new),
-                                             P(stats[b]), P(ws), wsz, s()), "state_newcov_dev")
+        _lib.check(L.syzcov_state_newcov_dev(st.h, P(cid), P(roff), P(pcs), nrec, npc,
+                                             P(is_new[b]), P(stats[b]), P(ws), wsz, s()),
+                   "state_newcov_dev")
         if ev is not None:
             ev[1].record()
-        nnew[b] = is_new.sum()
         it[0] += 1
     dt, phl = timed(run_step, 1, args, world, dev)
     sc = stats.cpu().tolist()
     if any(x[0] for x in sc):
         raise RuntimeError(f"newcov batch rejected: {sc}")
+    nnew = is_new.sum(dim=1).cpu().tolist()
     timed_pcs = sum(b[3] for b in batches[args.warmup:])
+    st.close()
+    return dt, phl, timed_pcs, [x[1] for x in sc[args.warmup:]], nnew[args.warmup:], hist_new
+
+
+def bench_newcov(args):
+    """C5: streaming new-coverage check (syz-fuzzer execute, fuzzer.go:456-480)
+    of batches of call records against the resident per-CallID maxCover and
+    the global flakes set.  Every step is a FRESH batch (W + K distinct batches
+    are generated into HBM up front), so maxCover evolves as in a fuzzer.  At
+    N=1 with the default 512 history batches (the steady state, maxCover near
+    saturation) the line also carries the early regime (32 history batches:
+    every record still brings new PCs) as the `early` sub-record."""
+    world, rank, dev = init_dist()
+    nrec = args.records
+    dt, phl, timed_pcs, cands, nnew, hist_new = newcov_run(args, args.history, world, rank, dev)
     value = timed_pcs * world / dt
     achieved = timed_pcs / args.steps * 4 / (phl[0] * 1e-3) / 1e9
     out = {
@@ -780,22 +795,34 @@ def bench_newcov(args):
                                 "universe" % args.log2_space if not args.no_universe
                                 else "window bitmaps (1 bit per PC offset)"),
                    "maxcover_bytes": args.ncalls * ((1 << args.log2_space) if not args.no_universe
-                                                    else span) // 8,
+                                                    else (16 << args.log2_space)) // 8,
                    "history_batches": args.history, "history_new_records": hist_new},
         "phases_ms": {"newcov": round(phl[0], 4)},
-        "results": {"candidates_per_batch": [x[1] for x in sc[args.warmup:]],
-                    "new_records_per_batch": nnew.cpu().tolist()[args.warmup:],
+        "results": {"candidates_per_batch": cands, "new_records_per_batch": nnew,
                     "records_per_s": nrec * args.steps * world / dt},
-        "roofline": {"bound": "hbm", "kernel": "newcov (cand+hash)", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "alg_bytes_per_launch": timed_pcs // args.steps * 4},
+        "roofline": {"bound": "hbm", "kernel": "newcov (split + fused check + hash)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": timed_pcs // args.steps * 4},
     }
     if world == 1 and args.history == 512:  # per timed batch of this command's shape
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_of("newcov",
                                                                                    "newcov")
+    if world == 1 and args.history == 512 and not args.no_early:
+        # the early regime (the fuzzer's first minutes), same batch shape
+        e_dt, e_phl, e_pcs, e_cands, e_new, e_hist = newcov_run(args, 32, world, rank, dev)
+        e_ach = e_pcs / args.steps * 4 / (e_phl[0] * 1e-3) / 1e9
+        out["early"] = {
+            "history_batches": 32, "history_new_records": e_hist,
+            "value": e_pcs / e_dt, "ms_per_step": e_dt / args.steps * 1e3,
+            "phases_ms": {"newcov": round(e_phl[0], 4)},
+            "results": {"candidates_per_batch": e_cands, "new_records_per_batch": e_new},
+            "roofline": {"achieved": e_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": e_ach / HBM_PEAK_GBS,
+                         "traffic": traffic_of("newcov_early", "newcov")[0],
+                         "alg_bytes_per_launch": e_pcs // args.steps * 4}}
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline_newcov(args, min(args.cpu_sample, 2000, nrec))
-    st.close()
     return rank, world, out
 
 

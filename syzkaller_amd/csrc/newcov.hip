@@ -735,17 +735,26 @@ constexpr uint32_t RSF = 18;
 constexpr size_t FUSED_LDS = ((size_t)1 << (RSF - 1)) + ((size_t)1 << (RSF - 3));  // 160 KB
 constexpr uint32_t FG_MAX = 4096;  // slices
 
-// Segment starts in the row stream, flat s = q * nc + c:
-// segb[q * (nc + 1) + c] = qoff[q] + Rq[q][coff[c]] (c <= nc), and for each
-// slice g the segment holding its first row (the last s starting at or before
-// it).  One workgroup.
+// The ranges' row offsets (row_offsets_kernel's qoff), the segment starts in
+// the row stream, flat s = q * nc + c: segb[q * (nc + 1) + c] = qoff[q] +
+// Rq[q][coff[c]] (c <= nc), and for each slice g the segment holding its first
+// row (the last s starting at or before it).  One workgroup.
 __global__ __launch_bounds__(1024) void fused_seg_kernel(const uint32_t *__restrict__ coff,
                                                          int ncalls, uint32_t nr,
                                                          const uint32_t *__restrict__ Rq,
-                                                         uint32_t stride,
-                                                         const uint32_t *__restrict__ qoff,
+                                                         uint32_t m, uint32_t stride,
+                                                         uint32_t *__restrict__ qoff,
                                                          uint32_t G, uint32_t *__restrict__ segb,
                                                          uint32_t *__restrict__ wg_seg) {
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (uint32_t q = 0; q < nr; q++) {
+            qoff[q] = o;
+            o += Rq[(uint64_t)q * stride + m];
+        }
+        qoff[nr] = o;
+    }
+    __syncthreads();
     const uint32_t nc = (uint32_t)ncalls, n = nr * (nc + 1);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint32_t q = i / (nc + 1), c = i - q * (nc + 1);
@@ -1725,8 +1734,16 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         if (!fused)
             hipLaunchKernelGGL(item_scan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
                                st->ncalls, nr, (const uint32_t *)rq, stride, CHR, ipre);
-        hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(64), 0, s, (const uint32_t *)rq,
-                           (uint32_t)nrec, stride, nr, qoff);
+        // the segment table lives in the item descriptors' space (unused here)
+        uint32_t *segb = (uint32_t *)desc, *wg_seg = segb + nr * (nc + 1);
+        const uint32_t fused_g = (uint32_t)std::min<int>(dev_cus(), (int)FG_MAX);
+        if (fused)  // qoff and the fused pass's segment table
+            hipLaunchKernelGGL(fused_seg_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
+                               st->ncalls, nr, (const uint32_t *)rq, (uint32_t)nrec, stride, qoff,
+                               fused_g, segb, wg_seg);
+        else
+            hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(64), 0, s, (const uint32_t *)rq,
+                               (uint32_t)nrec, stride, nr, qoff);
         const uint32_t ne = nc * nr;
         if (!fused)
             hipLaunchKernelGGL(desc_kernel, dim3(grid_for(ne, 256, 4096)), dim3(256), 0, s,
@@ -1740,12 +1757,6 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         const uint64_t items = nrows / CHR + std::min<uint64_t>((uint64_t)nc, nrec) * nr + 1;
         if (fused) {
             const uint64_t nib_words = ((st->X.span + (1ull << RSH) - 1) >> RSH) << (RSH - 3);
-            // the segment table in the item descriptors' space (unused here)
-            uint32_t *segb = (uint32_t *)desc, *wg_seg = segb + nr * (nc + 1);
-            const uint32_t fused_g = (uint32_t)std::min<int>(dev_cus(), (int)FG_MAX);
-            hipLaunchKernelGGL(fused_seg_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t *)coff,
-                               st->ncalls, nr, (const uint32_t *)rq, stride, (const uint32_t *)qoff,
-                               fused_g, segb, wg_seg);
             hipLaunchKernelGGL(newcov_fused_kernel, dim3(fused_g), dim3(LC_THREADS), FUSED_LDS, s,
                                pcs, (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
                                (const uint32_t *)st->nib, nib_words, st->X, nr, st->ncalls,

@@ -45,7 +45,7 @@ if has canon; then
   python3 tools/pmc_summary.py $o > $o/pmc_summary.txt 2>&1; grep -A18 "canon_key_kernel<32" $o/pmc_summary.txt | head -20
 fi
 if has newcov; then
-  N="$B --workload newcov --steps 10 --warmup 3"
+  N="$B --workload newcov --no-early --steps 10 --warmup 3"
   trace newcov $N
   python3 tools/trace_last.py $o/newcov_trace newcov_own_kernel 10 > $o/newcov_timed_summary.txt && head -14 $o/newcov_timed_summary.txt
   pmc_pair newcov newcov_own_kernel 10 $N
