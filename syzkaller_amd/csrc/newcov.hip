@@ -218,7 +218,10 @@ constexpr uint32_t ITEMS_MAX = 65536;    // chunk-count cap (items_target)
 constexpr int LC_THREADS = 1024;         // LDS: two workgroups per CU
 constexpr uint32_t LC_CBW = 16;          // candidates buffered per wave
 constexpr int LC_U = 4;                  // 256-PC rows per step (two steps in flight)
-constexpr int SQ_G = 8;                  // split queries in flight per wave
+#ifndef SYZ_NC_SQG
+#define SYZ_NC_SQG 8
+#endif
+constexpr int SQ_G = SYZ_NC_SQG;         // split queries in flight per wave
 #ifndef SYZ_NC_SPLIT_LNS
 #define SYZ_NC_SPLIT_LNS 5
 #endif
@@ -734,6 +737,10 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
 constexpr uint32_t RSF = 18;
 constexpr size_t FUSED_LDS = ((size_t)1 << (RSF - 1)) + ((size_t)1 << (RSF - 3));  // 160 KB
 constexpr uint32_t FG_MAX = 4096;  // slices
+#ifndef SYZ_NC_FU
+#define SYZ_NC_FU 4
+#endif
+constexpr int FU = SYZ_NC_FU;  // rows per step of the fused pass (two steps in flight)
 
 // The ranges' row offsets (row_offsets_kernel's qoff), the segment starts in
 // the row stream, flat s = q * nc + c: segb[q * (nc + 1) + c] = qoff[q] +
@@ -864,7 +871,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
     };
     auto issue = [&](uint32_t s0, uint4 *pc) {
 #pragma unroll
-        for (int u = 0; u < LC_U; u++) {
+        for (int u = 0; u < FU; u++) {
             const uint32_t i = (s0 + u) & 63;
             const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
             const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
@@ -880,7 +887,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
     uint32_t badv = 0, nonv = 0;
     auto test = [&](uint32_t s0, const uint4 *pc) {
 #pragma unroll
-        for (int u = 0; u < LC_U; u++) {
+        for (int u = 0; u < FU; u++) {
             if (s0 + u >= nrow) break;  // wave-uniform
             const uint32_t i = (s0 + u) & 63;
             const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
@@ -928,7 +935,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
         w0 = min(hi_, lo_ + wv * per);
         w1 = min(hi_, w0 + per);
     };
-    uint4 pcA[LC_U], pcB[LC_U];
+    uint4 pcA[FU], pcB[FU];
     uint32_t s = wg_seg[blockIdx.x], q, c, lo, hi;
     seg(s, q, c, lo, hi);
     share(lo, hi);
@@ -967,11 +974,11 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
                 rows64(rb);
                 issue(0, pcA);
             }
-            for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * LC_U) {
-                issue(s0 + LC_U, pcB);
+            for (uint32_t s0 = 0; s0 < nrow; s0 += 2 * FU) {
+                issue(s0 + FU, pcB);
                 test(s0, pcA);
-                issue(s0 + 2 * LC_U, pcA);
-                test(s0 + LC_U, pcB);
+                issue(s0 + 2 * FU, pcA);
+                test(s0 + FU, pcB);
             }
         }
         if (more) {  // the next segment's first loads, before the barrier

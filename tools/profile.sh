@@ -8,11 +8,11 @@
 #   -> OUT/traffic.json {"C3": phases, "C2": phases, "newcov": ..., "dedup": ...}
 # Counters are never combined with tracing; each pass is its own run within the
 # per-block limits (MI355X_MICROARCH.md, HBM / rocprofv3).
-#   usage: tools/profile.sh OUT [parts: corpus canon newcov newcov_early dedup prio]
+#   usage: tools/profile.sh OUT [parts: corpus canon newcov newcov_early dedup groups prio]
 set -o pipefail
 export TMPDIR=/tmp
 o=${1:-gpurun_out/prof}; shift
-parts=${*:-corpus canon newcov newcov_early dedup prio}
+parts=${*:-corpus canon newcov newcov_early dedup groups prio}
 mkdir -p $o
 B="python3 bench.py --no-cpu --no-c2 --no-dropin"
 has() { case " $parts " in *" $1 "*) return 0;; esac; return 1; }
@@ -61,6 +61,11 @@ if has dedup; then
   trace dedup $D
   python3 tools/trace_last.py $o/dedup_trace "narrow_kernel<4>" 10 > $o/dedup_timed_summary.txt
   pmc_pair dedup "narrow_kernel<4>" 10 $D
+fi
+if has groups; then  # Manager.minimizeCorpus from host buffers (C2 in 293 call groups)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/groups_trace -o run -- python3 tools/kbench.py groups --reps 2 > $o/groups_trace.log 2>&1 || { tail -20 $o/groups_trace.log; exit 1; }
+  python3 tools/trace_summary.py $o/groups_trace > $o/groups_summary.txt && head -24 $o/groups_summary.txt
+  python3 tools/trace_last.py $o/groups_trace group_min_kernel 1 > $o/groups_last_call.txt; head -30 $o/groups_last_call.txt
 fi
 if has prio; then
   trace prio $B --workload prio --steps 10 --warmup 3
