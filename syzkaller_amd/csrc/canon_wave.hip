@@ -213,40 +213,49 @@ __device__ __forceinline__ uint32_t aligned_delta(uint64_t start_mask, uint32_t 
 constexpr int NCLS = 5;
 struct Classes { uint32_t lo[NCLS], hi[NCLS]; };
 
+// BIN_K segments per thread per round, so a round takes one global atomic per
+// class for 256 * BIN_K segments (per 256 the six class counters saw 39 K
+// contended atomics each at C3: 0.45 ms)
+constexpr int BIN_K = 16;
 __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ off, uint64_t nseg,
                                                   Classes C, uint32_t *__restrict__ counts,
                                                   uint32_t *__restrict__ lists, uint64_t stride,
                                                   uint32_t *__restrict__ big_list,
                                                   uint32_t *__restrict__ big_cnt,
                                                   uint64_t max_len, uint32_t *__restrict__ err) {
-    // block-aggregated: LDS counts per class, ONE global atomic per block and class
+    // block-aggregated: LDS counts per class, ONE global atomic per round and class
     __shared__ uint32_t s_cnt[NCLS + 1], s_base[NCLS + 1];
-    const uint32_t l = __lane_id();
+    __shared__ uint32_t s_wofs[4][BIN_K][NCLS + 1];  // each wave's slots in the round
+    const uint32_t l = __lane_id(), wv = threadIdx.x >> 6;
     const uint64_t lt = (1ull << l) - 1ull;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nseg;
-         b0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t per = (uint64_t)blockDim.x * BIN_K;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * per; b0 < nseg; b0 += (uint64_t)gridDim.x * per) {
         if (threadIdx.x <= NCLS) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        const uint64_t i = b0 + threadIdx.x;
-        int c = -1;
-        if (i < nseg) {
-            const uint64_t n = off[i + 1] - off[i];
-            // the host launches only the classes the declared bound reaches:
-            // a longer segment would be left uncanonicalized, so it fails loudly
-            if (n > max_len) atomicOr(err, SYZCOV_ERR_SEGLEN);
-            c = n > WAVE_MAX ? NCLS : -1;  // NCLS = big list
+        int cj[BIN_K];
 #pragma unroll
-            for (int k = 0; k < NCLS; k++)
-                if (n >= C.lo[k] && n <= C.hi[k]) c = k;
-        }
-        uint32_t wofs[NCLS + 1];
-        uint64_t msk[NCLS + 1];
+        for (int j = 0; j < BIN_K; j++) {
+            const uint64_t i = b0 + (uint64_t)j * blockDim.x + threadIdx.x;
+            int c = -1;
+            if (i < nseg) {
+                const uint64_t n = off[i + 1] - off[i];
+                // the host launches only the classes the declared bound reaches:
+                // a longer segment would be left uncanonicalized, so it fails loudly
+                if (n > max_len) atomicOr(err, SYZCOV_ERR_SEGLEN);
+                c = n > WAVE_MAX ? NCLS : -1;  // NCLS = big list
 #pragma unroll
-        for (int k = 0; k <= NCLS; k++) {
-            msk[k] = __ballot(c == k);
-            wofs[k] = 0;
-            if (msk[k] && l == 0) wofs[k] = atomicAdd(&s_cnt[k], (uint32_t)__popcll(msk[k]));
+                for (int k = 0; k < NCLS; k++)
+                    if (n >= C.lo[k] && n <= C.hi[k]) c = k;
+            }
+            cj[j] = c;
         }
+#pragma unroll
+        for (int j = 0; j < BIN_K; j++)
+#pragma unroll
+            for (int k = 0; k <= NCLS; k++) {
+                const uint64_t msk = __ballot(cj[j] == k);
+                if (l == 0) s_wofs[wv][j][k] = msk ? atomicAdd(&s_cnt[k], (uint32_t)__popcll(msk)) : 0u;
+            }
         __syncthreads();
         if (threadIdx.x <= NCLS) {
             const uint32_t k = threadIdx.x;
@@ -254,11 +263,15 @@ __global__ __launch_bounds__(256) void bin_kernel(const uint64_t *__restrict__ o
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k <= NCLS; k++) {
-            const uint32_t wo = __builtin_amdgcn_readfirstlane(wofs[k]);  // lane 0's slot
-            if (c == k) {
-                const uint32_t slot = s_base[k] + wo + (uint32_t)__popcll(msk[k] & lt);
-                if (k < NCLS) lists[k * stride + slot] = (uint32_t)i; else big_list[slot] = (uint32_t)i;
+        for (int j = 0; j < BIN_K; j++) {
+            const uint64_t i = b0 + (uint64_t)j * blockDim.x + threadIdx.x;
+#pragma unroll
+            for (int k = 0; k <= NCLS; k++) {
+                const uint64_t msk = __ballot(cj[j] == k);
+                if (cj[j] == k) {
+                    const uint32_t slot = s_base[k] + s_wofs[wv][j][k] + (uint32_t)__popcll(msk & lt);
+                    if (k < NCLS) lists[k * stride + slot] = (uint32_t)i; else big_list[slot] = (uint32_t)i;
+                }
             }
         }
         __syncthreads();
@@ -1143,7 +1156,7 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
     uint32_t *clists = (uint32_t *)(w + 256 + 2 * align_up(nseg * sizeof(uint32_t), 256));
     uint32_t *ccnt = cnts + 2;
     SYZ_HIP(hipMemsetAsync(ccnt, 0, cw::NCLS * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256, 2048)), dim3(256), 0, s, off,
+    hipLaunchKernelGGL(cw::bin_kernel, dim3(grid_for(nseg, 256 * cw::BIN_K, 2048)), dim3(256), 0, s, off,
                        (uint64_t)nseg, C, ccnt, clists, (uint64_t)nseg, big, cnts + 1,
                        (uint64_t)max_seg_len, err_flag);
     for (int c = 0; c < cw::NCLS; c++) {
