@@ -66,11 +66,13 @@ for step in "$@"; do
     rc=$?; [ $rc -ne 0 ] && { tail -15 $o/$name.err; fatal $rc $name $o/$name.err; exit 1; }
     summ $o/$name.json $name
     ;;
-  trace:*)  # kernel trace + stats of one bench command (ARGS appended)
+  trace:*)  # kernel trace + stats of one bench command (ARGS appended, commas for spaces)
+    targs=${step#trace:}; targs=${targs//,/ }
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $o/trace -o run -- \
-        python3 bench.py --no-cpu --no-c2 --no-dropin ${step#trace:} > $o/trace.log 2>&1 ||
+        python3 bench.py --no-cpu --no-c2 --no-dropin $targs > $o/trace.log 2>&1 ||
         { tail -20 $o/trace.log; exit 1; }
-    python3 tools/trace_summary.py $o/trace | head -40
+    python3 tools/trace_summary.py $o/trace > $o/trace_summary.txt; head -30 $o/trace_summary.txt
+    find $o/trace -name '*kernel_trace.csv' -delete
     ;;
   kbench:*)
     timeout -k 10 300 python -u tools/kbench.py ${step#kbench:} > $o/kbench.log 2>&1
