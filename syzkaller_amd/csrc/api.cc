@@ -49,6 +49,7 @@ uint32_t force_flags() {
     if (strstr(e, "nc_probe")) f |= FORCE_NC_PROBE;
     if (strstr(e, "group_chunks")) f |= FORCE_GROUP_CHUNKS;
     if (strstr(e, "nc_sep")) f |= FORCE_NC_SEP;
+    if (strstr(e, "mr_bytes")) f |= FORCE_MR_BYTES;
     return f;
 }
 

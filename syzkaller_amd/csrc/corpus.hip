@@ -149,8 +149,16 @@ __global__ __launch_bounds__(256) void corpus_popcount_kernel(const uint32_t *__
 }
 
 // Minimize's LDS-resident ranges: 2^20 window PCs (128 KB of covered bits);
-// in key mode 2^17 keys (128 KB of membership bytes | covered bits)
-constexpr uint32_t kRangeShiftWindow = 20, kRangeShiftKeys = 17;
+// in key mode 2^17 keys (128 KB of membership bytes | covered bits), or 2^18
+// keys of nibbles when every low value fits 2 bits (kshift <= 2, the x86 shape)
+constexpr uint32_t kRangeShiftWindow = 20, kRangeShiftKeys = 17, kRangeShiftKeysN4 = 18;
+int minimize_range_keys_n4(const uint64_t *off, const uint32_t *len, const uint32_t *words,
+                           const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                           size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                           const uint64_t *range_tot, const uint8_t *low_of_key,
+                           uint32_t *covered, int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
+                           uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
+                           uint32_t *err_flag, void *ws, hipStream_t s);
 
 struct Corpus {
     std::mutex mu;
@@ -310,6 +318,10 @@ static int setup(Corpus &c, const syzcov_corpus_cfg *cfg) {
         set_error("key space of %llu keys > 2^25", (unsigned long long)c.span);
         return SYZCOV_ERANGE;
     }
+    // nibble tables (CSR key words; SYZCOV_FORCE=mr_bytes keeps the bytes)
+    if (c.key_mode && c.kshift <= 2 && g.canon_layout == 0 &&
+        !(force_flags() & FORCE_MR_BYTES))
+        c.rshift = kRangeShiftKeysN4;
     c.nrange = (uint32_t)nrange_of(c.span, c.rshift);
     if (c.nrange > 256) {
         set_error("PC window too wide for the range engine (> 256 ranges of 2^20)");
@@ -520,6 +532,14 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
             c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
             c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2,
             (uint32_t *)(scal(c) + SC_ERR), c.buf<void>(SYZCOV_CORPUS_WS), s);
+    if (c.key_mode && c.rshift == kRangeShiftKeysN4)
+        return minimize_range_keys_n4(
+            c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
+            c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY), c.buf<uint32_t>(SYZCOV_CORPUS_COVERED),
+            c.buf<int32_t>(SYZCOV_CORPUS_FIRST), c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap,
+            scal(c) + SC_REC, c.buf<uint8_t>(SYZCOV_CORPUS_CAND),
+            c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, (uint32_t *)(scal(c) + SC_ERR),
+            c.buf<void>(SYZCOV_CORPUS_WS), s);
     if (c.key_mode)
         return syzcov_dev_minimize_range_keys(
             c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,

@@ -11,6 +11,7 @@ enum : uint32_t {
     FORCE_NC_PROBE = 8u,
     FORCE_GROUP_CHUNKS = 16u,  // minimizeCorpus: the per-group chunked engine for small groups too
     FORCE_NC_SEP = 32u,        // newcov key mode: candidate pass + separate membership pass
+    FORCE_MR_BYTES = 64u,      // corpus key mode, kshift <= 2: byte tables, not nibbles
 };
 uint32_t force_flags();
 }  // namespace syz

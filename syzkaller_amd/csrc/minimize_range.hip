@@ -470,10 +470,15 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
 //  - anything else (uncovered: a record; covered but not the universe PC:
 //    SYZCOV_ERR_UNIVERSE) is sorted out on a rare, wave-uniform slow path.
 // A record's membership is checked there too (its byte's low 7 bits).
-template <int UG>
+// N4 (kshift <= 2, ranges of 2^18 keys): the table entry is a NIBBLE, the
+// universe PC's low bits (7: none) | UNcovered << 3, 2^18 of them in the same
+// 128 KB — half the ranges of the byte table, so half the sub-run boundary
+// lines (C2X: 32 ranges instead of 64); a low value never reaches 7.
+template <int UG, bool N4 = false>
 __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a, uint32_t b,
                                                              uint32_t P, int load_cov) {
     constexpr uint32_t CW = 8;  // words per lane chunk
+    constexpr uint32_t LOWM = N4 ? 7u : 0x7Fu, USH = N4 ? 3u : 7u;  // entry: low | unc << USH
     // one dynamic block, the range's table at LDS address 0 so that a
     // table read is ds_read_u8 of (word & mask) with no base add; then
     // (KEYS_LDS_EXTRA bytes) the wave descriptors and the piece plan
@@ -508,7 +513,26 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     }
     uint32_t rho, i0, i1;
     if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
-    if (rho != cur_rho) {  // table bytes | UNcovered << 7, 16 keys per uint4
+    if (N4 && rho != cur_rho) {  // nibbles: 8 keys per word from 8 bytes + a covered byte
+        const uint32_t nq = (1u << A.rshift) >> 3;
+        const uint2 *t2 = reinterpret_cast<const uint2 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
+        const uint8_t *cb8 =
+            reinterpret_cast<const uint8_t *>(A.covered) + (((uint64_t)rho << A.rshift) >> 3);
+        for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
+            const uint2 lb = t2[q];
+            const uint32_t unc = load_cov ? ~(uint32_t)cb8[q] : 0xFFu;
+            uint32_t x = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t low = ((j < 4 ? lb.x >> (8 * j) : lb.y >> (8 * (j - 4)))) & 7u;
+                x |= (low | (((unc >> j) & 1u) << 3)) << (4 * j);
+            }
+            s_cov[q] = x;
+        }
+        cur_rho = rho;
+        __syncthreads();
+    }
+    if (!N4 && rho != cur_rho) {  // table bytes | UNcovered << 7, 16 keys per uint4
         uint4 *s4 = reinterpret_cast<uint4 *>(s_cov);
         const uint32_t nq = (1u << A.rshift) >> 4;
         const uint4 *t4 = reinterpret_cast<const uint4 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
@@ -626,7 +650,12 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
 #pragma unroll
                 for (int k = 0; k < (int)CW; k++) {
                     wd[u * CW + k] = vv[k];
-                    tb[u * CW + k] = s_cov8[vv[k] & bm];
+                    if (N4) {
+                        const uint32_t o = vv[k] & bm;
+                        tb[u * CW + k] = (s_cov[o >> 3] >> ((o & 7u) << 2)) & 15u;
+                    } else {
+                        tb[u * CW + k] = s_cov8[vv[k] & bm];
+                    }
                 }
             }
             // element k of a lane's chunk is in its sub-run iff lo <= k < hi
@@ -654,8 +683,8 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
                         const uint32_t t = tb[u * CW + k], lw = wd[u * CW + k] >> SYZ_KEY_BITS;
                         const uint32_t in = (uint32_t)((uint32_t)(k - lo[u]) < span[u]) &
                                             (uint32_t)(t != lw);
-                        nonmem |= in & (uint32_t)((t & 0x7Fu) != lw);
-                        um |= (in & (t >> 7)) << (u * CW + k);
+                        nonmem |= in & (uint32_t)((t & LOWM) != lw);
+                        um |= (in & (t >> USH)) << (u * CW + k);
                     }
                 if (__ballot(um != 0)) {
                     const uint32_t cnt = (uint32_t)__popc(um);
@@ -1062,7 +1091,7 @@ static int minimize_range_impl(
     uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
     size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, const uint8_t *low_of_key,
     uint32_t *err_flag, void *ws, void *stream, const uint64_t *grp_off = nullptr,
-    uint32_t ngroups = 0, int aligned = 0) {
+    uint32_t ngroups = 0, int aligned = 0, bool n4 = false) {
     hipStream_t s = (hipStream_t)stream;
     if (n_items == 0) {
         if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
@@ -1078,8 +1107,8 @@ static int minimize_range_impl(
         A.ak = SYZ_ALIGN_K(A.nrange);
     }
     const bool keym = low_of_key != nullptr;
-    if (keym) {  // key words over <= 2^25 keys, 2^rshift table bytes in LDS
-        if (!err_flag || pc_lo != 0 || range_shift > 17 || pc_span > (1ull << 25))
+    if (keym) {  // key words over <= 2^25 keys, 2^rshift table bytes (N4: nibbles) in LDS
+        if (!err_flag || pc_lo != 0 || range_shift > (n4 ? 18u : 17u) || pc_span > (1ull << 25))
             return SYZCOV_EINVAL;
         A.keymask = SYZ_KEY_MASK;
         A.low_of_key = low_of_key;
@@ -1098,11 +1127,13 @@ static int minimize_range_impl(
 #define SYZ_MR_KEYS_UG 2
 #endif
 #ifndef SYZ_MR_OLD_KEYS
-    const K k1 = keym ? mr::pass1_keys_kernel<SYZ_MR_KEYS_UG> : mr::pass1_stream_kernel<2, false>;
+    const K k1 = keym && n4 ? mr::pass1_keys_kernel<SYZ_MR_KEYS_UG, true>
+                 : keym     ? mr::pass1_keys_kernel<SYZ_MR_KEYS_UG>
+                            : mr::pass1_stream_kernel<2, false>;
 #else
     const K k1 = keym ? mr::pass1_stream_kernel<2, true> : mr::pass1_stream_kernel<2, false>;
 #endif
-    static std::atomic<uint32_t> attr_set[2];
+    static std::atomic<uint32_t> attr_set[3];
 #ifndef SYZ_MR_OLD_KEYS
     // (the table at LDS 0 holds 2^range_shift <= 2^17 bytes, the rest past 2^17)
     const size_t lds1 = keym ? ((size_t)1 << 17) + mr::KEYS_LDS_EXTRA : lds;
@@ -1110,7 +1141,7 @@ static int minimize_range_impl(
     const size_t lds1 = lds;
 #endif
     if ((rc = set_dyn_lds_once((const void *)k1, (uint32_t)std::max<size_t>(lds1, 128 * 1024),
-                               attr_set[keym ? 1 : 0])))
+                               attr_set[keym && n4 ? 2 : keym ? 1 : 0])))
         return rc;
 #ifndef SYZ_MR_FIRST
 #define SYZ_MR_FIRST 64
@@ -1217,6 +1248,22 @@ static int minimize_range_impl(
 // Minimize per call group over one rank space (corpus.hip: the grouped
 // drop-in for Manager.minimizeCorpus); key mode when low_of_key is given.
 namespace syz {
+// Key mode over NIBBLE tables (kshift <= 2: every low value < 4), ranges of
+// 2^18 keys (corpus.hip picks it; the public entry keeps byte tables)
+int minimize_range_keys_n4(const uint64_t *off, const uint32_t *len, const uint32_t *words,
+                           const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                           size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                           const uint64_t *range_tot, const uint8_t *low_of_key,
+                           uint32_t *covered, int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
+                           uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
+                           uint32_t *err_flag, void *ws, hipStream_t s) {
+    if (!low_of_key) return SYZCOV_EINVAL;
+    return minimize_range_impl(off, len, words, split, order, ranks, n_items, 0, nkeys,
+                               range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt,
+                               cand, kept, do_pass2, 0, 0, 0, low_of_key, err_flag, ws, s, nullptr,
+                               0, 0, true);
+}
+
 int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
                           const uint32_t *split, const int32_t *order, size_t n_items,
                           uint32_t pc_lo, uint64_t pc_span, uint32_t range_shift,

@@ -74,6 +74,41 @@ def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2, layout):
     assert np.array_equal(res2.union.cpu().numpy().view(np.uint32), exp_union)
 
 
+@pytest.mark.parametrize("force", ["", "mr_bytes"], ids=["nibbles", "bytes"])
+def test_engine_key_mode_x86_vs_oracle(torch, force, monkeypatch):
+    """The x86-like universe (PC pairs per 16-byte block, kshift 2): Minimize's
+    tables are nibbles over 2^18 keys (every low value fits 2 bits) or, with
+    SYZCOV_FORCE=mr_bytes, bytes over 2^17; both against the oracle, then a
+    non-universe PC (a universe PC + 1: same key, other low bits) in early,
+    middle and last inputs is never aliased (the step recomputes in window
+    mode and returns the reference's results)."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
+    from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
+    n, log2, seed = 3000, 19, 0x5EED0002
+    u = synth_universe(log2, seed, x86=True)
+    uh = u.cpu().numpy().view(np.uint32)
+    lo, span = synth_window(log2, x86=True)
+    off, raw, lens, total = synth_corpus(n, seed, mean=1200, sigma=500, log2_space=log2, x86=True)
+    eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u)
+    assert eng.kshift == 2 and eng.nrange == (4 if not force else 8)
+    exp_kept, exp_union = _oracle_of(off, raw, n)
+    res = eng.step(off, raw, n)
+    assert not res.fallback
+    assert res.kept_idx.cpu().numpy().tolist() == exp_kept
+    assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union)
+    for where in (0, 1500, 2999):
+        off, raw, lens, total = synth_corpus(n, seed, mean=1200, sigma=500, log2_space=log2,
+                                             x86=True)
+        j = int(off[where].item()) + int(lens[where].item()) // 2
+        k = int(raw[j].item()) & 0xFFFFFFFF
+        raw[j] = np.int32(np.uint32(_stray(uh, int(np.searchsorted(uh, k)))))
+        exp_kept, exp_union = _oracle_of(off, raw, n)
+        res = eng.step(off, raw, n)
+        assert res.fallback and res.err_flags & 4, where
+        assert res.kept_idx.cpu().numpy().tolist() == exp_kept, where
+        assert np.array_equal(res.union.cpu().numpy().view(np.uint32), exp_union), where
+
+
 def test_engine_key_mode_window_error(torch):
     """A PC far below the universe's first key: out of the key range, and the
     corpus' PC extent (2^31 PCs) is too wide for the window-mode recompute, so
