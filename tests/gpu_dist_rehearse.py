@@ -25,10 +25,12 @@ def worker(rank, world, port, cfg, keys):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     n = cfg["n"] // world
-    lo, span = synth_window(cfg["log2_space"])
+    x86 = cfg.get("synth_mode", 0) == 2  # C2X: the x86-like universe
+    lo, span = synth_window(cfg["log2_space"], x86=x86)
     off, raw, lens, total = synth_corpus(n, cfg["seed"], first=rank * n, mean=cfg["mean"],
-                                         sigma=cfg["sigma"], log2_space=cfg["log2_space"])
-    univ = synth_universe(cfg["log2_space"], cfg["seed"]) if keys else None
+                                         sigma=cfg["sigma"], log2_space=cfg["log2_space"],
+                                         x86=x86)
+    univ = synth_universe(cfg["log2_space"], cfg["seed"], x86=x86) if keys else None
     inplace = cfg["n"] > 1_000_000
     eng = ShardedEngine(n, total, int(lens.max().item()), lo, span, rank, world, universe=univ,
                         canon_in_place=inplace)
@@ -40,7 +42,7 @@ def worker(rank, world, port, cfg, keys):
             del off, raw
             off, raw, lens, total = synth_corpus(n, cfg["seed"], first=rank * n,
                                                  mean=cfg["mean"], sigma=cfg["sigma"],
-                                                 log2_space=cfg["log2_space"])
+                                                 log2_space=cfg["log2_space"], x86=x86)
         res = eng.step(off, raw, n)
         kept = res.kept_idx.cpu().numpy().astype("<i4").tobytes()
         union = res.union.cpu().numpy().astype("<i4").tobytes()

@@ -139,6 +139,16 @@ def test_world8_rehearsal_c2(torch, keys):
     assert r.returncode == 0 and r.stdout.count("OK") == 8, r.stdout[-3000:] + r.stderr[-3000:]
 
 
+def test_world4_rehearsal_c2x(torch):
+    """Four ranks over C2X (the x86-like universe: kshift 2, Minimize's nibble
+    tables) on one GPU against the oracle's C2X digests."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(HERE, "gpu_dist_rehearse.py"), "4", "C2X",
+                        "keys"], capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and r.stdout.count("OK") == 4, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 def test_world8_rehearsal_c3(torch):
     """Eight ranks over C3 (10M inputs, 82 GB of raw PCs, 1.25M per rank,
     canonicalized in place) on one GPU: the 8-GPU bench's workload and data
