@@ -546,20 +546,23 @@ constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
 
 // exclusive scan of the 2048 u16 counts in bin order, in place
+// (WQ uint4 of words per lane: 4 for the 1024 words of 2048 bins, 8 for the
+// 2048 words of a 12-bit digit's 4096 bins)
+template <int WQ = 4>
 __device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(h);
-    uint4 v[4];
+    uint4 v[WQ];
     uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        v[q] = h4[4 * l + q];
+    for (int q = 0; q < WQ; q++) {
+        v[q] = h4[WQ * l + q];
         const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
         for (int i = 0; i < 4; i++) sum += (w4[i] & 0xFFFFu) + (w4[i] >> 16);
     }
     uint32_t p = wave_incl_scan(sum) - sum;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < WQ; q++) {
         uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -567,15 +570,15 @@ __device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
             w4[i] = p | ((p + lo) << 16);
             p += lo + hi;
         }
-        h4[4 * l + q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        h4[WQ * l + q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
 }
 
-template <int NQ>
+template <int NQ, int WQ = 4>
 __device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
     uint4 *h4 = reinterpret_cast<uint4 *>(h);
 #pragma unroll
-    for (int q = 0; q < 4; q++) h4[4 * l + q] = make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < WQ; q++) h4[WQ * l + q] = make_uint4(0, 0, 0, 0);
 }
 
 // Gapped key words (the sort's register/LDS form in canon_key_kernel): the
@@ -590,9 +593,13 @@ __device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
 __device__ __forceinline__ uint32_t gap_key(uint32_t key, uint32_t low) {
     return key + (key & ~2047u) + (low << SYZ_KEY_BITS);  // key < 2^22
 }
+// D12 (keys < 2^23): the high digit has 12 bits (bits 12-23 of the gapped
+// word, 4096 bins in 2048 words); a pad's high field is 4096 + 2l (bit 24), so
+// its dummy word is 2048 + l
+template <bool D12 = false>
 __device__ __forceinline__ uint32_t pad_word(uint32_t l) {
     const uint32_t d = 2048u + 2u * l;
-    return d | (d << 12);
+    return d | ((D12 ? 4096u + 2u * l : d) << 12);
 }
 // the key word of common.h (key | low << SYZ_KEY_BITS) of a gapped word: bits
 // 0-10 and 25-31 stay, bits 12-25 move down by one (bits 23-25 are zero)
@@ -601,14 +608,19 @@ __device__ __forceinline__ uint32_t ungap_word(uint32_t g) {
     return (g & KEEP) | ((g >> 1) & ~KEEP);  // one v_bfi_b32
 }
 constexpr uint32_t GAP_KEY_MASK = 2047u | (2047u << 12);
+constexpr uint32_t GAP_KEY_MASK12 = 2047u | (4095u << 12);
 static_assert(SYZ_KEY_BITS == 26, "gapped words keep the low bits in place");
 
 // the histogram word of digit field x (bins 2w, 2w + 1 share word w): one
 // bit-field extract and one shift-add (the compiler rewrites a constant
 // extract as (x << 1) & 0x1FFC plus the base, three operations)
+template <int WB = 11>
 __device__ __forceinline__ uint32_t *pair_word(uint32_t *h, uint32_t x) {
     uint32_t w;
-    asm("v_bfe_u32 %0, %1, 1, 11" : "=v"(w) : "v"(x));
+    if (WB == 12)
+        asm("v_bfe_u32 %0, %1, 1, 12" : "=v"(w) : "v"(x));
+    else
+        asm("v_bfe_u32 %0, %1, 1, 11" : "=v"(w) : "v"(x));
     return &h[w];
 }
 
@@ -616,7 +628,7 @@ __device__ __forceinline__ uint32_t *pair_word(uint32_t *h, uint32_t x) {
 // their lane's dummy digit).  Inactive row quads hold pads too.  The bin
 // pair's half is selected by hs = digit << 4: shifts and v_bfe_u32 read only
 // its low 5 bits, (digit & 1) << 4.
-template <int NK>
+template <int NK, int WB = 11>
 __device__ __forceinline__ void count_gap(const uint32_t (&k)[NK], uint32_t nq, uint32_t *h,
                                           uint32_t sh) {
     constexpr int NQ = NK / 4;
@@ -626,12 +638,12 @@ __device__ __forceinline__ void count_gap(const uint32_t (&k)[NK], uint32_t nq, 
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 const uint32_t x = k[q * 4 + c] >> sh;
-                atomicAdd(pair_word(h, x), 1u << ((x << 4) & 31u));
+                atomicAdd(pair_word<WB>(h, x), 1u << ((x << 4) & 31u));
             }
         }
 }
 
-template <int NK, int BQ = SYZ_CANON_BQ>
+template <int NK, int BQ = SYZ_CANON_BQ, int WB = 11>
 __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq, uint32_t *buf,
                                             uint32_t *h, uint32_t sh) {
     constexpr int NQ = NK / 4;
@@ -642,7 +654,7 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++) {
             const uint32_t x = k[q0 * 4 + j] >> sh;
-            r[j] = atomicAdd(pair_word(h, x), 1u << ((x << 4) & 31u));
+            r[j] = atomicAdd(pair_word<WB>(h, x), 1u << ((x << 4) & 31u));
         }
         // every rank atomic of the batch is in flight before the first result
         // is used (interleaved, the extracts waited on each atomic in turn)
@@ -655,13 +667,17 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
     }
 }
 
-template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ>
+template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ,
+          bool D12 = false>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, const uint32_t *list,
                                                                    const uint32_t *count) {
+    constexpr uint32_t HW = D12 ? 2 * KWORDS : KWORDS;  // the high pass's histogram words
+    constexpr int HQ = D12 ? 8 : 4, HB = D12 ? 12 : 11;
+    constexpr uint32_t GMASK = D12 ? GAP_KEY_MASK12 : GAP_KEY_MASK;
     constexpr int CAP = 64 * NK;
     constexpr int NQ = NK / 4;
     __shared__ uint32_t s_buf[WPB][CAP + NK];  // + the lane's pads (<= NK) past CAP
-    __shared__ __attribute__((aligned(16))) uint32_t s_h[WPB][KWORDS + 64];
+    __shared__ __attribute__((aligned(16))) uint32_t s_h[WPB][HW + 64];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
@@ -669,7 +685,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     const uint32_t span_m1 = (uint32_t)(P.span - 1);
     const uint32_t kmax = (uint32_t)(P.nkeys - 1);
     const bool inplace = P.out == P.raw;
-    const uint32_t pad = pad_word(l);
+    const uint32_t pad = pad_word<D12>(l);
     // the previous word of slot 0: the sentinel's key word (cover.go:31,
     // `last := sent`), gapped; ~0 never equals a gapped word
     const uint32_t sent_g = P.sent_key == 0xFFFFFFFFu
@@ -764,14 +780,14 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
 #pragma unroll
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
-        hist16_zero<NQ>(h, l);
+        hist16_zero<NQ, HQ>(h, l);
         wave_sync();
-        count_gap<NK>(k, nq, h, 12);
+        count_gap<NK, HB>(k, nq, h, 12);
         wave_sync();
-        hist16_scan(h, l);
-        h[KWORDS + l] = CAP;
+        hist16_scan<HQ>(h, l);
+        h[HW + l] = CAP;
         wave_sync();
-        scatter_gap<NK, BQK>(k, nq, buf, h, 12);
+        scatter_gap<NK, BQK, HB>(k, nq, buf, h, 12);
         wave_sync();
         // slots [n, 256 nq) take the last key: the unique loop drops them as
         // repeats and the order check passes them, with no per-slot bound test
@@ -803,7 +819,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                         const uint32_t prev = shift_up(v, carry);
                         carry = __builtin_amdgcn_readlane(v, 63);
                         // (slot 0's predecessor is the sentinel: no order)
-                        bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (q + c > 0 || l > 0);
+                        bad |= ((v & GMASK) < (prev & GMASK)) & (q + c > 0 || l > 0);
                     }
                 }
             if (__ballot(bad)) {
@@ -822,7 +838,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     const uint32_t v = k[q * 4 + c];
                     const uint32_t prev = shift_up(v, carry);
                     carry = __builtin_amdgcn_readlane(v, 63);
-                    bad |= ((v & GAP_KEY_MASK) < (prev & GAP_KEY_MASK)) & (q + c > 0 || l > 0);
+                    bad |= ((v & GMASK) < (prev & GMASK)) & (q + c > 0 || l > 0);
                     // whole words: distinct PCs stay distinct even if they share a key
                     const bool keep = v != prev;
                     const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
@@ -1019,7 +1035,7 @@ static unsigned resident_grid(uint64_t nseg) {
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nseg + cw::WPB - 1) / cw::WPB, cap));
 }
 
-template <int NK, int MW, bool AL>
+template <int NK, int MW, bool AL, bool D12 = false>
 static unsigned resident_grid_key(uint64_t nseg) {
     static unsigned cap = 0;
     if (!cap) {
@@ -1029,7 +1045,8 @@ static unsigned resident_grid_key(uint64_t nseg) {
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess) ncu = pr.multiProcessorCount;
         }
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &nb, reinterpret_cast<const void *>(cw::canon_key_kernel<NK, MW, AL>),
+                &nb, reinterpret_cast<const void *>(
+                         cw::canon_key_kernel<NK, MW, AL, AL ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ, D12>),
                 64 * cw::WPB, 0) != hipSuccess || nb < 1)
             nb = 1;
         cap = (unsigned)(nb * ncu);
@@ -1040,7 +1057,11 @@ static unsigned resident_grid_key(uint64_t nseg) {
 template <int NK, int MW>
 static void launch_key_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
                              uint64_t nseg, hipStream_t s) {
-    if (P.ak)  // line-aligned sub-runs: a separate build of the kernel (no per-word branch)
+    if (P.nkeys > (1ull << 22) && !P.ak)  // keys < 2^23: a 12-bit high digit
+        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, false, SYZ_CANON_BQ, true>),
+                           dim3(resident_grid_key<NK, MW, false, true>(nseg)), dim3(64 * cw::WPB),
+                           0, s, P, lc, cnt);
+    else if (P.ak)  // line-aligned sub-runs: a separate build of the kernel (no per-word branch)
         hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, true>),
                            dim3(resident_grid_key<NK, MW, true>(nseg)), dim3(64 * cw::WPB), 0, s,
                            P, lc, cnt);
@@ -1134,8 +1155,11 @@ static int canon_split_impl(const uint64_t *off, const uint32_t *raw, uint32_t *
 #define SYZ_CANON_KEY2 2
 #endif
     const uint32_t force = force_flags();
-    const int key2 =
-        (key_out && nkeys <= (1ull << 22) && !(force & FORCE_CANON3)) ? SYZ_CANON_KEY2 : 0;
+    // 2 passes: 11 + 11 bits up to 2^22 keys, 11 + 12 (CSR) up to 2^23
+    const int key2 = (key_out && !(force & FORCE_CANON3) &&
+                      (nkeys <= (1ull << 22) || (nkeys <= (1ull << 23) && !aligned)))
+                         ? SYZ_CANON_KEY2
+                         : 0;
     P.force_redo = (force & FORCE_REDO) ? 1u : 0u;
     P.ak = aligned ? SYZ_ALIGN_K((uint32_t)nrange) : 0u;
     cw::Params PK = P;  // the key kernel's unique loop compares (key | low bits) words
