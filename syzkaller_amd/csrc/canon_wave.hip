@@ -361,9 +361,10 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     uint32_t li = blockIdx.x * WPB + w;
     if (li < nl) issue(li);
     for (; li < nl; li += nw) {
-        const uint32_t seg = seg_n;
-        const uint64_t base = base_n;
-        const uint32_t n = n_n;
+        // wave-uniform descriptor in scalar registers (canon_key_kernel)
+        const uint32_t seg = uniform_u32(seg_n);
+        const uint64_t base = uniform_u64(base_n);
+        const uint32_t n = uniform_u32(n_n);
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
         const uint32_t nq = (end + 255) >> 8;  // active row quads (256 keys each)
@@ -751,9 +752,11 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     uint32_t li = blockIdx.x * WPB + w;
     if (li < nl) issue(li);
     for (; li < nl; li += nw) {
-        const uint32_t seg = seg_n;
-        const uint64_t base = base_n;
-        const uint32_t n = n_n;
+        // the descriptor is wave-uniform: scalar registers, so the output
+        // pointer is not re-read from a VGPR (v_readfirstlane + s_nop) per store
+        const uint32_t seg = uniform_u32(seg_n);
+        const uint64_t base = uniform_u64(base_n);
+        const uint32_t n = uniform_u32(n_n);
         const uint64_t a0 = base & ~3ull;
         const uint32_t head = (uint32_t)(base - a0), end = head + n;
         // (an empty segment sorts nothing: with an unaligned start its one row

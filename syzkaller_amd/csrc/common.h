@@ -75,6 +75,15 @@ __device__ __forceinline__ T issue_fence(T x) {
     return x;
 }
 
+// A wave-uniform value into scalar registers (the builtin returns int: both
+// halves go through uint32_t, or a low half with bit 31 set sign-extends)
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | uniform_u32((uint32_t)v);
+}
+
 // Wave-wide inclusive scan of a u32 (64 lanes) in DPP, no LDS: row_shr 1, 2,
 // 4, 8 scan each row of 16 lanes (lanes shifted in from outside the row read
 // the identity 0), then row_bcast:15 adds row r-1's total to rows 1 and 3 and
