@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
             }
         uint32_t bad = P.force_redo;
         if (inplace) {  // nothing may be written before the order is known
-            uint32_t carry = P.sent_key;
+            uint32_t rprev = P.sent_key;  // predecessors as in canon_key_kernel
 #pragma unroll
             for (int q = 0; q < NQ; q++)
                 if ((uint32_t)q < nq) {
@@ -441,8 +441,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                     for (int c = 0; c < 4; c++) {
                         const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
                         const uint32_t v = k[q * 4 + c];
-                        const uint32_t prev = shift_up(v, carry);
-                        carry = __builtin_amdgcn_readlane(v, 63);
+                        const uint32_t r = rotate_up(v);
+                        const uint32_t prev = l == 0 ? rprev : r;
+                        rprev = r;
                         bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
                     }
                 }
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = P.sent_key, dcar = 0;
+        uint32_t cnt = 0, rprev = P.sent_key, dcar = 0;
         uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
 #pragma unroll
         for (int q = 0; q < NQ; q++)
@@ -460,8 +461,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
                 for (int c = 0; c < 4; c++) {
                     const uint32_t e = (uint32_t)((q * 4 + c) * 64) + l;
                     const uint32_t v = k[q * 4 + c];
-                    const uint32_t prev = shift_up(v, carry);
-                    carry = __builtin_amdgcn_readlane(v, 63);
+                    const uint32_t r = rotate_up(v);
+                    const uint32_t prev = l == 0 ? rprev : r;
+                    rprev = r;
                     bad |= (uint32_t)(v < prev) & (uint32_t)(e - 1u < n - 1u);
                     // keys outside [0, span) (flagged at load) sort last and are
                     // dropped, so nothing downstream indexes past the key range
@@ -845,16 +847,21 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 for (int c = 0; c < 4; c++) k[q * 4 + c] = buf[(q * 4 + c) * 64 + l];
             }
         bool bad = P.force_redo != 0;
+        // a slot's predecessor words: the slot rotated up one lane, lane 0 taking
+        // the previous slot's rotated word (its lane 63) — two VALU operations,
+        // where a shift with the carry read out by v_readlane took three
+        const bool lane0 = l == 0;
         if (inplace) {  // nothing may be written before the order is known
-            uint32_t carry = sent_g;
+            uint32_t rprev = sent_g;
 #pragma unroll
             for (int q = 0; q < NQ; q++)
                 if ((uint32_t)q < nq) {
 #pragma unroll
                     for (int c = 0; c < 4; c++) {
                         const uint32_t v = k[q * 4 + c];
-                        const uint32_t prev = shift_up(v, carry);
-                        carry = __builtin_amdgcn_readlane(v, 63);
+                        const uint32_t r = rotate_up(v);
+                        const uint32_t prev = lane0 ? rprev : r;
+                        rprev = r;
                         // (slot 0's predecessor is the sentinel: no order)
                         bad |= ((v & GMASK) < (prev & GMASK)) & (q + c > 0 || l > 0);
                     }
@@ -864,7 +871,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 continue;
             }
         }
-        uint32_t cnt = 0, carry = sent_g;
+        uint32_t cnt = 0, rprev = sent_g;
         uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
         constexpr bool direct = !ALIGNED;  // line-aligned: written from buf below
 #pragma unroll
@@ -873,8 +880,9 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
 #pragma unroll
                 for (int c = 0; c < 4; c++) {
                     const uint32_t v = k[q * 4 + c];
-                    const uint32_t prev = shift_up(v, carry);
-                    carry = __builtin_amdgcn_readlane(v, 63);
+                    const uint32_t r = rotate_up(v);
+                    const uint32_t prev = lane0 ? rprev : r;
+                    rprev = r;
                     bad |= ((v & GMASK) < (prev & GMASK)) & (q + c > 0 || l > 0);
                     // whole words: distinct PCs stay distinct even if they share a key
                     const bool keep = v != prev;

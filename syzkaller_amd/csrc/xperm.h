@@ -55,4 +55,10 @@ namespace syz {
 __device__ __forceinline__ uint32_t shift_up(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xF, 0xF, false);
 }
+// Lane l receives v of lane l-1, lane 0 that of lane 63 (DPP wave_ror:1).
+__device__ __forceinline__ uint32_t rotate_up(uint32_t v) {
+    // (mov_dpp with bound_ctrl: no `old` operand, which update_dpp copies
+    // into the destination first although every lane has a source)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, true);
+}
 }  // namespace syz
