@@ -124,8 +124,11 @@ __device__ __forceinline__ void hist_zero(uint32_t *hist, uint32_t l) {
 #ifndef SYZ_CANON_BQ
 #define SYZ_CANON_BQ 2
 #endif
+#ifndef SYZ_CANON_BQK  // row quads per rank batch of the key kernel
+#define SYZ_CANON_BQK SYZ_CANON_BQ
+#endif
 #ifndef SYZ_CANON_BQ_AL
-#define SYZ_CANON_BQ_AL SYZ_CANON_BQ
+#define SYZ_CANON_BQ_AL SYZ_CANON_BQK
 #endif
 // Only REAL keys take part: slots outside the segment (the aligned head, the
 // tail of the last row quad) are skipped rather than ranked as maximal pads,
@@ -688,8 +691,10 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
     for (int q0 = 0; q0 < NQ; q0 += BQ) {
         if ((uint32_t)q0 >= nq) continue;
         uint32_t r[4 * BQ];
+        // (a last batch may be partial: NQ need not be a multiple of BQ)
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++) {
+            if (q0 * 4 + j >= NK) break;
             const uint32_t x = k[q0 * 4 + j] >> sh;
             r[j] = atomicAdd(pair_word<WB>(h, x), 1u << ((x << 4) & 31u));
         }
@@ -698,13 +703,14 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 4 * BQ; j++) {
+            if (q0 * 4 + j >= NK) break;
             const uint32_t hs = (k[q0 * 4 + j] >> sh) << 4;
             buf[__builtin_amdgcn_ubfe(r[j], hs, 16)] = k[q0 * 4 + j];  // offset = hs & 31
         }
     }
 }
 
-template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ,
+template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQK,
           bool D12 = false>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, const uint32_t *list,
                                                                    const uint32_t *count) {
@@ -1091,7 +1097,7 @@ static unsigned resident_grid_key(uint64_t nseg) {
         }
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
                 &nb, reinterpret_cast<const void *>(
-                         cw::canon_key_kernel<NK, MW, AL, AL ? SYZ_CANON_BQ_AL : SYZ_CANON_BQ, D12>),
+                         cw::canon_key_kernel<NK, MW, AL, AL ? SYZ_CANON_BQ_AL : SYZ_CANON_BQK, D12>),
                 64 * cw::WPB, 0) != hipSuccess || nb < 1)
             nb = 1;
         cap = (unsigned)(nb * ncu);
@@ -1103,7 +1109,7 @@ template <int NK, int MW>
 static void launch_key_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
                              uint64_t nseg, hipStream_t s) {
     if (P.nkeys > (1ull << 22) && !P.ak)  // keys < 2^23: a 12-bit high digit
-        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, false, SYZ_CANON_BQ, true>),
+        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, false, SYZ_CANON_BQK, true>),
                            dim3(resident_grid_key<NK, MW, false, true>(nseg)), dim3(64 * cw::WPB),
                            0, s, P, lc, cnt);
     else if (P.ak)  // line-aligned sub-runs: a separate build of the kernel (no per-word branch)
