@@ -566,60 +566,7 @@ constexpr uint32_t KWORDS = 1u << (KB - 1);  // 2048 u16 bins in 1024 words
 
 __device__ __forceinline__ uint32_t hinc(uint32_t d) { return 1u << ((d & 1u) << 4); }
 
-// exclusive scan of the 2048 u16 counts in bin order, in place
-// (WQ uint4 of words per lane: 4 for the 1024 words of 2048 bins, 8 for the
-// 2048 words of a 12-bit digit's 4096 bins).  Lane l holds chunks q * 64 + l
-// (lane-contiguous 16-byte accesses, conflict-free; a lane-contiguous run of
-// WQ chunks put lanes 4 (WQ 8: 2) apart on the same banks, a 4-way (8-way)
-// conflict on every read and write), so chunk row q's prefix is the rows
-// before it plus a wave scan within the row: two rows per scan, packed as
-// u16 pairs (a segment's counts stay below 2^16).
-template <int WQ = 4>
-__device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
-    static_assert(WQ % 2 == 0, "rows are scanned in pairs");
-    uint4 *h4 = reinterpret_cast<uint4 *>(h);
-    uint4 v[WQ];
-    uint32_t s[WQ];
-#pragma unroll
-    for (int q = 0; q < WQ; q++) {
-        v[q] = h4[q * 64 + l];
-        const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-        s[q] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) s[q] += (w4[i] & 0xFFFFu) + (w4[i] >> 16);
-    }
-    uint32_t base = 0;
-#pragma unroll
-    for (int q = 0; q < WQ; q += 2) {
-        const uint32_t inc = wave_incl_scan(s[q] | (s[q + 1] << 16));
-        const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
-        uint32_t pq[2];
-        pq[0] = base + (inc & 0xFFFFu) - s[q];
-        base += tot & 0xFFFFu;
-        pq[1] = base + (inc >> 16) - s[q + 1];
-        base += tot >> 16;
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const uint4 vv = v[q + r];
-            uint32_t w4[4] = {vv.x, vv.y, vv.z, vv.w};
-            uint32_t p = pq[r];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t lo = w4[i] & 0xFFFFu, hi = w4[i] >> 16;
-                w4[i] = p | ((p + lo) << 16);
-                p += lo + hi;
-            }
-            h4[(q + r) * 64 + l] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
-    }
-}
-
-template <int NQ, int WQ = 4>
-__device__ __forceinline__ void hist16_zero(uint32_t *h, uint32_t l) {
-    uint4 *h4 = reinterpret_cast<uint4 *>(h);
-#pragma unroll
-    for (int q = 0; q < WQ; q++) h4[q * 64 + l] = make_uint4(0, 0, 0, 0);
-}
+// hist16_scan / hist16_zero: common.h (shared with dedup.hip's radix kernel)
 
 // Gapped key words (the sort's register/LDS form in canon_key_kernel): the
 // 22-bit key's digits 12 bits apart, lo11 | hi11 << 12, and the PC's low bits

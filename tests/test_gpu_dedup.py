@@ -26,6 +26,12 @@ def _buf(rng, n, kind):
             b[rng.integers(0, n, 3)] = np.uint64(2**64 - 1)
             b[rng.integers(0, n, 2)] = 0
         return b
+    if kind == "cross":  # u32 keys across a 2^32 boundary; spans up to 2^32 - 1
+        b = np.uint64(0xFFFFFF00) + rng.integers(0, 512, n).astype(np.uint64)
+        if n > 4 and n % 2:
+            b[0] = np.uint64(0x1_0000_0000 - 7)
+            b[1] = np.uint64(0x1_0000_0000 - 7 + 0xFFFFFFFF)  # span exactly 2^32 - 1
+        return b
     if kind == "sorted":
         return np.sort(rng.integers(1, 1 << 40, n).astype(np.uint64))
     return np.sort(rng.integers(1, 1 << 40, n).astype(np.uint64))[::-1].copy()  # reversed
@@ -52,9 +58,9 @@ def _run(lens, bufs, out32=True):
     return off, pcs, nl, o32
 
 
-@pytest.mark.parametrize("kind", ["kernel", "dense", "wide", "sorted", "reversed"])
+@pytest.mark.parametrize("kind", ["kernel", "dense", "wide", "sorted", "reversed", "cross"])
 def test_dedup_batch_vs_oracle(kind):
-    rng = np.random.default_rng(["kernel", "dense", "wide", "sorted", "reversed"].index(kind))
+    rng = np.random.default_rng(["kernel", "dense", "wide", "sorted", "reversed", "cross"].index(kind))
     lens = list(LENS) + list(rng.integers(0, 3000, 40))
     rng.shuffle(lens)
     bufs = [_buf(rng, int(n), kind) for n in lens]
