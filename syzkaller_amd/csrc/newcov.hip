@@ -753,28 +753,41 @@ __global__ __launch_bounds__(1024) void fused_seg_kernel(const uint32_t *__restr
                                                          uint32_t *__restrict__ qoff,
                                                          uint32_t G, uint32_t *__restrict__ segb,
                                                          uint32_t *__restrict__ wg_seg) {
-    if (threadIdx.x == 0) {
-        uint32_t o = 0;
-        for (uint32_t q = 0; q < nr; q++) {
-            qoff[q] = o;
-            o += Rq[(uint64_t)q * stride + m];
+    // qoff: one wave, lane q loads range q's row count (nr <= NR_MAX = 32),
+    // a DPP scan (thread 0 walking the ranges paid a dependent load each)
+    __shared__ uint32_t s_qoff[NR_MAX + 1];
+    if (threadIdx.x < 64) {
+        const uint32_t q = threadIdx.x;
+        const uint32_t rc = q < nr ? Rq[(uint64_t)q * stride + m] : 0u;
+        const uint32_t inc = wave_incl_scan(rc);
+        if (q <= nr) {
+            qoff[q] = inc - rc;
+            s_qoff[q] = inc - rc;
         }
-        qoff[nr] = o;
     }
     __syncthreads();
+    // the segment starts also go to LDS when they fit: the slices' binary
+    // searches then wait on LDS reads, not on ~13 dependent global loads each
+    // (17 us of the C5 batch with the table read from L2)
+    constexpr uint32_t SB_LDS = 12288;
+    __shared__ uint32_t s_sb[SB_LDS];
     const uint32_t nc = (uint32_t)ncalls, n = nr * (nc + 1);
+    const bool in_lds = n <= SB_LDS;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint32_t q = i / (nc + 1), c = i - q * (nc + 1);
-        segb[i] = qoff[q] + Rq[(uint64_t)q * stride + coff[c]];
+        const uint32_t v = s_qoff[q] + Rq[(uint64_t)q * stride + coff[c]];
+        segb[i] = v;
+        if (in_lds) s_sb[i] = v;
     }
     __syncthreads();
-    const uint32_t rt = qoff[nr], ns = nr * nc;
+    const uint32_t *sb = in_lds ? s_sb : segb;
+    const uint32_t rt = s_qoff[nr], ns = nr * nc;
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
         const uint32_t a = (uint32_t)((uint64_t)rt * g / G);
         uint32_t lo = 0, hi = ns;  // largest s with start(s) <= a (start(0) = 0)
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1, q = mid / nc;
-            if (segb[q * (nc + 1) + (mid - q * nc)] <= a) lo = mid; else hi = mid;
+            if (sb[q * (nc + 1) + (mid - q * nc)] <= a) lo = mid; else hi = mid;
         }
         wg_seg[g] = lo;
     }
