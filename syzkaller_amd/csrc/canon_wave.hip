@@ -1055,9 +1055,12 @@ static unsigned resident_grid_key(uint64_t nseg) {
 template <int NK, int MW>
 static void launch_key_class(const cw::Params &P, const uint32_t *lc, const uint32_t *cnt,
                              uint64_t nseg, hipStream_t s) {
-    if (P.nkeys > (1ull << 22) && !P.ak)  // keys < 2^23: a 12-bit high digit
-        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, false, SYZ_CANON_BQK, true>),
-                           dim3(resident_grid_key<NK, MW, false, true>(nseg)), dim3(64 * cw::WPB),
+    // keys < 2^23: a 12-bit high digit (its 8.4 KB histogram leaves LDS for
+    // at most 2 waves per SIMD, so that is the register budget too)
+    constexpr int MW12 = MW > 2 ? 2 : MW;
+    if (P.nkeys > (1ull << 22) && !P.ak)
+        hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW12, false, SYZ_CANON_BQK, true>),
+                           dim3(resident_grid_key<NK, MW12, false, true>(nseg)), dim3(64 * cw::WPB),
                            0, s, P, lc, cnt);
     else if (P.ak)  // line-aligned sub-runs: a separate build of the kernel (no per-word branch)
         hipLaunchKernelGGL((cw::canon_key_kernel<NK, MW, true>),
