@@ -1236,6 +1236,73 @@ __global__ __launch_bounds__(256) void newcov_own_kernel(
     }
 }
 
+// Packed slots, when ncalls x span < 2^32 (C5: 293 x 2^22): one u64 per slot,
+// (call x span + index) << 32 | min record, so a probe, its insert (CAS, then
+// atomicMin on the same word) and the owner test touch one line, where the
+// key and value arrays took two; the clear writes 8 bytes per slot, not 12.
+__device__ __forceinline__ uint32_t slot_key(const Index &X, uint32_t c, uint32_t pc) {
+    uint32_t ix;
+    pc_index_range(X, pc, &ix);  // candidates are inside (checked by the cand pass)
+    return c * (uint32_t)X.span + ix;
+}
+
+__global__ void hash_clear32_kernel(const uint32_t *__restrict__ stats,
+                                    unsigned long long *__restrict__ slots) {
+    if (stats[0] || !stats[1]) return;
+    const uint64_t cap = hash_cap(stats[1]);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        slots[i] = EMPTY_KEY;
+}
+
+__global__ __launch_bounds__(256) void newcov_insert32_kernel(
+    const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
+    const uint32_t *__restrict__ stats, unsigned long long *__restrict__ slots, Index X) {
+    if (stats[0] || !stats[1]) return;
+    const uint32_t n = stats[1];
+    const uint64_t mask = hash_cap(n) - 1;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 kp = clist[i];
+        const uint32_t key = slot_key(X, (uint32_t)callid[kp.x], kp.y);
+        const unsigned long long mine = (unsigned long long)key << 32 | kp.x;
+        uint64_t h = hash64(key) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&slots[h], EMPTY_KEY, mine);
+            if (prev == EMPTY_KEY) break;
+            if ((uint32_t)(prev >> 32) == key) {  // same key: the smaller record stays
+                if (prev > mine) atomicMin(&slots[h], mine);
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void newcov_own32_kernel(
+    const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
+    const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ slots,
+    uint8_t *__restrict__ is_new, uint32_t *__restrict__ maxcov, uint32_t *__restrict__ mfl,
+    uint64_t words_per_call, Index X, uint32_t *__restrict__ stats_out) {
+    if (stats_out && blockIdx.x == 0 && threadIdx.x < 2) stats_out[threadIdx.x] = stats[threadIdx.x];
+    if (stats[0] || !stats[1]) return;
+    const uint32_t n = stats[1];
+    const uint64_t mask = hash_cap(n) - 1;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 kp = clist[i];
+        const uint32_t c = (uint32_t)callid[kp.x];
+        const uint32_t key = slot_key(X, c, kp.y);
+        uint64_t h = hash64(key) & mask;
+        unsigned long long v;
+        while ((uint32_t)((v = slots[h]) >> 32) != key) h = (h + 1) & mask;
+        if ((uint32_t)v == kp.x) {
+            is_new[kp.x] = 1;
+            const uint32_t ix = key - c * (uint32_t)X.span;
+            atomicOr(&maxcov[(uint64_t)c * words_per_call + (ix >> 5)], 1u << (ix & 31));
+            if (mfl) atomicOr(&mfl[(uint64_t)c * words_per_call + (ix >> 5)], 1u << (ix & 31));
+        }
+    }
+}
+
 // mfl[c] = maxcov[c] | flakes for every call
 __global__ void mfl_build_kernel(const uint4 *__restrict__ maxcov, const uint4 *__restrict__ flakes,
                                  uint64_t vec_per_call, uint64_t n, uint4 *__restrict__ mfl) {
@@ -1800,14 +1867,25 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                            (const uint32_t *)perm, (const uint32_t *)coff, st->ncalls, clist, stats);
     }
     const unsigned gh = grid_for(std::max<uint64_t>(npc, 512), 256, 8192);
-    hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats, hkey,
-                       hval);
-    hipLaunchKernelGGL(newcov_insert_kernel, dim3(gh), dim3(256), 0, s, callid,
-                       (const uint2 *)clist, (const uint32_t *)stats, hkey, hval);
-    hipLaunchKernelGGL(newcov_own_kernel, dim3(gh), dim3(256), 0, s, callid, (const uint2 *)clist,
-                       (const uint32_t *)stats, (const unsigned long long *)hkey,
-                       (const uint32_t *)hval, is_new, st->maxcov, st->mfl, st->words, st->X,
-                       stats_user);
+    if ((uint64_t)st->ncalls * st->X.span <= 0xFFFFFFFFull && !(ff & FORCE_NC_HASH64)) {
+        hipLaunchKernelGGL(hash_clear32_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats,
+                           hkey);
+        hipLaunchKernelGGL(newcov_insert32_kernel, dim3(gh), dim3(256), 0, s, callid,
+                           (const uint2 *)clist, (const uint32_t *)stats, hkey, st->X);
+        hipLaunchKernelGGL(newcov_own32_kernel, dim3(gh), dim3(256), 0, s, callid,
+                           (const uint2 *)clist, (const uint32_t *)stats,
+                           (const unsigned long long *)hkey, is_new, st->maxcov, st->mfl,
+                           st->words, st->X, stats_user);
+    } else {
+        hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats,
+                           hkey, hval);
+        hipLaunchKernelGGL(newcov_insert_kernel, dim3(gh), dim3(256), 0, s, callid,
+                           (const uint2 *)clist, (const uint32_t *)stats, hkey, hval);
+        hipLaunchKernelGGL(newcov_own_kernel, dim3(gh), dim3(256), 0, s, callid,
+                           (const uint2 *)clist, (const uint32_t *)stats,
+                           (const unsigned long long *)hkey, (const uint32_t *)hval, is_new,
+                           st->maxcov, st->mfl, st->words, st->X, stats_user);
+    }
     SYZ_LAUNCH_CHECK();
     return 0;
 }

@@ -142,8 +142,10 @@ def newcov_path(request, monkeypatch):
     """Every candidate pass of newcov.hip: LDS-staged key ranges (in key mode
     with kshift <= 4 one fused pass, membership from LDS nibbles; "sep": the
     candidate pass, then the separate membership pass) and global bitmap
-    probes (the library picks one per batch from its shape)."""
-    monkeypatch.setenv("SYZCOV_FORCE", {"lds": "nc_lds", "sep": "nc_lds,nc_sep",
+    probes (the library picks one per batch from its shape).  "sep" also takes
+    the ownership hash with u64 keys and separate values (the packed u64 slots
+    otherwise, whenever calls x index span < 2^32)."""
+    monkeypatch.setenv("SYZCOV_FORCE", {"lds": "nc_lds", "sep": "nc_lds,nc_sep,nc_hash64",
                                         "probe": "nc_probe"}[request.param])
     return request.param
 
