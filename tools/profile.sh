@@ -47,14 +47,14 @@ fi
 if has newcov; then
   N="$B --workload newcov --no-early --steps 10 --warmup 3"
   trace newcov $N
-  python3 tools/trace_last.py $o/newcov_trace newcov_own_kernel 10 > $o/newcov_timed_summary.txt && head -14 $o/newcov_timed_summary.txt
-  pmc_pair newcov newcov_own_kernel 10 $N
+  python3 tools/trace_last.py $o/newcov_trace newcov_own 10 > $o/newcov_timed_summary.txt && head -14 $o/newcov_timed_summary.txt
+  pmc_pair newcov newcov_own 10 $N
 fi
 if has newcov_early; then  # the early regime: 32 history batches, every record still new
   E="$B --workload newcov --history 32 --steps 10 --warmup 3"
   trace newcov_early $E
-  python3 tools/trace_last.py $o/newcov_early_trace newcov_own_kernel 10 > $o/newcov_early_timed_summary.txt && head -14 $o/newcov_early_timed_summary.txt
-  pmc_pair newcov_early newcov_own_kernel 10 $E
+  python3 tools/trace_last.py $o/newcov_early_trace newcov_own 10 > $o/newcov_early_timed_summary.txt && head -14 $o/newcov_early_timed_summary.txt
+  pmc_pair newcov_early newcov_own 10 $E
 fi
 if has dedup; then
   D="$B --workload dedup --steps 10 --warmup 3"
