@@ -236,6 +236,36 @@ def test_newcov_multi_range(newcov_path):
     st.close()
 
 
+@pytest.mark.parametrize("span", [(1 << 30) - 1, 1 << 30])
+def test_newcov_ownership_slot_boundary(span):
+    """The ownership hash packs (call x span + index) << 32 | record into one
+    u64 slot while calls x span < 2^32 (span 2^30 - 1 with 4 calls: keys up to
+    2^32 - 5, next to the empty slot's all-ones) and falls back to u64 keys
+    with separate values at 2^32 (span 2^30): both against the oracle, with
+    many records on the top keys of the last call and shared new PCs."""
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(41)
+    ncalls, lo = 4, 0
+    st = CoverState(ncalls, lo, span)
+    mc = [[] for _ in range(ncalls)]
+    for batch in range(2):
+        nrec = 3000
+        cids = rng.integers(0, ncalls, size=nrec).astype(np.int32)
+        cids[: nrec // 2] = ncalls - 1
+        recs = []
+        for k in range(nrec):
+            top = int(cids[k]) == ncalls - 1
+            base = lo + span - 4096 if top else lo
+            width = 4096 if top else span
+            recs.append(np.unique(rng.integers(base, base + width,
+                                               size=int(rng.integers(0, 200)))).astype(np.uint32))
+        exp, mc = orc.newcov_batch(mc, [], cids, recs)
+        assert np.array_equal(st.new_coverage(cids, recs), exp), (span, batch)
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (span, batch, c)
+    st.close()
+
+
 def test_newcov_sentinel_full_window():
     """Full 2^32 window (the CoverState default): a record whose only new PC
     is 0xFFFFFFFF is NOT new (Difference drops the sentinel, cover.go:43-48,
