@@ -657,6 +657,22 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
     }
 }
 
+// Wave priority by how far the wave is into its segment (s_setprio): 0
+// converting the raw rows (and issuing the next segment's loads), 1 in the
+// low-digit pass, 2 in the high-digit pass, 3 in unique + output + split.  Of
+// the 3 waves a SIMD holds, the one furthest along issues first, so the
+// waves spread over the phases and one wave's LDS-bound ranks overlap another's
+// VALU-bound conversion or unique loop instead of all three queueing on the
+// LDS together.  C3 canon 57.2 → 48.9 ms (DESIGN.md §4.1 with the other
+// placements measured).  SYZ_CANON_AGE_PRIO=0 builds leave every wave at 0.
+#ifndef SYZ_CANON_AGE_PRIO
+#define SYZ_CANON_AGE_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void age_prio() {
+    if constexpr (SYZ_CANON_AGE_PRIO != 0) __builtin_amdgcn_s_setprio(P);
+}
+
 template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQK,
           bool D12 = false>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, const uint32_t *list,
@@ -709,6 +725,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     for (; li < nl; li += nw) {
         // the descriptor is wave-uniform: scalar registers, so the output
         // pointer is not re-read from a VGPR (v_readfirstlane + s_nop) per store
+        age_prio<0>();
         const uint32_t seg = uniform_u32(seg_n);
         const uint64_t base = uniform_u64(base_n);
         const uint32_t n = uniform_u32(n_n);
@@ -747,6 +764,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         // (before the next segment's loads: deferred, the slots' masks stayed alive)
         if (__builtin_amdgcn_ballot_w64(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
         if (li + nw < nl) issue(li + nw);
+        age_prio<1>();
         // ---------------------------------------- pass 0: low 11 bits
         hist16_zero<NQ>(h, l);
         wave_sync();
@@ -766,6 +784,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         }
         wave_sync();
         // ---------------------------- pass 1: high 11 bits, stable (row-major)
+        age_prio<2>();
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
@@ -781,6 +800,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
         wave_sync();
         scatter_gap<NK, BQK, HB>(k, nq, buf, h, 12);
         wave_sync();
+        age_prio<3>();
         // slots [n, 256 nq) take the last key: the unique loop drops them as
         // repeats and the order check passes them, with no per-slot bound test
         if (n) {
