@@ -314,6 +314,23 @@ __device__ __forceinline__ uint32_t split_bound(const Params &P, uint32_t j) {
 // scatters (packed histogram), so a pass is one read-back and one scatter
 // loop; the keys of the pass being scattered live in registers only between
 // those two loops.
+// Wave priority by how far the wave is into its segment (s_setprio): 0
+// converting the raw rows (and issuing the next segment's loads), 1 in the
+// low-digit pass, 2 in the high-digit pass, 3 in unique + output + split.  Of
+// the 3 waves a SIMD holds, the one furthest along issues first, so the
+// waves spread over the phases and one wave's LDS-bound ranks overlap another's
+// VALU-bound conversion or unique loop instead of all three queueing on the
+// LDS together.  C3 canon 57.2 → 48.9 ms (DESIGN.md §4.1 with the other
+// placements measured; the window-mode kernel: its first pass, later passes,
+// unique).  SYZ_CANON_AGE_PRIO=0 builds leave every wave at 0.
+#ifndef SYZ_CANON_AGE_PRIO
+#define SYZ_CANON_AGE_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void age_prio() {
+    if constexpr (SYZ_CANON_AGE_PRIO != 0) __builtin_amdgcn_s_setprio(P);
+}
+
 template <int NK, int MINW, int HB>
 __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, const uint32_t *list,
                                                                     const uint32_t *count) {
@@ -365,6 +382,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     if (li < nl) issue(li);
     for (; li < nl; li += nw) {
         // wave-uniform descriptor in scalar registers (canon_key_kernel)
+        age_prio<0>();
         const uint32_t seg = uniform_u32(seg_n);
         const uint64_t base = uniform_u64(base_n);
         const uint32_t n = uniform_u32(n_n);
@@ -390,6 +408,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
         }
         if (li + nw < nl) issue(li + nw);
         if (__ballot(oob) && l == 0) atomicOr(P.err, SYZCOV_ERR_WINDOW);
+        age_prio<1>();
         // ------------------------------------------- pass 0 (unstable)
         hist_zero<HIST>(s_hist[w], l);
         wave_sync();
@@ -407,6 +426,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
         const bool two = npass > 1;
         scatter_rows<true, NK, HIST>(k, nq, l, head, end, buf, s_hist[w], 0, dmask, dbits, two);
         wave_sync();
+        age_prio<2>();
         // --------------------------------------------- stable passes
         for (uint32_t p = 1; p < npass; p++) {
             const uint32_t sh = p * dbits;
@@ -422,6 +442,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
             scatter_rows<false, NK, HIST>(k, nq, l, 0, n, buf, s_hist[w], sh, dmask, dbits, more);
             wave_sync();
         }
+        age_prio<3>();
         // --------------------------------- order check + unique + write
         // prev of slot e is slot e-1 (lane l-1 of the row, or lane 63 of the
         // previous row); the reference's `last := sent` for e == 0.
@@ -657,21 +678,6 @@ __device__ __forceinline__ void scatter_gap(const uint32_t (&k)[NK], uint32_t nq
     }
 }
 
-// Wave priority by how far the wave is into its segment (s_setprio): 0
-// converting the raw rows (and issuing the next segment's loads), 1 in the
-// low-digit pass, 2 in the high-digit pass, 3 in unique + output + split.  Of
-// the 3 waves a SIMD holds, the one furthest along issues first, so the
-// waves spread over the phases and one wave's LDS-bound ranks overlap another's
-// VALU-bound conversion or unique loop instead of all three queueing on the
-// LDS together.  C3 canon 57.2 → 48.9 ms (DESIGN.md §4.1 with the other
-// placements measured).  SYZ_CANON_AGE_PRIO=0 builds leave every wave at 0.
-#ifndef SYZ_CANON_AGE_PRIO
-#define SYZ_CANON_AGE_PRIO 1
-#endif
-template <int P>
-__device__ __forceinline__ void age_prio() {
-    if constexpr (SYZ_CANON_AGE_PRIO != 0) __builtin_amdgcn_s_setprio(P);
-}
 
 template <int NK, int MINW, bool ALIGNED = false, int BQK = ALIGNED ? SYZ_CANON_BQ_AL : SYZ_CANON_BQK,
           bool D12 = false>
