@@ -104,6 +104,10 @@ def parse():
     ap.add_argument("--canon-layout", type=int, default=0, choices=[0, 1],
                     help="canonical lists: 0 CSR slots, 1 line-aligned sub-runs "
                          "(syzcov_corpus_cfg.canon_layout)")
+    ap.add_argument("--no-rank-share", action="store_true",
+                    help="N=1: skip the c3_rank_of_8 sub-record (rank 0's share of C3 over 8 GPUs)")
+    ap.add_argument("--rank-share-only", action="store_true",
+                    help="run only the c3_rank_of_8 leg and print it (a probe)")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group, run no workload (a check of "
                          "the --gpus N launcher; runs on a host without a GPU)")
@@ -392,6 +396,129 @@ def corpus_run(args, world, rank, dev, glob, seed, steps, warmup, traffic_key, x
     return out
 
 
+def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPUTS,
+                   seed: int = SEED_C3, steps: int = 10, warmup: int = 2) -> dict:
+    """Rank `rank`'s exact share of the `world`-GPU step over C3, on this one
+    GPU: its n = glob / world inputs canonicalized (out of place), its part of
+    Go's order over ALL glob canonical lengths (syzcov_corpus_order_part: the
+    replicated early rounds plus the late rounds of the segments starting in
+    its block), Minimize pass 1 over its own items at GLOBAL ranks, pass 2 and
+    finish — every kernel the rank runs in `dist.ShardedEngine.step`.  The
+    collectives cannot run on one GPU; each is replaced by what it leaves in the
+    buffer: the other ranks' canonical lengths are computed before the timed
+    steps (the all-gather's result) and the merged order is copied in (the MAX
+    all-reduce's result, a 40 MB device copy inside the timed order phase);
+    the MIN merge of first ranks and the MAX merge of kept flags are skipped
+    (pass 2 reads this rank's own first ranks: the same kernels and bytes).
+    Their bytes are reported apart (`collectives`)."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    from syzkaller_amd.dist import ShardedEngine
+    from syzkaller_amd.engine import synth_corpus, synth_universe, synth_window
+    L = _lib.lib()
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n = glob // world
+    N = n * world
+    lo, span = synth_window(args.log2_space)
+    totals, max_len = [], 0
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    for r in range(world):  # every rank's raw size (synth_lens is the generator's own)
+        _lib.check(L.syzcov_dev_synth_lens(seed, r * n, n, args.mean, args.sigma,
+                                           C.c_void_p(lens.data_ptr()), s), "synth_lens")
+        totals.append(int(lens.to(torch.int64).sum().item()))
+        max_len = max(max_len, int(lens.max().item()))
+    del lens
+    univ = None if args.no_universe else synth_universe(args.log2_space, seed, device=dev)
+    eng = ShardedEngine(n, max(totals), max_len, lo, span, rank, world, device=dev, universe=univ,
+                        canon_layout=args.canon_layout)
+    del univ
+    # the all-gather's result: every other rank's canonical lengths (its canon
+    # on this GPU, outside the timed steps)
+    glens = eng.glens[:N]
+    for r in range(world):
+        if r == rank:
+            continue
+        off_r, raw_r, _, _ = synth_corpus(n, seed, first=r * n, mean=args.mean, sigma=args.sigma,
+                                          log2_space=args.log2_space, device=dev)
+        eng.canonicalize(off_r, raw_r, n)
+        glens[r * n:(r + 1) * n].copy_(eng.new_len[:n])
+        del off_r, raw_r
+        torch.cuda.empty_cache()
+    off, raw, _, total = synth_corpus(n, seed, first=rank * n, mean=args.mean, sigma=args.sigma,
+                                      log2_space=args.log2_space, device=dev)
+    eng.canonicalize(off, raw, n)
+    glens[rank * n:(rank + 1) * n].copy_(eng.new_len[:n])
+    # the MAX all-reduce's result: Go's order over all N lengths
+    _lib.check(L.syzcov_corpus_order(eng.h, C.c_void_p(glens.data_ptr()), N, s), "corpus_order")
+    full_order = eng.order[:N].clone()
+    torch.cuda.synchronize()
+    phases = ("canon", "order", "minimize", "exchange", "finish")
+
+    def step(ev):
+        k = [0]
+
+        def mark():
+            if ev is not None:
+                ev[k[0]].record()
+            k[0] += 1
+        mark()
+        eng.canonicalize(off, raw, n)
+        mark()
+        glens[rank * n:(rank + 1) * n].copy_(eng.new_len[:n])  # this rank's part of the gather
+        _lib.check(L.syzcov_corpus_order_part(eng.h, C.c_void_p(glens.data_ptr()), N, s),
+                   "corpus_order_part")
+        eng.order[:N].copy_(full_order)                         # stands in for the MAX merge
+        mark()
+        eng.minimize(do_pass2=False)
+        mark()
+        _lib.check(L.syzcov_corpus_pass2(eng.h, s), "corpus_pass2")
+        mark()
+        eng.finish()
+        mark()
+    a = argparse.Namespace(steps=steps, warmup=warmup)
+    dt, phl = timed(step, len(phases), a, 1, dev)
+    ph = dict(zip(phases, phl))
+    res = eng.result()
+    canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
+    alg = eng.alg_bytes(total, canon_pcs)
+    cf = alg["canon"] / (ph["canon"] * 1e-3) / 1e9
+    mf = alg["minimize"] / (ph["minimize"] * 1e-3) / 1e9
+    # what the rank's collectives move (ring algorithms: an all-gather receives
+    # (w-1)/w of the result, an all-reduce sends and receives 2(w-1)/w of it)
+    f_ag, f_ar = (world - 1) / world, 2 * (world - 1) / world
+    coll = {"lens_allgather_int32": N * 4, "order_max_allreduce_int32": N * 4,
+            "first_min_allreduce_int32": eng.span * 4, "kept_max_allreduce_u8": N + 4}
+    ring = (f_ag * coll["lens_allgather_int32"] + f_ar * (coll["order_max_allreduce_int32"]
+            + coll["first_min_allreduce_int32"] + coll["kept_max_allreduce_u8"]))
+    out = {
+        "workload": (f"rank {rank} of {world} over C3 ({glob} inputs, seed {seed:#x}): its {n} "
+                     f"inputs, Go's order over all {N} lengths, pass 1 at global ranks"),
+        "ms_per_step": dt / steps * 1e3,
+        "rank_input_pcs_per_s": total * steps / dt,
+        "raw_pcs": total, "canonical_pcs": canon_pcs,
+        "phases_ms": {k: round(v, 4) for k, v in ph.items()},
+        "canon_roofline": {"achieved": cf, "frac": cf / HBM_PEAK_GBS,
+                           "alg_bytes_per_launch": alg["canon"],
+                           "traffic": traffic_of("C3R8", "canon")[0]},
+        "minimize_roofline": {"achieved": mf, "frac": mf / HBM_PEAK_GBS,
+                              "alg_bytes_per_launch": alg["minimize"],
+                              "traffic": traffic_of("C3R8", "minimize")[0]},
+        # Minimize + union as the metric counts it: order + minimize + the
+        # exchange phase's pass 2 + finish
+        "minimize_union_ms": ph["order"] + ph["minimize"] + ph["exchange"] + ph["finish"],
+        "collectives": {"bytes": coll, "ring_bytes_per_rank": int(ring),
+                        "note": "not run on one GPU; the 8-GPU step adds their time"},
+        "results": {"kept_local_first": res.n_kept, "union_local": res.n_union},
+        "stand_ins": "other ranks' lengths precomputed; merged order copied in; own first ranks "
+                     "for the MIN merge; kept MAX skipped",
+    }
+    eng.close()
+    del eng, off, raw, full_order
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_corpus(args):
     """The headline: config C3 (10M inputs, seed 0x5EED0003) at EVERY N — the
     whole corpus on one GPU at N=1, sharded by input over the ranks at N>1
@@ -399,6 +526,9 @@ def bench_corpus(args):
     one-GPU config of BASELINE.json) as the `c2` sub-record, the drop-in legs
     and the CPU baseline."""
     world, rank, dev = init_dist()
+    if args.rank_share_only:
+        return rank, world, {"c3_rank_of_8": rank_share_run(args, dev, steps=args.steps,
+                                                            warmup=args.warmup)}
     glob = args.global_inputs or C3_INPUTS
     cname, seed, workload = corpus_workload(glob)
     if args.x86:
@@ -447,6 +577,10 @@ def bench_corpus(args):
                               "apart, kshift 2)")
             cx["seed"] = SEED
             out["c2x"] = cx
+        if not args.no_rank_share and glob == C3_INPUTS and not args.x86:
+            # the 8-GPU step's per-rank work, measured on this GPU
+            out["c3_rank_of_8"] = rank_share_run(args, dev, steps=max(args.steps, 10),
+                                                 warmup=args.warmup)
         if not args.no_dropin:
             out["dropin"] = dropin_legs(args, dev)
             out["dropin"]["pairwise"] = pairwise_leg()
@@ -485,6 +619,7 @@ def dropin_legs(args, dev):
         h_off = off.cpu().numpy().astype(np.uint64)
         h_pcs = raw[:total].cpu().numpy().view(np.uint32)
         max_len = int(lens.max().item())
+        canon_pcs = canonical_total(off, raw, n, max_len, args.log2_space, dev)  # (in place)
         del off, raw, lens
         torch.cuda.empty_cache()
         out = np.empty(n, np.int32)
@@ -547,14 +682,55 @@ def dropin_legs(args, dev):
                             "minimize_corpus")
             tgs.append(time.perf_counter() - t0)
         tg = tgs[1]
+        gs = _lib.GroupsStats()
+        _lib.check(L.syzcov_minimize_corpus_stats(C.byref(gs)), "minimize_corpus_stats")
+        # device part: one canonicalization (4 B read per raw PC, 4 B written per
+        # canonical PC) and one grouped Minimize pass (4 B per canonical PC); the
+        # path's extra union step is not counted
+        g_alg = 4 * total + 8 * canon_pcs
         leg.update({"groups": 293, "minimize_corpus_ms": round(tg * 1e3, 2),
                     "minimize_corpus_first_call_ms": round(tgs[0] * 1e3, 2),
                     "minimize_corpus_kept": kg, "minimize_corpus_input_pcs_per_s": total / tg,
-                    "minimize_corpus_vs_handle": tg / min(tk[1:])})
+                    "minimize_corpus_vs_handle": tg / min(tk[1:]),
+                    "minimize_corpus_path": _lib.GROUPS_PATHS.get(gs.path, gs.path),
+                    "minimize_corpus_upload_ms": round(gs.upload_ms, 3),
+                    "minimize_corpus_device_ms": round(gs.device_ms, 3),
+                    "minimize_corpus_download_ms": round(gs.download_ms, 3),
+                    "minimize_corpus_device_roofline": (
+                        {"achieved": g_alg / (gs.device_ms * 1e-3) / 1e9,
+                         "frac": g_alg / (gs.device_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "unit": "GB/s", "alg_bytes": g_alg, "canonical_pcs": canon_pcs,
+                         "note": "device_ms includes the path's union step and its host "
+                                 "read-backs; alg bytes count one canon + one Minimize pass"}
+                        if gs.device_ms > 0 else None)})
         L.syzcov_pool_trim()
         legs[name] = leg
         del h_pcs, h_off
     return legs
+
+
+def canonical_total(off, raw, n: int, max_len: int, log2_space: int, dev) -> int:
+    """Canonical PCs of a synthetic corpus (its raw lists canonicalized IN PLACE
+    on the device, syzcov_dev_canon_split): the algorithmic-bytes count of a
+    leg that only sees host buffers."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import synth_window
+    L = _lib.lib()
+    lo, span = synth_window(log2_space)
+    nl = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    err = torch.zeros(4, dtype=torch.int32, device=dev)
+    wsz = L.syzcov_dev_canon_split_ws_size(n)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(L.syzcov_dev_canon_split(P(off), P(raw), P(raw), P(nl), n, max_len, lo, span, 20,
+                                        None, None, P(err), P(ws), wsz,
+                                        C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+               "canon_split")
+    if int(err[0].item()):
+        raise RuntimeError(f"canonicalize flags {int(err[0].item()):#x}")
+    return int(nl[:n].to(torch.int64).sum().item())
 
 
 def pairwise_leg(reps: int = 2000, nthreads: int = 32) -> dict:

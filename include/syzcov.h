@@ -125,6 +125,23 @@ int64_t syzcov_minimize(const uint64_t *offsets, const uint32_t *pcs, size_t n,
 int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
                                size_t n, int sort_variant, int32_t *out_idx);
 
+/* What the calling thread's last syzcov_minimize_corpus did: the path it took
+ * and, on the two corpus-size paths, where its time went (HIP events on its
+ * stream): host -> device staging, the device work between the last upload
+ * and the kept list's download (two canonicalizations, the Go orders and the
+ * grouped Minimize, host syncs included), and the download. */
+#define SYZCOV_GROUPS_PATH_NONE 0   /* no call yet, or it failed */
+#define SYZCOV_GROUPS_PATH_LDS 1    /* every group <= 2^16 inputs: one LDS pass (group_min) */
+#define SYZCOV_GROUPS_PATH_ENGINE 2 /* the per-group engine on the cached handle */
+#define SYZCOV_GROUPS_PATH_SLABS 3  /* < 65,536 inputs (or no engine): per-group slabs */
+typedef struct syzcov_groups_stats {
+    int32_t path;        /* SYZCOV_GROUPS_PATH_* */
+    float upload_ms;     /* corpus paths: offsets, PCs, grouping, lengths to the device */
+    float device_ms;     /* corpus paths: the device part of the call */
+    float download_ms;   /* corpus paths: the kept indices back */
+} syzcov_groups_stats;
+int syzcov_minimize_corpus_stats(syzcov_groups_stats *out);
+
 /* Go sort.Sort(minInputArray) restatement: order[r] for inputs of the given
  * lengths (len(cov) including duplicates).  Computed on the GPU. */
 int syzcov_sort_order(const int64_t *lens, size_t n, int sort_variant, int32_t *order);

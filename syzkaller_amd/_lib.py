@@ -51,6 +51,7 @@ _SIGS = {
     "syzcov_minimize": (i64, [p_, p_, sz, p_, C.c_int, p_]),
     "syzcov_sort_order": (C.c_int, [p_, sz, C.c_int, p_]),
     "syzcov_minimize_corpus": (i64, [p_, p_, p_, sz, C.c_int, p_]),
+    "syzcov_minimize_corpus_stats": (C.c_int, [p_]),
     "syzcov_union_all": (i64, [p_, p_, sz, p_]),
     "syzcov_unique_cover": (i64, [p_, p_, p_, sz, p_]),
     "syzcov_ui_stats": (i64, [p_, p_, p_, sz, u32, p_, p_, p_, p_]),
@@ -211,6 +212,15 @@ def header_symbols() -> list[str]:
 
 
 # ---------------------------------------------------------------- corpus ABI
+class GroupsStats(C.Structure):
+    """syzcov_groups_stats (syzcov.h): the calling thread's last minimizeCorpus."""
+    _fields_ = [("path", C.c_int32), ("upload_ms", C.c_float), ("device_ms", C.c_float),
+                ("download_ms", C.c_float)]
+
+
+GROUPS_PATHS = {0: "none", 1: "lds", 2: "engine", 3: "slabs"}
+
+
 class CorpusCfg(C.Structure):
     """syzcov_corpus_cfg (include/syzcov.h)."""
     _fields_ = [("n_max", sz), ("n_global", sz), ("rank", sz), ("p_max", u64),

@@ -377,6 +377,9 @@ int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,
 // engine (per-group Minimize over one rank space, corpus.hip); below it the
 // per-group launches cost more than the dictionary path's batched slabs
 constexpr size_t kGroupEngineMinInputs = 65536;
+void groups_stats_slabs();
+void groups_stats_reset();
+int groups_stats(syzcov_groups_stats *out);
 int minimize_corpus_via_engine(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
                                size_t n, int32_t *out_idx, int64_t *out_n);
 int minmax_pcs(const uint32_t *pcs, size_t n, uint32_t *out2, hipStream_t s);
@@ -633,6 +636,7 @@ static int64_t minimize_corpus_impl(Ctx *c, const int32_t *call, const uint64_t 
 
 int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, const uint32_t *pcs,
                                size_t n, int sort_variant, int32_t *out_idx) {
+    groups_stats_reset();
     if (n == 0) return 0;
     if (!call || !offsets || !out_idx || n > 0x7FFFFFFF || sort_variant != 0)
         return SYZCOV_EINVAL;
@@ -649,8 +653,11 @@ int64_t syzcov_minimize_corpus(const int32_t *call, const uint64_t *offsets, con
     const int64_t rc = minimize_corpus_impl(c, call, offsets, pcs, n, sort_variant, out_idx);
     hipStreamSynchronize(c->s);
     release_large(c);
+    if (rc >= 0) groups_stats_slabs();
     return rc;
 }
+
+int syzcov_minimize_corpus_stats(syzcov_groups_stats *out) { return groups_stats(out); }
 
 // Manager.uniqueCover (syz-manager/html.go:213-238).
 static int64_t unique_cover_impl(Ctx *c, const int32_t *call, const uint64_t *offsets,

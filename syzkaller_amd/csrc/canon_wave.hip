@@ -89,7 +89,7 @@ __device__ __forceinline__ void hist_scan(uint32_t *hist, uint32_t l) {
 #pragma unroll
     for (int q = 0; q < PL; q += 2) {
         const uint32_t inc = wave_incl_scan(s[q] | (s[q + 1] << 16));
-        const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+        const uint32_t tot = wave_readlane(inc, 63);
         uint32_t pq[2];
         pq[0] = base + (inc & 0xFFFFu) - s[q];
         base += tot & 0xFFFFu;
@@ -218,7 +218,7 @@ __device__ __forceinline__ uint32_t aligned_delta(uint64_t start_mask, uint32_t 
         while (rem) {
             const uint32_t b = (uint32_t)__builtin_ctzll(rem);
             rem &= rem - 1;
-            const uint32_t db = __builtin_amdgcn_readlane(dl, b);
+            const uint32_t db = wave_readlane(dl, b);
             if (l >= b) delta = db;
             dcar = db;
         }
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_wave_kernel(Params P, co
     constexpr int NQ = NK / 4;  // 16-byte loads per lane = row quads
     __shared__ uint32_t s_buf[WPB][CAP + 64];  // + one pad dummy per lane
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[WPB][HIST + 64];
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
     const uint32_t nbits = P.nbits < 1 ? 1 : P.nbits;
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
     constexpr int NQ = NK / 4;
     __shared__ uint32_t s_buf[WPB][CAP + NK];  // + the lane's pads (<= NK) past CAP
     __shared__ __attribute__((aligned(16))) uint32_t s_h[WPB][HW + 64];
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = __lane_id();
     uint32_t *buf = s_buf[w];
     uint32_t *h = s_h[w];

@@ -6,6 +6,7 @@
 #include <stddef.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "../../include/syzcov.h"
 #include "force.h"
@@ -75,11 +76,32 @@ __device__ __forceinline__ T issue_fence(T x) {
     return x;
 }
 
-// A wave-uniform value into scalar registers (the builtin returns int: both
-// halves go through uint32_t, or a low half with bit 31 set sign-extends)
-__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+// The ONLY door to the readlane builtins (tests/test_source_guards.py fails
+// on any other use).  They move 32
+// bits and return int: a 64-bit value or a pointer passed straight in loses
+// its high half, and an int result widened to 64 bits sign-extends a low half
+// >= 2^31 (two GPU faults).  These keep the caller's 32-bit
+// type, reject anything else at compile time, and 64-bit values go through
+// uniform_u64 / wave_readlane_u64 (both halves as uint32_t).
+template <class T>
+__device__ __forceinline__ T wave_readfirstlane(T v) {
+    static_assert(sizeof(T) == 4 && std::is_integral<T>::value,
+                  "readfirstlane moves 32 bits: use uniform_u64 for 64-bit values / pointers");
+    return (T)__builtin_amdgcn_readfirstlane((int)v);  // readlane-door
 }
+template <class T>
+__device__ __forceinline__ T wave_readlane(T v, int lane) {
+    static_assert(sizeof(T) == 4 && std::is_integral<T>::value,
+                  "readlane moves 32 bits: use wave_readlane_u64 for 64-bit values / pointers");
+    return (T)__builtin_amdgcn_readlane((int)v, lane);  // readlane-door
+}
+__device__ __forceinline__ uint64_t wave_readlane_u64(uint64_t v, int lane) {
+    return ((uint64_t)wave_readlane((uint32_t)(v >> 32), lane) << 32) |
+           wave_readlane((uint32_t)v, lane);
+}
+
+// A wave-uniform value into scalar registers
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return wave_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
     return ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32) | uniform_u32((uint32_t)v);
 }
@@ -127,7 +149,7 @@ __device__ __forceinline__ void hist16_scan(uint32_t *h, uint32_t l) {
 #pragma unroll
     for (int q = 0; q < WQ; q += 2) {
         const uint32_t inc = wave_incl_scan(s[q] | (s[q + 1] << 16));
-        const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+        const uint32_t tot = wave_readlane(inc, 63);
         uint32_t pq[2];
         pq[0] = base + (inc & 0xFFFFu) - s[q];
         base += tot & 0xFFFFu;

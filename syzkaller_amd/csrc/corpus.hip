@@ -79,6 +79,10 @@ __global__ void corpus_clear_bit_kernel(uint32_t *covered, uint32_t bit) {
 // (every rank fails a step any shard flagged, with the same flags: its aliased
 // first covers went into the MIN merge)
 constexpr uint32_t kErrBytes = 4;  // SYZCOV_ERR_WINDOW .. SYZCOV_ERR_ORDER
+// a flag bit added past SYZCOV_ERR_ORDER needs a kept byte of its own (and
+// KEPT / the exchange grow with it: syzcov.h "N + 4")
+static_assert((SYZCOV_ERR_ORDER << 1) == (1u << kErrBytes),
+              "one spare kept byte per SYZCOV_ERR_* bit");
 __global__ void corpus_err_to_kept_kernel(const uint32_t *err, uint8_t *kept_n) {
     for (uint32_t b = 0; b < kErrBytes; b++) kept_n[b] = (uint8_t)((*err >> b) & 1u);
 }
@@ -1250,6 +1254,33 @@ struct DropinCache {
     uint64_t span = 0;
     void *stage = nullptr;  // off u64[n+1] | pcs u32[P+1] | order i32[n] | min/max
     size_t stage_cap = 0;
+    void *gscratch = nullptr;  // groups_lds: lengths, split points, kept, workspace
+    size_t gscratch_cap = 0;
+};
+// the calling thread's last syzcov_minimize_corpus (syzcov_minimize_corpus_stats)
+thread_local syzcov_groups_stats g_gstats{};
+// HIP events around a corpus-size minimizeCorpus call: upload | device | download
+struct GroupTimer {
+    hipEvent_t e[4] = {};
+    bool ok = true;
+    GroupTimer() {
+        for (auto &x : e) ok = ok && hipEventCreate(&x) == hipSuccess;
+    }
+    ~GroupTimer() {
+        for (auto &x : e)
+            if (x) hipEventDestroy(x);
+    }
+    void mark(int i, hipStream_t s) {
+        if (ok) ok = hipEventRecord(e[i], s) == hipSuccess;
+    }
+    void finish(int path) {
+        g_gstats = {};
+        g_gstats.path = path;
+        if (!ok || hipEventSynchronize(e[3]) != hipSuccess) return;
+        hipEventElapsedTime(&g_gstats.upload_ms, e[0], e[1]);
+        hipEventElapsedTime(&g_gstats.device_ms, e[1], e[2]);
+        hipEventElapsedTime(&g_gstats.download_ms, e[2], e[3]);
+    }
 };
 constexpr int kMaxDev = 16;
 static DropinCache g_dropin[kMaxDev];
@@ -1257,9 +1288,10 @@ static DropinCache g_dropin[kMaxDev];
 static void dropin_release(DropinCache &dc) {
     if (dc.h) syzcov_corpus_destroy(dc.h);
     if (dc.stage) hipFree(dc.stage);
+    if (dc.gscratch) hipFree(dc.gscratch);
     dc.h = 0;
-    dc.stage = nullptr;
-    dc.stage_cap = dc.n_cap = dc.seg_cap = dc.p_cap = dc.span = 0;
+    dc.stage = dc.gscratch = nullptr;
+    dc.stage_cap = dc.gscratch_cap = dc.n_cap = dc.seg_cap = dc.p_cap = dc.span = 0;
 }
 
 void dropin_trim() {
@@ -1275,10 +1307,11 @@ void dropin_trim() {
 }
 
 // the handle for a corpus of n inputs / P PCs / longest max_len over [lo, hi]
+// (out_of_place: the caller needs the staged raw PCs after the step)
 static int dropin_handle(DropinCache &dc, size_t n, uint64_t P, size_t max_len, uint32_t lo,
-                         uint32_t hi) {
+                         uint32_t hi, bool out_of_place = false) {
     if (dc.h && n <= dc.n_cap && P <= dc.p_cap && max_len <= dc.seg_cap && lo >= dc.lo &&
-        (uint64_t)hi - dc.lo < dc.span)
+        (uint64_t)hi - dc.lo < dc.span && (!out_of_place || !get(dc.h)->cfg.canon_in_place))
         return 1;
     // grow: capacities only rise, the window widens to cover both corpora
     // (whole 2^20-PC ranges) while it stays within the engine's 256 ranges
@@ -1303,7 +1336,9 @@ static int dropin_handle(DropinCache &dc, size_t n, uint64_t P, size_t max_len, 
     cfg.pc_lo = (uint32_t)nlo;
     cfg.pc_span = nhi - nlo + 1;
     cfg.order_by = 1;  // Go sorts by len(cov), duplicates included
-    cfg.canon_in_place = cfg.max_seg_len <= 16384;  // the staged copy is the cache's own
+    // the staged copy is the cache's own; out of place once a caller asked
+    cfg.canon_in_place = cfg.max_seg_len <= 16384 && !out_of_place &&
+                         !(dc.h && !get(dc.h)->cfg.canon_in_place);
     if (dc.h) syzcov_corpus_destroy(dc.h);
     dc.h = 0;
     int rc = syzcov_corpus_create(&cfg, nullptr, 0, &dc.h);
@@ -1382,9 +1417,10 @@ static int64_t dropin_run(DropinCache &dc, const uint64_t *offsets, const uint32
 int minimize_groups_order(const int32_t *ord_g, const int32_t *perm, const uint64_t *goff_dev,
                           uint32_t ngroups, uint32_t n, int32_t *order_c, uint32_t *rank_grp,
                           hipStream_t s);
-static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, const uint64_t *d_off,
-                          uint32_t *d_pcs, const int32_t *d_ordc, const uint64_t *d_goff,
-                          uint32_t lo, uint32_t hi, int32_t *out_idx, hipStream_t s);
+static int64_t groups_lds(DropinCache &dc, size_t n, uint64_t P, size_t max_len, uint32_t G,
+                          const uint64_t *d_off, uint32_t *d_pcs, const int32_t *d_ordc,
+                          const uint64_t *d_goff, uint32_t lo, uint32_t hi, int32_t *out_idx,
+                          GroupTimer &tm, hipStream_t s);
 
 // Manager.minimizeCorpus (manager.go:504-524) on the cached engine: the
 // corpus is staged as it is; the groups (inputs of one RpcInput.Call, corpus
@@ -1403,7 +1439,8 @@ constexpr uint32_t kGroupLdsMaxItems = 1u << 16;  // minimize_range.hip GM_MAX_I
 constexpr uint32_t kGroupLdsShift = 15;           // keys per LDS piece: 2^15 ranks
 
 static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uint64_t *offsets,
-                                 const uint32_t *pcs, size_t n, int32_t *out_idx, hipStream_t s) {
+                                 const uint32_t *pcs, size_t n, int32_t *out_idx,
+                                 GroupTimer &tm, hipStream_t s) {
     const uint64_t base = offsets[0], P = offsets[n] - base;
     std::vector<uint64_t> hoff(n + 1);
     size_t max_len = 1;
@@ -1460,11 +1497,13 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
     uint32_t *d_pcs = (uint32_t *)(st + o_pcs), *d_mm = (uint32_t *)(st + o_mm);
     int32_t *d_perm = (int32_t *)(st + o_perm), *d_ordg = (int32_t *)(st + o_ordg),
             *d_ordc = (int32_t *)(st + o_ordc);
+    tm.mark(0, s);
     SYZ_HIP(hipMemcpyAsync(d_off, hoff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(d_perm, perm.data(), n * 4, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(d_goff, goff.data(), (G + 1) * 8, hipMemcpyHostToDevice, s));
     SYZ_HIP(hipMemcpyAsync(st + o_lens, lens.data(), n * 8, hipMemcpyHostToDevice, s));
+    tm.mark(1, s);
     int rc = minmax_pcs(d_pcs, P, d_mm, s);
     if (rc) return rc;
     uint32_t mm[2];
@@ -1480,9 +1519,12 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
     uint64_t gmax = 0;
     for (uint32_t g = 0; g < G; g++) gmax = std::max<uint64_t>(gmax, goff[g + 1] - goff[g]);
     if (gmax <= kGroupLdsMaxItems && !(force_flags() & FORCE_GROUP_CHUNKS)) {
-        const int64_t k = groups_lds(n, P, max_len, G, d_off, d_pcs, d_ordc, d_goff, mm[0], mm[1],
-                                     out_idx, s);
-        if (k != 0) return k;  // taken (or failed); 0: the per-group engine below
+        const int64_t k = groups_lds(dc, n, P, max_len, G, d_off, d_pcs, d_ordc, d_goff, mm[0],
+                                     mm[1], out_idx, tm, s);
+        if (k != 0) {  // taken (or failed); 0: the per-group engine below
+            if (k > 0) tm.finish(SYZCOV_GROUPS_PATH_LDS);
+            return k;
+        }
         SYZ_HIP(hipMemcpyAsync(d_pcs, pcs + base, P * 4, hipMemcpyHostToDevice, s));
     }
     rc = dropin_handle(dc, n, P, max_len, mm[0], mm[1]);
@@ -1495,12 +1537,15 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
     if (!rc) rc = ph_finish(c, s);
     syzcov_corpus_res r{};
     if (!rc) rc = ph_result(c, &r, s);
+    tm.mark(2, s);
     if (!rc && r.n_kept)
         rc = hipMemcpyAsync(out_idx, r.kept_idx, (size_t)r.n_kept * 4, hipMemcpyDeviceToHost, s) ==
                      hipSuccess
                  ? 0
                  : SYZCOV_EHIP;
+    tm.mark(3, s);
     if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = SYZCOV_EHIP;
+    if (!rc) tm.finish(SYZCOV_GROUPS_PATH_ENGINE);
     return rc ? rc : (int64_t)r.n_kept + 1;
 }
 
@@ -1515,22 +1560,24 @@ static int64_t dropin_run_groups(DropinCache &dc, const int32_t *call, const uin
 // are canonicalized into key words over ranges of 2^15 keys and every (group,
 // range) piece takes its first covers in LDS (group_min_kernel): no chunks,
 // no records, no per-group launches.  Returns kept + 1 (0: not taken).
-static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, const uint64_t *d_off,
-                          uint32_t *d_pcs, const int32_t *d_ordc, const uint64_t *d_goff,
-                          uint32_t lo, uint32_t hi, int32_t *out_idx, hipStream_t s) {
-    syzcov_corpus_cfg cfg{};
-    cfg.n_max = n;
-    cfg.p_max = P;
-    cfg.max_seg_len = max_len;
-    cfg.pc_lo = lo;
-    cfg.pc_span = (uint64_t)hi - lo + 1;
-    cfg.order_by = 1;
-    syzcov_corpus h = 0;
-    int rc = syzcov_corpus_create(&cfg, nullptr, 0, &h);
-    if (rc) return rc == SYZCOV_ENOMEM || rc == SYZCOV_ERANGE ? 0 : rc;
-    Corpus &c = *get(h);
+static int64_t groups_lds(DropinCache &dc, size_t n, uint64_t P, size_t max_len, uint32_t G,
+                          const uint64_t *d_off, uint32_t *d_pcs, const int32_t *d_ordc,
+                          const uint64_t *d_goff, uint32_t lo, uint32_t hi, int32_t *out_idx,
+                          GroupTimer &tm, hipStream_t s) {
+    // the union step runs on the drop-in cache's window-mode engine (no second
+    // corpus-sized engine per call), out of place: (2) below canonicalizes the
+    // staged raw PCs again, into key words
+    int rc = dropin_handle(dc, n, P, max_len, lo, hi, true);
+    if (rc <= 0) return rc;
+    Corpus &c = *get(dc.h);
+    Use u(&c);
     int64_t ret = 0;
-    void *scratch = nullptr;
+    // a HIP error inside the block ends it with rc set (the cleanup below runs)
+#define GL_HIP(x)                   \
+    if ((x) != hipSuccess) {        \
+        rc = SYZCOV_EHIP;           \
+        break;                      \
+    }
     do {
         // (1) the corpus union: one window-mode Minimize (its own order)
         rc = ph_canon(c, d_off, d_pcs, n, s);
@@ -1547,15 +1594,15 @@ static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, cons
         if (r.union_pcs != univ) break;  // (no side buffer in window mode: not taken)
         if (hi == 0xFFFFFFFFu) {
             const uint32_t sent = 0xFFFFFFFFu;
-            SYZ_HIP(hipMemcpyAsync(univ + r.n_union, &sent, 4, hipMemcpyHostToDevice, s));
+            GL_HIP(hipMemcpyAsync(univ + r.n_union, &sent, 4, hipMemcpyHostToDevice, s));
         }
         uint32_t *d_ks = (uint32_t *)(scal(c) + SC_MM);
         if ((rc = universe_shift_dev(univ, nu, d_ks, s))) break;
         uint32_t ks = 0, ends[2];
-        SYZ_HIP(hipMemcpyAsync(&ks, d_ks, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipMemcpyAsync(&ends[0], univ, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipMemcpyAsync(&ends[1], univ + nu - 1, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        GL_HIP(hipMemcpyAsync(&ks, d_ks, 4, hipMemcpyDeviceToHost, s));
+        GL_HIP(hipMemcpyAsync(&ends[0], univ, 4, hipMemcpyDeviceToHost, s));
+        GL_HIP(hipMemcpyAsync(&ends[1], univ + nu - 1, 4, hipMemcpyDeviceToHost, s));
+        GL_HIP(hipStreamSynchronize(s));
         ks = std::min<uint32_t>(ks, SYZCOV_KSHIFT_MAX);
         const uint32_t kbase = ends[0] >> ks;
         const uint64_t nkeys = (uint64_t)(ends[1] >> ks) - kbase + 1;
@@ -1571,18 +1618,24 @@ static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, cons
                                        minimize_groups_lds_ws_size(n, nkeys, kGroupLdsShift),
                                        syzcov_dev_compact_ws_size(n)}),
                      need = o_ws + align_up(ws_sz, 256);
-        if (hipMalloc(&scratch, need) != hipSuccess) {
-            scratch = nullptr;
-            break;  // short of memory: not taken
+        if (need > dc.gscratch_cap) {  // grow-only, kept in the drop-in cache
+            if (dc.gscratch) hipFree(dc.gscratch);
+            dc.gscratch = nullptr;
+            dc.gscratch_cap = 0;
+            if (hipMalloc(&dc.gscratch, need) != hipSuccess) {
+                dc.gscratch = nullptr;
+                break;  // short of memory: not taken
+            }
+            dc.gscratch_cap = need;
         }
-        uint8_t *sc8 = (uint8_t *)scratch;
+        uint8_t *sc8 = (uint8_t *)dc.gscratch;
         uint32_t *nl = (uint32_t *)(sc8 + o_nl), *split = (uint32_t *)(sc8 + o_split);
         uint32_t *err = (uint32_t *)(sc8 + o_err);
         uint8_t *kept = sc8 + o_kept;
         int32_t *d_out = (int32_t *)(sc8 + o_out);
         uint32_t *d_cnt = (uint32_t *)(sc8 + o_cnt);
-        SYZ_HIP(hipMemsetAsync(sc8 + o_rt, 0, R * 8 + 256, s));  // range totals, err
-        uint32_t *words = c.buf<uint32_t>(SYZCOV_CORPUS_CANON);
+        GL_HIP(hipMemsetAsync(sc8 + o_rt, 0, R * 8 + 256, s));  // range totals, err
+        uint32_t *words = c.buf<uint32_t>(SYZCOV_CORPUS_CANON);  // key words, out of place
         rc = syzcov_dev_canon_split_keys(d_off, d_pcs, words, nl, n, max_len, ends[0],
                                          (uint64_t)ends[1] - ends[0] + 1, ks, kbase, nkeys,
                                          kGroupLdsShift, split, (uint64_t *)(sc8 + o_rt), err,
@@ -1594,21 +1647,22 @@ static int64_t groups_lds(size_t n, uint64_t P, size_t max_len, uint32_t G, cons
         if (!rc) rc = syzcov_dev_compact_kept(kept, d_ordc, n, d_out, d_cnt, sc8 + o_ws, s);
         if (rc) break;
         uint32_t hk[2];
-        SYZ_HIP(hipMemcpyAsync(&hk[0], d_cnt, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipMemcpyAsync(&hk[1], err, 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        GL_HIP(hipMemcpyAsync(&hk[0], d_cnt, 4, hipMemcpyDeviceToHost, s));
+        GL_HIP(hipMemcpyAsync(&hk[1], err, 4, hipMemcpyDeviceToHost, s));
+        GL_HIP(hipStreamSynchronize(s));
         if (hk[1]) {  // every corpus PC is in its own union: cannot happen
             set_error("grouped minimize: canonicalize flags %#x", hk[1]);
             rc = SYZCOV_EHIP;
             break;
         }
-        if (hk[0]) SYZ_HIP(hipMemcpyAsync(out_idx, d_out, (size_t)hk[0] * 4, hipMemcpyDeviceToHost, s));
-        SYZ_HIP(hipStreamSynchronize(s));
+        tm.mark(2, s);
+        if (hk[0]) GL_HIP(hipMemcpyAsync(out_idx, d_out, (size_t)hk[0] * 4, hipMemcpyDeviceToHost, s));
+        tm.mark(3, s);
+        GL_HIP(hipStreamSynchronize(s));
         ret = (int64_t)hk[0] + 1;
     } while (0);
+#undef GL_HIP
     hipStreamSynchronize(s);
-    if (scratch) hipFree(scratch);
-    syzcov_corpus_destroy(h);
     return rc ? rc : ret;
 }
 
@@ -1622,11 +1676,27 @@ int minimize_corpus_via_engine(const int32_t *call, const uint64_t *offsets, con
     if (!lk.owns_lock()) return 0;
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return SYZCOV_EHIP;
-    const int64_t k = dropin_run_groups(dc, call, offsets, pcs, n, out_idx, s);
+    int64_t k;
+    {
+        GroupTimer tm;
+        k = dropin_run_groups(dc, call, offsets, pcs, n, out_idx, tm, s);
+    }
     hipStreamDestroy(s);
     if (k <= 0) return (int)k;
     *out_n = k - 1;
     return 1;
+}
+
+// the slab path's record (api.cc), and the query
+void groups_stats_slabs() {
+    g_gstats = {};
+    g_gstats.path = SYZCOV_GROUPS_PATH_SLABS;
+}
+void groups_stats_reset() { g_gstats = {}; }
+int groups_stats(syzcov_groups_stats *out) {
+    if (!out) return SYZCOV_EINVAL;
+    *out = g_gstats;
+    return 0;
 }
 
 int minimize_via_engine(const uint64_t *offsets, const uint32_t *pcs, size_t n,

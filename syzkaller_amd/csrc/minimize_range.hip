@@ -282,7 +282,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         __syncthreads();
     }
     const uint32_t l = __lane_id();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
     const uint32_t rbase = rho << A.rshift;
     const uint32_t bmask = (1u << A.rshift) - 1u;
     const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
         if (ib + 64 < w1) load_desc(ib + 64);
         const uint32_t incl = wave_incl_scan(nch);
         const uint32_t ex_l = incl - nch;  // lane j: item j's first chunk
-        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t tot = wave_readlane(incl, 63);
         s_a0[w][l] = a0;
         s_he[w][l] = he;
         s_ex[w][l] = ex_l;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(THREADS) void pass1_stream_kernel(Args A, uint32_t 
                 s_own[w][l] = 0u;
                 const uint32_t pm = wave_incl_max(mk);
                 const uint32_t j = pm ? max(sj, pm - 1u) : sj;
-                sj = __builtin_amdgcn_readlane(j, 63);
+                sj = wave_readlane(j, 63);
                 jj[u] = j;
                 dj[u] = c < tot ? j : 64u;
             }
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
         __syncthreads();
     }
     const uint32_t l = __lane_id();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
     const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
     const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
     uint32_t d_s0 = 0, d_s1 = 0;
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
         if (ib + 64 < w1) load_desc(ib + 64);
         const uint32_t incl = wave_incl_scan(nch);
         const uint32_t ex_l = incl - nch;
-        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t tot = wave_readlane(incl, 63);
         s_a0[w][l] = a0;
         s_he[w][l] = he;
         s_ex[w][l] = ex_l;
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
                 s_own[w][l] = 0u;
                 const uint32_t pm = wave_incl_max(mk);
                 const uint32_t j = pm ? max(sj, pm - 1u) : sj;
-                sj = __builtin_amdgcn_readlane(j, 63);
+                sj = wave_readlane(j, 63);
                 jj[u] = j;
                 dj[u] = c < tot ? j : 64u;
             }
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(THREADS) void group_min_kernel(GmArgs A) {
     uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_own + NWAVE);  // GM_MAX_ITEMS bits
     uint32_t &s_next = s_bits[GM_MAX_ITEMS / 32];
     const uint32_t l = __lane_id();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
     s_own[w][l] = 0u;
     const uint32_t npieces = A.ngroups * A.nrange;
     const uint32_t kmask = (1u << A.rshift) - 1u;
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(THREADS) void group_min_kernel(GmArgs A) {
             }
             const uint32_t incl = wave_incl_scan(nch);
             const uint32_t ex_l = incl - nch;
-            const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t tot = wave_readlane(incl, 63);
             s_a0[w][l] = a0;
             s_he[w][l] = he;
             s_ex[w][l] = ex_l;
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(THREADS) void group_min_kernel(GmArgs A) {
                 s_own[w][l] = 0u;
                 const uint32_t pm = wave_incl_max(mk);
                 const uint32_t j = pm ? max(sj, pm - 1u) : sj;
-                sj = __builtin_amdgcn_readlane(j, 63);
+                sj = wave_readlane(j, 63);
                 if (c < tot) {
                     const uint64_t ba = s_a0[w][j];
                     const uint32_t hv = s_he[w][j];

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(NC_THREADS) void newcov_cand_kernel(
                 // last PC of the previous row for lane 0
                 uint32_t prev = __shfl_up(pc[u], 1, 64);
                 if (l == 0) prev = carry;
-                carry = __builtin_amdgcn_readlane(pc[u], 63);
+                carry = wave_readlane(pc[u], 63);
                 if (q < n && q > 0 && prev > pc[u]) bad |= 2u;
                 // maxCover first: once it saturates, flakes are rarely probed
                 const bool cand =
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
     auto flush = [&]() {
         uint32_t base = 0;
         if (l == 0) base = atomicAdd(&stats[1], nc);
-        base = __builtin_amdgcn_readfirstlane(base);
+        base = wave_readfirstlane(base);
         if (l < nc) clist[base + l] = cb[l];
         nc = 0;
     };
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             if (n > LC_CBW) {  // a row with many: straight to the list
                 uint32_t base = 0;
                 if (l == 0) base = atomicAdd(&stats[1], n);
-                base = __builtin_amdgcn_readfirstlane(base);
+                base = wave_readfirstlane(base);
                 if (cand) clist[base + rank] = make_uint2(k, pc);
             } else {
                 if (cand) cb[nc + rank] = make_uint2(k, pc);
@@ -597,8 +597,8 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
 #pragma unroll
         for (int u = 0; u < LC_U; u++) {
             const uint32_t i = (s0 + u) & 63;
-            const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
-            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t ra = wave_readlane(my.x, i);
+            const uint32_t z = wave_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
             const bool any = s0 + u < nrow && 4 * l + 3 >= lo && 4 * l < hi;
             pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
 #pragma unroll
         for (int u = 0; u < LC_U; u++) {
             const uint32_t i = (s0 + u) & 63;
-            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t z = wave_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
             const bool row = s0 + u < nrow;  // wave-uniform
             const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
         for (int u = 0; u < LC_U; u++) {
             if (s0 + u >= nrow) break;  // wave-uniform
             const uint32_t i = (s0 + u) & 63;
-            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t z = wave_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
             const uint32_t lo1 = lo + first, n = hi - lo, n1 = hi - lo1;
             const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
             // element 4l's predecessor: lane l-1's last element (DPP wave shift),
             // for lane 0 the PC before the row
             const uint32_t p0 =
-                __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
+                __builtin_amdgcn_update_dpp(wave_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
             uint32_t cand = 0;
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -673,7 +673,7 @@ __global__ __launch_bounds__(LC_THREADS, KEY ? SYZ_NC_KEY_WPE : 8) __attribute__
                             lr, mine ? (v[c] >> ks) - obase + (q << RSH) : 0xFFFFFFF0u, 0, 0);
                         nonv |= (uint32_t)(mine & (mc != (v[c] & lowmask)));
                     }
-                    emit(mine, __builtin_amdgcn_readlane(my.y, i), v[c]);
+                    emit(mine, wave_readlane(my.y, i), v[c]);
                 }
             }
         }
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
     auto flush = [&]() {
         uint32_t base = 0;
         if (l == 0) base = atomicAdd(&stats[1], ncb);
-        base = __builtin_amdgcn_readfirstlane(base);
+        base = wave_readfirstlane(base);
         if (l < ncb) clist[base + l] = make_uint2(cbk, cbp);
         ncb = 0;
     };
@@ -886,8 +886,8 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
 #pragma unroll
         for (int u = 0; u < FU; u++) {
             const uint32_t i = (s0 + u) & 63;
-            const uint32_t ra = __builtin_amdgcn_readlane(my.x, i);
-            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t ra = wave_readlane(my.x, i);
+            const uint32_t z = wave_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u;
             const bool any = s0 + u < nrow && 4 * l + 3 >= lo && 4 * l < hi;
             pc[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
         for (int u = 0; u < FU; u++) {
             if (s0 + u >= nrow) break;  // wave-uniform
             const uint32_t i = (s0 + u) & 63;
-            const uint32_t z = __builtin_amdgcn_readlane(my.z, i);
+            const uint32_t z = wave_readlane(my.z, i);
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
             const uint32_t lo1 = lo + first, n = hi - lo, n1 = hi - lo1;  // (hi > lo)
             const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
                 nw[c] = s_nb[(o[c] >> 3) & (NBW - 1)];
             }
             const uint32_t p0 =
-                __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
+                __builtin_amdgcn_update_dpp(wave_readlane(p0v, i), v[3], 0x138, 0xF, 0xF, false);
             uint32_t cand = 0;
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
                     const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
                         lr, (cm >> l) & 1u ? (v[c] >> ks) - X.kbase : 0xFFFFFFF0u, 0, 0);
                     nonv |= (uint32_t)(((cm >> l) & 1u) & (mc != (v[c] & lowmask)));
-                    emit(cm, __builtin_amdgcn_readlane(my.y, i), v[c]);
+                    emit(cm, wave_readlane(my.y, i), v[c]);
                 }
             }
         }
@@ -1100,8 +1100,8 @@ __global__ __launch_bounds__(MB_THREADS) void newcov_memb_kernel(
 #pragma unroll
                 for (int u = 0; u < MB_U; u++) {
                     const uint32_t i = (s0 + u) & 63;
-                    const uint32_t st = __builtin_amdgcn_readlane(dsc.x, i);
-                    const uint32_t z = __builtin_amdgcn_readlane(dsc.z, i);
+                    const uint32_t st = wave_readlane(dsc.x, i);
+                    const uint32_t z = wave_readlane(dsc.z, i);
                     const bool row = s0 + u < nrow;  // wave-uniform
                     const uint32_t lo = z & 511u, hi = row ? (z >> 9) & 511u : 0u;
                     const bool any = 4 * l + 3 >= lo && 4 * l < hi;
@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(MB_THREADS) void newcov_memb_kernel(
 #pragma unroll
                 for (int u = 0; u < MB_U; u++) {
                     const uint32_t i = (s0 + u) & 63;
-                    const uint32_t z = __builtin_amdgcn_readlane(dsc.z, i);
+                    const uint32_t z = wave_readlane(dsc.z, i);
                     const bool row = s0 + u < nrow;
                     const uint32_t lo = z & 511u, hi = row ? (z >> 9) & 511u : 0u;
                     const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};

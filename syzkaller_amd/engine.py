@@ -161,6 +161,7 @@ class CorpusEngine:
         (key mode: key words, common.h)."""
         check(self.L.syzcov_corpus_canon(self.h, _p(off), _p(raw), n, _stream()), "corpus_canon")
         self.canon = raw if self.canon_in_place else self.canon_buf
+        self._canon_step = (off.data_ptr(), n)  # the offsets/n the handle holds
 
     def sort_order(self, lens32: torch.Tensor | None = None, n: int | None = None):
         """Go sort.Sort order over int32 lengths (None: this step's own);
@@ -224,6 +225,11 @@ class CorpusEngine:
         decoded from the key words canon wrote there)."""
         lists = self.canon
         if self.canon_align_k:  # line-aligned layout: back into the CSR slots
+            # syzcov_corpus_canonical unpacks by the handle's own offsets and n
+            # (the last canon step's): another off or n would size the output
+            # below what the kernel writes
+            if getattr(self, "_canon_step", None) != (off.data_ptr(), n):
+                raise ValueError("canonical_pcs: off / n differ from the last canonicalize step")
             lists = torch.zeros(int(off[n].item()) + 1, dtype=torch.int32, device=self.dev)
             check(self.L.syzcov_corpus_canonical(self.h, _p(lists), _stream()),
                   "corpus_canonical")

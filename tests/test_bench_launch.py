@@ -66,6 +66,7 @@ def test_same_workload_at_every_n(monkeypatch):
     monkeypatch.setattr(bench, "init_dist", lambda: (1, 0, None))
     monkeypatch.setattr(bench, "corpus_run", fake_run)
     monkeypatch.setattr(bench, "stream_peak", lambda dev: {"flat_float4": 1.0})
+    monkeypatch.setattr(bench, "rank_share_run", lambda *a, **k: {"ms_per_step": 1.0})
     monkeypatch.setattr(sys, "argv", ["bench.py", "--no-c2", "--no-dropin", "--no-cpu"])
     _, _, one = bench.bench_corpus(bench.parse())
     assert seen == {"glob": bench.C3_INPUTS, "seed": bench.SEED_C3, "key": "C3"}
@@ -78,3 +79,4 @@ def test_same_workload_at_every_n(monkeypatch):
     assert one["config"]["workload"] == lines[1]["config"]["workload"] \
         == lines[2]["config"]["workload"], (one["config"], lines)
     assert one["config"]["workload"].startswith("C3: ") and one["scaling"] == "strong"
+    assert "c3_rank_of_8" in one  # the 8-GPU step's per-rank share, measured at N=1

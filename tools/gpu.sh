@@ -27,6 +27,12 @@ summ() {  # one line of a bench JSON
   python3 - "$1" "$2" <<'EOF'
 import json, sys
 d = json.load(open(sys.argv[1]))
+if "c3_rank_of_8" in d:  # the rank-share leg (alone, or as a sub-record)
+    q = d["c3_rank_of_8"]
+    print(sys.argv[2], "rank_of_8", round(q["ms_per_step"], 4), q["phases_ms"],
+          "canon", round(q["canon_roofline"]["frac"], 4), "min", round(q["minimize_roofline"]["frac"], 4))
+    if "ms_per_step" not in d:
+        sys.exit(0)
 r = d.get("roofline", {})
 print(sys.argv[2], round(d["ms_per_step"], 4), d.get("phases_ms"), "frac", round(r.get("frac", 0), 4),
       d.get("results", {}).get("kept"), d.get("results", {}).get("union"),
