@@ -850,9 +850,21 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                 continue;
             }
         }
-        uint32_t cnt = 0, rprev = sent_g;
+        uint32_t cnt = 0, rprev = sent_g, dcar = 0;
         uint32_t *outp = P.out + aligned_base(base, seg, P.ak);
-        constexpr bool direct = !ALIGNED;  // line-aligned: written from buf below
+        // line-aligned: each kept word straight to its aligned sub-run (the
+        // range transitions of a row by one ballot, aligned_delta), or with
+        // SYZ_CANON_AL_COPY from buf after the split search (round 5's form)
+#ifdef SYZ_CANON_AL_COPY
+        constexpr bool direct = !ALIGNED;
+        constexpr bool al_direct = false;
+#else
+        constexpr bool direct = true;
+        constexpr bool al_direct = ALIGNED;
+#endif
+        // a gapped word's range: key bits rshift.. sit one bit higher (bits 12+)
+        const uint32_t rsh1 = P.rshift + 1;
+        const uint32_t rmask = (GMASK >> rsh1) << rsh1;
 #pragma unroll
         for (int q = 0; q < NQ; q++)
             if ((uint32_t)q < nq) {
@@ -866,13 +878,31 @@ __global__ __launch_bounds__(64 * WPB, MINW) void canon_key_kernel(Params P, con
                     // whole words: distinct PCs stay distinct even if they share a key
                     const bool keep = v != prev;
                     const uint64_t m = __builtin_amdgcn_ballot_w64(keep);
+                    const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
+                                                   (uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    uint32_t delta = dcar;
+                    if (al_direct) {
+                        // a range starts where a kept word's range bits differ
+                        // from its predecessor's (a non-kept slot repeats the
+                        // previous kept word); the segment's first word always
+                        const bool st = keep & ((((v ^ prev) & rmask) != 0u) |
+                                                (q == 0 && c == 0 && lane0));
+                        uint64_t sm = __builtin_amdgcn_ballot_w64(st);
+                        while (sm) {  // uniform; about one start per row of 64
+                            const uint32_t b = (uint32_t)__builtin_ctzll(sm);
+                            sm &= sm - 1;
+                            const uint32_t pb = wave_readlane(pos, (int)b);
+                            const uint32_t jb = ((wave_readlane(v, (int)b) & GMASK) >> rsh1);
+                            const uint32_t db = aligned_sub(pb, jb, P.ak) - pb;
+                            delta = l >= b ? db : delta;
+                            dcar = db;
+                        }
+                    }
                     if (keep) {
-                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
-                                                       (uint32_t)(m >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                         const uint32_t w = ungap_word(v);
-                        // the key word: the PC is kept exactly (line-aligned: from buf below)
-                        if (direct) outp[pos] = w;
+                        // the key word: the PC is kept exactly
+                        if (direct) outp[pos + (al_direct ? delta : 0u)] = w;
                         buf[pos] = w;  // (the split search masks the key)
                     }
                     cnt += (uint32_t)__popcll(m);

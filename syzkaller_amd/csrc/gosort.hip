@@ -401,7 +401,6 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
         __syncthreads();  // wcnt / wpre / wtot are rewritten by the next item
         if (j == 0 && threadIdx.x == 0) plan[s].cnt = (int)cnt;
         const int L = g.a + (int)cnt;  // left region [a+1, L]
-        uint32_t mloc = 0;
         for (int c0 = w0; c0 < w1; c0 += 64) {
             const int x = c0 + (int)l;
             const bool in = x < w1;
@@ -410,15 +409,15 @@ __global__ __launch_bounds__(WG) void rank_kernel(const Seg *__restrict__ cur,
             const uint32_t pf = base + (uint32_t)__popcll(m & lt);
             if (in) {
                 if (x > L && f) PR[g.a + ((int)cnt - (int)pf - 1)] = x;
-                if (x <= L && !f) {
-                    PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
-                    mloc++;
-                }
+                if (x <= L && !f) PL[g.a + ((x - (g.a + 1)) - (int)pf)] = x;
+                // m = the left-misplaced elements = the positions of [a+1, L]
+                // less the left-group elements among them, known at x = L with
+                // no atomic (one per wave and item on ONE address serialised
+                // at L2: 10 K of them made the first round's ranking 167 us)
+                if (x == L) plan[s].m = (L - g.a) - (int)(pf + (f ? 1u : 0u));
             }
             base += (uint32_t)__popcll(m);
         }
-        mloc = wave_sum(mloc);
-        if (l == 0 && mloc) atomicAdd(&plan[s].m, (int)mloc);
     }
 }
 

@@ -78,6 +78,7 @@ for step in "$@"; do
         python3 bench.py --no-cpu --no-c2 --no-dropin $targs > $o/trace.log 2>&1 ||
         { tail -20 $o/trace.log; exit 1; }
     python3 tools/trace_summary.py $o/trace > $o/trace_summary.txt; head -30 $o/trace_summary.txt
+    [ -n "$TL_MARK" ] && python3 tools/trace_timeline.py $o/trace "$TL_MARK" > $o/timeline.txt
     find $o/trace -name '*kernel_trace.csv' -delete
     ;;
   kbench:*)
