@@ -802,6 +802,15 @@ int syzcov_dev_prio_build_at(int key_mode, const int32_t *lens, const uint64_t *
                              size_t ldp, uint32_t *err_flag, void *stream);
 int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog, int C, int32_t *counts,
                            void *stream);
+/* The same contraction on 256 x 256 tiles (a 128 x 128 sub-tile per wave, one
+ * workgroup per CU, K split over the workgroups with partial tiles in ws and
+ * one reduction): LDS traffic under the MFMA time instead of over it.  ws:
+ * syzcov_dev_prio_counts_ws_size(nprog, C) bytes (0: the rows are not a
+ * multiple of 256; then, or with a smaller ws, syzcov_dev_prio_counts runs).
+ * Accumulates into counts like syzcov_dev_prio_counts. */
+size_t syzcov_dev_prio_counts_ws_size(size_t nprog, int C);
+int syzcov_dev_prio_counts_ws(const int8_t *at, size_t ldp, size_t nprog, int C, int32_t *counts,
+                              void *ws, size_t ws_size, void *stream);
 /* Positional counts (key_mode 0) over the ACTIVE keys only: A[p][k] is zero
  * for k >= max_len, so AT is built for the first roundup(max_len, 128) keys,
  * the MFMA tiles are K-split with partial tiles + a reduction, and the

@@ -157,6 +157,8 @@ _SIGS = {
     "syzcov_dev_prio_ldp": (sz, [sz]),
     "syzcov_dev_prio_build_at": (C.c_int, [C.c_int, p_, p_, p_, sz, C.c_int, p_, sz, p_, p_]),
     "syzcov_dev_prio_counts": (C.c_int, [p_, sz, sz, C.c_int, p_, p_]),
+    "syzcov_dev_prio_counts_ws_size": (sz, [sz, C.c_int]),
+    "syzcov_dev_prio_counts_ws": (C.c_int, [p_, sz, sz, C.c_int, p_, p_, sz, p_]),
     "syzcov_dev_prio_pos_ws_size": (sz, [sz, C.c_int, C.c_int]),
     "syzcov_dev_prio_counts_pos": (C.c_int, [p_, sz, C.c_int, C.c_int, p_, p_, sz, p_]),
     "syzcov_dev_prio_finish": (C.c_int, [p_, C.c_int, p_, p_, p_, p_]),

@@ -882,7 +882,7 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
            i_ids = p.add(key_mode ? ncalls * 2 : 0), i_at = p.add(rows * ldp),
            i_cnt = p.add(rows * rows * 4), i_st = p.add((size_t)C * C * 4),
            i_out = p.add((size_t)C * C * 4), i_raw = p.add(raw_counts ? (size_t)C * C * 4 : 0),
-           i_err = p.add(4);
+           i_err = p.add(4), i_dws = p.add(syzcov_dev_prio_counts_ws_size(nprog, C));
     std::vector<uint8_t *> b;
     RC(reserve(c, p, b));
     CK(hipMemsetAsync(b[i_err], 0, 4, c->s));
@@ -896,7 +896,8 @@ int syzcov_calculate_priorities(const uint64_t *prog_off, const uint16_t *call_i
                                 (uint16_t *)b[i_ids], nprog, C, (int8_t *)b[i_at], ldp,
                                 (uint32_t *)b[i_err], c->s));
     CK(hipMemsetAsync(b[i_cnt], 0, rows * rows * 4, c->s));
-    RC(syzcov_dev_prio_counts((int8_t *)b[i_at], ldp, nprog, C, (int32_t *)b[i_cnt], c->s));
+    RC(syzcov_dev_prio_counts_ws((int8_t *)b[i_at], ldp, nprog, C, (int32_t *)b[i_cnt], b[i_dws],
+                                 p.sizes[i_dws], c->s));
     RC(syzcov_dev_prio_finish((int32_t *)b[i_cnt], C, static_prios ? (float *)b[i_st] : nullptr,
                               (float *)b[i_out], raw_counts ? (uint32_t *)b[i_raw] : nullptr,
                               c->s));

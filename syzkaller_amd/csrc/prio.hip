@@ -290,17 +290,152 @@ __global__ __launch_bounds__(256) void prio_gemm_kernel(const int8_t *__restrict
             }
 }
 
+// Dense mode, 256 x 256 tiles (rows a multiple of 256): the 128 x 128 tile
+// above reads 2 KB of LDS per 32x32x32 MFMA pair and writes 16 KB per K step
+// for 8 MFMAs per wave, so its LDS traffic (384 cycles per step) exceeds its
+// MFMA time (256 cycles per SIMD): LDS-bound at 0.30 of the i8 peak.  Here
+// 8 waves (two per SIMD) each own a 64 x 128 sub-tile (2 x 4 MFMA 32x32x32,
+// 128 accumulators): per K step a SIMD's two waves issue 32 MFMAs (1024
+// cycles) against 96 KB of fragment reads and 32 KB of staging writes per CU
+// (1024 cycles of LDS), with the second wave hiding the first's waits.  (One
+// wave per SIMD with a 128 x 128 sub-tile: the 256 accumulators made the
+// compiler shuttle them between AGPRs and VGPRs, ~1000 moves per K loop.)
+// One workgroup per CU, every tile an equal share of K (diagonal tiles too),
+// so the grid of tiles x splits runs in one round; partial tiles go to `part`
+// and prio_reduce_kernel<256> sums the splits.
+constexpr int PT2 = 256;
+constexpr int G2_THREADS = 512;
+__device__ __forceinline__ void mfma_step256(const int8_t *Asrc, const int8_t *Bsrc, uint32_t l,
+                                             uint32_t wr, uint32_t wc, v16i (&acc)[2][4]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+        const uint32_t ch = ks * 2 + (l >> 5);
+        v4i fa[2], fb[4];
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+            fa[mi] = *(const v4i *)(Asrc + lds_off(wr * 64 + mi * 32 + (l & 31), ch));
+#pragma unroll
+        for (int ni = 0; ni < 4; ni++)
+            fb[ni] = *(const v4i *)(Bsrc + lds_off(wc * 128 + ni * 32 + (l & 31), ch));
+#pragma unroll
+        for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+            for (int ni = 0; ni < 4; ni++)
+                acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+    }
+}
+
+// Operands go global -> LDS directly (global_load_lds, 16 bytes a lane): a
+// wave-instruction writes 1 KB = 16 rows x 64 programs contiguously, so the
+// XOR swizzle of lds_off is applied to each lane's SOURCE chunk.  G2_NS stages
+// of 32 KB (A rows, then B rows) in one dynamic LDS block; step k + G2_NS - 1
+// is issued right after step k's barrier, and the wait before a barrier is a
+// counted vmcnt (the later steps' loads stay in flight across it) with a raw
+// s_barrier (__syncthreads would drain vmcnt to 0).  (Register staging, two
+// sets in flight: 1.22 ms for the C4 contraction, load latency exposed.)
+constexpr int G2_NS = 4;
+constexpr size_t G2_STAGE = 2 * PT2 * PK;
+constexpr size_t G2_LDS = G2_NS * G2_STAGE;  // 128 KB
+__device__ __forceinline__ void g2_glds(const int8_t *src, int8_t *dst) {
+    __builtin_amdgcn_global_load_lds((const void *)src,
+                                     (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(G2_THREADS, 1) void prio_gemm256_kernel(const int8_t *__restrict__ at,
+                                                                     size_t ldp, size_t kchunk,
+                                                                     int ntile_dim, int ntiles,
+                                                                     int gpx, size_t rows,
+                                                                     int32_t *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) int8_t g2_lds[];
+    // splits grouped by XCD (prio_gemm_kernel): an XCD's splits run with all
+    // their tiles, so each K block of AT comes from HBM once per XCD
+    const uint32_t xcd = blockIdx.x & 7u, slot = blockIdx.x >> 3;
+    const int tile = (int)(slot % (uint32_t)ntiles);
+    const size_t split = (size_t)xcd * gpx + slot / (uint32_t)ntiles;
+    int I = 0, rem = tile;
+    while (rem >= ntile_dim - I) {
+        rem -= ntile_dim - I;
+        I++;
+    }
+    const int J = I + rem;
+    const bool diag = I == J;
+    const size_t i0 = (size_t)I * PT2, j0 = (size_t)J * PT2;
+    const size_t kb0 = std::min(split * kchunk, ldp), kb1 = std::min(kb0 + kchunk, ldp);
+    const uint32_t nsteps = (uint32_t)((kb1 - kb0) / PK);
+    const uint32_t t = threadIdx.x, l = __lane_id(), w = wave_readfirstlane(t >> 6);
+    const uint32_t wr = w >> 1, wc = w & 1;
+    v16i acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[a][b][r] = 0;
+    // wave w stages rows 32 w .. 32 w + 31 of A (and of B): two 16-row blocks;
+    // lane l of block q lands at row 32 w + 16 q + l / 4, slot l & 3, which
+    // holds chunk (l & 3) ^ ((row >> 2) & 3)
+    const uint32_t r0 = 32 * w + (l >> 2), r1 = r0 + 16;
+    const size_t sa0 = (i0 + r0) * PK + (((l & 3u) ^ ((r0 >> 2) & 3u)) << 4);
+    const size_t sa1 = (i0 + r1) * PK + (((l & 3u) ^ ((r1 >> 2) & 3u)) << 4);
+    const size_t sb0 = (j0 + r0) * PK + (((l & 3u) ^ ((r0 >> 2) & 3u)) << 4);
+    const size_t sb1 = (j0 + r1) * PK + (((l & 3u) ^ ((r1 >> 2) & 3u)) << 4);
+    const uint32_t d0 = 32 * w * PK, d1 = d0 + 16 * PK;
+    auto issue = [&](uint32_t k) {
+        const int8_t *src = at + (kb0 / PK + k) * (rows * PK);
+        int8_t *st = g2_lds + (k % G2_NS) * G2_STAGE;
+        g2_glds(src + sa0, st + d0);
+        g2_glds(src + sa1, st + d1);
+        if (!diag) {
+            g2_glds(src + sb0, st + PT2 * PK + d0);
+            g2_glds(src + sb1, st + PT2 * PK + d1);
+        }
+    };
+    for (uint32_t k = 0; k < (uint32_t)G2_NS - 1 && k < nsteps; k++) issue(k);
+    for (uint32_t k = 0; k < nsteps; k++) {
+        // this wave's loads of step k are done once at most the later steps'
+        // (2 or 4 a step) are outstanding
+        const uint32_t ahead = min((uint32_t)G2_NS - 2, nsteps - 1 - k);
+        if (diag) {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        // (stage (k + NS - 1) % NS was read in step k - 1, before the barrier)
+        if (k + G2_NS - 1 < nsteps) issue(k + G2_NS - 1);
+        const int8_t *st = g2_lds + (k % G2_NS) * G2_STAGE;
+        mfma_step256(st, diag ? st : st + PT2 * PK, l, wr, wc, acc);
+    }
+    // epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    int32_t *pt = part + (split * (size_t)ntiles + tile) * (PT2 * PT2);
+#pragma unroll
+    for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+        for (int ni = 0; ni < 4; ni++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const uint32_t lr = wr * 64 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+                const uint32_t lc = wc * 128 + ni * 32 + (l & 31);
+                pt[lr * PT2 + lc] = acc[mi][ni][r];
+            }
+}
+
 // counts (ldc stride, zeroed) += the partial tiles of the K splits, mirrored
 // below the diagonal.  blockIdx.y takes every gridDim.y-th split, so each
 // count gets gridDim.y atomic adds (coalesced loads, 8 splits in flight per
 // thread) instead of one thread summing all splits in a latency chain.
 // The ones row (index `ones`, >= every nonzero key) yields colsum in its
 // column: it goes to column C, the slot prio_finish reads it from.
+template <int TT = PT>
 __global__ __launch_bounds__(256) void prio_reduce_kernel(const int32_t *__restrict__ part,
                                                           size_t splits, int ntiles, int ntile_dim,
                                                           int32_t *__restrict__ counts,
                                                           size_t ldc, int ones, int C) {
-    const size_t per = (size_t)ntiles * PT * PT;
+    const size_t per = (size_t)ntiles * TT * TT;
     const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= per) return;
     int32_t sum = 0;
@@ -314,24 +449,29 @@ __global__ __launch_bounds__(256) void prio_reduce_kernel(const int32_t *__restr
     }
     for (; sp < splits; sp += gridDim.y) sum += part[sp * per + e];
     if (!sum) return;
-    const int tile = (int)(e / (PT * PT));
-    const uint32_t lr = (uint32_t)(e % (PT * PT)) / PT, lc = (uint32_t)(e % PT);
+    const int tile = (int)(e / (TT * TT));
+    const uint32_t lr = (uint32_t)(e % (TT * TT)) / TT, lc = (uint32_t)(e % TT);
     int I = 0, rem = tile;
     while (rem >= ntile_dim - I) {
         rem -= ntile_dim - I;
         I++;
     }
-    const size_t row = (size_t)I * PT + lr, col = (size_t)(I + rem) * PT + lc;
+    const size_t row = (size_t)I * TT + lr, col = (size_t)(I + rem) * TT + lc;
     // the ones row lies in the last row block, so every key meets it once as
     // a COLUMN (tiles (I, last) and the diagonal last tile); its row copy in
     // the diagonal tile is the same numbers and is skipped
     if ((int)row == ones) return;
+    // one writer per count when every split is summed here (gridDim.y == 1):
+    // a plain read-add-write, else atomics
+    auto add = [&](size_t x) {
+        if (gridDim.y == 1) counts[x] += sum; else atomicAdd(&counts[x], sum);
+    };
     if ((int)col == ones) {
-        if ((int)row < C) atomicAdd(&counts[row * ldc + C], sum);
+        if ((int)row < C) add(row * ldc + C);
         return;
     }
-    atomicAdd(&counts[row * ldc + col], sum);
-    if (rem) atomicAdd(&counts[col * ldc + row], sum);
+    add(row * ldc + col);
+    if (rem) add(col * ldc + row);
 }
 
 // Positional colsum: counts[i][C] = #{p : len(p) > i} (the diagonal
@@ -633,6 +773,59 @@ extern "C" int syzcov_dev_prio_counts(const int8_t *at, size_t ldp, size_t nprog
     return 0;
 }
 
+// Dense mode on 256 x 256 tiles (prio_gemm256_kernel): one workgroup per CU,
+// 8 * gpx K splits grouped by XCD, partial tiles in ws, one reduction.
+static bool g256_plan(size_t nprog, int C, int *nt, int *ntiles, int *gpx, size_t *kchunk) {
+    const size_t rows = prio_rows(C);
+    if (rows % PT2) return false;
+    *nt = (int)(rows / PT2);
+    *ntiles = *nt * (*nt + 1) / 2;
+    int cus = 256, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const size_t nk = prio_ldp(nprog) / PK;
+    // the most splits (a multiple of the 8 XCDs) with tiles x splits <= CUs
+    *gpx = std::max(1, cus / (8 * *ntiles));
+    *gpx = (int)std::min<size_t>(*gpx, (nk + 7) / 8);
+    const size_t splits = 8 * (size_t)*gpx;
+    *kchunk = (nk + splits - 1) / splits * PK;
+    return true;
+}
+
+extern "C" size_t syzcov_dev_prio_counts_ws_size(size_t nprog, int C) {
+    int nt, ntiles, gpx;
+    size_t kc;
+    if (C <= 0 || nprog == 0 || !g256_plan(nprog, C, &nt, &ntiles, &gpx, &kc)) return 0;
+    return align_up(8 * (size_t)gpx * ntiles * PT2 * PT2 * 4, 256);
+}
+
+extern "C" int syzcov_dev_prio_counts_ws(const int8_t *at, size_t ldp, size_t nprog, int C,
+                                         int32_t *counts, void *ws, size_t ws_size, void *stream) {
+    if (C <= 0 || !at || !counts || ldp % PK || ldp < nprog) return SYZCOV_EINVAL;
+    if (nprog == 0) return 0;
+    const size_t need = syzcov_dev_prio_counts_ws_size(nprog, C);
+    if (!need || !ws || ws_size < need)  // no 256-row tiling (or no workspace): 128 x 128 tiles
+        return syzcov_dev_prio_counts(at, ldp, nprog, C, counts, stream);
+    int nt, ntiles, gpx;
+    size_t kc;
+    g256_plan(nprog, C, &nt, &ntiles, &gpx, &kc);
+    const size_t rows = prio_rows(C), splits = 8 * (size_t)gpx;
+    hipStream_t s = (hipStream_t)stream;
+    static std::atomic<uint32_t> g2_attr{0};
+    if (int rc = set_dyn_lds_once((const void *)prio_gemm256_kernel, (uint32_t)G2_LDS, g2_attr))
+        return rc;
+    hipLaunchKernelGGL(prio_gemm256_kernel, dim3((unsigned)(ntiles * splits)), dim3(G2_THREADS), G2_LDS, s, at,
+                       ldp, kc, nt, ntiles, gpx, rows, (int32_t *)ws);
+    // the ones row (index C) yields colsum in column C, as prio_gemm_kernel's
+    // atomics leave it
+    hipLaunchKernelGGL(prio_reduce_kernel<PT2>,
+                       dim3((unsigned)(((size_t)ntiles * PT2 * PT2 + 255) / 256), 1), dim3(256), 0,
+                       s, (const int32_t *)ws, splits, ntiles, nt, counts, rows, C, C);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int syzcov_dev_prio_finish(const int32_t *counts, int C, const float *static_prios,
                                       float *out, uint32_t *raw_out, void *stream) {
     if (C <= 0 || !counts || !out) return SYZCOV_EINVAL;
@@ -714,7 +907,7 @@ extern "C" int syzcov_dev_prio_counts_pos(const int32_t *lens, size_t nprog, int
     hipLaunchKernelGGL(prio_gemm_kernel<true>, dim3((unsigned)(tiles * sp)), dim3(256), 0, s,
                        (const int8_t *)nullptr, ldp, kc, nt, (int)tiles, (int)(sp / 8), counts, ra,
                        ldc, part, lens, nprog, ones);
-    hipLaunchKernelGGL(prio_reduce_kernel,
+    hipLaunchKernelGGL(prio_reduce_kernel<PT>,
                        dim3((unsigned)((tiles * PT * PT + 255) / 256), (unsigned)std::min<size_t>(sp, 16)),
                        dim3(256), 0, s, (const int32_t *)part, sp, (int)tiles, nt, counts, ldc, ones,
                        C);

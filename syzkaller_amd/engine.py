@@ -276,10 +276,21 @@ class PrioEngine:
         self.active_rows = active_rows
         self.max_len = None
         self.pos_ws = None
+        # dense mode: 256 x 256 tiles with a partial-tile workspace (prio.hip
+        # prio_gemm256_kernel); 0 bytes: 128 x 128 tiles with atomics
+        self.tile = 128
+        self.dense_ws = None
+        if not active_rows:
+            wsz = L.syzcov_dev_prio_counts_ws_size(nprog, C_)
+            if wsz:
+                self.dense_ws = torch.empty(wsz, dtype=torch.uint8, device=self.dev)
+                self.tile = 256
 
     def gemm_ops(self) -> int:
         """MFMA ops one counts launch executes (upper-triangle 128x128 tiles)."""
-        nt = self.rows // 128
+        nt = self.rows // self.tile
+        if not self.active_rows:
+            return nt * (nt + 1) // 2 * self.tile * self.tile * 2 * self.ldp
         if self.active_rows and self.max_len is not None:
             # the active block holds the ones row too: roundup(min(max_len, C) + 1, 128)
             # rows, as pos_plan sizes it (prio.hip)
@@ -319,8 +330,13 @@ class PrioEngine:
                   "dev_prio_build_at")
             self.counts.zero_()
             mark_ev(2)
-            check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
-                                           _p(self.counts), s), "dev_prio_counts")
+            if self.dense_ws is not None:
+                check(L.syzcov_dev_prio_counts_ws(_p(self.at), self.ldp, self.nprog, self.C,
+                                                  _p(self.counts), _p(self.dense_ws),
+                                                  self.dense_ws.numel(), s), "dev_prio_counts_ws")
+            else:
+                check(L.syzcov_dev_prio_counts(_p(self.at), self.ldp, self.nprog, self.C,
+                                               _p(self.counts), s), "dev_prio_counts")
         if reduce is not None:
             reduce(self.counts)
         mark_ev(3)

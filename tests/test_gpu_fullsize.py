@@ -200,6 +200,35 @@ def test_c4_closed_form_1m(torch):
     assert out is eng.out
 
 
+def test_c4_dense_closed_form(torch):
+    """The dense contraction (all C keys, AT in HBM: the bench's --prio-dense
+    line, 256 x 256 MFMA tiles with partial tiles and one reduction) gives the
+    same exact counts as the closed form D[i][j] = #{p : len(p) > max(i, j)}."""
+    import ctypes as C
+    from syzkaller_amd import _lib
+    from syzkaller_amd.engine import PrioEngine, _stream
+    L = _lib.lib()
+    nprog, seed = 300_000, 0x5EED0004
+    eng = PrioEngine(nprog, active_rows=False)
+    assert eng.tile == 256  # C = 1170: 1280 rows, five 256-row tile rows
+    lens = torch.empty(nprog, dtype=torch.int32, device="cuda")
+    _lib.check(L.syzcov_dev_synth_lens(seed, 0, nprog, 30, 8, C.c_void_p(lens.data_ptr()),
+                                       _stream()), "synth_lens")
+    eng.step(lens)
+    Cn = eng.C
+    raw = torch.empty(Cn * Cn, dtype=torch.int32, device="cuda")
+    _lib.check(L.syzcov_dev_prio_finish(C.c_void_p(eng.counts.data_ptr()), Cn, None,
+                                        C.c_void_p(eng.out.data_ptr()), C.c_void_p(raw.data_ptr()),
+                                        _stream()), "prio_finish")
+    hl = lens.cpu().numpy()
+    h = np.bincount(hl, minlength=Cn + 1)
+    gt = nprog - np.cumsum(h)[:Cn + 1].astype(np.int64)
+    idx = np.arange(Cn)
+    D = gt[np.maximum(idx[:, None], idx[None, :])]
+    np.fill_diagonal(D, 0)
+    assert np.array_equal(raw.cpu().numpy().astype(np.int64).reshape(Cn, Cn), D)
+
+
 @pytest.mark.parametrize("name,keys", [("C5", True), ("C5", False), ("C5S", True)],
                          ids=["early-key-mode", "early-window-mode", "steady-key-mode"])
 def test_c5_newcov_stream_fullsize(torch, name, keys):
