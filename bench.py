@@ -581,6 +581,8 @@ def bench_corpus(args):
             # the 8-GPU step's per-rank work, measured on this GPU
             out["c3_rank_of_8"] = rank_share_run(args, dev, steps=max(args.steps, 10),
                                                  warmup=args.warmup)
+        if not args.no_c2:
+            out["c4"] = c4_subrecord(args, dev)
         if not args.no_dropin:
             out["dropin"] = dropin_legs(args, dev)
             out["dropin"]["pairwise"] = pairwise_leg()
@@ -794,17 +796,18 @@ def pairwise_leg(reps: int = 2000, nthreads: int = 32) -> dict:
     return out
 
 
-def bench_prio(args):
+def prio_run(args, world, rank, dev, dense: bool, steps: int, warmup: int):
+    """K timed steps of CalculatePriorities over `args.inputs` synthetic
+    programs per GPU: positional counts over the active keys (reference-exact,
+    prio.go:142-150), or the dense contraction over all C keys (the MFMA GEMM
+    over an AT in HBM).  Returns (seconds, phase ms, engine)."""
     import ctypes as C
     import torch
-    world, rank, dev = init_dist()
     from syzkaller_amd import _lib
     from syzkaller_amd.engine import PrioEngine
     L = _lib.lib()
     nprog = args.inputs
-    # default: positional counts over the active keys (reference-exact, prio.go:142-150);
-    # --prio-dense: the full 1170-key contraction (the dense MFMA GEMM)
-    eng = PrioEngine(nprog, device=dev, active_rows=not args.prio_dense)
+    eng = PrioEngine(nprog, device=dev, active_rows=not dense)
     lens = torch.empty(nprog, dtype=torch.int32, device=dev)
     _lib.check(L.syzcov_dev_synth_lens(SEED_PRIO, rank * nprog, nprog, 30, 8,
                                        C.c_void_p(lens.data_ptr()),
@@ -816,8 +819,35 @@ def bench_prio(args):
     if world > 1:  # sharded by program: int32 SUM all-reduce of the counts
         from syzkaller_amd.dist import merge_counts
         reduce = merge_counts
-    dt, phl = timed(lambda ev: eng.step(lens, ev, reduce), len(phases), args, world, dev)
-    ph = dict(zip(phases, phl))
+    a = argparse.Namespace(steps=steps, warmup=warmup)
+    dt, phl = timed(lambda ev: eng.step(lens, ev, reduce), len(phases), a, world, dev)
+    return dt, dict(zip(phases, phl)), eng
+
+
+def c4_subrecord(args, dev) -> dict:
+    """Config C4 beside the corpus headline (N=1): CalculatePriorities over 1M
+    programs, positional (the reference's semantics) and dense (all 1170 keys
+    on i8 MFMA, the contraction north_star names), each with its MFMA roofline."""
+    out = {"programs": args.inputs}
+    for name, dense in (("positional", False), ("dense", True)):
+        dt, ph, eng = prio_run(args, 1, 0, dev, dense, 10, 3)
+        ops = eng.gemm_ops()
+        ach = ops / (ph["gemm"] * 1e-3) / 1e12
+        out[name] = {"ms_per_step": dt / 10 * 1e3, "phases_ms": {k: round(v, 4) for k, v in ph.items()},
+                     "programs_per_s": args.inputs * 10 / dt,
+                     "mfma_roofline": {"achieved": ach, "peak": I8_PEAK_TOPS, "unit": "TOPS",
+                                       "frac": ach / I8_PEAK_TOPS, "mfma_ops_per_launch": ops,
+                                       "tile": eng.tile if dense else 128}}
+        del eng
+    return out
+
+
+def bench_prio(args):
+    world, rank, dev = init_dist()
+    nprog = args.inputs
+    # default: positional counts over the active keys (reference-exact, prio.go:142-150);
+    # --prio-dense: the full 1170-key contraction (the dense MFMA GEMM)
+    dt, ph, eng = prio_run(args, world, rank, dev, args.prio_dense, args.steps, args.warmup)
     ops = eng.gemm_ops()
     achieved = ops / (ph["gemm"] * 1e-3) / 1e12
     out = {

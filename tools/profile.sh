@@ -8,11 +8,15 @@
 #   -> OUT/traffic.json {"C3": phases, "C2": phases, "newcov": ..., "dedup": ...}
 # Counters are never combined with tracing; each pass is its own run within the
 # per-block limits (MI355X_MICROARCH.md, HBM / rocprofv3).
-#   usage: tools/profile.sh OUT [parts: corpus canon newcov newcov_early dedup groups prio]
+#   rank: rank 0's share of C3 over 8 GPUs (bench --rank-share-only): trace +
+#     FETCH / WRITE of its one timed step -> traffic.json["C3R8"]
+#   prio_mfma: SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES of the C4 GEMMs
+#     (positional and dense) -> OUT/prio_mfma_pmc.txt
+#   usage: tools/profile.sh OUT [parts: corpus rank canon newcov newcov_early dedup groups prio prio_mfma]
 set -o pipefail
 export TMPDIR=/tmp
 o=${1:-gpurun_out/prof}; shift
-parts=${*:-corpus canon newcov newcov_early dedup groups prio}
+parts=${*:-corpus rank canon newcov newcov_early dedup groups prio prio_mfma}
 mkdir -p $o
 B="python3 bench.py --no-cpu --no-c2 --no-dropin"
 has() { case " $parts " in *" $1 "*) return 0;; esac; return 1; }
@@ -34,6 +38,11 @@ if has corpus; then
   pmc_pair C2 "" "" $B --global-inputs 1000000 --steps 1 --warmup 0
   trace C2X $B --global-inputs 1000000 --x86 --steps 10 --warmup 2
   pmc_pair C2X "" "" $B --global-inputs 1000000 --x86 --steps 1 --warmup 0
+fi
+if has rank; then  # the 8-GPU step's per-rank share (its timed step: the last bin_kernel on)
+  trace C3R8 $B --rank-share-only --steps 5 --warmup 2
+  python3 tools/trace_timeline.py $o/C3R8_trace bin_kernel 0 > $o/C3R8_timeline.txt
+  pmc_pair C3R8 bin_kernel 1 $B --rank-share-only --steps 1 --warmup 0
 fi
 if has canon; then
   i=0
@@ -69,6 +78,14 @@ if has groups; then  # Manager.minimizeCorpus from host buffers (C2 in 293 call 
 fi
 if has prio; then
   trace prio $B --workload prio --steps 10 --warmup 3
+  trace prio_dense $B --workload prio --prio-dense --steps 10 --warmup 3
+fi
+if has prio_mfma; then  # MFMA utilisation of the contraction (one pass per mode)
+  for m in pos dense; do
+    a=""; [ $m = dense ] && a="--prio-dense"
+    timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $o/pmcprio_$m -o run -- $B --workload prio $a --steps 3 --warmup 1 > $o/pmcprio_$m.log 2>&1 || { tail -3 $o/pmcprio_$m.log; echo "prio pmc $m failed"; exit 1; }
+  done
+  python3 tools/mfma_summary.py $o/pmcprio_pos $o/pmcprio_dense > $o/prio_mfma_pmc.txt; cat $o/prio_mfma_pmc.txt
 fi
 python3 - $o <<'PY'
 import glob, json, os, sys
