@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # per-phase HBM bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over
 # this same bench command (tools/profile.sh -> tools/traffic.py), committed per round:
 # {"C3": {phase: ...}, "C2": ..., "newcov": ..., "dedup": ...}
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r06_traffic.json")
 
 
 def traffic_of(workload: str, phase: str):

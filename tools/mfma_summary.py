@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """MFMA utilisation of the C4 GEMM kernels from rocprofv3 --pmc passes
 (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE per dispatch).
-gfx950 counts SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs of every CU, so
-the busy fraction of the matrix cores is MFMA_BUSY / (GRBM_GUI_ACTIVE x CUs x
-4 SIMDs) while the kernel runs.  Usage: tools/mfma_summary.py DIR...  (each
+On gfx950 SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs (a
+v_mfma_i32_32x32x32_i8 adds its 32 cycles: the C4 dense contraction's 30 M
+MFMAs read 9.6e8) and GRBM_GUI_ACTIVE over the 8 XCDs, so the matrix cores'
+busy fraction while the kernel runs is MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 x 256
+CUs x 4 SIMDs).  Usage: tools/mfma_summary.py DIR...  (each
 DIR one rocprofv3 -d output)."""
 import collections
 import csv
@@ -11,7 +13,7 @@ import glob
 import os
 import sys
 
-CUS, SIMDS = 256, 4
+CUS, SIMDS, XCDS = 256, 4, 8
 for d in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     n = collections.defaultdict(set)
@@ -27,7 +29,7 @@ for d in sys.argv[1:]:
         nd = len(n[k])
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / nd
         gui = c.get("GRBM_GUI_ACTIVE", 0) / nd
-        frac = busy / (gui * CUS * SIMDS) if gui else float("nan")
+        frac = busy / (gui / XCDS * CUS * SIMDS) if gui else float("nan")
         print(f"{os.path.basename(d)}  {k}: dispatches {nd}, per dispatch "
               + ", ".join(f"{name} {v / nd:.4g}" for name, v in sorted(c.items()))
-              + f"; MFMA busy / (GRBM_GUI_ACTIVE x {CUS} CUs x {SIMDS} SIMDs) = {frac:.3f}")
+              + f"; MFMA busy / (GRBM_GUI_ACTIVE / {XCDS} x {CUS} CUs x {SIMDS} SIMDs) = {frac:.3f}")

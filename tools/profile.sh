@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 o=${1:-gpurun_out/prof}; shift
 parts=${*:-corpus rank canon newcov newcov_early dedup groups prio prio_mfma}
 mkdir -p $o
-B="python3 bench.py --no-cpu --no-c2 --no-dropin"
+B="python3 bench.py --no-cpu --no-c2 --no-dropin --no-rank-share"
 has() { case " $parts " in *" $1 "*) return 0;; esac; return 1; }
 pmc_pair() {  # name, step kernel ("" = bin_kernel), last-N ("" = all steps), bench args...
   local name=$1 sk=$2 last=$3; shift 3
