@@ -410,7 +410,8 @@ enum {
     SYZCOV_CORPUS_MAX_COVER,   /* u32 [nwords] resident maxCover */
     SYZCOV_CORPUS_TAB,         /* u64 [nwords] dictionary of the union */
     SYZCOV_CORPUS_FIRST,       /* i32 [span] first-cover ranks (INT32_MAX between steps) */
-    SYZCOV_CORPUS_REC,         /* u64 [rec_cap] first-cover records */
+    SYZCOV_CORPUS_REC,         /* u64 [rec_cap] first-cover records (key mode: 2 rec_cap, the
+                                  second half their copy sorted by key bucket) */
     SYZCOV_CORPUS_CAND,        /* u8  [n_max + 1] */
     SYZCOV_CORPUS_KEPT,        /* u8  [n_global + 4] kept flag per global rank, + 4 error-flag bytes */
     SYZCOV_CORPUS_LENS,        /* i64 [n_global + 1] */

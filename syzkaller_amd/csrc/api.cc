@@ -51,6 +51,7 @@ uint32_t force_flags() {
     if (strstr(e, "nc_sep")) f |= FORCE_NC_SEP;
     if (strstr(e, "mr_bytes")) f |= FORCE_MR_BYTES;
     if (strstr(e, "nc_hash64")) f |= FORCE_NC_HASH64;
+    if (strstr(e, "min_atomics")) f |= FORCE_MIN_ATOMICS;
     return f;
 }
 

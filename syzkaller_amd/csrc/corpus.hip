@@ -162,7 +162,15 @@ int minimize_range_keys_n4(const uint64_t *off, const uint32_t *len, const uint3
                            const uint64_t *range_tot, const uint8_t *low_of_key,
                            uint32_t *covered, int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
                            uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
-                           uint32_t *err_flag, void *ws, hipStream_t s);
+                           uint32_t *err_flag, void *ws, hipStream_t s, uint64_t *rsort);
+int minimize_range_keys_sorted(const uint64_t *off, const uint32_t *len, const uint32_t *words,
+                               const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                               size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                               const uint64_t *range_tot, const uint8_t *low_of_key,
+                               uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                               uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
+                               int do_pass2, uint32_t *err_flag, void *ws, hipStream_t s,
+                               uint64_t *rsort);
 
 struct Corpus {
     std::mutex mu;
@@ -241,7 +249,9 @@ static int64_t plan(Corpus &c) {
     sz[SYZCOV_CORPUS_MAX_COVER] = c.nwords * 4;
     sz[SYZCOV_CORPUS_TAB] = c.nwords * 8;
     sz[SYZCOV_CORPUS_FIRST] = c.span * 4;
-    sz[SYZCOV_CORPUS_REC] = g.rec_cap * 8;
+    // key mode: the records, then their copy sorted by key bucket (Minimize's
+    // bucketed first covers, minimize_range.hip bmin_kernel)
+    sz[SYZCOV_CORPUS_REC] = g.rec_cap * 8 * (c.key_mode ? 2 : 1);
     sz[SYZCOV_CORPUS_CAND] = n + 1;
     sz[SYZCOV_CORPUS_KEPT] = N + kErrBytes;
     sz[SYZCOV_CORPUS_LENS] = (N + 1) * 8;
@@ -536,6 +546,7 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
             c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap, scal(c) + SC_REC,
             c.buf<uint8_t>(SYZCOV_CORPUS_CAND), c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2,
             (uint32_t *)(scal(c) + SC_ERR), c.buf<void>(SYZCOV_CORPUS_WS), s);
+    uint64_t *rsort = c.key_mode ? c.buf<uint64_t>(SYZCOV_CORPUS_REC) + c.cfg.rec_cap : nullptr;
     if (c.key_mode && c.rshift == kRangeShiftKeysN4)
         return minimize_range_keys_n4(
             c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
@@ -543,15 +554,15 @@ static int ph_minimize(Corpus &c, int do_pass2, hipStream_t s) {
             c.buf<int32_t>(SYZCOV_CORPUS_FIRST), c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap,
             scal(c) + SC_REC, c.buf<uint8_t>(SYZCOV_CORPUS_CAND),
             c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, (uint32_t *)(scal(c) + SC_ERR),
-            c.buf<void>(SYZCOV_CORPUS_WS), s);
+            c.buf<void>(SYZCOV_CORPUS_WS), s, rsort);
     if (c.key_mode)
-        return syzcov_dev_minimize_range_keys(
+        return minimize_range_keys_sorted(
             c.off, nl, c.canon, split, items, ranks, c.n, c.span, c.rshift, rt,
             c.buf<uint8_t>(SYZCOV_CORPUS_LOW_OF_KEY), c.buf<uint32_t>(SYZCOV_CORPUS_COVERED),
             c.buf<int32_t>(SYZCOV_CORPUS_FIRST), c.buf<uint64_t>(SYZCOV_CORPUS_REC), c.cfg.rec_cap,
             scal(c) + SC_REC, c.buf<uint8_t>(SYZCOV_CORPUS_CAND),
             c.buf<uint8_t>(SYZCOV_CORPUS_KEPT), do_pass2, (uint32_t *)(scal(c) + SC_ERR),
-            c.buf<void>(SYZCOV_CORPUS_WS), s);
+            c.buf<void>(SYZCOV_CORPUS_WS), s, rsort);
     return syzcov_dev_minimize_range(
         c.off, nl, c.canon, split, items, ranks, c.n, c.pc_lo, c.span, c.rshift, rt,
         c.buf<uint32_t>(SYZCOV_CORPUS_COVERED), c.buf<int32_t>(SYZCOV_CORPUS_FIRST),

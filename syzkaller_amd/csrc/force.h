@@ -13,6 +13,7 @@ enum : uint32_t {
     FORCE_NC_SEP = 32u,        // newcov key mode: candidate pass + separate membership pass
     FORCE_MR_BYTES = 64u,      // corpus key mode, kshift <= 2: byte tables, not nibbles
     FORCE_NC_HASH64 = 128u,    // newcov ownership: u64 keys + separate values, not packed slots
+    FORCE_MIN_ATOMICS = 256u,  // corpus key mode: min_records' atomics, not bucketed first covers
 };
 uint32_t force_flags();
 }  // namespace syz

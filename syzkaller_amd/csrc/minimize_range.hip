@@ -101,7 +101,15 @@ struct Args {
     const uint8_t *low_of_key; // [nrange << rshift] bytes, 0x7F past the keys
     uint32_t *err;             // SYZCOV_ERR_UNIVERSE
     uint32_t ak;               // line-aligned sub-runs (common.h), 0: CSR slots
+    // bucketed first covers (bmin_kernel): per-chunk record counts per bucket
+    // of 2^BSH keys [2][nb] (chunk parity), scatter cursors [2][nb], the
+    // records sorted by bucket; bh == nullptr: min_records_kernel's atomics
+    uint32_t *bh, *bcur;
+    unsigned long long *rsort;
+    uint32_t nb;
 };
+constexpr uint32_t BSH = 14;          // keys per bucket: 2^14 (64 KB of int32 in LDS)
+constexpr uint32_t MAX_NB = 1024;     // key spaces up to 2^24 (cover_from_first)
 
 
 // Gather the items' CSR bases and split columns into rank order, transposed
@@ -491,8 +499,11 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     auto *s_own = reinterpret_cast<uint32_t(*)[64]>(s_rk + NWAVE); // item + 1 per chunk
     uint32_t *s_plan = reinterpret_cast<uint32_t *>(s_own + NWAVE);
     uint32_t &s_next = s_plan[MAX_R + 1];
+    uint32_t *s_bh = s_plan + MAX_R + 2;  // this workgroup's records per key bucket
     const uint32_t G = A.npieces;
     s_own[threadIdx.x >> 6][__lane_id()] = 0u;
+    if (A.bh)
+        for (uint32_t i = threadIdx.x; i < A.nb; i += THREADS) s_bh[i] = 0u;
     plan_pieces(A, G, P, s_plan);
     const uint32_t region = blockIdx.x % NCTR;
     unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
@@ -703,10 +714,12 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
                             for (int k = 0; k < (int)CW; k++)
                                 if ((um >> (u * CW + k)) & 1u) {
                                     const uint32_t wo = wd[u * CW + k] & SYZ_KEY_MASK;
-                                    if (slot < A.cap_k)
+                                    if (slot < A.cap_k) {
                                         rrec[slot] = ((unsigned long long)(uint32_t)rki << 32) | wo;
-                                    else  // no room: its min cannot wait
+                                        if (A.bh) atomicAdd(&s_bh[wo >> BSH], 1u);
+                                    } else {  // no room: its min cannot wait
                                         atomicMin(&A.first_w[wo], rki);
+                                    }
                                     slot++;
                                 }
                         }
@@ -728,6 +741,10 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     __syncthreads();
     }
     if (__ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
+    if (A.bh) {  // (the piece loop ended on a barrier)
+        for (uint32_t i = threadIdx.x; i < A.nb; i += THREADS)
+            if (s_bh[i]) atomicAdd(&A.bh[i], s_bh[i]);
+    }
 }
 
 // Manager.minimizeCorpus (syz-manager/manager.go:504-524) when every call
@@ -851,7 +868,7 @@ constexpr size_t GM_LDS = GM_TAB * 4 + NWAVE * 64 * (8 + 3 * 4) + GM_MAX_ITEMS /
 
 // dynamic LDS of pass1_keys_kernel past its 2^17-byte table
 constexpr size_t KEYS_LDS_EXTRA =
-    NWAVE * 64 * (8 + 4 * 4) + (MAX_R + 2) * 4;
+    NWAVE * 64 * (8 + 4 * 4) + (MAX_R + 2) * 4 + MAX_NB * 4;
 
 // Region loops: block b serves region b % NCTR (the grid is a multiple of
 // NCTR), records [lo_k, min(ctr_k, cap_k)) of it.
@@ -883,6 +900,119 @@ __global__ void min_records_kernel(Args A, int par, int or_cover) {
             const uint32_t mbit = 1u << (wo & 31);
             if (!(A.covered[wo >> 5] & mbit)) atomicOr((uint32_t *)&A.covered[wo >> 5], mbit);
         }
+    }
+}
+
+// Bucketed first covers, the chunk's replacement for min_records_kernel +
+// first_to_bits (key spaces <= 2^24): min_records' atomicMin per record on
+// random first_w words ran at ~19 G/s (0.37 ms of C2's and of a C3/8 rank's
+// Minimize), and the covered rebuild read all of first_w after every chunk.
+// rec_scatter_kernel copies the chunk's new records into buckets of 2^BSH
+// keys (pass 1 counted them per bucket: A.bh, this chunk's parity half);
+// bmin_kernel then gives each bucket to one workgroup, which takes the
+// minimum rank per key in LDS (ds_min, no global atomics), writes first_w of
+// its keys once (min with what is there: a record that found its region full
+// took its atomicMin directly) and rebuilds its covered words from first_w.
+__device__ uint32_t bucket_scan(const uint32_t *bh, uint32_t nb, uint32_t b, uint32_t *s_tmp) {
+    // exclusive prefix of bucket b (one workgroup, nb <= MAX_NB)
+    uint32_t v = 0;
+    for (uint32_t i = threadIdx.x; i < b; i += blockDim.x) v += bh[i];
+    v = wave_sum(v);
+    if (__lane_id() == 0) s_tmp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) tot += s_tmp[w];
+    __syncthreads();
+    return tot;
+}
+
+constexpr int RS_TILE = 8;  // records per thread per round of rec_scatter_kernel
+__global__ __launch_bounds__(256) void rec_scatter_kernel(Args A, int par) {
+    __shared__ uint32_t s_pre[MAX_NB], s_cnt[MAX_NB], s_base[MAX_NB];
+    const uint32_t *bh = A.bh + par * A.nb;
+    uint32_t *cur = A.bcur + par * A.nb;
+    // every bucket's exclusive prefix (the scan of the <= 1024 counts, once
+    // per workgroup)
+    {
+        uint32_t run = 0;
+        for (uint32_t i0 = 0; i0 < A.nb; i0 += 256) {
+            const uint32_t i = i0 + threadIdx.x;
+            const uint32_t v = i < A.nb ? bh[i] : 0u;
+            __shared__ uint32_t tmp[256 / 64 + 1];
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan<256>(v, tmp, &tot);
+            if (i < A.nb) s_pre[i] = run + ex;
+            run += tot;
+        }
+    }
+    const unsigned long long *done_in = A.done + (par ? 1 : 0) * NCTR * CTR_STRIDE;
+    unsigned long long *done_out = A.done + (par ? 0 : 1) * NCTR * CTR_STRIDE;
+    if (blockIdx.x < NCTR && threadIdx.x == 0)  // (as min_records_kernel)
+        done_out[blockIdx.x * CTR_STRIDE] =
+            std::min<uint64_t>(A.ctr[blockIdx.x * CTR_STRIDE], A.cap_k);
+    const uint32_t k_ = blockIdx.x % NCTR, sub_ = blockIdx.x / NCTR, nsub_ = gridDim.x / NCTR;
+    const uint64_t lo = done_in[k_ * CTR_STRIDE];
+    const uint64_t hi = std::min<uint64_t>(A.ctr[k_ * CTR_STRIDE], A.cap_k);
+    const unsigned long long *rk = A.rec + k_ * A.cap_k;
+    const uint64_t per = (uint64_t)256 * RS_TILE;
+    for (uint64_t t0 = lo + (uint64_t)sub_ * per; t0 < hi; t0 += (uint64_t)nsub_ * per) {
+        for (uint32_t i = threadIdx.x; i < A.nb; i += 256) s_cnt[i] = 0u;
+        __syncthreads();
+        unsigned long long r[RS_TILE];
+        uint32_t slot[RS_TILE];
+#pragma unroll
+        for (int j = 0; j < RS_TILE; j++) {
+            const uint64_t i = t0 + (uint64_t)j * 256 + threadIdx.x;
+            r[j] = i < hi ? rk[i] : ~0ull;
+            slot[j] = r[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)r[j] >> BSH], 1u) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < A.nb; i += 256)
+            s_base[i] = s_cnt[i] ? s_pre[i] + atomicAdd(&cur[i], s_cnt[i]) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RS_TILE; j++)
+            if (r[j] != ~0ull) A.rsort[s_base[(uint32_t)r[j] >> BSH] + slot[j]] = r[j];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void bmin_kernel(Args A, int par, uint64_t span) {
+    __shared__ int32_t s_min[1u << BSH];
+    __shared__ uint32_t s_tmp[16];
+    const uint32_t b = blockIdx.x;
+    const uint32_t *bh = A.bh + par * A.nb;
+    const uint32_t r0 = bucket_scan(bh, A.nb, b, s_tmp), n = bh[b];
+    const uint64_t k0 = (uint64_t)b << BSH;
+    const uint32_t nk = (uint32_t)std::min<uint64_t>(1u << BSH, span - k0);
+    if (n) {
+        for (uint32_t i = threadIdx.x; i < (1u << BSH); i += 1024) s_min[i] = INT32_MAX;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n; i += 1024) {
+            const unsigned long long r = A.rsort[r0 + i];
+            atomicMin(&s_min[(uint32_t)r & ((1u << BSH) - 1u)], (int32_t)(r >> 32));
+        }
+        __syncthreads();
+    }
+    // first_w of the bucket's keys, then its covered words (32 keys each,
+    // one ballot half per word): covered = {key : first_w[key] != INT32_MAX}
+    for (uint32_t i = threadIdx.x; i < ((nk + 63) & ~63u); i += 1024) {
+        int32_t f = INT32_MAX;
+        if (i < nk) {
+            f = A.first_w[k0 + i];
+            if (n && s_min[i] < f) {
+                f = s_min[i];
+                A.first_w[k0 + i] = f;
+            }
+        }
+        const uint64_t m = __ballot(f != INT32_MAX);
+        if ((__lane_id() & 31) == 0 && i < nk)
+            const_cast<uint32_t *>(A.covered)[(k0 + i) >> 5] = (uint32_t)(m >> (__lane_id() & 32));
+    }
+    // the other parity's counts and cursors start the next chunk at zero
+    if (threadIdx.x == 0) {
+        A.bh[(par ^ 1) * A.nb + b] = 0u;
+        A.bcur[(par ^ 1) * A.nb + b] = 0u;
     }
 }
 
@@ -994,8 +1124,9 @@ using namespace syz;
  *     split_t [nrange][n_items] u32 */
 // region counters | done marks x 2 | per-chunk piece counters (dynamic pieces)
 static constexpr int MR_MAX_CHUNKS = 64;
+static constexpr size_t MR_BKT = 4 * mr::MAX_NB * sizeof(uint32_t);  // bh[2][nb], bcur[2][nb]
 static constexpr size_t MR_HDR = 3 * mr::NCTR * mr::CTR_STRIDE * sizeof(uint64_t) +
-                                 MR_MAX_CHUNKS * 256;
+                                 MR_MAX_CHUNKS * 256 + MR_BKT;
 static uint64_t mr_nrange(uint64_t span, uint32_t rshift) {
     return (span + (1ull << rshift) - 1) >> rshift;
 }
@@ -1057,6 +1188,9 @@ static int mr_args(mr::Args &A, const uint64_t *off, const uint32_t *len, const 
     A.low_of_key = nullptr;
     A.err = nullptr;
     A.ak = 0;
+    A.bh = A.bcur = nullptr;
+    A.rsort = nullptr;
+    A.nb = 0;
     return 0;
 }
 
@@ -1091,7 +1225,7 @@ static int minimize_range_impl(
     uint64_t *rec, uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
     size_t first_chunk, uint32_t growth, uint64_t pcs_per_wg_hint, const uint8_t *low_of_key,
     uint32_t *err_flag, void *ws, void *stream, const uint64_t *grp_off = nullptr,
-    uint32_t ngroups = 0, int aligned = 0, bool n4 = false) {
+    uint32_t ngroups = 0, int aligned = 0, bool n4 = false, uint64_t *rsort = nullptr) {
     hipStream_t s = (hipStream_t)stream;
     if (n_items == 0) {
         if (rec_cnt) SYZ_HIP(hipMemsetAsync(rec_cnt, 0, sizeof(uint64_t), s));
@@ -1163,6 +1297,16 @@ static int minimize_range_impl(
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     // below 2^24 keys (64 MB of first_w) the covered set is rebuilt from first_w
     const bool cover_from_first = pc_span <= (1ull << 24);
+    // key mode with room for a sorted copy of the records (the corpus engine):
+    // first covers by bucket in LDS (bmin_kernel) instead of global atomics
+    const bool bucketed = rsort && keym && cover_from_first && !grp_off &&
+                          !(force_flags() & FORCE_MIN_ATOMICS);
+    if (bucketed) {
+        A.nb = (uint32_t)((pc_span + (1ull << mr::BSH) - 1) >> mr::BSH);
+        A.bh = (uint32_t *)((uint8_t *)ws + MR_HDR - MR_BKT);
+        A.bcur = A.bh + 2 * mr::MAX_NB;
+        A.rsort = (unsigned long long *)rsort;
+    }
     // pass 1 over the items [a0, a1) in geometric chunks (covered empty at a0)
     auto run_span = [&](uint64_t a0, uint64_t a1, uint64_t step0) -> int {
         uint64_t a = a0, step = step0;
@@ -1184,16 +1328,25 @@ static int minimize_range_impl(
             A.npieces = (uint32_t)G;
             const unsigned grid = (unsigned)std::min<uint64_t>(G, (uint64_t)dev_cus());
             nchunk++;
-            hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds1, s, A, (uint32_t)a,
+            mr::Args A1 = A;  // pass 1 counts this chunk's records per bucket
+            if (bucketed) A1.bh = A.bh + par * A.nb;
+            hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds1, s, A1, (uint32_t)a,
                                (uint32_t)b, (uint32_t)P, (int)(a != a0));
-            // the chunk's first covers (+ covered, unless rebuilt below)
-            hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
-                               (int)!cover_from_first);
-            // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
-            // first_w (16 MB at 2^22 keys) instead of an atomicOr per record (C2
-            // key mode: 5 vs 74-274 us per early chunk)
-            if (cover_from_first && b < a1)
-                RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
+            if (bucketed) {
+                // the chunk's first covers and covered words, bucket by bucket
+                hipLaunchKernelGGL(mr::rec_scatter_kernel, dim3(1024), dim3(256), 0, s, A, par);
+                hipLaunchKernelGGL(mr::bmin_kernel, dim3(A.nb), dim3(1024), 0, s, A, par,
+                                   pc_span);
+            } else {
+                // the chunk's first covers (+ covered, unless rebuilt below)
+                hipLaunchKernelGGL(mr::min_records_kernel, dim3(1024), dim3(256), 0, s, A, par,
+                                   (int)!cover_from_first);
+                // covered = {pc : first_w[pc] != INT32_MAX}: one coalesced pass over
+                // first_w (16 MB at 2^22 keys) instead of an atomicOr per record (C2
+                // key mode: 5 vs 74-274 us per early chunk)
+                if (cover_from_first && b < a1)
+                    RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
+            }
             par ^= 1;
             a = b;
             step *= growth;
@@ -1232,7 +1385,7 @@ static int minimize_range_impl(
         return 0;
     }
     RC_(run_span(0, n_items, first_chunk));
-    if (cover_from_first) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
+    if (cover_from_first && !bucketed) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
     // record overflow: the union comes from first_w instead (cover_from_first
     // already rebuilt covered from first_w)
     if (!cover_from_first)
@@ -1256,12 +1409,28 @@ int minimize_range_keys_n4(const uint64_t *off, const uint32_t *len, const uint3
                            const uint64_t *range_tot, const uint8_t *low_of_key,
                            uint32_t *covered, int32_t *first_w, uint64_t *rec, uint64_t rec_cap,
                            uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept, int do_pass2,
-                           uint32_t *err_flag, void *ws, hipStream_t s) {
+                           uint32_t *err_flag, void *ws, hipStream_t s, uint64_t *rsort) {
     if (!low_of_key) return SYZCOV_EINVAL;
     return minimize_range_impl(off, len, words, split, order, ranks, n_items, 0, nkeys,
                                range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt,
                                cand, kept, do_pass2, 0, 0, 0, low_of_key, err_flag, ws, s, nullptr,
-                               0, 0, true);
+                               0, 0, true, rsort);
+}
+// the corpus engine's key mode with byte tables: rsort (rec_cap records) for
+// the bucketed first covers
+int minimize_range_keys_sorted(const uint64_t *off, const uint32_t *len, const uint32_t *words,
+                               const uint32_t *split, const int32_t *order, const int32_t *ranks,
+                               size_t n_items, uint64_t nkeys, uint32_t range_shift,
+                               const uint64_t *range_tot, const uint8_t *low_of_key,
+                               uint32_t *covered, int32_t *first_w, uint64_t *rec,
+                               uint64_t rec_cap, uint64_t *rec_cnt, uint8_t *cand, uint8_t *kept,
+                               int do_pass2, uint32_t *err_flag, void *ws, hipStream_t s,
+                               uint64_t *rsort) {
+    if (!low_of_key) return SYZCOV_EINVAL;
+    return minimize_range_impl(off, len, words, split, order, ranks, n_items, 0, nkeys,
+                               range_shift, range_tot, covered, first_w, rec, rec_cap, rec_cnt,
+                               cand, kept, do_pass2, 0, 0, 0, low_of_key, err_flag, ws, s, nullptr,
+                               0, 0, false, rsort);
 }
 
 int minimize_range_groups(const uint64_t *off, const uint32_t *len, const uint32_t *pcs,
