@@ -422,8 +422,8 @@ enum {
     SYZCOV_CORPUS_PC_OF_KEY,   /* u32 [span] key mode */
     SYZCOV_CORPUS_LOW_OF_KEY,  /* u8  [span] key mode: membership table */
     SYZCOV_CORPUS_GLENS,       /* i32 [n_global] sharded: gathered lengths */
-    SYZCOV_CORPUS_SEL,         /* u8  [n_global] sharded */
-    SYZCOV_CORPUS_IOTA,        /* i32 [n_global] sharded */
+    SYZCOV_CORPUS_SEL,         /* unused (0 bytes): kept so the ids below stay */
+    SYZCOV_CORPUS_IOTA,        /* unused (0 bytes) */
     SYZCOV_CORPUS_ITEMS,       /* i32 [n_max + 1] sharded: local inputs in order */
     SYZCOV_CORPUS_RANKS,       /* i32 [n_max + 1] sharded: their global ranks */
     SYZCOV_CORPUS_FIRST_DENSE, /* i32 [union_cap] sharded window mode */

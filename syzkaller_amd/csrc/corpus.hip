@@ -36,17 +36,6 @@ __global__ void corpus_lens_kernel(const uint32_t *__restrict__ len32,
         lens[i] = len32 ? (int64_t)len32[i] : (int64_t)(off[i + 1] - off[i]);
 }
 
-// local work items of shard `rank`: sel[r] = order[r] lives here
-__global__ void corpus_sel_kernel(const int32_t *__restrict__ order, uint64_t N, uint32_t base,
-                                  uint32_t n_local, uint8_t *__restrict__ sel,
-                                  int32_t *__restrict__ iota) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        sel[i] = (uint32_t)order[i] - base < n_local;
-        iota[i] = (int32_t)i;
-    }
-}
-
 // a caller's order into ORDER; an entry outside [0, N) becomes 0 (no kernel
 // indexes past the corpus) and fails the step
 __global__ void corpus_order_copy_kernel(const int32_t *__restrict__ src, uint64_t N,
@@ -60,11 +49,6 @@ __global__ void corpus_order_copy_kernel(const int32_t *__restrict__ src, uint64
         bad |= !ok;
     }
     if (__ballot(bad) && __lane_id() == 0) atomicOr(err, SYZCOV_ERR_ORDER);
-}
-
-__global__ void corpus_sub_kernel(int32_t *__restrict__ v, uint32_t n, int32_t base) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        v[i] -= base;
 }
 
 // the union drops the sentinel (cover.go:97): its covered bit goes before the
@@ -263,8 +247,8 @@ static int64_t plan(Corpus &c) {
     sz[SYZCOV_CORPUS_LOW_OF_KEY] = c.key_mode ? (uint64_t)c.nrange << c.rshift : 0;
     if (c.shard) {
         sz[SYZCOV_CORPUS_GLENS] = N * 4;
-        sz[SYZCOV_CORPUS_SEL] = N;
-        sz[SYZCOV_CORPUS_IOTA] = N * 4;
+        sz[SYZCOV_CORPUS_SEL] = 0;   // (unused since the items' one compaction; kept in the ABI)
+        sz[SYZCOV_CORPUS_IOTA] = 0;
         sz[SYZCOV_CORPUS_ITEMS] = (n + 1) * 4;
         sz[SYZCOV_CORPUS_RANKS] = (n + 1) * 4;
         sz[SYZCOV_CORPUS_FIRST_DENSE] = c.key_mode ? 0 : c.union_cap * 4;
@@ -498,6 +482,9 @@ static int ph_order(Corpus &c, const int32_t *lens32, size_t N, hipStream_t s, u
                                (uint32_t *)(scal(c) + SC_ERR), s);
 }
 
+int compact_shard_items(const int32_t *order, size_t n, uint32_t base, uint32_t n_local,
+                        int32_t *ranks, int32_t *items, uint32_t *n_out, void *ws, hipStream_t s);
+
 // Work items: (input, rank).  One GPU: every input, ranks = positions of
 // the order.  Sharded: this shard's inputs in global processing order with
 // their GLOBAL ranks, by two ordered compactions (no host sync).
@@ -508,21 +495,12 @@ static int items_of(Corpus &c, const int32_t **items, const int32_t **ranks, hip
         return 0;
     }
     const uint32_t base = (uint32_t)(c.cfg.rank * c.cfg.n_max);
-    uint8_t *sel = c.buf<uint8_t>(SYZCOV_CORPUS_SEL);
-    int32_t *iota = c.buf<int32_t>(SYZCOV_CORPUS_IOTA);
     int32_t *it = c.buf<int32_t>(SYZCOV_CORPUS_ITEMS), *rk = c.buf<int32_t>(SYZCOV_CORPUS_RANKS);
     const int32_t *order = c.buf<int32_t>(SYZCOV_CORPUS_ORDER);
-    void *ws2 = c.buf<void>(SYZCOV_CORPUS_WS2);
-    hipLaunchKernelGGL(corpus_sel_kernel, dim3(grid_for(c.N, 256, 8192)), dim3(256), 0, s, order,
-                       (uint64_t)c.N, base, (uint32_t)c.n, sel, iota);
-    SYZ_LAUNCH_CHECK();
-    int rc = syzcov_dev_compact_kept(sel, iota, c.N, rk, (uint32_t *)(scal(c) + SC_CR), ws2, s);
+    // one ordered compaction writes both (minimize.hip compact_shard_items)
+    int rc = compact_shard_items(order, c.N, base, (uint32_t)c.n, rk, it,
+                                 (uint32_t *)(scal(c) + SC_CR), c.buf<void>(SYZCOV_CORPUS_WS2), s);
     if (rc) return rc;
-    rc = syzcov_dev_compact_kept(sel, order, c.N, it, (uint32_t *)(scal(c) + SC_CI), ws2, s);
-    if (rc) return rc;
-    hipLaunchKernelGGL(corpus_sub_kernel, dim3(grid_for(c.n, 256, 4096)), dim3(256), 0, s, it,
-                       (uint32_t)c.n, (int32_t)base);
-    SYZ_LAUNCH_CHECK();
     *items = it;
     *ranks = rk;
     return 0;

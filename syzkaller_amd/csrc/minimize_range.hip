@@ -122,13 +122,23 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
     extern __shared__ uint32_t s_tile[];
     __shared__ uint32_t s_seg[64];
     const uint32_t n = A.n_items, R = A.nrange, ld = R + 1;
-    for (uint32_t t0 = blockIdx.x * 64; t0 < n; t0 += gridDim.x * 64) {
+    // the next tile's order entries are loaded while this tile moves (one
+    // dependent global round trip fewer per tile: order -> rows)
+    const uint32_t tstride = gridDim.x * 64;
+    uint32_t segc = 0;
+    if (threadIdx.x < 64 && blockIdx.x * 64 + threadIdx.x < n)
+        segc = (uint32_t)A.order[blockIdx.x * 64 + threadIdx.x];
+    for (uint32_t t0 = blockIdx.x * 64; t0 < n; t0 += tstride) {
         const uint32_t rows = min(64u, n - t0);
+        uint32_t segn = 0;
+        if (threadIdx.x < 64 && (uint64_t)t0 + tstride + threadIdx.x < n)
+            segn = (uint32_t)A.order[t0 + tstride + threadIdx.x];
         if (threadIdx.x < rows) {
-            const uint32_t seg = (uint32_t)A.order[t0 + threadIdx.x];
+            const uint32_t seg = segc;
             s_seg[threadIdx.x] = seg;
             base_r[t0 + threadIdx.x] = aligned_base(A.off[seg], seg, A.ak);
         }
+        segc = segn;
         __syncthreads();
         if (!A.split) {  // one range: the column is the canonical length
             if (threadIdx.x < rows) split_t[t0 + threadIdx.x] = A.len[s_seg[threadIdx.x]];
