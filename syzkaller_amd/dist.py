@@ -1,5 +1,6 @@
-"""The corpus engine sharded by input over the GPUs of one node (weak
-scaling: each rank holds a contiguous slice of the global corpus).
+"""The corpus engine sharded by input over the GPUs of one node: each rank
+holds a contiguous slice of a global corpus of fixed size (C3's 10M inputs
+at every N, so the bench's curve is strong scaling).
 
 One process per GPU, torch.distributed over RCCL ("nccl" backend on ROCm).
 The only exchanges are the reductions the first-cover formulation needs
