@@ -472,7 +472,11 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
         mark()
         eng.minimize(do_pass2=False)
         mark()
+        if eng.bitmap_union:  # the shard bitmap as a byte map (its MAX all-reduce not run)
+            eng._to_bytes(eng.covered, eng.cov_u8)
         _lib.check(L.syzcov_corpus_pass2(eng.h, s), "corpus_pass2")
+        if eng.bitmap_union:
+            eng._to_bits(eng.cov_u8, eng.covered)
         mark()
         eng.finish()
         mark()
@@ -488,9 +492,11 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
     # (w-1)/w of the result, an all-reduce sends and receives 2(w-1)/w of it)
     f_ag, f_ar = (world - 1) / world, 2 * (world - 1) / world
     coll = {"lens_allgather_int32": N * 4, "order_max_allreduce_int32": N * 4,
-            "first_min_allreduce_int32": eng.span * 4, "kept_max_allreduce_u8": N + 4}
+            "first_min_allreduce_int32": eng.span * 4, "kept_max_allreduce_u8": N + 4,
+            "covered_max_allreduce_u8": eng.cov_u8.numel() if eng.bitmap_union else 0}
     ring = (f_ag * coll["lens_allgather_int32"] + f_ar * (coll["order_max_allreduce_int32"]
-            + coll["first_min_allreduce_int32"] + coll["kept_max_allreduce_u8"]))
+            + coll["first_min_allreduce_int32"] + coll["kept_max_allreduce_u8"]
+            + coll["covered_max_allreduce_u8"]))
     out = {
         "workload": (f"rank {rank} of {world} over C3 ({glob} inputs, seed {seed:#x}): its {n} "
                      f"inputs, Go's order over all {N} lengths, pass 1 at global ranks"),
@@ -511,7 +517,8 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
                         "note": "not run on one GPU; the 8-GPU step adds their time"},
         "results": {"kept_local_first": res.n_kept, "union_local": res.n_union},
         "stand_ins": "other ranks' lengths precomputed; merged order copied in; own first ranks "
-                     "for the MIN merge; kept MAX skipped",
+                     "for the MIN merge; own byte map for the covered MAX merge (converted both "
+                     "ways); kept MAX skipped",
     }
     eng.close()
     del eng, off, raw, full_order

@@ -757,6 +757,12 @@ int syzcov_dev_sort_order_segmented(const int64_t *lens, const uint64_t *goff, s
  * op 2: dst &= ~src (Difference) op 3: dst ^= src  (SymmetricDifference)
  * Maps are uint8 per PC; *popcount_out (device u64, nullable) receives the
  * number of nonzero bytes of the result. */
+/* A bitmap of nwords u32 words <-> its byte map (32 bytes per word, byte b of
+ * word w = bit b of w, 0 or 1; any nonzero byte reads back as a set bit): the
+ * form the shard bitmaps take for their uint8 MAX all-reduce (north_star;
+ * syzkaller_amd/dist.py merge_bitmap_u8).  bytes: 16-byte aligned, 32 nwords. */
+int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nwords, uint8_t *bytes, void *stream);
+int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nwords, uint32_t *bits, void *stream);
 int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, uint64_t nbytes,
                           uint64_t *popcount_out, void *stream);
 

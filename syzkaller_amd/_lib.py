@@ -158,6 +158,8 @@ _SIGS = {
     "syzcov_dev_prio_build_at": (C.c_int, [C.c_int, p_, p_, p_, sz, C.c_int, p_, sz, p_, p_]),
     "syzcov_dev_prio_counts": (C.c_int, [p_, sz, sz, C.c_int, p_, p_]),
     "syzcov_dev_prio_counts_ws_size": (sz, [sz, C.c_int]),
+    "syzcov_dev_bits_to_bytes": (C.c_int, [p_, u64, p_, p_]),
+    "syzcov_dev_bytes_to_bits": (C.c_int, [p_, u64, p_, p_]),
     "syzcov_dev_prio_counts_ws": (C.c_int, [p_, sz, sz, C.c_int, p_, p_, sz, p_]),
     "syzcov_dev_prio_pos_ws_size": (sz, [sz, C.c_int, C.c_int]),
     "syzcov_dev_prio_counts_pos": (C.c_int, [p_, sz, C.c_int, C.c_int, p_, p_, sz, p_]),

@@ -435,6 +435,68 @@ extern "C" int syzcov_dev_bytemap_op(int op, uint8_t *dst, const uint8_t *src, u
 }
 
 namespace syz {
+// A bitmap <-> a byte map (one byte per bit, 0 or 1): the shard bitmaps'
+// uint8 MAX all-reduce of north_star (dist.py merge_bitmap_u8).  One thread
+// per 32-bit word: 32 bytes written as two 16-byte stores, or read back.
+__global__ __launch_bounds__(256) void bits_to_bytes_kernel(const uint32_t *__restrict__ bits,
+                                                            uint64_t nwords,
+                                                            uint8_t *__restrict__ bytes) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = bits[w];
+        uint32_t q[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t n = (x >> (4 * j)) & 15u;  // bits 4j..4j+3 -> bytes 4j..4j+3
+            q[j] = (n & 1u) | ((n & 2u) << 7) | ((n & 4u) << 14) | ((n & 8u) << 21);
+        }
+        uint4 *o = reinterpret_cast<uint4 *>(bytes + w * 32);
+        o[0] = make_uint4(q[0], q[1], q[2], q[3]);
+        o[1] = make_uint4(q[4], q[5], q[6], q[7]);
+    }
+}
+__global__ __launch_bounds__(256) void bytes_to_bits_kernel(const uint8_t *__restrict__ bytes,
+                                                            uint64_t nwords,
+                                                            uint32_t *__restrict__ bits) {
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 *in = reinterpret_cast<const uint4 *>(bytes + w * 32);
+        const uint4 a = in[0], b = in[1];
+        const uint32_t q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t v = q[j];
+            const uint32_t n = ((v & 0xFFu) != 0) | (((v >> 8) & 0xFFu) != 0) << 1 |
+                               (((v >> 16) & 0xFFu) != 0) << 2 | ((v >> 24) != 0) << 3;
+            x |= n << (4 * j);
+        }
+        bits[w] = x;
+    }
+}
+}  // namespace syz
+
+extern "C" int syzcov_dev_bits_to_bytes(const uint32_t *bits, uint64_t nwords, uint8_t *bytes,
+                                        void *stream) {
+    if (!nwords) return 0;
+    if (!bits || !bytes || ((uintptr_t)bytes & 15)) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(syz::bits_to_bytes_kernel, dim3(grid_for(nwords, 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, bits, nwords, bytes);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int syzcov_dev_bytes_to_bits(const uint8_t *bytes, uint64_t nwords, uint32_t *bits,
+                                        void *stream) {
+    if (!nwords) return 0;
+    if (!bits || !bytes || ((uintptr_t)bytes & 15)) return SYZCOV_EINVAL;
+    hipLaunchKernelGGL(syz::bytes_to_bits_kernel, dim3(grid_for(nwords, 256, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, bytes, nwords, bits);
+    SYZ_LAUNCH_CHECK();
+    return 0;
+}
+
+namespace syz {
 // Sorted PC list of a bitmap over [pc_lo, pc_lo + pc_span) (sentinel
 // dropped, as a Union result would).  out == NULL: count only.
 // pc_of_key (nullable): the bitmap is over dense keys (keys.hip); the list is

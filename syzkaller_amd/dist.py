@@ -10,6 +10,8 @@ The only exchanges are the reductions the first-cover formulation needs
     order          int32 MAX all-reduce    -> each rank finished its part of it
     first[]        int32 MIN all-reduce    -> global first-cover rank per key
                                               (key mode: the union = keys with one)
+    covered bitmap uint8 MAX all-reduce    -> key mode: the union (north_star's shard
+                                              bitmap merge; one byte per key)
     covered bitmap all-gather + OR          -> window mode: the union = identical
                                               dictionary, first[] MIN over its ids
     kept flags     uint8 MAX all-reduce    -> identical kept list on every rank
@@ -91,6 +93,17 @@ def merge_covered(covered: torch.Tensor, world: int, or_into) -> None:
         or_into(covered, parts[r])
 
 
+def merge_bitmap_u8(covered: torch.Tensor, u8: torch.Tensor, to_bytes, to_bits) -> None:
+    """Union of the shards' covered bitmaps (u32 words) as north_star names it:
+    each bitmap as a byte map (one byte per key, 0 or 1: `to_bytes(words,
+    u8)`), a uint8 MAX all-reduce over RCCL, and back into `covered`
+    (`to_bits(u8, words)`).  The HIP converters on the GPU
+    (syzcov_dev_bits_to_bytes / _bytes_to_bits), numpy ones under gloo."""
+    to_bytes(covered, u8)
+    _all_reduce(u8, dist.ReduceOp.MAX)
+    to_bits(u8, covered)
+
+
 def gather_lens(local_lens: torch.Tensor, world: int) -> torch.Tensor:
     """Canonical lengths of every shard, in global input order."""
     out = torch.empty(local_lens.numel() * world, dtype=local_lens.dtype,
@@ -124,7 +137,7 @@ class ShardedEngine(CorpusEngine):
 
     def __init__(self, n: int, p_max: int, max_seg_len: int, pc_lo: int, pc_span: int,
                  rank: int, world: int, device="cuda", universe=None, canon_in_place=False,
-                 split_order: bool = True, canon_layout: int = 0):
+                 split_order: bool = True, canon_layout: int = 0, bitmap_union: bool = True):
         super().__init__(n, p_max, max_seg_len, pc_lo, pc_span, device=device,
                          n_global=n * world, rank=rank, universe=universe,
                          canon_in_place=canon_in_place, canon_layout=canon_layout)
@@ -132,6 +145,20 @@ class ShardedEngine(CorpusEngine):
         # the ranks split the Go order's late rounds and finisher (each finishes
         # the segments starting in its block), merged by an int32 MAX all-reduce
         self.split_order = split_order and world > 1
+        # key mode: the union is the uint8 MAX all-reduce of the shards' covered
+        # byte maps (north_star); False derives it from the MIN-merged first
+        # ranks alone (pass 2's first_to_bits), 4 MB less per rank at 2^22 keys
+        self.bitmap_union = bitmap_union and self.key_mode
+        self.cov_u8 = (torch.empty(self.covered.numel() * 32, dtype=torch.uint8, device=self.dev)
+                       if self.bitmap_union else None)
+
+    def _to_bytes(self, words, u8):
+        check(self.L.syzcov_dev_bits_to_bytes(_p(words), words.numel(), _p(u8), _stream()),
+              "dev_bits_to_bytes")
+
+    def _to_bits(self, u8, words):
+        check(self.L.syzcov_dev_bytes_to_bits(_p(u8), words.numel(), _p(words), _stream()),
+              "dev_bytes_to_bits")
 
     def _or_into(self, dst, src):
         check(self.L.syzcov_dev_bitmap_op(0, _p(dst), _p(src), dst.numel(), None, _stream()),
@@ -166,11 +193,18 @@ class ShardedEngine(CorpusEngine):
             # dense key space: the first-cover array itself is the exchange
             # (nkeys int32, 16 MB at 2^22 keys; no dictionary, no host sync)
             merge_first(self.first[:self.span])                      # RCCL int32 MIN
+            if self.bitmap_union:  # the shard bitmaps as byte maps, RCCL uint8 MAX
+                self._to_bytes(self.covered, self.cov_u8)
+                _all_reduce(self.cov_u8, dist.ReduceOp.MAX)
         else:
             merge_covered(self.covered[:self.nwords], self.world, self._or_into)
             n_ids = check(L.syzcov_corpus_dense_first(h, s), "corpus_dense_first")
             merge_first(self.first_dense[:n_ids])                   # RCCL int32 MIN
         check(L.syzcov_corpus_pass2(h, s), "corpus_pass2")          # kept against the global first
+        if self.bitmap_union:
+            # the union finish publishes: the MAX-merged shard bitmaps (the same
+            # set pass 2 rebuilt from the global first ranks)
+            self._to_bits(self.cov_u8, self.covered)
         # RCCL uint8 MAX of kept flags by global rank; kept[N..N+3] carry the
         # shard's error flags, one byte per flag bit (pass 2 wrote them, finish
         # ORs the merged bytes back: a shard that saw a non-universe PC fed its

@@ -48,7 +48,21 @@ def _worker_range(rank, world, port, q):
             first_w[w] = np.minimum(first_w[w], r)
         bits = np.packbits((first_w != 0x7FFFFFFF).astype(np.uint8), bitorder="little")
         covered = torch.from_numpy(bits.view(np.int32).copy())
+        # key mode's form of the same union: the shard bitmaps as byte maps,
+        # uint8 MAX all-reduce (north_star), back to bits
+        cov_u8 = covered.clone()
+        u8 = torch.empty(cov_u8.numel() * 32, dtype=torch.uint8)
+
+        def to_bytes(words, out):
+            out.copy_(torch.from_numpy(np.unpackbits(words.numpy().view(np.uint8),
+                                                     bitorder="little")))
+
+        def to_bits(b, words):
+            words.copy_(torch.from_numpy(np.packbits(b.numpy() != 0, bitorder="little")
+                                         .view(np.int32).copy()))
+        sdist.merge_bitmap_u8(cov_u8, u8, to_bytes, to_bits)
         sdist.merge_covered(covered, world, lambda d, s_: d.bitwise_or_(s_))
+        assert torch.equal(cov_u8, covered), "u8 MAX merge != OR merge"
         gbits = np.unpackbits(covered.numpy().view(np.uint8), bitorder="little")[:span]
         present = np.nonzero(gbits)[0]
         # dictionary (dense id = rank of the PC in the merged union) and MIN merge

@@ -311,3 +311,31 @@ def test_sort_order_parts_merge_to_go_order(cover, nparts):
         assert int(seen.min().item()) >= 1  # every position final on some part
         if n == 1_000_000:  # the late rounds were split: most positions on one part only
             assert float((seen == 1).float().mean().item()) > 0.5
+
+
+def test_bits_bytes_roundtrip():
+    """The byte-map form of a bitmap (the key-mode union's uint8 MAX
+    all-reduce, dist.merge_bitmap_u8): bit b of word w <-> byte 32 w + b, and
+    the MAX of byte maps is the OR of the bitmaps."""
+    import ctypes as C
+    import torch
+    from syzkaller_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(61)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    for nwords in (1, 5, 4099, 131072):
+        a = rng.random(nwords * 32) < 0.3
+        b = rng.random(nwords * 32) < 0.3
+        aw = torch.from_numpy(np.packbits(a, bitorder="little").view(np.int32).copy()).cuda()
+        bw = torch.from_numpy(np.packbits(b, bitorder="little").view(np.int32).copy()).cuda()
+        au = torch.empty(nwords * 32, dtype=torch.uint8, device="cuda")
+        bu = torch.empty_like(au)
+        _lib.check(L.syzcov_dev_bits_to_bytes(P(aw), nwords, P(au), s), "bits_to_bytes")
+        _lib.check(L.syzcov_dev_bits_to_bytes(P(bw), nwords, P(bu), s), "bits_to_bytes")
+        assert np.array_equal(au.cpu().numpy(), a.astype(np.uint8))
+        m = torch.maximum(au, bu * 7)  # any nonzero byte reads back as a set bit
+        out = torch.empty_like(aw)
+        _lib.check(L.syzcov_dev_bytes_to_bits(P(m), nwords, P(out), s), "bytes_to_bits")
+        exp = np.packbits(a | b, bitorder="little").view(np.int32)
+        assert np.array_equal(out.cpu().numpy(), exp), nwords
