@@ -484,6 +484,27 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
     dt, phl = timed(step, len(phases), a, 1, dev)
     ph = dict(zip(phases, phl))
     res = eng.result()
+    # every rank's part of the order (the phase's critical path is the slowest
+    # part): syzcov_dev_sort_order_part over the same lengths, part r of world
+    lens64 = glens.to(torch.int64)
+    wsz = L.syzcov_dev_sort_ws_size(N)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
+    po = torch.empty(N, dtype=torch.int32, device=dev)
+    part_ms = []
+    for r in range(world):
+        for rep in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.check(L.syzcov_dev_sort_order_part(C.c_void_p(lens64.data_ptr()), N, r, world,
+                                                    C.c_void_p(po.data_ptr()),
+                                                    C.c_void_p(ws.data_ptr()), wsz, s),
+                       "dev_sort_order_part")
+            e1.record()
+            torch.cuda.synchronize()
+            if rep:
+                part_ms.append((r, e0.elapsed_time(e1)))
+    order_parts = [round(min(t for q, t in part_ms if q == r), 4) for r in range(world)]
+    del lens64, ws, po
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
     alg = eng.alg_bytes(total, canon_pcs)
     cf = alg["canon"] / (ph["canon"] * 1e-3) / 1e9
@@ -513,6 +534,9 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
         # Minimize + union as the metric counts it: order + minimize + the
         # exchange phase's pass 2 + finish
         "minimize_union_ms": ph["order"] + ph["minimize"] + ph["exchange"] + ph["finish"],
+        # each rank's order part alone (device tier, this GPU): the slowest is
+        # the 8-GPU order phase's critical path
+        "order_part_ms_by_rank": order_parts,
         "collectives": {"bytes": coll, "ring_bytes_per_rank": int(ring),
                         "note": "not run on one GPU; the 8-GPU step adds their time"},
         "results": {"kept_local_first": res.n_kept, "union_local": res.n_union},

@@ -47,6 +47,9 @@ constexpr int SMALL = SYZ_GSORT_SMALL;  // segment finished in one workgroup's L
 #endif
 constexpr int TINY = SYZ_GSORT_TINY;  // leaf finished by one lane
 static_assert(TINY <= 64, "leaf pdqsort: BitStack holds 3 parked tasks of a <= 64-element leaf");
+#ifndef SYZ_GSORT_SPLIT_MUL
+#define SYZ_GSORT_SPLIT_MUL 4  // sharded order: split once >= this many large segments per part
+#endif
 constexpr int CH = 4096;     // elements per work item in the global rounds
 constexpr unsigned ITEM_GRID = 1024;  // workgroups looping over a round's work items
 constexpr int WG = 256;
@@ -997,7 +1000,7 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t pa
     bool exact = true;  // ncur is the device's count (a read-back), not a bound
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
-        if (!split && exact && ncur >= 4 * nparts) split_now(cur, ccount, ncur);
+        if (!split && exact && ncur >= SYZ_GSORT_SPLIT_MUL * nparts) split_now(cur, ccount, ncur);
         exact = false;
         // the children of this round go to nxt
         // (lead_kernel zeroes ncount / nmax)
