@@ -205,6 +205,42 @@ __device__ bool map_piece(const Args &A, uint32_t G, uint32_t P, uint32_t a, uin
     return true;
 }
 
+// The next piece for the calling workgroup (key-mode pass 1), XCD-LOCAL
+// SLICES: slice sl belongs to XCD sl mod 8 (workgroup b runs on XCD b mod 8,
+// the dispatcher's round robin), and an XCD's workgroups draw its slices'
+// pieces in slice order from its own counter (pctr[8x]), so the pieces of one
+// item slice (every range of the same items) run at the same time on one XCD.
+// The 128-byte line where an item's range-rho sub-run ends and its rho+1
+// sub-run starts is then read twice from that XCD's L2, not twice from HBM:
+// the range-major order (all workgroups on one range, the next range a whole
+// range's bytes later) fetched every such line twice, 1.70x the algorithmic
+// bytes of a C3/8 rank's Minimize; here 1.41x (C3 Minimize 21.5 -> 17.3 ms).
+// A workgroup whose XCD has no pieces left takes the other XCDs' (every piece
+// is drawn exactly once, so the assignment never affects the result).  The
+// price is a table restage at nearly every piece (the next piece is another
+// range), which the unrolled loads below keep to a few microseconds.
+// Returns G when every piece is drawn.  (SYZ_MR_RANGE_MAJOR: one counter,
+// range-major order.)
+__device__ uint32_t draw_piece(uint32_t *pctr, uint32_t G, uint32_t P, uint32_t *xdone) {
+    const uint32_t S = G / P;
+#ifdef SYZ_MR_RANGE_MAJOR
+    (void)xdone;
+    const uint32_t g = atomicAdd(pctr, 1u);
+    return g < G ? (g % S) * P + g / S : G;  // g = position * S + slice
+#else
+    const uint32_t me = blockIdx.x & 7u;
+    for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t x = (me + j) & 7u;
+        if (*xdone >> x & 1u) continue;
+        const uint32_t nk = x < S ? ((S - 1 - x) / 8 + 1) * P : 0u;  // XCD x's pieces
+        const uint32_t k = nk ? atomicAdd(pctr + 8 * x, 1u) : 0u;
+        if (k < nk) return (x + 8 * (k / P)) * P + k % P;
+        *xdone |= 1u << x;
+    }
+    return G;
+#endif
+}
+
 // Pass 1 as a CHUNK STREAM (first covers deferred to min_records_kernel).
 // A wave takes 64 items at a time and concatenates their sub-runs into one
 // list of 16-byte chunks (an exclusive scan of the per-item chunk counts;
@@ -522,16 +558,13 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     const uint32_t bmask = (1u << A.rshift) - 1u;
     uint32_t cur_rho = 0xFFFFFFFFu;
     uint32_t nonmem = 0;
+    uint32_t xdone = 0;  // (thread 0) XCDs whose slices are all drawn
     for (;;) {
-    if (threadIdx.x == 0) s_next = atomicAdd(A.pctr, 1u);
+    if (threadIdx.x == 0) s_next = draw_piece(A.pctr, G, P, &xdone);
     __syncthreads();
     uint32_t g = s_next;
     __syncthreads();
     if (g >= G) break;
-    {
-        const uint32_t S = G / P;  // range-major: g = position * S + slice
-        g = (g % S) * P + g / S;
-    }
     uint32_t rho, i0, i1;
     if (!map_piece(A, G, P, a, b, g, &rho, &i0, &i1, s_plan)) continue;
     if (N4 && rho != cur_rho) {  // nibbles: 8 keys per word from 8 bytes + a covered byte
@@ -539,16 +572,28 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
         const uint2 *t2 = reinterpret_cast<const uint2 *>(A.low_of_key + ((uint64_t)rho << A.rshift));
         const uint8_t *cb8 =
             reinterpret_cast<const uint8_t *>(A.covered) + (((uint64_t)rho << A.rshift) >> 3);
-        for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
-            const uint2 lb = t2[q];
-            const uint32_t unc = load_cov ? ~(uint32_t)cb8[q] : 0xFFu;
-            uint32_t x = 0;
+        constexpr uint32_t TL = 8;  // all of a thread's loads first (below)
+        for (uint32_t q0 = 0; q0 < nq; q0 += TL * THREADS) {
+            uint2 lb[TL];
+            uint32_t unc[TL];
 #pragma unroll
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t low = ((j < 4 ? lb.x >> (8 * j) : lb.y >> (8 * (j - 4)))) & 7u;
-                x |= (low | (((unc >> j) & 1u) << 3)) << (4 * j);
+            for (uint32_t u = 0; u < TL; u++) {
+                const uint32_t q = q0 + u * THREADS + threadIdx.x;
+                lb[u] = q < nq ? t2[q] : make_uint2(0, 0);
+                unc[u] = load_cov && q < nq ? ~(uint32_t)cb8[q] : 0xFFu;
             }
-            s_cov[q] = x;
+#pragma unroll
+            for (uint32_t u = 0; u < TL; u++) {
+                const uint32_t q = q0 + u * THREADS + threadIdx.x;
+                uint32_t x = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 8; j++) {
+                    const uint32_t low =
+                        ((j < 4 ? lb[u].x >> (8 * j) : lb[u].y >> (8 * (j - 4)))) & 7u;
+                    x |= (low | (((unc[u] >> j) & 1u) << 3)) << (4 * j);
+                }
+                if (q < nq) s_cov[q] = x;
+            }
         }
         cur_rho = rho;
         __syncthreads();
@@ -561,15 +606,29 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
         auto spread = [](uint32_t x) {  // bit i -> bit 8i + 7
             return ((x & 1u) << 7) | ((x & 2u) << 14) | ((x & 4u) << 21) | ((x & 8u) << 28);
         };
-        for (uint32_t q = threadIdx.x; q < nq; q += THREADS) {
-            uint4 t = t4[q];
-            const uint32_t ub =
-                load_cov ? ~(cw[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu : 0xFFFFu;
-            t.x |= spread(ub);
-            t.y |= spread(ub >> 4);
-            t.z |= spread(ub >> 8);
-            t.w |= spread(ub >> 12);
-            s4[q] = t;
+        // all of a thread's loads first (8 per thread at 2^17 keys): a piece
+        // change reloads the table, and a loop of dependent round trips made
+        // that a visible share of a 2 MB piece
+        constexpr uint32_t TL = 8;
+        for (uint32_t q0 = 0; q0 < nq; q0 += TL * THREADS) {
+            uint4 t[TL];
+            uint32_t cv[TL];
+#pragma unroll
+            for (uint32_t u = 0; u < TL; u++) {
+                const uint32_t q = q0 + u * THREADS + threadIdx.x;
+                t[u] = q < nq ? t4[q] : make_uint4(0, 0, 0, 0);
+                cv[u] = load_cov && q < nq ? cw[q >> 1] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < TL; u++) {
+                const uint32_t q = q0 + u * THREADS + threadIdx.x;
+                const uint32_t ub = ~(cv[u] >> ((q & 1) * 16)) & 0xFFFFu;
+                t[u].x |= spread(ub);
+                t[u].y |= spread(ub >> 4);
+                t[u].z |= spread(ub >> 8);
+                t[u].w |= spread(ub >> 12);
+                if (q < nq) s4[q] = t[u];
+            }
         }
         cur_rho = rho;
         __syncthreads();
@@ -1302,6 +1361,9 @@ static int minimize_range_impl(
 #ifndef SYZ_MR_PPS
 #define SYZ_MR_PPS 16
 #endif
+#ifndef SYZ_MR_KEYS_PPS  // key mode, XCD-local slices (draw_piece): 1/2/4/8 -> C3
+#define SYZ_MR_KEYS_PPS 2  // Minimize 19.3/17.3/18.3/19.3 ms, C3/8 rank 3.81/2.80/2.83/3.05
+#endif
     if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << SYZ_MR_HINT_LOG;
     const uint64_t g_min = 256;     // at least one workgroup per CU
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
@@ -1326,10 +1388,10 @@ static int minimize_range_impl(
             const uint64_t b = std::min<uint64_t>(a1, a + step);
             // about pcs_per_wg_hint PCs per workgroup, at least one CU's worth;
             // P = 16R pieces per slice (fewer, larger pieces in the small chunks,
-            // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2)
+            // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2); key mode 2R
             uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
             G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
-            const uint64_t P = SYZ_MR_PPS * (uint64_t)nrange;  // pieces per slice
+            const uint64_t P = (keym ? SYZ_MR_KEYS_PPS : SYZ_MR_PPS) * (uint64_t)nrange;
             G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
             // dynamic pieces: one workgroup per CU draws them
             if (nchunk >= MR_MAX_CHUNKS) return SYZCOV_EINVAL;
