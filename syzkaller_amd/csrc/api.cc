@@ -52,6 +52,8 @@ uint32_t force_flags() {
     if (strstr(e, "mr_bytes")) f |= FORCE_MR_BYTES;
     if (strstr(e, "nc_hash64")) f |= FORCE_NC_HASH64;
     if (strstr(e, "min_atomics")) f |= FORCE_MIN_ATOMICS;
+    if (strstr(e, "no_init_block")) f |= FORCE_NO_INIT_BLOCK;
+    if (strstr(e, "small_init")) f |= FORCE_SMALL_INIT;
     return f;
 }
 

@@ -14,6 +14,8 @@ enum : uint32_t {
     FORCE_MR_BYTES = 64u,      // corpus key mode, kshift <= 2: byte tables, not nibbles
     FORCE_NC_HASH64 = 128u,    // newcov ownership: u64 keys + separate values, not packed slots
     FORCE_MIN_ATOMICS = 256u,  // corpus key mode: min_records' atomics, not bucketed first covers
+    FORCE_NO_INIT_BLOCK = 512u,  // corpus key mode: chunks from item 0, no initial LDS block
+    FORCE_SMALL_INIT = 1024u,    // corpus key mode: an initial block of one first chunk (tests)
 };
 uint32_t force_flags();
 }  // namespace syz

@@ -816,6 +816,259 @@ __global__ __launch_bounds__(THREADS) void pass1_keys_kernel(Args A, uint32_t a,
     }
 }
 
+// ---- The initial block: exact first covers of items [a, a + K) in LDS.
+// The geometric chunks start small because every uncovered occurrence of a
+// chunk becomes a record, and at the start nearly every occurrence is
+// uncovered: at a C3/8 rank the first five chunks (21.8 K items, 1.7 % of
+// the bytes) took 0.47 ms of pass 1 + rec_scatter + bmin, ~17 % of its
+// Minimize.  Nothing precedes the block, so a key's first cover there is the
+// minimum item holding it, which a min table finds without records:
+// init_min_kernel: workgroup (piece, q) streams the range-rho sub-runs of
+// one part of the block's items (pass1_keys_kernel's chunk stream; a range
+// gets parts in proportion to its key count, plan_pieces) and keeps, for
+// each key of part q of the range (2^IQ_SH keys, 128 KB of u32),
+// min((item - a) << 7 | low bits) in LDS.  An entry starts as
+// (INIT_NONE << 7) | low_of_key, so a word whose low bits differ from its
+// entry's is not a universe PC (SYZCOV_ERR_UNIVERSE, as pass 1).  The parts
+// of a range meet in the scratch table tab[key] by a global atomicMin per
+// held key.  The q parts of one range read the same sub-runs: they and the
+// neighbouring ranges run on one XCD (workgroup b on XCD b mod 8), so the
+// re-reads are L2 hits.
+// init_flush_kernel: per key, tab's minimum is the key's first cover ->
+// first_w, the covered words, and ONE record (rank, key) per covered
+// key, pass 2's evidence (kept(r) <=> first(k) == r for some key k; across
+// shards, a key's global first cover on this shard is its local one).  A
+// record that finds its region full flags its item as a candidate (the
+// overflow fallback rescans candidates), as in pass 1.
+constexpr uint32_t IQ_SH = 15;             // keys per init table: 2^15 u32 (128 KB)
+constexpr uint32_t INIT_NONE = 0xFFFFFFu;  // entry >> 7 of a key no item of the block holds
+constexpr size_t INIT_LDS_EXTRA = NWAVE * 64 * (8 + 3 * 4) + (MAX_R + 2) * 4;
+
+template <int UG>
+__global__ __launch_bounds__(THREADS) void init_min_kernel(Args A, uint32_t a, uint32_t K, uint32_t P,
+                                                           uint32_t *__restrict__ tab) {
+    constexpr uint32_t CW = 8;  // words per lane chunk
+    extern __shared__ uint32_t s_tab[];  // 2^IQ_SH entries at LDS 0, then the wave descriptors
+    auto *s_a0 = reinterpret_cast<uint64_t(*)[64]>(
+        reinterpret_cast<uint8_t *>(s_tab) + ((size_t)4 << IQ_SH));
+    auto *s_he = reinterpret_cast<uint32_t(*)[64]>(s_a0 + NWAVE);  // (end << 3) | head
+    auto *s_ex = s_he + NWAVE;                                     // first chunk of the item
+    auto *s_own = s_ex + NWAVE;                                    // item + 1 per chunk
+    uint32_t *s_plan = reinterpret_cast<uint32_t *>(s_own + NWAVE);
+    // workgroup -> (piece, part q of the range's keys); the pieces of a range
+    // and its neighbours' on one XCD
+    const uint32_t nq = 1u << (A.rshift - IQ_SH);
+    uint32_t idx = blockIdx.x;
+    if ((gridDim.x & 7u) == 0) idx = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const uint32_t pi = idx / nq, q = idx % nq;
+    // P pieces over the ranges by their key counts (plan_pieces): range j's
+    // items are cut into p_j parts (one range per workgroup took 6.1 ms for
+    // 87 K items, the hot ranges' workgroups alone)
+    plan_pieces(A, 0, P, s_plan);
+    if (pi >= s_plan[A.nrange]) return;
+    uint32_t rho = 0, hi_ = A.nrange;  // largest j with sh[j] <= pi
+    while (hi_ - rho > 1) {
+        const uint32_t mid = (rho + hi_) >> 1;
+        if (s_plan[mid] <= pi) rho = mid; else hi_ = mid;
+    }
+    const uint32_t parts = s_plan[rho + 1] - s_plan[rho], part = pi - s_plan[rho];
+    const uint32_t k0 = (rho << A.rshift) + (q << IQ_SH);  // the table's first key
+    s_own[threadIdx.x >> 6][__lane_id()] = 0u;
+    {  // entries (INIT_NONE << 7) | low, 16 keys per 16-byte load
+        const uint4 *lk = reinterpret_cast<const uint4 *>(A.low_of_key + k0);
+        for (uint32_t i = threadIdx.x; i < (1u << IQ_SH) / 16; i += THREADS) {
+            const uint4 v = lk[i];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            uint4 *d = reinterpret_cast<uint4 *>(s_tab + 16 * i);
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                d[j] = make_uint4(INIT_NONE << 7 | (w4[j] & 0xFFu), INIT_NONE << 7 | (w4[j] >> 8 & 0xFFu),
+                                  INIT_NONE << 7 | (w4[j] >> 16 & 0xFFu), INIT_NONE << 7 | (w4[j] >> 24));
+        }
+    }
+    __syncthreads();
+    const uint32_t i0 = a + (uint32_t)((uint64_t)K * part / parts),
+                   i1 = a + (uint32_t)((uint64_t)K * (part + 1) / parts);
+    const uint32_t bmask = (1u << A.rshift) - 1u, qoff = q << IQ_SH;
+    uint32_t nonmem = 0;
+    const uint32_t l = __lane_id();
+    const uint32_t w = wave_readfirstlane(threadIdx.x >> 6);
+    const uint32_t per = (i1 - i0 + NWAVE - 1) / NWAVE;
+    const uint32_t w0 = i0 + w * per, w1 = min(i1, w0 + per);
+    uint32_t d_s0 = 0, d_s1 = 0;
+    uint64_t d_base = 0;
+    auto load_desc = [&](uint32_t ib_) {
+        const uint32_t item = ib_ + l;
+        d_s0 = d_s1 = 0;
+        d_base = 0;
+        if (item < w1) {
+            d_s1 = A.split_t[(uint64_t)rho * A.n_items + item];
+            d_s0 = rho ? A.split_t[(uint64_t)(rho - 1) * A.n_items + item] : 0u;
+            d_base = A.base_r[item];
+        }
+    };
+    if (w0 < w1) load_desc(w0);
+    for (uint32_t ib = w0; ib < w1; ib += 64) {
+        const uint32_t item = ib + l;
+        uint32_t m = 0, nch = 0, he = 0;
+        uint64_t a0 = 0;
+        if (item < w1) {
+            const uint64_t st = d_base + aligned_sub(d_s0, rho, A.ak);
+            m = d_s1 - d_s0;
+            a0 = st & ~7ull;
+            const uint32_t head = (uint32_t)(st - a0);
+            he = ((head + m) << 3) | head;
+            nch = m ? (head + m + CW - 1) / CW : 0u;
+        }
+        if (ib + 64 < w1) load_desc(ib + 64);
+        const uint32_t incl = wave_incl_scan(nch);
+        const uint32_t ex_l = incl - nch;
+        const uint32_t tot = wave_readlane(incl, 63);
+        s_a0[w][l] = a0;
+        s_he[w][l] = he;
+        s_ex[w][l] = ex_l;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t sj = 0;
+        uint4 v0[UG], v1[UG];
+        uint32_t cj[UG], co[UG], hv[UG];
+        auto issue = [&](uint32_t c0, uint4 (&d0)[UG], uint4 (&d1)[UG], uint32_t (&dj)[UG],
+                         uint32_t (&dc)[UG], uint32_t (&dh)[UG]) {
+            uint32_t jj[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t cb = c0 + u * 64;
+                const uint32_t c = cb + l;
+                if (ex_l - cb < 64u) atomicMax(&s_own[w][ex_l - cb], l + 1u);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t mk = s_own[w][l];
+                s_own[w][l] = 0u;
+                const uint32_t pm = wave_incl_max(mk);
+                const uint32_t j = pm ? max(sj, pm - 1u) : sj;
+                sj = wave_readlane(j, 63);
+                jj[u] = j;
+                dj[u] = c < tot ? j : 64u;
+            }
+            uint64_t ba[UG];
+            uint32_t bx[UG];
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                ba[u] = s_a0[w][jj[u]];
+                bx[u] = s_ex[w][jj[u]];
+                dh[u] = s_he[w][jj[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t c = c0 + u * 64 + l;
+                dc[u] = dj[u] < 64 ? c - bx[u] : 0u;  // past the end: chunk 0, never used
+                const uint4 *p = reinterpret_cast<const uint4 *>(A.pcs + ba[u]) + 2 * dc[u];
+                d0[u] = p[0];
+                d1[u] = p[dc[u] * CW + 4 < (dh[u] >> 3) ? 1 : 0];
+            }
+        };
+        issue(0, v0, v1, cj, co, hv);
+        for (uint32_t c0 = 0; c0 < tot; c0 += 64 * UG) {
+            uint4 n0[UG], n1[UG];
+            uint32_t nj[UG], nc[UG], nh[UG];
+            issue(c0 + 64 * UG, n0, n1, nj, nc, nh);
+            const uint32_t bm = issue_fence(bmask);
+            // every table read unconditional and issued together (a read or
+            // an atomic under a per-element branch waits for each LDS access,
+            // and for every outstanding load, in turn): entries at a clamped
+            // index, then the element tests; a lower value than the entry's
+            // (the first items of a key, rare past the start) takes ds_min on
+            // a wave-uniform slow path.  The read first also spares the hot
+            // keys (in nearly every item) whole wave instructions of ds_min
+            // serialised on one address.
+            uint32_t wd[UG * CW], tb[UG * CW], vl[UG * CW];
+            uint32_t need = 0;
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                const uint32_t vv[CW] = {v0[u].x, v0[u].y, v0[u].z, v0[u].w,
+                                         v1[u].x, v1[u].y, v1[u].z, v1[u].w};
+#pragma unroll
+                for (int k = 0; k < (int)CW; k++) {
+                    wd[u * CW + k] = (vv[k] & bm) - qoff;
+                    tb[u * CW + k] = s_tab[wd[u * CW + k] & ((1u << IQ_SH) - 1u)];
+                }
+                // element k of the lane's chunk is in its sub-run iff lo <= k < hi
+                const int lo = (int)(hv[u] & 7u) - (int)(co[u] * CW);
+                const int hi = cj[u] < 64 ? (int)(hv[u] >> 3) - (int)(co[u] * CW) : lo;
+                const uint32_t lr = ib + cj[u] - a;  // the item, block-relative
+#pragma unroll
+                for (int k = 0; k < (int)CW; k++) {
+                    const uint32_t lw = vv[k] >> SYZ_KEY_BITS, v = lr << 7 | lw;
+                    const uint32_t in = (uint32_t)(k >= lo) & (uint32_t)(k < hi) &
+                                        (uint32_t)(wd[u * CW + k] < (1u << IQ_SH));
+                    nonmem |= in & (uint32_t)((tb[u * CW + k] & 0x7Fu) != lw);
+                    need |= (in & (uint32_t)(v < tb[u * CW + k])) << (u * CW + k);
+                    vl[u * CW + k] = v;
+                }
+            }
+            if (__ballot(need != 0)) {
+#pragma unroll
+                for (int j = 0; j < UG * (int)CW; j++)
+                    if ((need >> j) & 1u) atomicMin(&s_tab[wd[j]], vl[j]);
+            }
+#pragma unroll
+            for (int u = 0; u < UG; u++) {
+                v0[u] = n0[u];
+                v1[u] = n1[u];
+                cj[u] = nj[u];
+                co[u] = nc[u];
+                hv[u] = nh[u];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (__ballot(nonmem) && __lane_id() == 0) atomicOr(A.err, SYZCOV_ERR_UNIVERSE);
+    __syncthreads();
+    // the parts of a range meet in tab (all ones before the kernel)
+    for (uint32_t i = threadIdx.x; i < (1u << IQ_SH); i += THREADS) {
+        const uint32_t e = s_tab[i];
+        if ((e >> 7) != INIT_NONE) atomicMin(&tab[k0 + i], e);
+    }
+}
+
+__global__ __launch_bounds__(256) void init_flush_kernel(Args A, uint32_t a,
+                                                         const uint32_t *__restrict__ tab, uint64_t T,
+                                                         uint64_t span) {
+    const uint32_t region = blockIdx.x % NCTR;
+    unsigned long long *const rctr = A.ctr + region * CTR_STRIDE;
+    unsigned long long *const rrec = A.rec + region * A.cap_k;
+    uint32_t *const covered = const_cast<uint32_t *>(A.covered);
+    const uint32_t l = __lane_id();
+    for (uint64_t key = (uint64_t)blockIdx.x * 256 + threadIdx.x; key - threadIdx.x < T;
+         key += (uint64_t)gridDim.x * 256) {
+        const uint32_t lr = key < T ? tab[key] >> 7 : INIT_NONE;
+        const bool has = key < span && lr < INIT_NONE;  // (past the span: flagged by init_min)
+        const int32_t rank = has ? (A.ranks ? A.ranks[a + lr] : (int32_t)(a + lr)) : INT32_MAX;
+        if (key < span) A.first_w[key] = rank;
+        const uint64_t m = __ballot(has);
+        if ((l & 31) == 0 && key < T) covered[key >> 5] = (uint32_t)(m >> (l & 32));
+        if (m) {  // one reservation per wave
+            unsigned long long b0 = 0;
+            if (l == 0) b0 = atomicAdd(rctr, (unsigned long long)__popcll(m));
+            b0 = __shfl(b0, 0, 64);
+            if (has) {
+                const uint64_t slot = b0 + __popcll(m & ((1ull << l) - 1ull));
+                if (slot < A.cap_k)
+                    rrec[slot] = (unsigned long long)(uint32_t)rank << 32 | (uint32_t)key;
+                else
+                    A.cand[a + lr] = 1;  // no room: the overflow fallback rescans the item
+            }
+        }
+    }
+}
+
+// the first chunk's records start after the block's: done marks (parity 0) = ctr
+__global__ void init_done_kernel(Args A) {
+    const uint32_t k = threadIdx.x;
+    if (k < NCTR) A.done[k * CTR_STRIDE] = std::min<uint64_t>(A.ctr[k * CTR_STRIDE], A.cap_k);
+}
+
 // Manager.minimizeCorpus (syz-manager/manager.go:504-524) when every call
 // group is small: per group, exact first covers in LDS, with no chunks and
 // no records.  Piece (g, rho): a workgroup streams the range-rho sub-runs of
@@ -1380,7 +1633,7 @@ static int minimize_range_impl(
         A.rsort = (unsigned long long *)rsort;
     }
     // pass 1 over the items [a0, a1) in geometric chunks (covered empty at a0)
-    auto run_span = [&](uint64_t a0, uint64_t a1, uint64_t step0) -> int {
+    auto run_span = [&](uint64_t a0, uint64_t a1, uint64_t step0, bool cov0) -> int {
         uint64_t a = a0, step = step0;
         int par = 0;  // done-mark set of this chunk
         uint32_t nchunk = 0;
@@ -1403,7 +1656,7 @@ static int minimize_range_impl(
             mr::Args A1 = A;  // pass 1 counts this chunk's records per bucket
             if (bucketed) A1.bh = A.bh + par * A.nb;
             hipLaunchKernelGGL(k1, dim3(grid), dim3(mr::THREADS), lds1, s, A1, (uint32_t)a,
-                               (uint32_t)b, (uint32_t)P, (int)(a != a0));
+                               (uint32_t)b, (uint32_t)P, (int)(a != a0 || cov0));
             if (bucketed) {
                 // the chunk's first covers and covered words, bucket by bucket
                 hipLaunchKernelGGL(mr::rec_scatter_kernel, dim3(1024), dim3(256), 0, s, A, par);
@@ -1441,7 +1694,7 @@ static int minimize_range_impl(
             if (g) SYZ_HIP(hipMemsetAsync(ws, 0, MR_HDR, s));  // region counters, done marks
             if (!cover_from_first)
                 SYZ_HIP(hipMemsetAsync(covered, 0, (((uint64_t)nrange << range_shift) + 7) / 8, s));
-            RC_(run_span(a0, a1, 256));
+            RC_(run_span(a0, a1, 256, false));
             hipLaunchKernelGGL(mr::pass2_kernel, dim3(1024), dim3(256), 0, s, A,
                                (const uint64_t *)nullptr, (const int32_t *)nullptr, kept);
             hipLaunchKernelGGL(mr::ovf_pass2_kernel, dim3(1024), dim3(256), 0, s, A, A.n_items,
@@ -1456,7 +1709,44 @@ static int minimize_range_impl(
         SYZ_HIP(hipMemsetAsync(covered, 0, (((uint64_t)nrange << range_shift) + 7) / 8, s));
         return 0;
     }
-    RC_(run_span(0, n_items, first_chunk));
+    // the initial block (init_min_kernel): the first SYZ_MR_INIT_CHUNKS chunks'
+    // items, exact first covers in LDS; the chunks go on from there
+#ifndef SYZ_MR_INIT_CHUNKS
+#define SYZ_MR_INIT_CHUNKS 4
+#endif
+    uint64_t k_init = 0, step0 = first_chunk;
+    const int init_chunks = force_flags() & FORCE_SMALL_INIT ? 1 : SYZ_MR_INIT_CHUNKS;
+    for (int c = 0; c < init_chunks; c++) {
+        k_init += step0;
+        step0 *= growth;
+    }
+    const uint64_t T = nrange << range_shift;  // keys of the tables (covered bits)
+    const uint64_t nq = range_shift >= mr::IQ_SH ? 1ull << (range_shift - mr::IQ_SH) : 0;
+    const bool init = bucketed && nq && k_init > 0 && T * 4 <= rec_cap * 8 &&
+                      nrange <= mr::MAX_R && !(force_flags() & FORCE_NO_INIT_BLOCK);
+    if (init) {
+        k_init = std::min<uint64_t>(k_init, n_items);
+        static std::atomic<uint32_t> init_attr{0};
+        const size_t lds_i = ((size_t)4 << mr::IQ_SH) + mr::INIT_LDS_EXTRA;
+        if ((rc = set_dyn_lds_once((const void *)mr::init_min_kernel<2>, (uint32_t)lds_i, init_attr)))
+            return rc;
+        // pieces: every workgroup slot of the GPU, at least one per range
+#ifndef SYZ_MR_INIT_WG
+#define SYZ_MR_INIT_WG 1  // workgroups per CU
+#endif
+        const uint64_t P = std::max<uint64_t>(nrange, (SYZ_MR_INIT_WG * dev_cus() + nq - 1) / nq);
+        uint32_t *tab = (uint32_t *)rsort;  // free until the first chunk's rec_scatter
+        SYZ_HIP(hipMemsetAsync(tab, 0xFF, T * 4, s));
+        hipLaunchKernelGGL(mr::init_min_kernel<2>, dim3((unsigned)(nq * P)), dim3(mr::THREADS),
+                           lds_i, s, A, 0u, (uint32_t)k_init, (uint32_t)P, tab);
+        hipLaunchKernelGGL(mr::init_flush_kernel, dim3((unsigned)std::min<uint64_t>(
+                               std::max<uint64_t>(T / 256, mr::NCTR), 4096)),
+                           dim3(256), 0, s, A, 0u, (const uint32_t *)tab, T, pc_span);
+        hipLaunchKernelGGL(mr::init_done_kernel, dim3(1), dim3(64), 0, s, A);
+        RC_(run_span(k_init, n_items, step0, true));
+    } else {
+        RC_(run_span(0, n_items, first_chunk, false));
+    }
     if (cover_from_first && !bucketed) RC_(syzcov_dev_first_to_bits(first_w, pc_span, covered, s));
     // record overflow: the union comes from first_w instead (cover_from_first
     // already rebuilt covered from first_w)

@@ -42,11 +42,18 @@ def test_keymap_roundtrip(torch):
         universe_keymap(np.array([5, 3], np.uint32), "cuda")
 
 
+@pytest.mark.parametrize("force", ["", "small_init", "no_init_block"],
+                         ids=["init-block", "init-64", "chunks-only"])
 @pytest.mark.parametrize("layout", [0, 1], ids=["csr", "aligned"])
 @pytest.mark.parametrize("n,mean,sigma,log2", [(4000, 2048, 512, 22), (3000, 300, 200, 12),
                                                (500, 9000, 6000, 20), (2000, 600, 300, 17),
                                                (3000, 1500, 900, 19)])
-def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2, layout):
+def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2, layout, force, monkeypatch):
+    """Key-mode steps against the oracle (cover.go:28-40, 104-131).  Minimize's
+    first items go through the initial LDS block (every item at these sizes),
+    a one-chunk block followed by geometric chunks (small_init), or chunks
+    only (no_init_block)."""
+    monkeypatch.setenv("SYZCOV_FORCE", force)
     from syzkaller_amd.engine import CorpusEngine, synth_corpus, synth_universe, synth_window
     seed = 0x5EED0002
     off, raw, lens, total = synth_corpus(n, seed, mean=mean, sigma=sigma, log2_space=log2)
@@ -74,7 +81,8 @@ def test_engine_key_mode_vs_oracle(torch, n, mean, sigma, log2, layout):
     assert np.array_equal(res2.union.cpu().numpy().view(np.uint32), exp_union)
 
 
-@pytest.mark.parametrize("force", ["", "mr_bytes"], ids=["nibbles", "bytes"])
+@pytest.mark.parametrize("force", ["", "mr_bytes", "small_init", "mr_bytes,small_init"],
+                         ids=["nibbles", "bytes", "nibbles-init-64", "bytes-init-64"])
 def test_engine_key_mode_x86_vs_oracle(torch, force, monkeypatch):
     """The x86-like universe (PC pairs per 16-byte block, kshift 2): Minimize's
     tables are nibbles over 2^18 keys (every low value fits 2 bits) or, with
@@ -90,7 +98,7 @@ def test_engine_key_mode_x86_vs_oracle(torch, force, monkeypatch):
     lo, span = synth_window(log2, x86=True)
     off, raw, lens, total = synth_corpus(n, seed, mean=1200, sigma=500, log2_space=log2, x86=True)
     eng = CorpusEngine(n, total, int(lens.max().item()), lo, span, universe=u)
-    assert eng.kshift == 2 and eng.nrange == (4 if not force else 8)
+    assert eng.kshift == 2 and eng.nrange == (8 if "mr_bytes" in force else 4)
     exp_kept, exp_union = _oracle_of(off, raw, n)
     res = eng.step(off, raw, n)
     assert not res.fallback
