@@ -741,6 +741,11 @@ constexpr uint32_t FG_MAX = 4096;  // slices
 #define SYZ_NC_FU 4
 #endif
 constexpr int FU = SYZ_NC_FU;  // rows per step of the fused pass (two steps in flight)
+#ifndef SYZ_NC_CBD
+#define SYZ_NC_CBD 4
+#endif
+constexpr int CBD = SYZ_NC_CBD;  // candidate buffer rows per wave (fused pass): 1/4/8 ->
+                                 // early-regime fused pass 1083/774/850 us per batch
 
 // The ranges' row offsets (row_offsets_kernel's qoff), the segment starts in
 // the row stream, flat s = q * nc + c: segb[q * (nc + 1) + c] = qoff[q] +
@@ -852,26 +857,40 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
     };
     uint4 my = make_uint4(0, 0, 0, 0);
     uint32_t nrow = 0, p0v = 0, obase = 0, w1 = 0;
-    uint32_t cbk = 0, cbp = 0, ncb = 0;  // candidate buffer: lane j < ncb holds the j-th
+    // candidate buffer, CBD rows of 64: the j-th candidate sits in lane j % 64
+    // of row j / 64, so a wave appends to the batch's list (one atomic on one
+    // counter for the whole GPU) once per up to 64 CBD candidates: in the
+    // early regime (~8 M candidates per batch) one append per 64 serialised
+    // ~120 K atomics on that address
+    uint32_t cbk[CBD], cbp[CBD], ncb = 0;
     auto flush = [&]() {
         uint32_t base = 0;
         if (l == 0) base = atomicAdd(&stats[1], ncb);
         base = wave_readfirstlane(base);
-        if (l < ncb) clist[base + l] = make_uint2(cbk, cbp);
+#pragma unroll
+        for (int d = 0; d < CBD; d++)
+            if (d * 64 + l < ncb) clist[base + d * 64 + l] = make_uint2(cbk[d], cbp[d]);
         ncb = 0;
     };
     auto emit = [&](uint64_t m, uint32_t k, uint32_t pc) {
         const uint32_t n = (uint32_t)__popcll(m);
-        if (ncb + n > 64) flush();
+        if (ncb + n > 64u * CBD) flush();
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const bool cand = (m >> l) & 1u;
-        const uint32_t dst = cand ? ncb + rank : (ncb + n + (l - rank)) & 63u;
+        // a bijection on the lanes: candidates to the lanes of slots ncb.., the
+        // others to the rest
+        const uint32_t dst = (cand ? ncb + rank : ncb + n + (l - rank)) & 63u;
         const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)k);
         const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4u), (int)pc);
-        const bool in = l - ncb < n;
-        cbk = in ? pk : cbk;
-        cbp = in ? pp : cbp;
+        const uint32_t off = (l - ncb) & 63u;  // this lane's slot ncb + off, if off < n
+        const uint32_t row = (ncb + off) >> 6;
+#pragma unroll
+        for (int d = 0; d < CBD; d++) {
+            const bool here = off < n && row == (uint32_t)d;
+            cbk[d] = here ? pk : cbk[d];
+            cbp[d] = here ? pp : cbp[d];
+        }
         ncb += n;
     };
     auto rows64 = [&](uint32_t rb_) {

@@ -79,6 +79,8 @@ for step in "$@"; do
         { tail -20 $o/trace.log; exit 1; }
     python3 tools/trace_summary.py $o/trace > $o/trace_summary.txt; head -30 $o/trace_summary.txt
     [ -n "$TL_MARK" ] && python3 tools/trace_timeline.py $o/trace "$TL_MARK" > $o/timeline.txt
+    # TL_LAST="KERNEL N": per-step kernel times of the last N steps (trace_last.py)
+    [ -n "$TL_LAST" ] && python3 tools/trace_last.py $o/trace $TL_LAST > $o/last.txt && head -8 $o/last.txt
     find $o/trace -name '*kernel_trace.csv' -delete
     ;;
   kbench:*)
