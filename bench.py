@@ -108,6 +108,9 @@ def parse():
                     help="N=1: skip the c3_rank_of_8 sub-record (rank 0's share of C3 over 8 GPUs)")
     ap.add_argument("--rank-share-only", action="store_true",
                     help="run only the c3_rank_of_8 leg and print it (a probe)")
+    ap.add_argument("--no-order-parts", action="store_true",
+                    help="c3_rank_of_8 without the per-rank order parts timed after its steps "
+                         "(profiles: the counters then cover the step alone)")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group, run no workload (a check of "
                          "the --gpus N launcher; runs on a host without a GPU)")
@@ -491,7 +494,7 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
     ws = torch.empty(wsz, dtype=torch.uint8, device=dev)
     po = torch.empty(N, dtype=torch.int32, device=dev)
     part_ms = []
-    for r in range(world):
+    for r in range(0 if getattr(args, "no_order_parts", False) else world):
         for rep in range(3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -503,7 +506,8 @@ def rank_share_run(args, dev, world: int = 8, rank: int = 0, glob: int = C3_INPU
             torch.cuda.synchronize()
             if rep:
                 part_ms.append((r, e0.elapsed_time(e1)))
-    order_parts = [round(min(t for q, t in part_ms if q == r), 4) for r in range(world)]
+    order_parts = [round(min(t for q, t in part_ms if q == r), 4)
+                   for r in range(world)] if part_ms else None
     del lens64, ws, po
     canon_pcs = int(eng.new_len[:n].to(torch.int64).sum().item())
     alg = eng.alg_bytes(total, canon_pcs)

@@ -40,9 +40,9 @@ if has corpus; then
   pmc_pair C2X "" "" $B --global-inputs 1000000 --x86 --steps 1 --warmup 0
 fi
 if has rank; then  # the 8-GPU step's per-rank share (its timed step: the last bin_kernel on)
-  trace C3R8 $B --rank-share-only --steps 5 --warmup 2
+  trace C3R8 $B --rank-share-only --no-order-parts --steps 5 --warmup 2
   python3 tools/trace_timeline.py $o/C3R8_trace bin_kernel 0 > $o/C3R8_timeline.txt
-  pmc_pair C3R8 bin_kernel 1 $B --rank-share-only --steps 1 --warmup 0
+  pmc_pair C3R8 bin_kernel 1 $B --rank-share-only --no-order-parts --steps 1 --warmup 0
 fi
 if has canon; then
   i=0

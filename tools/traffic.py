@@ -22,6 +22,8 @@ PHASES = {
     "minimize": ("prep_kernel", "pass1_kernel", "pass1_stream_kernel", "pass1_keys_kernel",
                  "min_records_kernel", "group_min_kernel",
                  "cover_records_kernel", "first_to_bits_kernel",
+                 "rec_scatter_kernel", "bmin_kernel", "init_min_kernel", "init_flush_kernel",
+                 "init_done_kernel",
                  "pass2_kernel", "ovf_", "reset_kernel", "total_kernel"),
     "newcov": ("newcov_", "hash_clear_kernel", "grp_hist", "grp_scan", "grp_scatter", "nc_zero",
                "range_sum", "range_scan", "item_scan", "row_offsets", "desc_kernel", "row_fill",
