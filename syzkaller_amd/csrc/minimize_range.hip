@@ -143,9 +143,39 @@ __global__ __launch_bounds__(256) void prep_kernel(Args A, uint64_t *base_r, uin
         if (!A.split) {  // one range: the column is the canonical length
             if (threadIdx.x < rows) split_t[t0 + threadIdx.x] = A.len[s_seg[threadIdx.x]];
         } else {
-            for (uint32_t e = threadIdx.x; e < rows * R; e += blockDim.x) {
-                const uint32_t r = e / R, c = e - r * R;
-                s_tile[r * ld + c] = A.split[(uint64_t)s_seg[r] * R + c];
+            if ((R & 3u) == 0 && ((uintptr_t)A.split & 15u) == 0) {
+                // 16-byte pieces of the rows, every load of the tile issued
+                // before the LDS stores (a load-store loop waited on each
+                // load in turn: 112 us for a C3/8 rank's 1.25 M items)
+                const uint32_t R4 = R >> 2, ne = rows * R4;
+                constexpr uint32_t PB = 4;
+                for (uint32_t e0 = 0; e0 < ne; e0 += PB * 256) {
+                    uint4 v[PB];
+#pragma unroll
+                    for (uint32_t u = 0; u < PB; u++) {
+                        const uint32_t e = e0 + u * 256 + threadIdx.x;
+                        const uint32_t r = e / R4, c4 = e - r * R4;
+                        v[u] = e < ne ? reinterpret_cast<const uint4 *>(A.split + (uint64_t)s_seg[r] * R)[c4]
+                                      : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < PB; u++) {
+                        const uint32_t e = e0 + u * 256 + threadIdx.x;
+                        const uint32_t r = e / R4, c = (e - r * R4) * 4;
+                        if (e < ne) {
+                            uint32_t *d = s_tile + r * ld + c;
+                            d[0] = v[u].x;
+                            d[1] = v[u].y;
+                            d[2] = v[u].z;
+                            d[3] = v[u].w;
+                        }
+                    }
+                }
+            } else {
+                for (uint32_t e = threadIdx.x; e < rows * R; e += blockDim.x) {
+                    const uint32_t r = e / R, c = e - r * R;
+                    s_tile[r * ld + c] = A.split[(uint64_t)s_seg[r] * R + c];
+                }
             }
             __syncthreads();
             for (uint32_t e = threadIdx.x; e < 64 * R; e += blockDim.x) {
@@ -1743,7 +1773,10 @@ static int minimize_range_impl(
                                std::max<uint64_t>(T / 256, mr::NCTR), 4096)),
                            dim3(256), 0, s, A, 0u, (const uint32_t *)tab, T, pc_span);
         hipLaunchKernelGGL(mr::init_done_kernel, dim3(1), dim3(64), 0, s, A);
-        RC_(run_span(k_init, n_items, step0, true));
+#ifndef SYZ_MR_POST_INIT_MUL
+#define SYZ_MR_POST_INIT_MUL 1
+#endif
+        RC_(run_span(k_init, n_items, step0 * SYZ_MR_POST_INIT_MUL, true));
     } else {
         RC_(run_span(0, n_items, first_chunk, false));
     }
