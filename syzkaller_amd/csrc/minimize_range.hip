@@ -1764,7 +1764,11 @@ static int minimize_range_impl(
 #ifndef SYZ_MR_INIT_WG
 #define SYZ_MR_INIT_WG 1  // workgroups per CU
 #endif
-        const uint64_t P = std::max<uint64_t>(nrange, (SYZ_MR_INIT_WG * dev_cus() + nq - 1) / nq);
+        // pieces: every workgroup slot of the GPU, at least two per range (at
+        // one per range the hot ranges are not split: C2X, 8 key parts per
+        // range, P = R: Minimize 3.40 ms; P = 2R 2.73; no block 2.89)
+        const uint64_t P =
+            std::max<uint64_t>(2 * nrange, (SYZ_MR_INIT_WG * dev_cus() + nq - 1) / nq);
         uint32_t *tab = (uint32_t *)rsort;  // free until the first chunk's rec_scatter
         SYZ_HIP(hipMemsetAsync(tab, 0xFF, T * 4, s));
         hipLaunchKernelGGL(mr::init_min_kernel<2>, dim3((unsigned)(nq * P)), dim3(mr::THREADS),
