@@ -994,10 +994,21 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t pa
     // (≈5 µs a round against ≈50 µs of host turnaround per read-back; a
     // pipelined read-back, the next rounds queued behind an event before the
     // host waits, measured slower: its bounds are a batch older).
+    // The first SYNC_EVERY-round batches hold the long rounds; past them the
+    // rounds are short and few are left, and a batch of 8 queued past the
+    // last large segment cost ~8 x 4 dispatches of ~7 us each (a C3/8 rank:
+    // ~0.23 ms of empty rounds), so the tail reads back every SYNC_TAIL.
     constexpr int SYNC_EVERY = 8;  // 4 and 16 measured no faster
+#ifndef SYZ_GSORT_SYNC_TAIL
+#define SYZ_GSORT_SYNC_TAIL 2  // 1 / 2 / 4 / 8: C3/8 rank order 1.57 / 1.55 / 1.62 / 1.62 ms
+#endif
+#ifndef SYZ_GSORT_SYNC_HEAD
+#define SYZ_GSORT_SYNC_HEAD 16  // rounds before the tail interval applies
+#endif
     const uint32_t cap_seg = std::min<uint32_t>(w.seg_cap, w.n / (SMALL + 1) + 1);
     uint32_t ncur = h[1], maxlen = h[4];
     bool exact = true;  // ncur is the device's count (a read-back), not a bound
+    int next_sync = SYNC_EVERY;
     for (int round = 0; ncur > 0 && !h[0]; round++) {
         if (round > 4096) return SYZCOV_EHIP;
         if (!split && exact && ncur >= SYZ_GSORT_SPLIT_MUL * nparts) split_now(cur, ccount, ncur);
@@ -1025,7 +1036,8 @@ static int run_rounds(SortWs &w, hipStream_t s, int64_t seeded = -1, uint32_t pa
         // bounds for the next round (exact after a read-back)
         ncur = std::min(2 * ncur, cap_seg);
         maxlen = maxlen > 1 ? maxlen - 1 : 0;
-        if ((round + 1) % SYNC_EVERY == 0 || maxlen <= SMALL) {
+        if (round + 1 == next_sync || maxlen <= SMALL) {
+            next_sync = round + 1 + (round + 1 < SYZ_GSORT_SYNC_HEAD ? SYNC_EVERY : SYZ_GSORT_SYNC_TAIL);
             if (int rc = read_ctl(h, w.ctl, 6, pin.get(), s)) return rc;
             ncur = h[ccount - w.ctl];
             maxlen = h[cmax - w.ctl];
