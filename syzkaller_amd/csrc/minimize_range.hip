@@ -1648,7 +1648,15 @@ static int minimize_range_impl(
 #define SYZ_MR_KEYS_PPS 2  // Minimize 19.3/17.3/18.3/19.3 ms, C3/8 rank 3.81/2.80/2.83/3.05
 #endif
     if (pcs_per_wg_hint == 0) pcs_per_wg_hint = 1 << SYZ_MR_HINT_LOG;
-    const uint64_t g_min = 256;     // at least one workgroup per CU
+    // pieces per chunk at least: 1 per CU, 4 in key mode, where the slices
+    // are XCD-local and a piece's table restage is cheap: the small chunks'
+    // few large pieces left a tail (g_min 256 / 512 / 768 / 1024 / 2048:
+    // C3/8 rank Minimize 2.63 / 2.60 / 2.60 / 2.59 / 2.71 ms, C2 2.34 / 2.27 /
+    // 2.28 / 2.24 / 2.26, pass 2 too: 0.11 -> 0.09)
+#ifndef SYZ_MR_GMIN_KEYS
+#define SYZ_MR_GMIN_KEYS 1024
+#endif
+    const uint64_t g_min = keym && !grp_off ? SYZ_MR_GMIN_KEYS : 256;
     const uint64_t avg_len = 2048;  // only sizes the grid; any value is exact
     // below 2^24 keys (64 MB of first_w) the covered set is rebuilt from first_w
     const bool cover_from_first = pc_span <= (1ull << 24);
