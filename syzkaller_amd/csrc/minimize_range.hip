@@ -1681,7 +1681,10 @@ static int minimize_range_impl(
             // P = 16R pieces per slice (fewer, larger pieces in the small chunks,
             // >= 256 KB of PCs each: 3.52 against 2.87 ms at C2); key mode 2R
             uint64_t G = ((b - a) * avg_len + pcs_per_wg_hint - 1) / pcs_per_wg_hint;
-            G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), 8192);
+#ifndef SYZ_MR_GMAX
+#define SYZ_MR_GMAX 8192
+#endif
+            G = std::min<uint64_t>(std::max<uint64_t>(G, g_min), SYZ_MR_GMAX);
             const uint64_t P = (keym ? SYZ_MR_KEYS_PPS : SYZ_MR_PPS) * (uint64_t)nrange;
             G = std::max<uint64_t>(G / P, 1) * P;  // whole slices
             // dynamic pieces: one workgroup per CU draws them
