@@ -1769,7 +1769,11 @@ static int minimize_range_impl(
         k_init = std::min<uint64_t>(k_init, n_items);
         static std::atomic<uint32_t> init_attr{0};
         const size_t lds_i = ((size_t)4 << mr::IQ_SH) + mr::INIT_LDS_EXTRA;
-        if ((rc = set_dyn_lds_once((const void *)mr::init_min_kernel<2>, (uint32_t)lds_i, init_attr)))
+#ifndef SYZ_MR_INIT_UG  // windows in flight: 1 / 2 / 3 / 4 -> C3/8 rank Minimize
+#define SYZ_MR_INIT_UG 2  // 2.61-2.67 / 2.59-2.68 / 2.78 / 2.98 ms (4: 316 B of spills)
+#endif
+        if ((rc = set_dyn_lds_once((const void *)mr::init_min_kernel<SYZ_MR_INIT_UG>, (uint32_t)lds_i,
+                                   init_attr)))
             return rc;
         // pieces: every workgroup slot of the GPU, at least one per range
 #ifndef SYZ_MR_INIT_WG
@@ -1782,7 +1786,7 @@ static int minimize_range_impl(
             std::max<uint64_t>(2 * nrange, (SYZ_MR_INIT_WG * dev_cus() + nq - 1) / nq);
         uint32_t *tab = (uint32_t *)rsort;  // free until the first chunk's rec_scatter
         SYZ_HIP(hipMemsetAsync(tab, 0xFF, T * 4, s));
-        hipLaunchKernelGGL(mr::init_min_kernel<2>, dim3((unsigned)(nq * P)), dim3(mr::THREADS),
+        hipLaunchKernelGGL(mr::init_min_kernel<SYZ_MR_INIT_UG>, dim3((unsigned)(nq * P)), dim3(mr::THREADS),
                            lds_i, s, A, 0u, (uint32_t)k_init, (uint32_t)P, tab);
         hipLaunchKernelGGL(mr::init_flush_kernel, dim3((unsigned)std::min<uint64_t>(
                                std::max<uint64_t>(T / 256, mr::NCTR), 4096)),
