@@ -60,6 +60,9 @@ struct CoverState {
     // maxCover changed outside the newcov kernels, which keep it in step)
     uint32_t *mfl = nullptr;
     bool mfl_stale = true;
+    // the device may leave mfl stale (newcov.hip, the fused pass's mfl mode:
+    // two words past mfl's bitmaps); a non-fused batch then rebuilds it
+    bool mfl_dev_mode = false;
     uint32_t *pc_of_key = nullptr;  // key mode: key -> PC (reads of maxCover)
     uint8_t *low_of_key = nullptr;  // key mode: membership table (pc_index)
     // key mode with kshift <= 4: the same table as nibbles over whole ranges

@@ -799,7 +799,9 @@ __global__ __launch_bounds__(1024) void fused_seg_kernel(const uint32_t *__restr
 }
 
 __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
-    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl,
+    const uint32_t *__restrict__ pcs, uint32_t npc, const uint32_t *__restrict__ mfl_,
+    const uint32_t *__restrict__ maxc, const uint32_t *__restrict__ flk,
+    const uint32_t *__restrict__ mode,
     uint64_t words_per_call, const uint32_t *__restrict__ nib, uint64_t nib_words, Index X,
     uint32_t nr, int ncalls, const uint32_t *__restrict__ segb,
     const uint32_t *__restrict__ wg_seg, const uint4 *__restrict__ rows,
@@ -828,10 +830,28 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
         lo = max(sb[0], a);
         hi = min(sb[1], b);
     };
+    // mfl mode 1 (nc_zero_kernel): mfl is stale, stage maxCover | flakes
+    const bool stale = mode && mode[0] == 1u;
+    const uint32_t *mfl = stale ? maxc : mfl_;
     auto load_bits = [&](uint32_t q, uint32_t c, uint4 (&sm)[SVM]) {
         const uint64_t mb = (uint64_t)q * MBW;
         const uint32_t nvm = (uint32_t)(min<uint64_t>(MBW, words_per_call - mb) >> 2);
         const uint4 *M4 = (const uint4 *)(mfl + (uint64_t)c * words_per_call + mb);
+        if (stale) {  // flakes: one bitmap for every call, L2-resident
+            const uint4 *F4 = (const uint4 *)(flk + mb);
+            uint4 fv[SVM];
+#pragma unroll
+            for (int i = 0; i < SVM; i++) {
+                const uint32_t j = t + i * LC_THREADS;
+                sm[i] = j < nvm ? M4[j] : make_uint4(~0u, ~0u, ~0u, ~0u);  // past the keys: covered
+                fv[i] = j < nvm ? F4[j] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < SVM; i++)
+                sm[i] = make_uint4(sm[i].x | fv[i].x, sm[i].y | fv[i].y, sm[i].z | fv[i].z,
+                                   sm[i].w | fv[i].w);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < SVM; i++) {
             const uint32_t j = t + i * LC_THREADS;
@@ -1218,13 +1238,40 @@ __global__ __launch_bounds__(256) void newcov_insert_kernel(
 }
 
 // The batch's zero fills in one launch: stats, the per-call counters, is_new
+// The mfl mode (fused pass, key mode).  In the early regime (millions of
+// candidates per batch) the ownership pass's atomicOr into mfl = maxCover |
+// flakes, one per owned candidate beside the one into maxCover, cost ~0.2 ms
+// of a 1.9 ms batch; in the steady state (no candidates) staging maxCover |
+// flakes per segment instead of mfl cost 14 us of 0.57 ms.  So the device
+// picks per batch, with no host round trip (mode[0] = this batch's, mode[1]
+// = the next one's, written by the ownership pass's block 0):
+//   0  mfl fresh: the fused pass stages mfl, the ownership pass keeps it;
+//   1  mfl stale: the fused pass stages maxCover | flakes, mfl untouched;
+//   3  stale, rebuild asked (a batch with few candidates saw mode 1): this
+//      kernel rebuilds mfl before the batch's fused pass, mode[0] = 0.
+// A batch above NOMFL_CANDS candidates leaves mfl stale (next mode 1).
+constexpr uint32_t NOMFL_CANDS = 1u << 19;
 __global__ __launch_bounds__(256) void nc_zero_kernel(uint32_t *__restrict__ stats,
                                                       uint32_t *__restrict__ ccnt, uint32_t nc,
-                                                      uint8_t *__restrict__ is_new, uint32_t nrec) {
+                                                      uint8_t *__restrict__ is_new, uint32_t nrec,
+                                                      uint32_t *__restrict__ mode,
+                                                      const uint4 *__restrict__ maxcov,
+                                                      const uint4 *__restrict__ flakes,
+                                                      uint64_t vec_per_call, uint64_t nv,
+                                                      uint4 *__restrict__ mfl) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
     if (t < 4) stats[t] = 0u;
     for (uint32_t c = t; c < nc; c += nt) ccnt[c] = 0u;
     for (uint32_t k = t; k < nrec; k += nt) is_new[k] = 0;
+    if (mode) {
+        const uint32_t nx = mode[1];  // (written only by the ownership pass)
+        if (nx == 3u)
+            for (uint64_t i = t; i < nv; i += nt) {
+                const uint4 m = maxcov[i], f = flakes[i % vec_per_call];
+                mfl[i] = make_uint4(m.x | f.x, m.y | f.y, m.z | f.z, m.w | f.w);
+            }
+        if (t == 0) mode[0] = nx == 1u ? 1u : 0u;
+    }
 }
 
 // stats_out (nullable): the caller's copy of stats[0..2), taken here (the
@@ -1301,8 +1348,13 @@ __global__ __launch_bounds__(256) void newcov_own32_kernel(
     const int32_t *__restrict__ callid, const uint2 *__restrict__ clist,
     const uint32_t *__restrict__ stats, const unsigned long long *__restrict__ slots,
     uint8_t *__restrict__ is_new, uint32_t *__restrict__ maxcov, uint32_t *__restrict__ mfl,
-    uint64_t words_per_call, Index X, uint32_t *__restrict__ stats_out) {
+    uint64_t words_per_call, Index X, uint32_t *__restrict__ stats_out, uint32_t *__restrict__ mode) {
     if (stats_out && blockIdx.x == 0 && threadIdx.x < 2) stats_out[threadIdx.x] = stats[threadIdx.x];
+    // the mfl mode (nc_zero_kernel): mode[0] is this batch's for every block
+    const uint32_t cand = stats[0] ? 0u : stats[1], cur = mode ? mode[0] : 0u;
+    if (mode && blockIdx.x == 0 && threadIdx.x == 0)
+        mode[1] = cand > NOMFL_CANDS ? 1u : cur == 1u ? 3u : 0u;
+    if (mode && (cand > NOMFL_CANDS || cur == 1u)) mfl = nullptr;  // left stale
     if (stats[0] || !stats[1]) return;
     const uint32_t n = stats[1];
     const uint64_t mask = hash_cap(n) - 1;
@@ -1758,8 +1810,14 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
     *stats_out = stats;
     const uint32_t nc = (uint32_t)st->ncalls;
     uint32_t *ccnt = st->grp, *coff = ccnt + nc + 1, *cur = coff + nc + 1, *ipre = cur + nc + 1;
+    // the mfl mode words (nc_zero_kernel) sit past mfl's bitmaps
+    // (this batch's fused and ownership passes get them only on the fused path)
+    uint32_t *mfl_mode = nullptr;
     hipLaunchKernelGGL(nc_zero_kernel, dim3(grid_for(std::max<uint64_t>(nrec, nc), 256, 256)),
-                       dim3(256), 0, s, stats, ccnt, nc, is_new, (uint32_t)nrec);
+                       dim3(256), 0, s, stats, ccnt, nc, is_new, (uint32_t)nrec,
+                       st->mfl ? st->mfl + (size_t)st->ncalls * st->words : nullptr,
+                       (const uint4 *)st->maxcov, (const uint4 *)st->flakes, st->words / 4,
+                       st->words / 4 * st->ncalls, (uint4 *)st->mfl);
     // records grouped by call (both passes)
     static std::atomic<uint32_t> gs_done{0};
     if (nc <= GRP_MAX_CALLS) {
@@ -1788,20 +1846,26 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
                      (forced == 1 ||
                       (forced == 0 && 2 * nr64 * (uint64_t)nc * range_bytes <= npc * 4));
     if (lds) {
-        if (!st->mfl) {
-            if (hipMalloc(&st->mfl, (size_t)st->ncalls * st->words * 4) != hipSuccess) {
+        if (!st->mfl) {  // + the mfl mode words
+            if (hipMalloc(&st->mfl, (size_t)st->ncalls * st->words * 4 + 256) != hipSuccess) {
                 st->mfl = nullptr;
                 return SYZCOV_ENOMEM;
             }
             st->mfl_stale = true;
         }
+        // a non-fused batch reads mfl itself: rebuild it if a fused batch may
+        // have left it stale
+        if (!fused && st->mfl_dev_mode) st->mfl_stale = true;
+        st->mfl_dev_mode = fused;
         if (st->mfl_stale) {
             const uint64_t vpc = st->words / 4, nv = vpc * st->ncalls;
             hipLaunchKernelGGL(mfl_build_kernel, dim3(grid_for(nv, 256, 16384)), dim3(256), 0, s,
                                (const uint4 *)st->maxcov, (const uint4 *)st->flakes, vpc, nv,
                                (uint4 *)st->mfl);
+            SYZ_HIP(hipMemsetAsync(st->mfl + (size_t)st->ncalls * st->words, 0, 8, s));  // mode 0
             st->mfl_stale = false;
         }
+        mfl_mode = fused ? st->mfl + (size_t)st->ncalls * st->words : nullptr;
         static std::atomic<uint32_t> lds_done[3], memb_done, fused_done;
         const bool sep = st->X.key_mode && st->nib && !fused;
         const int kv = !st->X.key_mode ? 0 : sep ? 2 : 1;
@@ -1864,7 +1928,9 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         if (fused) {
             const uint64_t nib_words = ((st->X.span + (1ull << RSH) - 1) >> RSH) << (RSH - 3);
             hipLaunchKernelGGL(newcov_fused_kernel, dim3(fused_g), dim3(LC_THREADS), FUSED_LDS, s,
-                               pcs, (uint32_t)npc, (const uint32_t *)st->mfl, st->words,
+                               pcs, (uint32_t)npc, (const uint32_t *)st->mfl,
+                               (const uint32_t *)st->maxcov, (const uint32_t *)st->flakes,
+                               (const uint32_t *)mfl_mode, st->words,
                                (const uint32_t *)st->nib, nib_words, st->X, nr, st->ncalls,
                                (const uint32_t *)segb, (const uint32_t *)wg_seg,
                                (const uint4 *)rows, (const uint32_t *)qoff, clist, stats);
@@ -1894,7 +1960,7 @@ static int newcov_launch(CoverState *st, const int32_t *callid, const uint64_t *
         hipLaunchKernelGGL(newcov_own32_kernel, dim3(gh), dim3(256), 0, s, callid,
                            (const uint2 *)clist, (const uint32_t *)stats,
                            (const unsigned long long *)hkey, is_new, st->maxcov, st->mfl,
-                           st->words, st->X, stats_user);
+                           st->words, st->X, stats_user, mfl_mode);
     } else {
         hipLaunchKernelGGL(hash_clear_kernel, dim3(gh), dim3(256), 0, s, (const uint32_t *)stats,
                            hkey, hval);
