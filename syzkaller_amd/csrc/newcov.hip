@@ -946,7 +946,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
             const uint32_t lo = z & 511u, hi = (z >> 9) & 511u, first = z >> 18 & 1u;
             const uint32_t lo1 = lo + first, n = hi - lo, n1 = hi - lo1;  // (hi > lo)
             const uint32_t v[4] = {pc[u].x, pc[u].y, pc[u].z, pc[u].w};
-            uint32_t o[4], wd[4], nw[4];
+            uint32_t o[4], wd[4], nw[4], nbs[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 o[c] = (v[c] >> ks) - obase;
@@ -963,6 +963,7 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
                 badv |= (uint32_t)(pv & ((c ? v[c - 1] : p0) > v[c]));
                 const bool cov = (wd[c] >> (o[c] & 31)) & 1u;
                 const uint32_t nb = (nw[c] >> ((o[c] & 7u) * 4u)) & 15u;
+                nbs[c] = nb;
                 nonv |= (uint32_t)(valid & cov & (nb != (v[c] & lowmask)));
                 cand |= (uint32_t)(valid & !cov) << c;
             }
@@ -971,10 +972,20 @@ __global__ __launch_bounds__(LC_THREADS, 1) void newcov_fused_kernel(
                 for (int c = 0; c < 4; c++) {
                     const uint64_t cm = __ballot((cand >> c) & 1u);
                     if (!cm) continue;
-                    // the candidates' membership, one byte each
-                    const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
-                        lr, (cm >> l) & 1u ? (v[c] >> ks) - X.kbase : 0xFFFFFFF0u, 0, 0);
-                    nonv |= (uint32_t)(((cm >> l) & 1u) & (mc != (v[c] & lowmask)));
+                    // the candidates' membership: the staged nibble settles it
+                    // unless it reads 15, which a key with no universe PC also
+                    // stages (0x7F & 15): only then the exact byte (every
+                    // candidate's byte load was ~1/3 of the early regime's
+                    // extra fused-pass time)
+                    const bool mine = (cm >> l) & 1u;
+                    const uint32_t lw = v[c] & lowmask;
+                    const bool exact = mine && nbs[c] == 15u && lw == 15u;
+                    nonv |= (uint32_t)(mine & !exact & (nbs[c] != lw));
+                    if (__ballot(exact)) {
+                        const uint32_t mc = __builtin_amdgcn_raw_buffer_load_b8(
+                            lr, exact ? (v[c] >> ks) - X.kbase : 0xFFFFFFF0u, 0, 0);
+                        nonv |= (uint32_t)(exact & (mc != lw));
+                    }
                     emit(cm, wave_readlane(my.y, i), v[c]);
                 }
             }

@@ -342,3 +342,46 @@ def test_newcov_batch_vs_sequential(torch):
         for c in range(ncalls):
             assert np.array_equal(st.max_cover(c), mc[c]), (batch, c)
     st.close()
+
+
+def test_newcov_key_mode_membership(torch):
+    """Key mode at kshift 4 (the fused candidate + membership pass of
+    newcov.hip) over a universe with gap keys (blocks of 16 PCs holding none)
+    and many PCs whose low bits are 15 — the value the staged nibble table
+    also holds for a gap key, so both the nibble test and the exact byte test
+    decide candidates.  Universe-only batches match the sequential reference
+    (syz-fuzzer/fuzzer.go:456-480); a batch holding a stray PC (a universe
+    PC's key, other low bits), a gap-key PC with low bits 15, or one with
+    other low bits is rejected and leaves maxCover as it was."""
+    from syzkaller_amd import SyzcovError
+    from syzkaller_amd.fuzzer import CoverState
+    rng = np.random.default_rng(5)
+    base, nblk, ncalls = 0x81000000, 1 << 15, 8
+    lows = rng.integers(0, 16, nblk)
+    lows[::7] = 15
+    gap = np.arange(nblk) % 3 == 0
+    univ = (base + 16 * np.arange(nblk, dtype=np.int64) + lows)[~gap].astype(np.uint32)
+    st = CoverState(ncalls, base, 16 * nblk)
+    st.set_universe(univ)
+    mc = [np.zeros(0, np.uint32) for _ in range(ncalls)]
+    flakes = np.zeros(0, np.uint32)
+    for batch in range(3):
+        nrec = 2000
+        cids = rng.integers(0, ncalls, size=nrec)
+        recs = [np.unique(rng.choice(univ, size=int(rng.integers(1, 300)))).astype(np.uint32)
+                for _ in range(nrec)]
+        exp_new, mc = orc.newcov_batch(mc, flakes, cids, recs)
+        assert np.array_equal(st.new_coverage(cids, recs), exp_new), batch
+    gk = np.flatnonzero(gap)
+    mk = np.flatnonzero(~gap)[123]
+    bad = [base + 16 * int(gk[5]) + 15, base + 16 * int(gk[9]) + 3,
+           base + 16 * int(mk) + (int(lows[mk]) + 1) % 16]
+    for pc in bad:
+        cids = rng.integers(0, ncalls, size=400)
+        recs = [np.unique(rng.choice(univ, size=60)).astype(np.uint32) for _ in range(400)]
+        recs[200] = np.unique(np.append(recs[200], np.uint32(pc))).astype(np.uint32)
+        with pytest.raises(SyzcovError):
+            st.new_coverage(cids, recs)
+        for c in range(ncalls):
+            assert np.array_equal(st.max_cover(c), mc[c]), (hex(pc), c)
+    st.close()
